@@ -1,0 +1,29 @@
+# Build the in-tree native libraries (gfx950 only).
+#   libghm_hip.so  : HIP kernels + C ABI (include/ghm_hip.h)
+#   libghm_host.so : host GHM sampler (include/ghm_sampler.h)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+LIBDIR := multimodal-ghm_amd/ghmclip/_lib
+SRC := multimodal-ghm_amd/csrc
+HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result
+HIP_SRCS := $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_optim.hip
+HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h include/ghm_hip.h
+
+all: $(LIBDIR)/libghm_hip.so $(LIBDIR)/libghm_host.so
+
+$(LIBDIR)/libghm_hip.so: $(HIP_SRCS) $(HIP_HDRS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -o $@ $(HIP_SRCS)
+
+$(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) -O3 -std=c++17 -fPIC -shared -o $@ $(SRC)/ghm_sampler.cpp
+
+resource-usage: $(HIP_SRCS) $(HIP_HDRS)
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_fwd.hip -o /tmp/ghm_fwd.o
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_bwd.hip -o /tmp/ghm_bwd.o
+
+clean:
+	rm -f $(LIBDIR)/*.so
+
+.PHONY: all clean resource-usage

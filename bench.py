@@ -1,0 +1,211 @@
+"""Benchmark: GHM CLIP training throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = the full CLIP training step of the default config
+(scripts/experiments/exp_clip_standardTF.sh:15-40: two 5-layer d=128 encoders
+over 81-token GHM sequences, K=4, batch 128 rows = 640 sequences per encoder,
+fwd + bwd + clip_grad_norm_ + AdamW), fp32 like the reference.  Per rank the
+batch is 128 rows (weak scaling); ranks average gradients with one RCCL
+all-reduce.  Inputs are GHM draws from the native sampler, pre-generated into
+a ring resident in HBM before the timed region.
+
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-ghm_amd"))
+
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+STEP_GFLOP = 625.87            # algorithmic work per step at B=128
+MLP_FWD_GFLOP_PER_LAUNCH = 4 * 51840 * 128 * 512 / 1e9  # one encoder-layer MLP: 2 GEMMs
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(n_gpus):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def build(rank, B, L, p, total_iters):
+    from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
+    from ghmclip.training.clip_trainer import ClipTrainer
+    p_y = np.ones(10) / 10
+    sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [p, p], K=4, seedtree=42)
+    seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
+    tm = EncoderTransformer(81, 10, 128, L).cuda()
+    im = EncoderTransformer(81, 10, 128, L).cuda()
+    sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, total_iters) for s in range(total_iters + 1)]
+    trainer = ClipTrainer(tm, im, 4, B, sched, device="cuda")
+    sampler.native.seed(224 + 1000 * rank)  # each rank draws its own shard of the global batch
+    return sampler, trainer
+
+
+def make_ring(sampler, B, R):
+    rows = B * 5
+    ring = torch.empty(R, 2, rows, 81, dtype=torch.uint8)
+    t = np.empty((rows, 81), np.uint8)
+    i = np.empty((rows, 81), np.uint8)
+    for r in range(R):
+        sampler.native.next_into(B, t, i)
+        ring[r, 0] = torch.from_numpy(t)
+        ring[r, 1] = torch.from_numpy(i)
+    return ring.cuda()
+
+
+def time_dominant_kernel(trainer, reps=20):
+    """Average duration of the dominant kernel (encoder-layer LN2+MLP forward,
+    k_ln_mlp_fwd) launched on the current stream, bracketed by HIP events."""
+    from ghmclip import _native
+    import ctypes
+    plan = trainer.plans[0]
+    pd = trainer.views[0][0]
+    s = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(s.cuda_stream)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def launch():
+        _native.call("ghm_ln_mlp_fwd", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
+                     ptr(pd["_mlps.0.0.weight"]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.weight"]),
+                     ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.U[0]), ptr(plan.st2[0]),
+                     plan.M, 128, 512, plan.eps, sp)
+    launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        launch()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps  # ms
+
+
+def cpu_baseline(B, L, steps=3):
+    from oracle import ghm_oracle as O
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    torch.set_num_threads(threads)
+    tr = O.OracleTrainer(p=0.2, B=B, L=L)
+    tr.step()  # warm-up
+    t0 = time.time()
+    for _ in range(steps):
+        tr.step()
+    dt = (time.time() - t0) / steps
+    return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} steps (after 1 warm-up) of the default CLIP config, B={B}, fp32 "
+                      f"PyTorch-CPU restatement of the reference (oracle/ghm_oracle.py); "
+                      f"{dt:.3f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128, help="rows per rank (default config: 128)")
+    ap.add_argument("--layers", type=int, default=5)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ring", type=int, default=16)
+    a = ap.parse_args()
+
+    ws, rank, local = setup_dist(a.gpus)
+    total_iters = max(3000, a.steps + a.warmup + 1)
+    sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters)
+    ring = make_ring(sampler, a.batch, a.ring)
+
+    def one(k):
+        tr.set_tokens(ring[k % a.ring, 0], ring[k % a.ring, 1])
+        tr.step()
+
+    for k in range(a.warmup):
+        one(k)
+        if k == 1 and not a.no_graph:
+            tr.capture()
+    if a.warmup < 2 and not a.no_graph:
+        tr.capture()
+
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        one(a.warmup + k)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    losses = tr.loss_history()
+    finite = bool(np.isfinite(losses).all())
+    kern_ms = time_dominant_kernel(tr)
+    if rank != 0:
+        if ws > 1:
+            dist.destroy_process_group()
+        return
+
+    ms = 1000.0 * elapsed / a.steps
+    steps_per_s = a.steps / elapsed
+    samples = a.batch * ws * a.steps
+    step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
+    achieved = MLP_FWD_GFLOP_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e3
+    out = {
+        "metric": "GHM training samples/sec (CLIP default config)",
+        "value": round(samples / elapsed, 2),
+        "unit": "samples/s",
+        "n_gpus": ws,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
+        "config": {"workload": "clip_default: 2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW",
+                   "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,
+                   "global_batch_rows": a.batch * ws, "n_layer": a.layers, "parallelism": f"dp{ws}",
+                   "hip_graph": not a.no_graph},
+        "roofline": {"bound": "mfma", "kernel": "k_ln_mlp_fwd (LN2+MLP fwd, one encoder-layer)",
+                     "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel_ms": round(kern_ms, 4)},
+        "steps_per_s": round(steps_per_s, 3),
+        "sequences_per_s": round(samples * 10 / elapsed, 1),
+        "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
+        "step_mfma_frac": round(step_gflop * steps_per_s / 1e3 / F32_MFMA_PEAK_TFLOPS, 4),
+        "loss_finite": finite,
+        "last_loss": float(losses[-1]) if len(losses) else None,
+    }
+    if ws == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.batch, a.layers)
+    print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

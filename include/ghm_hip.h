@@ -1,0 +1,135 @@
+/* ghm_hip.h — C ABI of libghm_hip.so, the MI355X (gfx950) kernels of the GHM
+ * CLIP training step.  Each entry point launches HIP work asynchronously on the
+ * caller's stream and returns 0, a hipError_t value (>0) or a negative GHM_E*
+ * code; ghm_last_error_string() gives detail.  No entry point allocates, frees
+ * or synchronises, so every call is graph-capturable.  All device buffers are
+ * caller-owned (PyTorch's caching allocator in the Python host).
+ *
+ * Layouts (one encoder): M = n_seq * T tokens; activations row-major [M][D]
+ * fp32 with D = 128; weights exactly as nn.Linear stores them ([out][in]).
+ * Every function replaces part of the reference's PyTorch-eager hot path; the
+ * reference file:line is given with each (paths under src/ghmclip/).
+ */
+#ifndef GHM_HIP_H
+#define GHM_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GHM_OK 0
+#define GHM_EINVAL (-22)   /* bad pointer / shape / unsupported configuration */
+
+const char* ghm_last_error_string(void);
+/* 1 when the library was built for gfx950 and a device is visible, else 0. */
+int ghm_device_ok(void);
+
+/* ---- forward ---------------------------------------------------------- */
+
+/* H0 = tok_w[tokens] + pos_w[t]  —  models/model.py:764-765 (EncoderTransformer.forward)
+ * tokens: uint8 [n_seq][T]; tok_w [V][D]; pos_w [T][D]; H0 [M][D]. */
+int ghm_embed_fwd(const uint8_t* tokens, const float* tok_w, const float* pos_w, float* H0,
+                  int64_t n_seq, int T, int V, int D, void* stream);
+
+/* qkv[:, 0:128|128:256|256:384] = LN1(H) Wq^T | Wk^T | Wv^T; stats[m] = (mean, rstd)
+ * —  models/model.py:772-775 (ln1 + _queries/_keys/_values). */
+int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln_b, const float* Wq,
+                   const float* Wk, const float* Wv, float* qkv, float* stats, int64_t M, int D,
+                   float eps, void* stream);
+
+/* H_mid = H + softmax(Q K^T / scale_div) V, single head over all D dims (no W_O);
+ * P (compact [n_seq][T][T]) saved for backward  —  models/model.py:778-782. */
+int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
+                 int D, float scale_div, void* stream);
+
+/* H_out = H_mid + W2 GELU(W1 LN2(H_mid) + b1) + b2; U = pre-GELU [M][F] saved;
+ * stats = LN2 (mean, rstd)  —  models/model.py:741-747,784-788. */
+int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float* ln_b, const float* W1,
+                   const float* b1, const float* W2, const float* b2, float* H_out, float* U,
+                   float* stats, int64_t M, int D, int F, float eps, void* stream);
+
+/* emb[n][c] = b_out + sum_t w_out[t] (b_ro[c] + H[n,t,:] . W_ro[c,:])
+ * —  models/model.py:802-805 (_read_out, transpose, _out). */
+int ghm_readout_fwd(const float* H, const float* W_ro, const float* b_ro, const float* w_out,
+                    const float* b_out, float* emb, int64_t n_seq, int T, int D, int C,
+                    void* stream);
+
+/* K-way symmetric CLIP loss (GuidedClipLoss, guide=False) and its gradient
+ * d(loss)/d(emb) for both towers; loss_out[0] = loss_out[1] = loss.  If hist is
+ * non-NULL, hist[*step] = loss (step read on device, for graph replay).
+ * —  models/model.py:877-907; train_CLIP.py:153-161. */
+int ghm_clip_loss(const float* t_emb, const float* i_emb, float* dt_emb, float* di_emb,
+                  float* loss_out, float* hist, const int32_t* step, int B, int K, int C,
+                  void* stream);
+
+/* ---- backward (autograd of train_CLIP.py:158) ------------------------- */
+
+/* dH_L and per-sequence partial parameter grads of the readout; reduce the
+ * partials with ghm_reduce_partials over n_seq  —  backward of model.py:802-805. */
+int ghm_readout_bwd(const float* H, const float* W_ro, const float* b_ro, const float* w_out,
+                    const float* d_emb, float* dH, float* part_wro, float* part_bro,
+                    float* part_wout, float* part_bout, int64_t n_seq, int T, int D, int C,
+                    void* stream);
+
+/* MLP + LN2 backward for one layer: writes dU [M][F] and dH_mid = dH_out + dLN2;
+ * part_ln [n_blocks][2][D] = partial (dgamma, dbeta) of LN2 where
+ * n_blocks = ghm_token_blocks(M)  —  backward of model.py:784-788. */
+int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
+                const float* W1, const float* W2, const float* U, float* dU, float* dH_mid,
+                float* part_ln, int64_t M, int D, int F, void* stream);
+
+/* Attention backward: dqkv[:, q|k|v] from dH_mid, qkv and P  —  backward of model.py:778-782. */
+int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dqkv,
+                 int64_t n_seq, int T, int D, float scale_div, void* stream);
+
+/* QKV + LN1 backward: dH = dH_mid + dLN1(dqkv W); part_ln as in ghm_mlp_bwd
+ * —  backward of model.py:772-775. */
+int ghm_qkv_bwd(const float* dqkv, const float* H, const float* stats, const float* ln_w,
+                const float* Wq, const float* Wk, const float* Wv, const float* dH_mid, float* dH,
+                float* part_ln, int64_t M, int D, void* stream);
+
+/* Split-K weight gradient C[a][b] = sum_m A[m][a] * op(B)[m][b] over token
+ * chunks of tok_per_split tokens: part [n_split][A_cols][B_cols];
+ * bias_part [n_split][A_cols] = sum_m A[m][a] (may be NULL).
+ * b_mode: 0 plain, 1 GELU(B), 2 LayerNorm(B; stats, ln_w, ln_b).
+ * A_cols and B_cols must be multiples of 128; tok_per_split a positive even number.
+ * Used for dW1/db1, dW2/db2, dWq|k|v (nn.Linear weight/bias grads). */
+int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols,
+              int b_mode, const float* stats, const float* ln_w, const float* ln_b, float* part,
+              float* bias_part, int64_t M, int tok_per_split, void* stream);
+
+/* Embedding backward partials: part_tok [n_chunk][V][D], part_pos [n_chunk][T][D],
+ * n_chunk = ceil(n_seq / seq_per_chunk)  —  backward of model.py:764-765. */
+int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, float* part_pos,
+                  int64_t n_seq, int T, int V, int D, int seq_per_chunk, void* stream);
+
+/* out[i] = sum_{s<n_split} part[s*n + i] in fixed order (deterministic).  The
+ * n outputs are written to up to 4 destination segments: segment k takes
+ * outputs [off[k], off[k+1]) into dst[k] (off[0] = 0, off[n_seg] = n). */
+int ghm_reduce_partials(const float* part, int n_split, int64_t n, int n_seg,
+                        float* const* dst, const int64_t* off, void* stream);
+
+/* ---- clip_grad_norm_ + AdamW (train_CLIP.py:163-167, optimizer.py:41-85) ---- */
+
+/* hyper[0] = ||g||_2, hyper[1] = min(1, max_norm/(||g|| + 1e-6)), then
+ * hyper[2..3] = sched[2*s .. 2*s+1] (lr_t, lr*weight_decay) for s = *step,
+ * and *step += 1.  work: >= 1024 floats of scratch. */
+int ghm_clip_prepare(const float* grad, int64_t n, float max_norm, const float* sched,
+                     int n_sched, int32_t* step, float* hyper, float* work, void* stream);
+
+/* In place over flat fp32 buffers (reference op order, IEEE rounding, no FMA
+ * contraction): g *= hyper[1]; m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+ * p -= lr_t m / (sqrt(v) + eps); p -= (lr wd) p. */
+int ghm_adamw(float* param, const float* grad, float* m, float* v, int64_t n, const float* hyper,
+              float b1, float one_minus_b1, float b2, float one_minus_b2, float eps,
+              void* stream);
+
+/* ---- helpers ----------------------------------------------------------- */
+/* number of 128-token blocks the token-parallel kernels use for M tokens */
+int64_t ghm_token_blocks(int64_t M);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,54 @@
+/* ghm_sampler.h — native host GHM sampler (C ABI), libghm_host.so.
+ *
+ * Replaces the per-step host producer of the reference CLIP loop:
+ *   ClipSampler.get_batch          src/ghmclip/data/data_random_GHM.py:753-784
+ *   GHMTree.gen_values (root given) src/ghmclip/data/data_random_GHM.py:145-165
+ * and reproduces numpy's legacy RandomState stream bit-exactly (MT19937,
+ * random_sample = (a>>5, b>>6) 53-bit doubles, randint via masked rejection), so
+ * a batch drawn here equals the reference's draw from the same numpy state.
+ *
+ * Ownership: the handle owns only host memory; output buffers are caller-owned.
+ * Errors: int return, 0 = success, negative GHM_E* on bad arguments.
+ * Threading: one handle per thread; no global state.
+ */
+#ifndef GHM_SAMPLER_H
+#define GHM_SAMPLER_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ghm_sampler ghm_sampler;
+
+/* t_trans / i_trans: [n_layer][n_child][V][V] float64 row-stochastic matrices
+ * (the distinct per-(layer, child-slot) templates of a translation-invariant
+ * GenTransition, data_random_GHM.py:43-89).  K = number of CLIP blocks minus one
+ * (batch rows = B*(K+1)).  Returns NULL on bad arguments. */
+ghm_sampler* ghm_sampler_create(const double* t_trans, const double* i_trans, int n_layer,
+                                int n_child, int V, int K);
+void ghm_sampler_destroy(ghm_sampler* s);
+
+/* Seed like numpy.random.seed(int) (init_genrand). */
+int ghm_sampler_seed(ghm_sampler* s, uint32_t seed);
+/* Import / export the numpy legacy MT19937 state: key[624] and pos (0..624). */
+int ghm_sampler_set_state(ghm_sampler* s, const uint32_t* key, int pos);
+int ghm_sampler_get_state(const ghm_sampler* s, uint32_t* key, int* pos);
+
+/* One ClipSampler.get_batch(batch_size=B, guide=False):
+ *   t_leaves, i_leaves : [B*(K+1)][n_child**n_layer] uint8, row = sequence
+ *   t_root, i_root     : [B*(K+1)] uint8 (may be NULL)
+ * Stream order: choice(V, B(K+1)) text roots, choice(V, B(K-1)) image roots
+ * (image rows [0,2B) reuse the text roots), text tree, image tree. */
+int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves,
+                     uint8_t* t_root, uint8_t* i_root);
+
+/* Raw stream access for tests: n doubles of numpy.random.random_sample(). */
+int ghm_sampler_random_sample(ghm_sampler* s, double* out, int64_t n);
+/* n draws of numpy.random.choice(V) (legacy masked rejection). */
+int ghm_sampler_choice(ghm_sampler* s, int V, int64_t n, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

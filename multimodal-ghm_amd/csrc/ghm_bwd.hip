@@ -1,0 +1,568 @@
+// Backward kernels of the GHM CLIP encoder step (the autograd of
+// src/ghmclip/training/train_CLIP.py:158 through models/model.py:760-808).
+// Parameter gradients are produced deterministically: per-block partials in a
+// fixed layout, summed in a fixed order by ghm_reduce_partials (no atomics).
+#include "ghm_common.h"
+#include "ghm_launch.h"
+
+// LayerNorm backward for one token held in accumulator layout (feature
+// f = 32*it + acc_row(r,h)); dy = dL/d(LN output).  Writes dH = dres + dx and,
+// reduced over the wave's 32 tokens, the (sum dy*xhat, sum dy) partials of
+// dgamma/dbeta into red_g/red_b[wave][f] (LDS).
+__device__ __forceinline__ void ln_bwd_acc(const f32x16* dy, const float* __restrict__ X,
+                                           float2 st, const float* __restrict__ lnw,
+                                           const float* __restrict__ dres, float* __restrict__ dH,
+                                           bool valid, int h, int j, float* red_g, float* red_b) {
+  const float mean = st.x, rstd = st.y;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f = 32 * it + acc_row(r, h);
+      const float xhat = (X[f] - mean) * rstd;
+      const float dyg = dy[it][r] * lnw[f];
+      s1 += dyg;
+      s2 += dyg * xhat;
+    }
+  }
+  s1 += xhalf(s1);
+  s2 += xhalf(s2);
+  const float m1 = s1 * (1.f / GHM_D), m2 = s2 * (1.f / GHM_D);
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f = 32 * it + acc_row(r, h);
+      const float xhat = (X[f] - mean) * rstd;
+      const float dyv = dy[it][r];
+      const float dx = rstd * (dyv * lnw[f] - m1 - xhat * m2);
+      if (valid) dH[f] = dres[f] + dx;
+      const float sg = sum32(valid ? dyv * xhat : 0.f);
+      const float sb = sum32(valid ? dyv : 0.f);
+      if (j == 0) {
+        red_g[f] = sg;
+        red_b[f] = sb;
+      }
+    }
+  }
+}
+
+// Sum the 4 waves' LN partials (fixed order) and write the block's partial.
+__device__ __forceinline__ void ln_partial_store(const float* red /*[2][4][128]*/, float* out) {
+  const int f = threadIdx.x;
+  if (f < GHM_D) {
+    out[f] = (red[f] + red[GHM_D + f]) + (red[2 * GHM_D + f] + red[3 * GHM_D + f]);
+    const float* rb = red + 4 * GHM_D;
+    out[GHM_D + f] = (rb[f] + rb[GHM_D + f]) + (rb[2 * GHM_D + f] + rb[3 * GHM_D + f]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MLP + LN2 backward, one wave = 32 tokens                    (model.py:784-788)
+//   dG^T = W2^T dY^T (per 32-unit chunk), dU = dG * GELU'(U) (stored),
+//   dX2^T += W1^T dU^T (accumulated in registers), then LN2 backward.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_mlp_bwd(
+    const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const float* __restrict__ W1, const float* __restrict__ W2,
+    const float* __restrict__ U, float* __restrict__ dU, float* __restrict__ dHmid,
+    float* __restrict__ part_ln, int64_t M) {
+  __shared__ float red[2 * 4 * GHM_D];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
+  const bool active = m0 < M;  // inactive waves still join the block reduction
+  for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  __syncthreads();
+  const int64_t m = m0 + j;
+  const bool valid = active && m < M;
+  const int64_t mc = m < M ? m : M - 1;
+  f32x16 dx[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) dx[it] = zero16();
+  if (active) {
+    float dy[64];
+    load64(dHout + mc * GHM_D + 64 * h, dy);  // dY[token][o = 64h + s]
+#pragma unroll 1
+    for (int c = 0; c < GHM_F / 32; ++c) {
+      // dG^T[hid][token] = sum_o W2[o][hid] dY[token][o]
+      f32x16 g = zero16();
+#pragma unroll
+      for (int s = 0; s < 64; ++s) g = mfma32(W2[static_cast<size_t>(64 * h + s) * GHM_F + 32 * c + j], dy[s], g);
+      float du[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int hid = 32 * c + acc_row(r, h);
+        const float v = g[r] * gelu_grad_f(U[mc * GHM_F + hid]);
+        du[r] = v;
+        if (valid) dU[m * GHM_F + hid] = v;
+      }
+      // dX2^T[in][token] += sum_hid W1[hid][in] dU[token][hid]
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          dx[it] = mfma32(W1[static_cast<size_t>(32 * c + acc_row(r, h)) * GHM_D + 32 * it + j], du[r], dx[it]);
+      }
+    }
+    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], lnw, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
+               red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
+  }
+  __syncthreads();
+  ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
+}
+
+// ---------------------------------------------------------------------------
+// QKV + LN1 backward, one wave = 32 tokens                    (model.py:772-775)
+//   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_qkv_bwd(
+    const float* __restrict__ dqkv, const float* __restrict__ H, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const float* __restrict__ Wq, const float* __restrict__ Wk,
+    const float* __restrict__ Wv, const float* __restrict__ dHmid, float* __restrict__ dH,
+    float* __restrict__ part_ln, int64_t M) {
+  __shared__ float red[2 * 4 * GHM_D];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
+  const bool active = m0 < M;
+  for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  __syncthreads();
+  const int64_t m = m0 + j;
+  const bool valid = active && m < M;
+  const int64_t mc = m < M ? m : M - 1;
+  f32x16 dx[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) dx[it] = zero16();
+  if (active) {
+#pragma unroll 1
+    for (int mat = 0; mat < 3; ++mat) {
+      const float* W = mat == 0 ? Wq : (mat == 1 ? Wk : Wv);
+      float g[64];
+      load64(dqkv + mc * (3 * GHM_D) + mat * GHM_D + 64 * h, g);  // dQ[token][o = 64h + s]
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+#pragma unroll
+        for (int s = 0; s < 64; ++s)
+          dx[it] = mfma32(W[static_cast<size_t>(64 * h + s) * GHM_D + 32 * it + j], g[s], dx[it]);
+      }
+    }
+    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], lnw, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
+               red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
+  }
+  __syncthreads();
+  ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
+}
+
+// ---------------------------------------------------------------------------
+// Attention backward, one workgroup per sequence               (model.py:778-782)
+// phase 1 (wave = query block): dP^T = V dO^T, dS = P (dP - rowsum(P dP)) / c,
+//          dQ^T = K^T dS^T; P and dS are staged to LDS as [query][key].
+// phase 2 (wave = key block):   dV^T = dO^T P, dK^T = Q^T dS  (sum over queries).
+// ---------------------------------------------------------------------------
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restrict__ qkv,
+                                                          const float* __restrict__ P,
+                                                          const float* __restrict__ dHmid,
+                                                          float* __restrict__ dqkv, int T,
+                                                          float scale_div) {
+  constexpr int TP = NKT * 32;
+  __shared__ float sP[TP][TP + 1];
+  __shared__ float sdS[TP][TP + 1];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  {
+    const int q = 32 * w + j;
+    const bool qv = q < T;
+    const int qc = qv ? q : T - 1;
+    float go[64];
+    load64(dHmid + (base + qc) * GHM_D + 64 * h, go);
+    f32x16 dp[NKT], p[NKT];
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const int key = 32 * kt + j;
+      const int kc = key < T ? key : T - 1;
+      const float4* vr = reinterpret_cast<const float4*>(qkv + (base + kc) * (3 * GHM_D) + 2 * GHM_D + 64 * h);
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float4 v = vr[i];
+        acc = mfma32(v.x, go[4 * i + 0], acc);
+        acc = mfma32(v.y, go[4 * i + 1], acc);
+        acc = mfma32(v.z, go[4 * i + 2], acc);
+        acc = mfma32(v.w, go[4 * i + 3], acc);
+      }
+      dp[kt] = acc;
+    }
+    float delta = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float pv = (qv && key < T) ? P[(base + q) * T + key] : 0.f;
+        p[kt][r] = pv;
+        delta += pv * dp[kt][r];
+      }
+    }
+    delta += xhalf(delta);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float ds = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+        dp[kt][r] = ds;
+        sP[q][key] = p[kt][r];
+        sdS[q][key] = ds;
+      }
+    }
+    // dQ^T[d][q] = sum_key K[key][d] dS[q][key]
+#pragma unroll 1
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x16 acc = zero16();
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = 32 * kt + acc_row(r, h);
+          const int kc = key < T ? key : T - 1;
+          acc = mfma32(qkv[(base + kc) * (3 * GHM_D) + GHM_D + 32 * dt + j], dp[kt][r], acc);
+        }
+      }
+      if (qv) {
+        float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[acc_row(r, h)] = acc[r];
+      }
+    }
+  }
+  __syncthreads();
+  {
+    const int key = 32 * w + j;
+    const bool kv = key < T;
+#pragma unroll 1
+    for (int dt = 0; dt < 4; ++dt) {
+      f32x16 aV = zero16(), aK = zero16();
+#pragma unroll 8
+      for (int s = 0; s < TP / 2; ++s) {
+        const int qq = 2 * s + h;
+        const int qc = qq < T ? qq : T - 1;
+        aV = mfma32(dHmid[(base + qc) * GHM_D + 32 * dt + j], sP[qq][key], aV);
+        aK = mfma32(qkv[(base + qc) * (3 * GHM_D) + 32 * dt + j], sdS[qq][key], aK);
+      }
+      if (kv) {
+        float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o[2 * GHM_D + acc_row(r, h)] = aV[r];
+          o[GHM_D + acc_row(r, h)] = aK[r];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split-K weight gradient: part[z][a][b] = sum_{m in chunk z} A[m][a] op(B)[m][b]
+// MFMA k-dimension = tokens (k-slot h = token parity).  4 waves as 2x2, each a
+// 64x64 tile; the workgroup covers 128 x 128 of the output.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, int lda,
+                                                  const float* __restrict__ Bs, int ldb,
+                                                  const float2* __restrict__ stats,
+                                                  const float* __restrict__ lnw,
+                                                  const float* __restrict__ lnb,
+                                                  float* __restrict__ part,
+                                                  float* __restrict__ bias_part, int64_t M,
+                                                  int tok_per_split, int Acols, int Bcols) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int a_base = blockIdx.x * 128 + (wave >> 1) * 64;
+  const int b_base = blockIdx.y * 128 + (wave & 1) * 64;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * tok_per_split;
+  int64_t m_end = m_begin + tok_per_split;
+  if (m_end > M) m_end = M;
+  float g0 = 1.f, g1 = 1.f, e0 = 0.f, e1 = 0.f;
+  if (MODE == 2) {
+    g0 = lnw[b_base + j]; g1 = lnw[b_base + 32 + j];
+    e0 = lnb[b_base + j]; e1 = lnb[b_base + 32 + j];
+  }
+  f32x16 acc00 = zero16(), acc01 = zero16(), acc10 = zero16(), acc11 = zero16();
+  float bs0 = 0.f, bs1 = 0.f;
+#pragma unroll 4
+  for (int64_t mm = m_begin; mm < m_end; mm += 2) {
+    const int64_t mt = mm + h;
+    const float msk = mt < m_end ? 1.f : 0.f;
+    const int64_t mc = mt < m_end ? mt : m_end - 1;
+    const float* ar = A + mc * lda + a_base + j;
+    const float* br = Bs + mc * ldb + b_base + j;
+    const float a0 = ar[0] * msk, a1 = ar[32] * msk;
+    float b0 = br[0], b1 = br[32];
+    if (MODE == 1) {
+      b0 = gelu_f(b0);
+      b1 = gelu_f(b1);
+    } else if (MODE == 2) {
+      const float2 st = stats[mc];
+      b0 = (b0 - st.x) * st.y * g0 + e0;
+      b1 = (b1 - st.x) * st.y * g1 + e1;
+    }
+    acc00 = mfma32(a0, b0, acc00);
+    acc01 = mfma32(a0, b1, acc01);
+    acc10 = mfma32(a1, b0, acc10);
+    acc11 = mfma32(a1, b1, acc11);
+    bs0 += a0;
+    bs1 += a1;
+  }
+  float* pz = part + static_cast<int64_t>(blockIdx.z) * Acols * Bcols;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t ra = a_base + acc_row(r, h);
+    pz[ra * Bcols + b_base + j] = acc00[r];
+    pz[ra * Bcols + b_base + 32 + j] = acc01[r];
+    pz[(ra + 32) * Bcols + b_base + j] = acc10[r];
+    pz[(ra + 32) * Bcols + b_base + 32 + j] = acc11[r];
+  }
+  if (bias_part && blockIdx.y == 0 && (wave & 1) == 0) {
+    bs0 += xhalf(bs0);
+    bs1 += xhalf(bs1);
+    if (h == 0) {
+      float* bz = bias_part + static_cast<int64_t>(blockIdx.z) * Acols;
+      bz[a_base + j] = bs0;
+      bz[a_base + 32 + j] = bs1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Readout backward, one workgroup per sequence                 (model.py:802-805)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_readout_bwd(
+    const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
+    const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
+    float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
+    float* __restrict__ part_bout, int T, int C) {
+  __shared__ float sW[16 * GHM_D];
+  __shared__ float sdP[128][17];
+  const int t = threadIdx.x, n = blockIdx.x;
+  const int64_t base = static_cast<int64_t>(n) * T;
+  for (int i = t; i < C * GHM_D; i += 128) sW[i] = Wro[i];
+  float de[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) de[c] = c < C ? demb[static_cast<int64_t>(n) * C + c] : 0.f;
+  __syncthreads();
+  if (t < T) {
+    float p[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) p[c] = 0.f;
+    const float4* row = reinterpret_cast<const float4*>(H + (base + t) * GHM_D);
+    for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
+      const float4 hv = row[d4];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c < C) {
+          const float* wc = sW + c * GHM_D + 4 * d4;
+          p[c] += hv.x * wc[0] + hv.y * wc[1] + hv.z * wc[2] + hv.w * wc[3];
+        }
+      }
+    }
+    float dw = 0.f;
+    const float wt = wout[t];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c < C) {
+        dw += de[c] * (p[c] + bro[c]);
+        sdP[t][c] = de[c] * wt;
+      }
+    }
+    part_wout[base + t] = dw;
+  }
+  __syncthreads();
+  // thread = feature d: dH[t][d] and the partial dW_ro[c][d]
+  const int d = t;
+  float aw[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) aw[c] = 0.f;
+  for (int tt = 0; tt < T; ++tt) {
+    const float hv = H[(base + tt) * GHM_D + d];
+    float dh = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c < C) {
+        const float dpv = sdP[tt][c];
+        aw[c] += dpv * hv;
+        dh += dpv * sW[c * GHM_D + d];
+      }
+    }
+    dH[(base + tt) * GHM_D + d] = dh;
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+    if (c < C) part_wro[(static_cast<int64_t>(n) * C + c) * GHM_D + d] = aw[c];
+  if (t < C) {
+    float s = 0.f;
+    for (int tt = 0; tt < T; ++tt) s += sdP[tt][t];
+    part_bro[static_cast<int64_t>(n) * C + t] = s;
+  }
+  if (t == 0) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += de[c];
+    part_bout[n] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Embedding backward partials; thread = feature d, workgroup = chunk of sequences
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0,
+                                                   const uint8_t* __restrict__ tok,
+                                                   float* __restrict__ part_tok,
+                                                   float* __restrict__ part_pos, int64_t n_seq,
+                                                   int T, int V, int spc) {
+  const int d = threadIdx.x;
+  const int64_t n_begin = static_cast<int64_t>(blockIdx.x) * spc;
+  int64_t n_end = n_begin + spc;
+  if (n_end > n_seq) n_end = n_seq;
+  float at[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) at[c] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    float ap = 0.f;
+    for (int64_t n = n_begin; n < n_end; ++n) {
+      const int64_t m = n * T + t;
+      const float v = dH0[m * GHM_D + d];
+      const int tv = tok[m];
+      ap += v;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) at[c] += (tv == c) ? v : 0.f;
+    }
+    part_pos[(static_cast<int64_t>(blockIdx.x) * T + t) * GHM_D + d] = ap;
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+    if (c < V) part_tok[(static_cast<int64_t>(blockIdx.x) * V + c) * GHM_D + d] = at[c];
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic partial reduction into up to 4 destination segments
+// ---------------------------------------------------------------------------
+struct SegDst {
+  float* dst[4];
+  int64_t off[5];
+  int n_seg;
+};
+
+__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ part, int n_split,
+                                                int64_t n, SegDst seg) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < n_split; ++k) s += part[static_cast<int64_t>(k) * n + i];
+  int g = 0;
+  while (g + 1 < seg.n_seg && i >= seg.off[g + 1]) ++g;
+  seg.dst[g][i - seg.off[g]] = s;
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI launchers
+// ---------------------------------------------------------------------------
+extern "C" int ghm_readout_bwd(const float* H, const float* W_ro, const float* b_ro,
+                               const float* w_out, const float* d_emb, float* dH, float* part_wro,
+                               float* part_bro, float* part_wout, float* part_bout, int64_t n_seq,
+                               int T, int D, int C, void* stream) {
+  GHM_CHECK(H && W_ro && b_ro && w_out && d_emb && dH && part_wro && part_bro && part_wout && part_bout,
+            "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= 128 && C >= 1 && C <= 16 && n_seq >= 1, "shape");
+  hipLaunchKernelGGL(k_readout_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0, ghm_stream(stream),
+                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T, C);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats,
+                           const float* ln_w, const float* W1, const float* W2, const float* U,
+                           float* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
+                           void* stream) {
+  GHM_CHECK(dH_out && H_mid && stats && ln_w && W1 && W2 && U && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  hipLaunchKernelGGL(k_mlp_bwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w, W1,
+                     W2, U, dU, dH_mid, part_ln, M);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dqkv,
+                            int64_t n_seq, int T, int D, float scale_div, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dqkv, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  hipStream_t s = ghm_stream(stream);
+  if (T <= 32)
+    hipLaunchKernelGGL(k_attn_bwd<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+  else if (T <= 64)
+    hipLaunchKernelGGL(k_attn_bwd<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+  else
+    hipLaunchKernelGGL(k_attn_bwd<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_qkv_bwd(const float* dqkv, const float* H, const float* stats, const float* ln_w,
+                           const float* Wq, const float* Wk, const float* Wv, const float* dH_mid,
+                           float* dH, float* part_ln, int64_t M, int D, void* stream) {
+  GHM_CHECK(dqkv && H && stats && ln_w && Wq && Wk && Wv && dH_mid && dH && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  hipLaunchKernelGGL(k_qkv_bwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dqkv, H, reinterpret_cast<const float2*>(stats), ln_w, Wq, Wk, Wv,
+                     dH_mid, dH, part_ln, M);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols,
+                         int b_mode, const float* stats, const float* ln_w, const float* ln_b,
+                         float* part, float* bias_part, int64_t M, int tok_per_split, void* stream) {
+  GHM_CHECK(A && B && part, "null pointer");
+  GHM_CHECK(A_cols > 0 && B_cols > 0 && A_cols % 128 == 0 && B_cols % 128 == 0, "A_cols/B_cols % 128");
+  GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
+  GHM_CHECK(tok_per_split > 0 && tok_per_split % 2 == 0, "tok_per_split must be positive and even");
+  GHM_CHECK(b_mode >= 0 && b_mode <= 2, "b_mode");
+  GHM_CHECK(b_mode != 2 || (stats && ln_w && ln_b), "layernorm mode needs stats/ln_w/ln_b");
+  const int64_t nsplit = (M + tok_per_split - 1) / tok_per_split;
+  GHM_CHECK(nsplit <= 65535, "too many splits");
+  dim3 grid(A_cols / 128, B_cols / 128, static_cast<unsigned>(nsplit));
+  hipStream_t s = ghm_stream(stream);
+  const float2* st = reinterpret_cast<const float2*>(stats);
+  if (b_mode == 0)
+    hipLaunchKernelGGL(k_wgrad<0>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                       tok_per_split, A_cols, B_cols);
+  else if (b_mode == 1)
+    hipLaunchKernelGGL(k_wgrad<1>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                       tok_per_split, A_cols, B_cols);
+  else
+    hipLaunchKernelGGL(k_wgrad<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                       tok_per_split, A_cols, B_cols);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok,
+                             float* part_pos, int64_t n_seq, int T, int V, int D, int seq_per_chunk,
+                             void* stream) {
+  GHM_CHECK(dH0 && tokens && part_tok && part_pos, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && V >= 1 && V <= 16 && n_seq >= 1 && seq_per_chunk >= 1, "shape");
+  const int64_t nchunk = (n_seq + seq_per_chunk - 1) / seq_per_chunk;
+  hipLaunchKernelGGL(k_embed_bwd, dim3(static_cast<unsigned>(nchunk)), dim3(128), 0, ghm_stream(stream), dH0,
+                     tokens, part_tok, part_pos, n_seq, T, V, seq_per_chunk);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_reduce_partials(const float* part, int n_split, int64_t n, int n_seg,
+                                   float* const* dst, const int64_t* off, void* stream) {
+  GHM_CHECK(part && dst && off, "null pointer");
+  GHM_CHECK(n_split >= 1 && n >= 1 && n_seg >= 1 && n_seg <= 4, "shape");
+  SegDst seg;
+  seg.n_seg = n_seg;
+  for (int k = 0; k < 4; ++k) seg.dst[k] = k < n_seg ? dst[k] : nullptr;
+  for (int k = 0; k < 5; ++k) seg.off[k] = k <= n_seg ? off[k] : n;
+  GHM_CHECK(seg.off[0] == 0 && seg.off[n_seg] == n, "segment offsets");
+  for (int k = 0; k < n_seg; ++k) GHM_CHECK(seg.dst[k] && seg.off[k] <= seg.off[k + 1], "segment");
+  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, ghm_stream(stream),
+                     part, n_split, n, seg);
+  return ghm_launch_status();
+}

@@ -1,0 +1,90 @@
+// Shared device helpers for the GHM CLIP kernels (gfx950 / CDNA4 only).
+//
+// Compute model:
+//   * fp32 everywhere (the reference trains in fp32).  Matrix products use the
+//     exact-f32 MFMA v_mfma_f32_32x32x2_f32: a k-ordered fmaf chain, no TF32.
+//   * "tokens on lanes": a wave owns 32 tokens; lane l = (j = l&31, h = l>>5).
+//     Activations enter MFMAs as the B operand (column j = token), weights as
+//     the A operand (row i = output feature), so every output tile is Yᵀ with
+//     the token on the lane and features in the 16 accumulator registers:
+//         feature(r, h) = (r & 3) + 8 * (r >> 2) + 4 * h      (r = 0..15)
+//     That accumulator is directly the B operand of the next product that sums
+//     over those features (MLP up -> GELU -> down stays in registers).
+//   * row layout: a token row of 128 features is held as x[s] = row[64h + s].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define GHM_D 128     // embedding width (n_embd); the kernels are built for 128
+#define GHM_F 512     // MLP hidden width = 4 * n_embd
+#define GHM_MAXT 96   // longest sequence (tokens) the attention kernels take
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// feature / row index held in accumulator register r by lane half h
+__device__ __forceinline__ constexpr int acc_row(int r, int h) {
+  return (r & 3) + 8 * (r >> 2) + 4 * h;
+}
+
+// lane-pair (l, l^32) exchange
+__device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32, 64); }
+
+// sum over the 32 lanes of one half (lanes j = 0..31 for fixed h)
+__device__ __forceinline__ float sum32(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+// load 64 consecutive floats (16 x float4) into x[0..63]
+__device__ __forceinline__ void load64(const float* __restrict__ p, float* x) {
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float4 v = q[i];
+    x[4 * i + 0] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+  }
+}
+
+// exact GELU, torch approximate='none': x * 0.5 * (1 + erf(x / sqrt(2)))
+__device__ __forceinline__ float gelu_f(float x) {
+  return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+}
+// torch GeluBackward (approximate='none'): dy * (cdf + x * pdf)
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Row LayerNorm statistics for a token held in row layout by lane pair (j,h):
+// two-pass mean / biased variance over 128 features.
+__device__ __forceinline__ void ln_stats64(const float* x, float eps, float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) s += x[k];
+  s += xhalf(s);
+  mean = s * (1.f / 128.f);
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 64; ++k) {
+    const float d = x[k] - mean;
+    v += d * d;
+  }
+  v += xhalf(v);
+  rstd = 1.f / sqrtf(v * (1.f / 128.f) + eps);
+}

@@ -1,0 +1,448 @@
+// Forward kernels of the GHM CLIP encoder step (gfx950, fp32 via exact-f32 MFMA).
+// Reference semantics: src/ghmclip/models/model.py:760-808 (EncoderTransformer.forward)
+// and :877-907 (GuidedClipLoss, guide=False).  See ghm_common.h for the
+// "tokens on lanes" register layout shared by all token-parallel kernels.
+#include "ghm_common.h"
+
+// ---------------------------------------------------------------------------
+// H0[m] = tok_w[tokens[m]] + pos_w[m % T]                      (model.py:764-765)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_embed_fwd(const uint8_t* __restrict__ tok,
+                                                   const float* __restrict__ tok_w,
+                                                   const float* __restrict__ pos_w,
+                                                   float* __restrict__ H, int64_t M, int T, int V) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= M * 32) return;
+  const int64_t m = idx >> 5;
+  const int c4 = static_cast<int>(idx & 31);
+  const int t = static_cast<int>(m % T);
+  int v = tok[m];
+  v = v < V ? v : V - 1;  // host validates; never read out of the table
+  const float4 a = reinterpret_cast<const float4*>(tok_w + v * GHM_D)[c4];
+  const float4 b = reinterpret_cast<const float4*>(pos_w + t * GHM_D)[c4];
+  reinterpret_cast<float4*>(H + m * GHM_D)[c4] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// Load one token row (row layout), LayerNorm it in place; returns stats.
+__device__ __forceinline__ void ln_row(const float* __restrict__ row, const float* __restrict__ lnw,
+                                       const float* __restrict__ lnb, int h, float eps, float* x,
+                                       float& mean, float& rstd) {
+  load64(row + 64 * h, x);
+  ln_stats64(x, eps, mean, rstd);
+  const float4* g4 = reinterpret_cast<const float4*>(lnw + 64 * h);
+  const float4* b4 = reinterpret_cast<const float4*>(lnb + 64 * h);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 g = g4[q], b = b4[q];
+    x[4 * q + 0] = (x[4 * q + 0] - mean) * rstd * g.x + b.x;
+    x[4 * q + 1] = (x[4 * q + 1] - mean) * rstd * g.y + b.y;
+    x[4 * q + 2] = (x[4 * q + 2] - mean) * rstd * g.z + b.z;
+    x[4 * q + 3] = (x[4 * q + 3] - mean) * rstd * g.w + b.w;
+  }
+}
+
+// Y^T tile (32 out features x 32 tokens) = W[o0:o0+32, :] . X^T, X in row layout.
+// A operand: lane (i=j, h) streams W[o0 + j][64h + s]; B operand: x[s].
+__device__ __forceinline__ f32x16 proj_tile(const float* __restrict__ W, int o0, int j, int h,
+                                            const float* x) {
+  const float4* wr = reinterpret_cast<const float4*>(W + static_cast<size_t>(o0 + j) * GHM_D + 64 * h);
+  f32x16 acc = zero16();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const float4 w = wr[q];
+    acc = mfma32(w.x, x[4 * q + 0], acc);
+    acc = mfma32(w.y, x[4 * q + 1], acc);
+    acc = mfma32(w.z, x[4 * q + 2], acc);
+    acc = mfma32(w.w, x[4 * q + 3], acc);
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// LN1 + Q/K/V projections                                       (model.py:772-775)
+// one wave = 32 tokens, 4 waves per workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd(
+    const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const float* __restrict__ Wq, const float* __restrict__ Wk, const float* __restrict__ Wv,
+    float* __restrict__ qkv, float2* __restrict__ stats, int64_t M, float eps) {
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  if (m0 >= M) return;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  float x[64], mean, rstd;
+  ln_row(H + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
+  if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+#pragma unroll 1
+  for (int mat = 0; mat < 3; ++mat) {
+    const float* W = mat == 0 ? Wq : (mat == 1 ? Wk : Wv);
+#pragma unroll 1
+    for (int ot = 0; ot < 4; ++ot) {
+      const f32x16 acc = proj_tile(W, ot * 32, j, h, x);
+      if (valid) {
+        float* o = qkv + m * (3 * GHM_D) + mat * GHM_D + ot * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[acc_row(r, h)] = acc[r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Single-head full-width softmax attention + residual           (model.py:778-782)
+// one workgroup = one sequence; wave w = query block [32w, 32w+32).
+// S^T = K Q^T keeps the query on the lane, so the softmax row lives in the
+// lane's registers (+ one lane-pair exchange) and the probabilities are the B
+// operand of O^T = V^T P^T without leaving registers.
+// ---------------------------------------------------------------------------
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restrict__ qkv,
+                                                          const float* __restrict__ H,
+                                                          float* __restrict__ Hmid,
+                                                          float* __restrict__ P, int T,
+                                                          float scale_div) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  float xq[64];
+  load64(qkv + (base + qc) * (3 * GHM_D) + 64 * h, xq);
+  f32x16 s[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int key = 32 * kt + j;
+    const int kc = key < T ? key : T - 1;
+    const float4* kr = reinterpret_cast<const float4*>(qkv + (base + kc) * (3 * GHM_D) + GHM_D + 64 * h);
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float4 kv = kr[i];
+      acc = mfma32(kv.x, xq[4 * i + 0], acc);
+      acc = mfma32(kv.y, xq[4 * i + 1], acc);
+      acc = mfma32(kv.z, xq[4 * i + 2], acc);
+      acc = mfma32(kv.w, xq[4 * i + 3], acc);
+    }
+    s[kt] = acc;
+  }
+  // softmax over keys for query q (= this lane's column)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * kt + acc_row(r, h);
+      const float v = key < T ? s[kt][r] / scale_div : -INFINITY;
+      s[kt][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  }
+  mx = fmaxf(mx, xhalf(mx));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kt][r] - mx);
+      s[kt][r] = e;
+      sum += e;
+    }
+  }
+  sum += xhalf(sum);
+  const float inv = 1.f / sum;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[kt][r] *= inv;
+      const int key = 32 * kt + acc_row(r, h);
+      if (qv && key < T) P[(base + q) * T + key] = s[kt][r];
+    }
+  }
+  // O^T[d][q] = sum_key V[key][d] P[q][key]
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const int kc = key < T ? key : T - 1;
+        const float a = qkv[(base + kc) * (3 * GHM_D) + 2 * GHM_D + 32 * dt + j];
+        acc = mfma32(a, s[kt][r], acc);
+      }
+    }
+    if (qv) {
+      const int64_t row = (base + q) * GHM_D + 32 * dt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = acc_row(r, h);
+        Hmid[row + d] = H[row + d] + acc[r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LN2 + MLP (128 -> 512 -> GELU -> 128) + residual             (model.py:784-788)
+// The 512-wide hidden activation never leaves registers: each 32-unit chunk of
+// U^T is GELU'd in place and is immediately the B operand of the down product.
+// U (pre-GELU) is stored for the backward pass.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
+    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
+    const float* __restrict__ b2, float* __restrict__ Hout, float* __restrict__ U,
+    float2* __restrict__ stats, int64_t M, float eps) {
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  if (m0 >= M) return;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  float x[64], mean, rstd;
+  ln_row(Hmid + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
+  if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  f32x16 y[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) y[ot] = zero16();
+#pragma unroll 1
+  for (int c = 0; c < GHM_F / 32; ++c) {
+    const f32x16 u = proj_tile(W1, 32 * c, j, h, x);
+    float g[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int hid = 32 * c + acc_row(r, h);
+      const float uu = u[r] + b1[hid];
+      if (valid) U[m * GHM_F + hid] = uu;
+      g[r] = gelu_f(uu);
+    }
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      // A operand: W2[32ot + j][hid(r, h)], hid(4q+t, h) = 32c + 8q + 4h + t
+      const float* w2 = W2 + static_cast<size_t>(32 * ot + j) * GHM_F + 32 * c + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = *reinterpret_cast<const float4*>(w2 + 8 * q);
+        y[ot] = mfma32(w.x, g[4 * q + 0], y[ot]);
+        y[ot] = mfma32(w.y, g[4 * q + 1], y[ot]);
+        y[ot] = mfma32(w.z, g[4 * q + 2], y[ot]);
+        y[ot] = mfma32(w.w, g[4 * q + 3], y[ot]);
+      }
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = 32 * ot + acc_row(r, h);
+        Hout[m * GHM_D + o] = Hmid[m * GHM_D + o] + (y[ot][r] + b2[o]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Readout: Linear(D->C) over every token, then Linear(T->1) over the token axis
+// (model.py:802-805).  One workgroup per sequence, thread = token.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_readout_fwd(const float* __restrict__ H,
+                                                     const float* __restrict__ Wro,
+                                                     const float* __restrict__ bro,
+                                                     const float* __restrict__ wout,
+                                                     const float* __restrict__ bout,
+                                                     float* __restrict__ emb, int T, int C) {
+  __shared__ float sW[16 * GHM_D];
+  __shared__ float red[2][16];
+  const int t = threadIdx.x, n = blockIdx.x;
+  for (int i = t; i < C * GHM_D; i += 128) sW[i] = Wro[i];
+  __syncthreads();
+  float p[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) p[c] = 0.f;
+  if (t < T) {
+    const float4* row = reinterpret_cast<const float4*>(H + (static_cast<int64_t>(n) * T + t) * GHM_D);
+    for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
+      const float4 hv = row[d4];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (c < C) {
+          const float* wc = sW + c * GHM_D + 4 * d4;
+          p[c] += hv.x * wc[0] + hv.y * wc[1] + hv.z * wc[2] + hv.w * wc[3];
+        }
+      }
+    }
+    const float wt = wout[t];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) p[c] = c < C ? (p[c] + bro[c]) * wt : 0.f;
+  }
+  const int lane = t & 63, wv = t >> 6;
+  // deterministic wave reduction: 32-lane butterfly, then the lane-pair exchange
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const float v = sum32(p[c]);
+    p[c] = v + __shfl_xor(v, 32, 64);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) red[wv][c] = p[c];
+  }
+  __syncthreads();
+  if (t < C) emb[static_cast<int64_t>(n) * C + t] = red[0][t] + red[1][t] + bout[0];
+}
+
+// ---------------------------------------------------------------------------
+// K-way symmetric CLIP loss + gradient, one workgroup        (model.py:877-907)
+// Rows are blocks b = 0..K of B rows; row i of block 0 (text) / 1 (image) is
+// scored against its matched partner and row i of blocks 2..K.  exp() is
+// unshifted, exactly as the reference.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float dotc(const float* a, const float* b, int C) {
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += a[c] * b[c];
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_clip_loss(const float* __restrict__ te,
+                                                   const float* __restrict__ ie,
+                                                   float* __restrict__ dte, float* __restrict__ die,
+                                                   float* __restrict__ loss_out,
+                                                   float* __restrict__ hist,
+                                                   const int32_t* __restrict__ step, int B, int K,
+                                                   int C) {
+  __shared__ float red[4];
+  const float invB = 1.f / static_cast<float>(B);
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    // direction 1: image i of block 0 vs text i of block 0 and of blocks 2..K
+    {
+      const float* tm = te + static_cast<int64_t>(i) * C;
+      const float* im = ie + static_cast<int64_t>(i) * C;
+      const float Sm = expf(dotc(tm, im, C));
+      float Sn = 0.f;
+      for (int k = 2; k <= K; ++k) Sn += expf(dotc(te + (static_cast<int64_t>(k) * B + i) * C, im, C));
+      acc += -logf(Sm / (Sm + Sn));
+      const float den = Sm + Sn;
+      const float ga = -(Sn / den) * invB;
+      float* dtm = dte + static_cast<int64_t>(i) * C;
+      float* dim = die + static_cast<int64_t>(i) * C;
+      for (int c = 0; c < C; ++c) { dtm[c] = ga * im[c]; dim[c] = ga * tm[c]; }
+      for (int k = 2; k <= K; ++k) {
+        const float* tk = te + (static_cast<int64_t>(k) * B + i) * C;
+        const float gb = (expf(dotc(tk, im, C)) / den) * invB;
+        float* dtk = dte + (static_cast<int64_t>(k) * B + i) * C;
+        for (int c = 0; c < C; ++c) { dtk[c] = gb * im[c]; dim[c] += gb * tk[c]; }
+      }
+    }
+    // direction 2: text i of block 1 vs image i of block 1 and of blocks 2..K
+    {
+      const float* tm = te + (static_cast<int64_t>(B) + i) * C;
+      const float* im = ie + (static_cast<int64_t>(B) + i) * C;
+      const float Sm = expf(dotc(tm, im, C));
+      float Sn = 0.f;
+      for (int k = 2; k <= K; ++k) Sn += expf(dotc(ie + (static_cast<int64_t>(k) * B + i) * C, tm, C));
+      acc += -logf(Sm / (Sm + Sn));
+      const float den = Sm + Sn;
+      const float ga = -(Sn / den) * invB;
+      float* dtm = dte + (static_cast<int64_t>(B) + i) * C;
+      float* dim = die + (static_cast<int64_t>(B) + i) * C;
+      for (int c = 0; c < C; ++c) { dtm[c] = ga * im[c]; dim[c] = ga * tm[c]; }
+      for (int k = 2; k <= K; ++k) {
+        const float* ik = ie + (static_cast<int64_t>(k) * B + i) * C;
+        const float gb = (expf(dotc(ik, tm, C)) / den) * invB;
+        float* dik = die + (static_cast<int64_t>(k) * B + i) * C;
+        for (int c = 0; c < C; ++c) { dik[c] = gb * tm[c]; dtm[c] += gb * ik[c]; }
+      }
+    }
+  }
+  // deterministic block reduction
+  acc = sum32(acc);
+  acc += __shfl_xor(acc, 32, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float loss = ((red[0] + red[1]) + (red[2] + red[3])) * invB;
+    loss_out[0] = loss;
+    loss_out[1] = loss;
+    if (hist) hist[*step] = loss;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI launchers
+// ---------------------------------------------------------------------------
+#include "ghm_launch.h"
+
+extern "C" int ghm_embed_fwd(const uint8_t* tokens, const float* tok_w, const float* pos_w,
+                             float* H0, int64_t n_seq, int T, int V, int D, void* stream) {
+  GHM_CHECK(tokens && tok_w && pos_w && H0, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && V >= 1 && n_seq >= 1, "shape");
+  const int64_t M = n_seq * T;
+  const int64_t n = M * 32;
+  hipLaunchKernelGGL(k_embed_fwd, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     ghm_stream(stream), tokens, tok_w, pos_w, H0, M, T, V);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln_b,
+                              const float* Wq, const float* Wk, const float* Wv, float* qkv,
+                              float* stats, int64_t M, int D, float eps, void* stream) {
+  GHM_CHECK(H && ln_w && ln_b && Wq && Wk && Wv && qkv && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  hipLaunchKernelGGL(k_ln_qkv_fwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H, ln_w, ln_b, Wq, Wk, Wv, qkv,
+                     reinterpret_cast<float2*>(stats), M, eps);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P,
+                            int64_t n_seq, int T, int D, float scale_div, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  hipStream_t s = ghm_stream(stream);
+  if (T <= 32)
+    hipLaunchKernelGGL(k_attn_fwd<1>, dim3(g), dim3(64), 0, s, qkv, H, H_mid, P, T, scale_div);
+  else if (T <= 64)
+    hipLaunchKernelGGL(k_attn_fwd<2>, dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div);
+  else
+    hipLaunchKernelGGL(k_attn_fwd<3>, dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float* ln_b,
+                              const float* W1, const float* b1, const float* W2, const float* b2,
+                              float* H_out, float* U, float* stats, int64_t M, int D, int F,
+                              float eps, void* stream) {
+  GHM_CHECK(H_mid && ln_w && ln_b && W1 && b1 && W2 && b2 && H_out && U && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  hipLaunchKernelGGL(k_ln_mlp_fwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2, b2, H_out, U,
+                     reinterpret_cast<float2*>(stats), M, eps);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_readout_fwd(const float* H, const float* W_ro, const float* b_ro,
+                               const float* w_out, const float* b_out, float* emb, int64_t n_seq,
+                               int T, int D, int C, void* stream) {
+  GHM_CHECK(H && W_ro && b_ro && w_out && b_out && emb, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= 128 && C >= 1 && C <= 16 && n_seq >= 1, "shape");
+  hipLaunchKernelGGL(k_readout_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0,
+                     ghm_stream(stream), H, W_ro, b_ro, w_out, b_out, emb, T, C);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_clip_loss(const float* t_emb, const float* i_emb, float* dt_emb, float* di_emb,
+                             float* loss_out, float* hist, const int32_t* step, int B, int K, int C,
+                             void* stream) {
+  GHM_CHECK(t_emb && i_emb && dt_emb && di_emb && loss_out, "null pointer");
+  GHM_CHECK(!hist || step, "hist needs step");
+  GHM_CHECK(B >= 1 && K >= 2 && C >= 1, "shape");
+  hipLaunchKernelGGL(k_clip_loss, dim3(1), dim3(256), 0, ghm_stream(stream), t_emb, i_emb, dt_emb,
+                     di_emb, loss_out, hist, step, B, K, C);
+  return ghm_launch_status();
+}

@@ -1,0 +1,96 @@
+"""ctypes bindings of the in-tree native libraries.
+
+libghm_hip.so  — HIP (gfx950) kernels behind the C ABI in include/ghm_hip.h
+libghm_host.so — host GHM sampler behind include/ghm_sampler.h
+
+There is no fallback: if a library is missing or a call fails, a RuntimeError
+is raised.  Build them with ``make`` (or ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+_LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
+HIP_LIB = os.path.join(_LIBDIR, "libghm_hip.so")
+HOST_LIB = os.path.join(_LIBDIR, "libghm_host.so")
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_u32 = ctypes.c_uint32
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+HIP_SIGNATURES = {
+    "ghm_last_error_string": [],
+    "ghm_device_ok": [],
+    "ghm_token_blocks": [_i64],
+    "ghm_embed_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_ln_qkv_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
+    "ghm_attn_fwd": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_ln_mlp_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_readout_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_clip_loss": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p],
+    "ghm_readout_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_mlp_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
+    "ghm_attn_bwd": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_qkv_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
+    "ghm_wgrad": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
+    "ghm_embed_bwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
+    "ghm_reduce_partials": [_p, _i, _i64, _i, _p, _p, _p],
+    "ghm_clip_prepare": [_p, _i64, _f, _p, _i, _p, _p, _p, _p],
+    "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
+}
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64}
+
+HOST_SIGNATURES = {
+    "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],
+    "ghm_sampler_destroy": [_p],
+    "ghm_sampler_seed": [_p, _u32],
+    "ghm_sampler_set_state": [_p, _p, _i],
+    "ghm_sampler_get_state": [_p, _p, _p],
+    "ghm_sampler_next": [_p, _i, _p, _p, _p, _p],
+    "ghm_sampler_random_sample": [_p, _p, _i64],
+    "ghm_sampler_choice": [_p, _i, _i64, _p],
+}
+_HOST_RESTYPE = {"ghm_sampler_create": ctypes.c_void_p, "ghm_sampler_destroy": None}
+
+_hip = None
+_host = None
+
+
+def _load(path, sigs, restypes):
+    if not os.path.exists(path):
+        raise RuntimeError(f"native library missing: {path} (run `make` in the repo root)")
+    lib = ctypes.CDLL(path)
+    for name, args in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = restypes.get(name, ctypes.c_int)
+    return lib
+
+
+def hip_lib():
+    """The HIP kernel library (loaded once)."""
+    global _hip
+    if _hip is None:
+        _hip = _load(HIP_LIB, HIP_SIGNATURES, _RESTYPE)
+    return _hip
+
+
+def host_lib():
+    """The host sampler library (loaded once)."""
+    global _host
+    if _host is None:
+        _host = _load(HOST_LIB, HOST_SIGNATURES, _HOST_RESTYPE)
+    return _host
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = hip_lib().ghm_last_error_string()
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def call(name, *args):
+    """Call a libghm_hip entry point and raise on a non-zero status."""
+    check(getattr(hip_lib(), name)(*args), name)

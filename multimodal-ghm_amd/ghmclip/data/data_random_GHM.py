@@ -1,0 +1,228 @@
+"""GHM sampler API of the reference (src/ghmclip/data/data_random_GHM.py).
+
+Per-step draws run in the native host sampler (libghm_host.so, C++), which
+reproduces numpy's legacy MT19937 stream bit-exactly.  ``ClipSampler.get_batch``
+takes numpy's global RandomState, advances it exactly as the reference's
+per-node Python loop would, and writes it back — so interleaving with other
+numpy RNG users (seed_everything, get_Bayes) gives the reference's draws.
+
+Transition matrices are generated once at start-up with numpy, in the
+reference's RNG order (GenTransition, :43-89).  get_Bayes runs a vectorised
+BP_CLS (:185-221) on the host once per run.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native
+
+__all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior",
+           "NativeClipSampler"]
+
+
+def _softmax_row(x):
+    """data_random_GHM.py:91-96"""
+    e_x = np.exp(x - np.max(x, axis=1, keepdims=True))
+    return e_x / e_x.sum(axis=1, keepdims=True)
+
+
+def GenTransition(n_layer, n_child, variable_type, p_flip=0.3, flip_scale=1.0,
+                  translation_invariance=True, verbose=False):
+    """data_random_GHM.py:43-89: list over layers of n_child**(layer+1) matrices."""
+    transition = [[] for _ in range(n_layer)]
+    skeleton = []
+    if translation_invariance:
+        for layer in range(n_layer):
+            skel = np.identity(variable_type)[np.random.permutation(variable_type), :]
+            templ = [(1 - p_flip) * skel + p_flip * _softmax_row(
+                np.random.normal(0, flip_scale, [variable_type, variable_type])) for _ in range(n_child)]
+            for _ in range(n_child ** layer):
+                transition[layer].extend(templ)
+            skeleton.append(skel)
+    else:
+        for layer in range(n_layer):
+            for _ in range(n_child ** layer):
+                transition[layer].extend([(1 - p_flip) * np.identity(variable_type)[np.random.permutation(variable_type), :]
+                                          + p_flip * _softmax_row(np.random.normal(0, flip_scale, [variable_type, variable_type]))
+                                          for _ in range(n_child)])
+    return (transition, skeleton) if verbose else transition
+
+
+def _templates(transition, n_child):
+    """Distinct per-(layer, child slot) matrices [n_layer, n_child, V, V]."""
+    out = np.stack([np.stack(layer[:n_child]) for layer in transition])
+    for l, layer in enumerate(transition):  # the native sampler needs translation invariance
+        for k, mat in enumerate(layer):
+            if not np.array_equal(mat, out[l, k % n_child]):
+                raise NotImplementedError("native sampler: translation_invariance=True only")
+    return np.ascontiguousarray(out)
+
+
+class NativeClipSampler:
+    """Thin owner of a libghm_host sampler handle."""
+
+    def __init__(self, t_templ, i_templ, V, K):
+        if t_templ.shape != i_templ.shape:
+            raise NotImplementedError("native sampler: text and image trees must have the same shape")
+        self.n_layer, self.n_child = t_templ.shape[0], t_templ.shape[1]
+        self.V, self.K = V, K
+        self.T = self.n_child ** self.n_layer
+        self._t, self._i = t_templ, i_templ  # keep alive
+        lib = _native.host_lib()
+        self._lib = lib
+        self._h = lib.ghm_sampler_create(t_templ.ctypes.data, i_templ.ctypes.data, self.n_layer,
+                                         self.n_child, V, K)
+        if not self._h:
+            raise RuntimeError("ghm_sampler_create failed")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.ghm_sampler_destroy(self._h)
+            self._h = None
+
+    def seed(self, seed):
+        self._lib.ghm_sampler_seed(self._h, int(seed) & 0xFFFFFFFF)
+
+    def set_state(self, key, pos):
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        assert key.shape == (624,)
+        _native_check(self._lib.ghm_sampler_set_state(self._h, key.ctypes.data, int(pos)))
+
+    def get_state(self):
+        key = np.zeros(624, dtype=np.uint32)
+        pos = ctypes.c_int(0)
+        _native_check(self._lib.ghm_sampler_get_state(self._h, key.ctypes.data, ctypes.byref(pos)))
+        return key, pos.value
+
+    def next_into(self, B, t_leaves, i_leaves, t_root=None, i_root=None):
+        """Fill caller-owned uint8 numpy/pinned buffers [B(K+1), T]."""
+        rc = self._lib.ghm_sampler_next(self._h, B, _addr(t_leaves), _addr(i_leaves),
+                                        _addr(t_root) if t_root is not None else None,
+                                        _addr(i_root) if i_root is not None else None)
+        _native_check(rc)
+
+    # numpy global-state bridge -------------------------------------------------
+    def pull_numpy_state(self):
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise RuntimeError("unexpected numpy RNG")
+        self._np_extra = (st[3], st[4])
+        self.set_state(st[1], st[2])
+
+    def push_numpy_state(self):
+        key, pos = self.get_state()
+        has_gauss, cached = getattr(self, "_np_extra", (0, 0.0))
+        np.random.set_state(("MT19937", key, pos, has_gauss, cached))
+
+
+def _addr(a):
+    if isinstance(a, torch.Tensor):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def _native_check(rc):
+    if rc != 0:
+        raise RuntimeError(f"native sampler call failed ({rc})")
+
+
+def bp_cls_posterior(templ, leaves, p_y):
+    """BP_CLS (data_random_GHM.py:185-221), vectorised over the nodes of a layer
+    (translation invariance makes their matrices equal per child slot).
+    templ [n_layer, n_child, V, V]; leaves [B, T] -> p(root | leaves) [B, V]."""
+    n_layer, n_child, V, _ = templ.shape
+    lv = np.asarray(leaves).T
+    n_par = lv.shape[0] // n_child
+    msg = np.zeros((n_par, V, lv.shape[1]))
+    for c in range(n_child):
+        msg += np.log(templ[-1, c][:, lv[c::n_child]].transpose(1, 0, 2))
+    msg -= msg.max(axis=1, keepdims=True)
+    for layer in range(n_layer - 2, -1, -1):
+        n_par = msg.shape[0] // n_child
+        new = np.zeros((n_par, V, msg.shape[2]))
+        for c in range(n_child):
+            new += np.log(np.einsum("ij,njb->nib", templ[layer, c], np.exp(msg[c::n_child])))
+        new -= new.max(axis=1, keepdims=True)
+        msg = new
+    h0 = msg[0] + np.log(p_y).reshape(-1, 1)
+    h0 -= h0.max(axis=0)
+    return (np.exp(h0) / np.exp(h0).sum(axis=0)).T
+
+
+def PPCLIPLoss(t_pp, i_pp, n_eval, K=4, variable_type=10):
+    """data_random_GHM.py:13-41 (posterior form of the CLIP loss), without the
+    dense kron: the K-1 negative blocks are folded by a reshape-sum."""
+    def fold(x):
+        return x.reshape(K - 1, n_eval).sum(axis=0)
+
+    S_match = np.sum(t_pp[:, :n_eval] * i_pp[:, :n_eval], 0) * variable_type
+    S_indep = fold(np.sum(t_pp[:, 2 * n_eval:] * np.tile(i_pp[:, :n_eval], (1, K - 1)), 0)) * variable_type
+    S = -np.log(S_match / (S_indep + S_match))
+    S_match = np.sum(t_pp[:, n_eval:2 * n_eval] * i_pp[:, n_eval:2 * n_eval], 0) * variable_type
+    S_indep = fold(np.sum(i_pp[:, 2 * n_eval:] * np.tile(t_pp[:, n_eval:2 * n_eval], (1, K - 1)), 0)) * variable_type
+    S = S - np.log(S_match / (S_indep + S_match))
+    return np.mean(S), np.std(S) / np.sqrt(n_eval)
+
+
+class DoubleSampler:
+    """data_random_GHM.py:641-658: seeds numpy with seedtree and builds both
+    modalities' transitions."""
+
+    def __init__(self, n_layers, n_childs, p_ys, p_flips, flip_scale=1, variable_type=10,
+                 translation_invariance=True, seedtree=42):
+        self.n_layers = n_layers
+        self.n_childs = n_childs
+        self.p_ys = p_ys
+        self.p_flips = p_flips
+        self.flip_scale = flip_scale
+        self.variable_type = variable_type
+        self.seedtree = seedtree
+        np.random.seed(seedtree)
+        self.t_transition = GenTransition(n_layers[0], n_childs[0], variable_type, p_flips[0], flip_scale,
+                                          translation_invariance=translation_invariance)
+        self.i_transition = GenTransition(n_layers[1], n_childs[1], variable_type, p_flips[1], flip_scale,
+                                          translation_invariance=translation_invariance)
+
+
+class ClipSampler(DoubleSampler):
+    """data_random_GHM.py:746-817 with the per-step draw in native code."""
+
+    def __init__(self, n_layers, n_childs, p_ys, p_flips, K=4, flip_scale=1, variable_type=10,
+                 translation_invariance=True, seedtree=42):
+        super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
+                         translation_invariance, seedtree)
+        self.K = K
+        self.t_templ = _templates(self.t_transition, n_childs[0])
+        self.i_templ = _templates(self.i_transition, n_childs[1])
+        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, K)
+        self.T = self.native.T
+
+    def draw_numpy(self, batch_size):
+        """One reference-identical draw from numpy's global state (uint8 arrays)."""
+        rows = batch_size * (self.K + 1)
+        tl = np.empty((rows, self.T), np.uint8)
+        il = np.empty((rows, self.T), np.uint8)
+        tr = np.empty(rows, np.uint8)
+        ir = np.empty(rows, np.uint8)
+        self.native.pull_numpy_state()
+        self.native.next_into(batch_size, tl, il, tr, ir)
+        self.native.push_numpy_state()
+        return tl, tr, il, ir
+
+    def get_batch(self, device="cpu", batch_size=128, guide=False):
+        """:753-784.  Returns [text_leaves, text_root, None, None], [image ...]
+        with leaves as int64 [B(K+1), T] on ``device``."""
+        if guide:
+            raise NotImplementedError("guide=True (BP guide targets) is not part of the HIP path yet")
+        tl, tr, il, ir = self.draw_numpy(batch_size)
+        to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
+        return [to(tl), to(tr), None, None], [to(il), to(ir), None, None]
+
+    def get_Bayes(self, n_eval=10000):
+        """:786-817 — exact Bayes CLIP loss from BP posteriors (host, once per run)."""
+        tl, _, il, _ = self.draw_numpy(n_eval)
+        p_y = np.ones(self.variable_type) / self.variable_type
+        tp = bp_cls_posterior(self.t_templ, tl, p_y).T
+        ip = bp_cls_posterior(self.i_templ, il, p_y).T
+        return PPCLIPLoss(tp, ip, n_eval, self.K, self.variable_type)

@@ -1,0 +1,3 @@
+"""Model, loss and optimizer exports (reference: src/ghmclip/models)."""
+from .model import *  # noqa: F401,F403
+from .optimizer import *  # noqa: F401,F403

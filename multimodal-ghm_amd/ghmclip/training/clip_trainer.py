@@ -1,0 +1,179 @@
+"""Fused CLIP training step on the HIP path — the hot loop of
+src/ghmclip/training/train_CLIP.py:139-167 (zero_grad, sample, 2 encoder
+forwards, GuidedClipLoss, backward, clip_grad_norm_, cosine LR, AdamW).
+
+Design:
+* both encoders' parameters live in ONE flat fp32 buffer (each nn.Parameter is a
+  view into it), likewise gradients and the AdamW moments, so the clip and the
+  optimizer are two launches over 1.84 M floats;
+* every per-step scalar (lr_t, lr*wd) comes from a device table indexed by a
+  device step counter, so the whole step is a static launch sequence that is
+  captured once into a HIP graph and replayed;
+* the loss of every step is written on device into ``hist`` (no host sync per
+  step; the host reads it at log intervals);
+* data parallel (optional): each rank owns a shard of the within-block index i
+  (the loss is a mean over i, model.py:906-907), grads are averaged with one
+  RCCL all-reduce of the flat buffer between the backward graph and the
+  optimizer graph.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.optimizer import adam_consts, adam_lr_t
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class ClipTrainer:
+    def __init__(self, tmodel, imodel, K, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
+                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None):
+        """lr_schedule: sequence of python-float learning rates, one per step
+        (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1))."""
+        self.device = torch.device(device)
+        self.tm, self.im = tmodel, imodel
+        self.K, self.B = K, batch_size
+        self.max_norm = float(max_norm)
+        self.pg = process_group
+        self.models = [tmodel, imodel]
+        params = [p for m in self.models for p in m.parameters()]
+        for p in params:
+            require_hip(p)
+        n = sum(p.numel() for p in params)
+        self.n_params = n
+        self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.gflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.views = []  # per model: (param dict, grad dict, m dict, v dict)
+        off = 0
+        with torch.no_grad():
+            for m in self.models:
+                pd, gd, md, vd = {}, {}, {}, {}
+                for name, p in m.named_parameters():
+                    k = p.numel()
+                    self.pflat[off:off + k].copy_(p.data.reshape(-1))
+                    p.data = self.pflat[off:off + k].view(p.shape)
+                    p.grad = self.gflat[off:off + k].view(p.shape)
+                    pd[name], gd[name] = p.data, p.grad
+                    md[name] = self.mflat[off:off + k].view(p.shape)
+                    vd[name] = self.vflat[off:off + k].view(p.shape)
+                    off += k
+                self.views.append((pd, gd, md, vd))
+        T = tmodel.n_token
+        n_seq = batch_size * (K + 1)
+        self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
+                                  n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device)
+                      for m in self.models]
+        self.T, self.n_seq = T, n_seq
+        self.C = tmodel.vocab_size
+        # optimizer constants and the per-step schedule table
+        self.betas, self.wd = betas, weight_decay
+        self.consts = adam_consts(betas, eps)
+        self.t_offset = t_offset
+        sched = np.zeros((len(lr_schedule), 2), dtype=np.float32)
+        for s, lr in enumerate(lr_schedule):
+            sched[s, 0] = adam_lr_t(lr, s + 1 + t_offset, betas)
+            sched[s, 1] = lr * weight_decay
+        self.lr_schedule = list(lr_schedule)
+        self.sched = torch.from_numpy(sched.reshape(-1)).to(self.device)
+        self.n_sched = len(lr_schedule)
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.work = torch.zeros(1024, dtype=torch.float32, device=self.device)
+        self.loss_out = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
+        self.graphs = None
+        self.steps_done = 0
+
+    # -- the launch sequence -----------------------------------------------------
+    def _fwd_bwd(self):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        pt, pi = self.plans
+        (tp, tg, _, _), (ip, ig, _, _) = self.views
+        pt.forward(tp)
+        pi.forward(ip)
+        _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
+                     _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
+        pt.backward(tp, tg)
+        pi.backward(ip, ig)
+
+    def _optim(self):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        b1, omb1, b2, omb2, eps = self.consts
+        _native.call("ghm_clip_prepare", _p(self.gflat), self.n_params, self.max_norm, _p(self.sched),
+                     self.n_sched, _p(self.step_ctr), _p(self.hyper), _p(self.work), s)
+        _native.call("ghm_adamw", _p(self.pflat), _p(self.gflat), _p(self.mflat), _p(self.vflat),
+                     self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
+
+    def _allreduce(self):
+        import torch.distributed as dist
+        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+
+    def set_tokens(self, t_tokens, i_tokens):
+        """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
+        the plans' token buffers, async on the current stream."""
+        self.plans[0].tokens.copy_(t_tokens, non_blocking=True)
+        self.plans[1].tokens.copy_(i_tokens, non_blocking=True)
+
+    def step(self):
+        """One training step on the staged tokens (async; no host sync)."""
+        if self.steps_done >= self.n_sched:
+            raise RuntimeError("schedule exhausted")
+        if self.graphs is not None:
+            self.graphs[0].replay()
+            if self.pg is not None or _dist_on():
+                self._allreduce()
+            self.graphs[1].replay()
+        else:
+            self._fwd_bwd()
+            if self.pg is not None or _dist_on():
+                self._allreduce()
+            self._optim()
+        self.steps_done += 1
+
+    def capture(self):
+        """Capture the step into HIP graphs (call after >= 1 eager step so all
+        lazy initialisation has happened).  Replays reuse the staged tokens."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._fwd_bwd()
+            with torch.cuda.graph(g2, stream=s):
+                self._optim()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graphs = (g1, g2)
+
+    # -- host-side views -----------------------------------------------------------
+    def loss_history(self, upto=None):
+        n = self.steps_done if upto is None else upto
+        return self.hist[:n].double().cpu().numpy()
+
+    def fill_optimizer_state(self, optimizer):
+        """Expose the flat moments as the reference AdamW's per-parameter state
+        ('t', 'm', 'v'), e.g. before optimizer.state_dict() for a checkpoint."""
+        t = self.steps_done + self.t_offset
+        for m, (_, _, md, vd) in zip(self.models, self.views):
+            for name, p in m.named_parameters():
+                optimizer.state[p] = {"t": t, "m": md[name], "v": vd[name]}
+
+    def load_optimizer_state(self, optimizer):
+        with torch.no_grad():
+            for m, (_, _, md, vd) in zip(self.models, self.views):
+                for name, p in m.named_parameters():
+                    st = optimizer.state.get(p)
+                    if st:
+                        md[name].copy_(st["m"])
+                        vd[name].copy_(st["v"])
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1

@@ -1,0 +1,223 @@
+"""HIP path vs the CPU oracle (and the reference's golden fixtures).
+
+Every test here calls the product path through the C ABI (libghm_hip.so) on
+an MI355X and compares against oracle/ on identical inputs.  Tolerances (fp32
+throughout; reductions run in a different order than PyTorch-CPU BLAS):
+  forward activations / embeddings : rtol 2e-5 relative to the tensor's max-abs
+  parameter gradients              : 1e-4 relative to the tensor's max-abs
+  AdamW update                     : bit-exact
+  loss curves                      : |delta| <= 1e-4 (BASELINE.json north_star)
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import ghm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = max(b.abs().max().item(), 1e-12)
+    return (a - b).abs().max().item() / scale
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ghmclip import _native
+    assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
+
+
+def _pair(L=2, T=81, seed=7):
+    """Product encoder on the GPU + oracle encoder on the CPU with equal weights."""
+    from ghmclip import EncoderTransformer
+    torch.manual_seed(seed)
+    prod = EncoderTransformer(T, 10, 128, L)
+    torch.manual_seed(seed)
+    ref = O.OracleEncoder(T, 10, 128, L)
+    for (kp, vp), (kr, vr) in zip(prod.state_dict().items(), ref.state_dict().items()):
+        assert kp == kr and vp.shape == vr.shape
+        assert torch.equal(vp, vr)
+    # perturb LN / biases away from their trivial init so every path is exercised
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for (kp, vp), (_, vr) in zip(prod.named_parameters(), ref.named_parameters()):
+            if "_lns_" in kp or kp.endswith("bias"):
+                d = 0.1 * torch.randn(vp.shape, generator=g)
+                vp.add_(d)
+                vr.add_(d)
+    return prod.to(DEV), ref
+
+
+def _oracle_intermediates(ref, x):
+    """Oracle forward that records the per-layer tensors the HIP plan stores."""
+    B, T = x.shape
+    out = {"H": [], "Hmid": [], "qkv": [], "P": [], "U": []}
+    H = ref.token_embeddings(x) + ref.position_embeddings(torch.arange(T).expand(B, T))
+    for q, k, v, mlp, ln1, ln2 in zip(ref._queries, ref._keys, ref._values, ref._mlps, ref._lns_1, ref._lns_2):
+        out["H"].append(H)
+        H1 = ln1(H)
+        Q, K_, V = q(H1), k(H1), v(H1)
+        out["qkv"].append(torch.cat([Q, K_, V], -1))
+        A = torch.softmax(Q @ K_.transpose(-2, -1) / np.sqrt(128), -1)
+        out["P"].append(A)
+        H = H + A @ V
+        out["Hmid"].append(H)
+        U = mlp[0](ln2(H))
+        out["U"].append(U)
+        H = H + mlp[2](mlp[1](U))
+    out["H"].append(H)
+    return out
+
+
+@pytest.mark.parametrize("T,nseq", [(81, 20), (81, 7), (27, 33), (9, 5)])
+def test_encoder_forward_stages(T, nseq):
+    prod, ref = _pair(L=2, T=T)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(0, 10, (nseq, T), generator=g)
+    emb, gl = prod(x.to(DEV))
+    assert gl == []
+    torch.cuda.synchronize()
+    plan = next(iter(prod._plans.values()))
+    want = _oracle_intermediates(ref, x)
+    M = nseq * T
+    for l in range(2):
+        assert _rel(plan.H[l].view(nseq, T, 128), want["H"][l]) < 2e-5, f"H[{l}]"
+        assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < 2e-5, f"qkv[{l}]"
+        assert _rel(plan.P[l], want["P"][l]) < 2e-5, f"P[{l}]"
+        assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < 2e-5, f"Hmid[{l}]"
+        assert _rel(plan.U[l].view(nseq, T, 512), want["U"][l]) < 2e-5, f"U[{l}]"
+    assert _rel(plan.H[2][:M].view(nseq, T, 128), want["H"][2]) < 2e-5, "H[L]"
+    ref_emb = ref(x)[0]
+    assert _rel(emb, ref_emb) < 2e-5
+
+
+@pytest.mark.parametrize("T,nseq", [(81, 20), (81, 7), (27, 33)])
+def test_encoder_backward(T, nseq):
+    prod, ref = _pair(L=2, T=T)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 10, (nseq, T), generator=g)
+    R = torch.randn(nseq, 10, generator=g)
+    emb, _ = prod(x.to(DEV))
+    (emb * R.to(DEV)).sum().backward()
+    (ref(x)[0] * R).sum().backward()
+    torch.cuda.synchronize()
+    for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
+        assert _rel(pp.grad, pr.grad) < 1e-4, k
+
+
+def test_clip_loss_and_grad():
+    from ghmclip import GuidedClipLoss
+    B, K = 16, 4
+    g = torch.Generator().manual_seed(11)
+    t = torch.randn(B * (K + 1), 10, generator=g) * 0.5
+    i = torch.randn(B * (K + 1), 10, generator=g) * 0.5
+    tr, ir = t.clone().requires_grad_(), i.clone().requires_grad_()
+    lr = O.clip_loss(tr, ir, K, B)
+    lr.backward()
+    tp, ip = t.to(DEV).requires_grad_(), i.to(DEV).requires_grad_()
+    lp, pen = GuidedClipLoss(K, B, 1e-3, False)((tp, []), (ip, []), [None, None])
+    lp.backward()
+    assert pen == 0
+    assert abs(lp.item() - lr.item()) < 1e-5 * max(1.0, abs(lr.item()))
+    assert _rel(tp.grad, tr.grad) < 1e-5
+    assert _rel(ip.grad, ir.grad) < 1e-5
+
+
+def test_adamw_bit_exact():
+    from ghmclip import AdamW
+    g = torch.Generator().manual_seed(2)
+    shapes = [(128, 128), (512,), (10, 128), (1, 81)]
+    ref_p = [torch.randn(s, generator=g) for s in shapes]
+    prod_p = [torch.nn.Parameter(p.clone().to(DEV)) for p in ref_p]
+    ref_p = [torch.nn.Parameter(p) for p in ref_p]
+    ropt = O.OracleAdamW(ref_p)
+    popt = AdamW(prod_p, lr=None)
+    for it in range(3):
+        lr = O.lr_cosine(it, 3e-4, 3e-7, 0, 3000)
+        for rp, pp in zip(ref_p, prod_p):
+            gr = torch.randn(rp.shape, generator=g)
+            rp.grad = gr
+            pp.grad = gr.to(DEV)
+        ropt.set_lr(lr)
+        ropt.step()
+        popt.set_lr(lr)
+        popt.step()
+    torch.cuda.synchronize()
+    for rp, pp in zip(ref_p, prod_p):
+        assert torch.equal(pp.detach().cpu(), rp.detach()), "AdamW not bit-exact"
+
+
+def _trainer(L, B, p, total_iters=3000, graph=False):
+    from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
+    from ghmclip.training.clip_trainer import ClipTrainer
+    p_y = np.ones(10) / 10
+    sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [p, p], K=4, seedtree=42)
+    seed_everything(224)
+    tm = EncoderTransformer(81, 10, 128, L).to(DEV)
+    im = EncoderTransformer(81, 10, 128, L).to(DEV)
+    sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, total_iters) for s in range(total_iters + 1)]
+    tr = ClipTrainer(tm, im, 4, B, sched, device=DEV)
+    return sampler, tr
+
+
+def _run(sampler, tr, B, steps, graph_after=None):
+    for s in range(steps):
+        tl, _, il, _ = sampler.draw_numpy(B)
+        tr.set_tokens(torch.from_numpy(tl), torch.from_numpy(il))
+        tr.step()
+        if graph_after is not None and s + 1 == graph_after:
+            tr.capture()
+    torch.cuda.synchronize()
+    return tr.loss_history()
+
+
+def test_train_steps_vs_reference_fixture():
+    """Two full steps of the d=128, L=2, B=8 config against the reference's own
+    numbers (tests/golden/clip_d128.npz)."""
+    gfx = np.load(os.path.join(GOLDEN, "clip_d128.npz"))
+    sampler, tr = _trainer(2, 8, 0.2)
+    hist = _run(sampler, tr, 8, 2)
+    for it in range(2):
+        assert abs(hist[it] - float(gfx[f"s{it}.loss"])) < 1e-5
+    torch.cuda.synchronize()
+    # post-step parameters vs reference checksums (sum of squares)
+    for pref, m in (("t", tr.tm), ("i", tr.im)):
+        for k, v in m.state_dict().items():
+            ck = gfx[f"s1.post.{pref}.{k}.cks"] if f"s1.post.{pref}.{k}.cks" in gfx else None
+            if ck is not None:
+                got = (v.double().cpu() ** 2).sum().item()
+                assert abs(got - ck[1]) <= 1e-5 * ck[1] + 1e-9, k
+
+
+def test_graph_replay_matches_eager():
+    s1, t1 = _trainer(1, 4, 0.2)
+    h1 = _run(s1, t1, 4, 6)
+    s2, t2 = _trainer(1, 4, 0.2)
+    h2 = _run(s2, t2, 4, 6, graph_after=2)
+    np.testing.assert_array_equal(h1, h2)
+    for a, b in zip(t1.tm.parameters(), t2.tm.parameters()):
+        assert torch.equal(a, b)
+
+
+def test_default_config_curve_vs_reference():
+    """North-star parity: the default CLIP config (p=0.2, L=5, d=128, B=128)
+    loss_history vs the reference PyTorch-CPU run on identical GHM draws."""
+    path = os.path.join(GOLDEN, "clip_default_curve.npz")
+    g = np.load(path)
+    ref = g["loss_history"]
+    n = len(ref)
+    sampler, tr = _trainer(5, 128, 0.2)
+    hist = _run(sampler, tr, 128, n, graph_after=3)
+    dev = np.abs(hist - ref)
+    print(f"default-config curve: {n} steps, max |dloss| = {dev.max():.3e}, final {hist[-1]:.6f} vs {ref[-1]:.6f}")
+    assert dev.max() <= 1e-4

@@ -1,0 +1,131 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every
+declared symbol (no compute calls without a GPU), the native sampler is
+bit-exact against the reference fixtures, and the module API mirrors the
+reference (parameter order, init, schedule)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+
+
+def _declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ghm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_hip_library_exports_every_declared_symbol():
+    import ctypes
+    from ghmclip import _native
+    lib = ctypes.CDLL(_native.HIP_LIB)
+    names = _declared("ghm_hip.h")
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_native.HIP_SIGNATURES), "ctypes table out of sync with ghm_hip.h"
+
+
+def test_host_library_exports_every_declared_symbol():
+    import ctypes
+    from ghmclip import _native
+    lib = ctypes.CDLL(_native.HOST_LIB)
+    names = _declared("ghm_sampler.h")
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_native.HOST_SIGNATURES)
+
+
+@pytest.mark.parametrize("name", ["sampler_p20.npz", "sampler_p40_b16.npz"])
+def test_native_sampler_bit_exact(name):
+    from ghmclip import ClipSampler, seed_everything
+    g = np.load(os.path.join(GOLDEN, name))
+    p, B = float(g["p"]), int(g["B"])
+    p_y = np.ones(10) / 10
+    s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [p, p], K=4, seedtree=42)
+    np.testing.assert_array_equal(s.t_templ, g["t_transition"])
+    np.testing.assert_array_equal(s.i_templ, g["i_transition"])
+    seed_everything(224)
+    for b in range(g["t_leaves"].shape[0]):
+        t, i = s.get_batch("cpu", B)
+        np.testing.assert_array_equal(t[0].numpy(), g["t_leaves"][b])
+        np.testing.assert_array_equal(i[0].numpy(), g["i_leaves"][b])
+        np.testing.assert_array_equal(t[1].numpy(), g["t_root"][b])
+        np.testing.assert_array_equal(i[1].numpy(), g["i_root"][b])
+
+
+def test_native_rng_matches_numpy_stream():
+    from ghmclip import ClipSampler
+    p_y = np.ones(10) / 10
+    s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    import ctypes
+    from ghmclip import _native
+    lib = _native.host_lib()
+    for seed in (0, 1, 224, 2**32 - 1):
+        s.native.seed(seed)
+        out = np.zeros(3000)
+        assert lib.ghm_sampler_random_sample(s.native._h, out.ctypes.data, 3000) == 0
+        rs = np.random.RandomState(seed)
+        np.testing.assert_array_equal(out, rs.random_sample(3000))
+        ch = np.zeros(500, np.int64)
+        assert lib.ghm_sampler_choice(s.native._h, 10, 500, ch.ctypes.data) == 0
+        np.testing.assert_array_equal(ch, rs.choice(10, size=500))
+
+
+def test_numpy_state_round_trip():
+    """get_batch advances numpy's global RNG exactly like the reference would."""
+    from ghmclip import ClipSampler, seed_everything
+    from oracle import ghm_oracle as O
+    p_y = np.ones(10) / 10
+    s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.3, 0.3], K=3, seedtree=42)
+    o = O.ClipSamplerOracle([4, 4], [3, 3], [0.3, 0.3], K=3, seedtree=42)
+    seed_everything(5)
+    s.get_batch("cpu", 7)
+    after_native = np.random.random_sample(5)
+    seed_everything(5)
+    o.get_batch(7)
+    after_oracle = np.random.random_sample(5)
+    np.testing.assert_array_equal(after_native, after_oracle)
+
+
+def test_param_order_and_init_match_oracle():
+    from ghmclip import EncoderTransformer
+    from ghmclip.models.hip_encoder import param_names
+    from oracle import ghm_oracle as O
+    torch.manual_seed(224)
+    a = EncoderTransformer(81, 10, 128, 3)
+    torch.manual_seed(224)
+    b = O.OracleEncoder(81, 10, 128, 3)
+    assert list(a.state_dict()) == list(b.state_dict()) == param_names(3)
+    assert [n for n, _ in a.named_parameters()] == param_names(3)
+    for (ka, va), (_, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert torch.equal(va, vb), ka
+
+
+def test_product_rejects_cpu_tensors():
+    from ghmclip import EncoderTransformer
+    m = EncoderTransformer(81, 10, 128, 1)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.zeros(2, 81, dtype=torch.long))
+
+
+def test_lr_schedule_matches_oracle():
+    from ghmclip import get_lr_cosine_schedule
+    from oracle import ghm_oracle as O
+    for t in (0, 1, 5, 1500, 2999, 3000, 3001):
+        for w in (0, 10):
+            assert get_lr_cosine_schedule(t, 3e-4, 3e-7, w, 3000) == O.lr_cosine(t, 3e-4, 3e-7, w, 3000)
+
+
+def test_bayes_product_matches_published():
+    import json
+    from ghmclip import ClipSampler
+    with open(os.path.join(GOLDEN, "bayes.json")) as f:
+        d = json.load(f)
+    p_y = np.ones(10) / 10
+    s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    bayes, _ = s.get_Bayes(10000)
+    np.testing.assert_allclose(bayes, d["Bayes"][9], rtol=1e-12)
