@@ -93,16 +93,17 @@ int ghm_qkv_bwd(const float* dqkv, const float* H, const float* stats, const flo
  * chunks of tok_per_split tokens: part [n_split][A_cols][B_cols];
  * bias_part [n_split][A_cols] = sum_m A[m][a] (may be NULL).
  * b_mode: 0 plain, 1 GELU(B), 2 LayerNorm(B; stats, ln_w, ln_b).
- * A_cols and B_cols must be multiples of 128; tok_per_split a positive even number.
+ * A_cols and B_cols must be multiples of 128; tok_per_split a positive multiple of 32.
  * Used for dW1/db1, dW2/db2, dWq|k|v (nn.Linear weight/bias grads). */
 int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols,
               int b_mode, const float* stats, const float* ln_w, const float* ln_b, float* part,
               float* bias_part, int64_t M, int tok_per_split, void* stream);
 
-/* Embedding backward partials: part_tok [n_chunk][V][D], part_pos [n_chunk][T][D],
- * n_chunk = ceil(n_seq / seq_per_chunk)  —  backward of model.py:764-765. */
-int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, float* part_pos,
-                  int64_t n_seq, int T, int V, int D, int seq_per_chunk, void* stream);
+/* Token-embedding backward partials part_tok [n_seq][V][D] (reduce over n_seq
+ * with ghm_reduce_partials); the position-embedding gradient is
+ * ghm_reduce_partials(dH0, n_seq, T*D, ...)  —  backward of model.py:764-765. */
+int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, int64_t n_seq, int T,
+                  int V, int D, void* stream);
 
 /* out[i] = sum_{s<n_split} part[s*n + i] in fixed order (deterministic).  The
  * n outputs are written to up to 4 destination segments: segment k takes

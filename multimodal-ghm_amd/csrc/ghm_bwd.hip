@@ -68,27 +68,43 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
     const float* __restrict__ lnw, const float* __restrict__ W1, const float* __restrict__ W2,
     const float* __restrict__ U, float* __restrict__ dU, float* __restrict__ dHmid,
     float* __restrict__ part_ln, int64_t M) {
+  // per 32-unit chunk c: W2[:, 32c:32c+32] as [o][32] and W1[32c:32c+32, :] as [32][in]
+  // in a double-buffered LDS ring; every MFMA A operand is a conflict-free ds_read_b32
+  __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * 32];
+  __shared__ __attribute__((aligned(16))) float s1[2][32 * GHM_D];
   __shared__ float red[2 * 4 * GHM_D];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
-  const bool active = m0 < M;  // inactive waves still join the block reduction
+  const bool active = m0 < M;  // inactive waves still stage tiles and join barriers
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
-  __syncthreads();
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
   f32x16 dx[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) dx[it] = zero16();
-  if (active) {
-    float dy[64];
-    load64(dHout + mc * GHM_D + 64 * h, dy);  // dY[token][o = 64h + s]
+  float dy[64];
+  if (active) load64(dHout + mc * GHM_D + 64 * h, dy);  // dY[token][o = 64h + s]
+  float4 st2[stage_n<GHM_D, 32>()], st1[stage_n<32, GHM_D>()];
+  stage_load<GHM_D, 32>(st2, W2, GHM_F);
+  stage_load<32, GHM_D>(st1, W1, GHM_D);
+  stage_store<GHM_D, 32, 32>(st2, s2[0]);
+  stage_store<32, GHM_D, GHM_D>(st1, s1[0]);
+  __syncthreads();
 #pragma unroll 1
-    for (int c = 0; c < GHM_F / 32; ++c) {
+  for (int c = 0; c < GHM_F / 32; ++c) {
+    const int cur = c & 1;
+    {
+      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
+      stage_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F);
+      stage_load<32, GHM_D>(st1, W1 + static_cast<size_t>(nc) * 32 * GHM_D, GHM_D);
+    }
+    if (active) {
       // dG^T[hid][token] = sum_o W2[o][hid] dY[token][o]
+      const float* w2 = s2[cur] + 64 * h * 32 + j;
       f32x16 g = zero16();
 #pragma unroll
-      for (int s = 0; s < 64; ++s) g = mfma32(W2[static_cast<size_t>(64 * h + s) * GHM_F + 32 * c + j], dy[s], g);
+      for (int s = 0; s < 64; ++s) g = mfma32(w2[s * 32], dy[s], g);
       float du[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -98,16 +114,20 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
         if (valid) dU[m * GHM_F + hid] = v;
       }
       // dX2^T[in][token] += sum_hid W1[hid][in] dU[token][hid]
+      const float* w1 = s1[cur] + j;
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          dx[it] = mfma32(W1[static_cast<size_t>(32 * c + acc_row(r, h)) * GHM_D + 32 * it + j], du[r], dx[it]);
+        for (int r = 0; r < 16; ++r) dx[it] = mfma32(w1[acc_row(r, h) * GHM_D + 32 * it], du[r], dx[it]);
       }
     }
+    stage_store<GHM_D, 32, 32>(st2, s2[cur ^ 1]);
+    stage_store<32, GHM_D, GHM_D>(st1, s1[cur ^ 1]);
+    __syncthreads();
+  }
+  if (active)
     ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], lnw, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
-  }
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
 }
@@ -121,34 +141,47 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd(
     const float* __restrict__ lnw, const float* __restrict__ Wq, const float* __restrict__ Wk,
     const float* __restrict__ Wv, const float* __restrict__ dHmid, float* __restrict__ dH,
     float* __restrict__ part_ln, int64_t M) {
+  // tile b = mat*4 + it: W_mat[:, 32it:32it+32] as [o][32] in a double-buffered LDS ring
+  __shared__ __attribute__((aligned(16))) float sw[2][GHM_D * 32];
   __shared__ float red[2 * 4 * GHM_D];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
   const bool active = m0 < M;
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
-  __syncthreads();
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
   f32x16 dx[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) dx[it] = zero16();
-  if (active) {
+  float4 st[stage_n<GHM_D, 32>()];
+  stage_load<GHM_D, 32>(st, Wq, GHM_D);
+  stage_store<GHM_D, 32, 32>(st, sw[0]);
+  __syncthreads();
 #pragma unroll 1
-    for (int mat = 0; mat < 3; ++mat) {
-      const float* W = mat == 0 ? Wq : (mat == 1 ? Wk : Wv);
-      float g[64];
-      load64(dqkv + mc * (3 * GHM_D) + mat * GHM_D + 64 * h, g);  // dQ[token][o = 64h + s]
+  for (int mat = 0; mat < 3; ++mat) {
+    float g[64];
+    if (active) load64(dqkv + mc * (3 * GHM_D) + mat * GHM_D + 64 * h, g);  // dQ[token][o = 64h + s]
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {
-#pragma unroll
-        for (int s = 0; s < 64; ++s)
-          dx[it] = mfma32(W[static_cast<size_t>(64 * h + s) * GHM_D + 32 * it + j], g[s], dx[it]);
+    for (int it = 0; it < 4; ++it) {
+      const int b = mat * 4 + it, cur = b & 1;
+      {
+        const int nb = b + 1 < 12 ? b + 1 : 11;
+        const float* Wn = nb < 4 ? Wq : (nb < 8 ? Wk : Wv);
+        stage_load<GHM_D, 32>(st, Wn + (nb & 3) * 32, GHM_D);
       }
+      if (active) {
+        const float* w = sw[cur] + 64 * h * 32 + j;
+#pragma unroll
+        for (int s = 0; s < 64; ++s) dx[it] = mfma32(w[s * 32], g[s], dx[it]);
+      }
+      stage_store<GHM_D, 32, 32>(st, sw[cur ^ 1]);
+      __syncthreads();
     }
+  }
+  if (active)
     ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], lnw, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
-  }
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
 }
@@ -264,8 +297,10 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restric
 
 // ---------------------------------------------------------------------------
 // Split-K weight gradient: part[z][a][b] = sum_{m in chunk z} A[m][a] op(B)[m][b]
-// MFMA k-dimension = tokens (k-slot h = token parity).  4 waves as 2x2, each a
-// 64x64 tile; the workgroup covers 128 x 128 of the output.
+// MFMA k-dimension = tokens (k-slot h = token parity).  The workgroup covers a
+// 128 x 128 output tile (4 waves as 2x2, 64x64 each); per 32-token k-step the A
+// and op(B) tiles ([32][128] each, op applied once while staging) pass through a
+// double-buffered LDS ring.
 // ---------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, int lda,
@@ -276,44 +311,82 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, i
                                                   float* __restrict__ part,
                                                   float* __restrict__ bias_part, int64_t M,
                                                   int tok_per_split, int Acols, int Bcols) {
+  constexpr int KT = 32, PT = 128;
+  __shared__ __attribute__((aligned(16))) float sA[2][KT * PT];
+  __shared__ __attribute__((aligned(16))) float sB[2][KT * PT];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int a_base = blockIdx.x * 128 + (wave >> 1) * 64;
-  const int b_base = blockIdx.y * 128 + (wave & 1) * 64;
+  const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+  const int a_blk = blockIdx.x * 128, b_blk = blockIdx.y * 128;
   const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * tok_per_split;
   int64_t m_end = m_begin + tok_per_split;
   if (m_end > M) m_end = M;
-  float g0 = 1.f, g1 = 1.f, e0 = 0.f, e1 = 0.f;
+  const int nsteps = static_cast<int>((m_end - m_begin + KT - 1) / KT);
+  // per-thread column constants of the B transform (columns 4*c4 .. +3 of the tile)
+  float4 gcol = make_float4(1.f, 1.f, 1.f, 1.f), ecol = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int c4 = threadIdx.x & 31;
   if (MODE == 2) {
-    g0 = lnw[b_base + j]; g1 = lnw[b_base + 32 + j];
-    e0 = lnb[b_base + j]; e1 = lnb[b_base + 32 + j];
+    gcol = *reinterpret_cast<const float4*>(lnw + b_blk + 4 * c4);
+    ecol = *reinterpret_cast<const float4*>(lnb + b_blk + 4 * c4);
   }
+  float4 va[4], vb[4];
+  float2 vs[4];
+  auto load = [&](int step) {
+    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = (threadIdx.x >> 5) + 8 * k;
+      const int64_t mt = mb + r;
+      const bool ok = mt < m_end;
+      const int64_t mcl = ok ? mt : m_begin;
+      va[k] = *reinterpret_cast<const float4*>(A + mcl * lda + a_blk + 4 * c4);
+      vb[k] = *reinterpret_cast<const float4*>(Bs + mcl * ldb + b_blk + 4 * c4);
+      if (!ok) va[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (MODE == 2) vs[k] = stats[mcl];
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = (threadIdx.x >> 5) + 8 * k;
+      float4 b = vb[k];
+      if (MODE == 1) {
+        b = make_float4(gelu_f(b.x), gelu_f(b.y), gelu_f(b.z), gelu_f(b.w));
+      } else if (MODE == 2) {
+        const float mu = vs[k].x, rs = vs[k].y;
+        b = make_float4((b.x - mu) * rs * gcol.x + ecol.x, (b.y - mu) * rs * gcol.y + ecol.y,
+                        (b.z - mu) * rs * gcol.z + ecol.z, (b.w - mu) * rs * gcol.w + ecol.w);
+      }
+      *reinterpret_cast<float4*>(sA[buf] + r * PT + 4 * c4) = va[k];
+      *reinterpret_cast<float4*>(sB[buf] + r * PT + 4 * c4) = b;
+    }
+  };
   f32x16 acc00 = zero16(), acc01 = zero16(), acc10 = zero16(), acc11 = zero16();
   float bs0 = 0.f, bs1 = 0.f;
-#pragma unroll 4
-  for (int64_t mm = m_begin; mm < m_end; mm += 2) {
-    const int64_t mt = mm + h;
-    const float msk = mt < m_end ? 1.f : 0.f;
-    const int64_t mc = mt < m_end ? mt : m_end - 1;
-    const float* ar = A + mc * lda + a_base + j;
-    const float* br = Bs + mc * ldb + b_base + j;
-    const float a0 = ar[0] * msk, a1 = ar[32] * msk;
-    float b0 = br[0], b1 = br[32];
-    if (MODE == 1) {
-      b0 = gelu_f(b0);
-      b1 = gelu_f(b1);
-    } else if (MODE == 2) {
-      const float2 st = stats[mc];
-      b0 = (b0 - st.x) * st.y * g0 + e0;
-      b1 = (b1 - st.x) * st.y * g1 + e1;
+  load(0);
+  store(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    load(st + 1 < nsteps ? st + 1 : st);
+    const float* pa = sA[cur] + h * PT + wa + j;
+    const float* pb = sB[cur] + h * PT + wb + j;
+#pragma unroll
+    for (int s = 0; s < KT / 2; ++s) {
+      const float a0 = pa[2 * s * PT], a1 = pa[2 * s * PT + 32];
+      const float b0 = pb[2 * s * PT], b1 = pb[2 * s * PT + 32];
+      acc00 = mfma32(a0, b0, acc00);
+      acc01 = mfma32(a0, b1, acc01);
+      acc10 = mfma32(a1, b0, acc10);
+      acc11 = mfma32(a1, b1, acc11);
+      bs0 += a0;
+      bs1 += a1;
     }
-    acc00 = mfma32(a0, b0, acc00);
-    acc01 = mfma32(a0, b1, acc01);
-    acc10 = mfma32(a1, b0, acc10);
-    acc11 = mfma32(a1, b1, acc11);
-    bs0 += a0;
-    bs1 += a1;
+    store(cur ^ 1);
+    __syncthreads();
   }
   float* pz = part + static_cast<int64_t>(blockIdx.z) * Acols * Bcols;
+  const int a_base = a_blk + wa, b_base = b_blk + wb;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t ra = a_base + acc_row(r, h);
@@ -411,35 +484,28 @@ __global__ __launch_bounds__(128) void k_readout_bwd(
 }
 
 // ---------------------------------------------------------------------------
-// Embedding backward partials; thread = feature d, workgroup = chunk of sequences
+// Token-embedding backward partials: one workgroup per sequence, thread = feature
+// d; part_tok[n][v][d] = sum_{t : tok[n,t] = v} dH0[n,t,d].  (The position
+// embedding gradient is a plain reduction of dH0 over sequences: ghm_reduce.)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0,
                                                    const uint8_t* __restrict__ tok,
-                                                   float* __restrict__ part_tok,
-                                                   float* __restrict__ part_pos, int64_t n_seq,
-                                                   int T, int V, int spc) {
+                                                   float* __restrict__ part_tok, int T, int V) {
   const int d = threadIdx.x;
-  const int64_t n_begin = static_cast<int64_t>(blockIdx.x) * spc;
-  int64_t n_end = n_begin + spc;
-  if (n_end > n_seq) n_end = n_seq;
+  const int64_t n = blockIdx.x;
   float at[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) at[c] = 0.f;
   for (int t = 0; t < T; ++t) {
-    float ap = 0.f;
-    for (int64_t n = n_begin; n < n_end; ++n) {
-      const int64_t m = n * T + t;
-      const float v = dH0[m * GHM_D + d];
-      const int tv = tok[m];
-      ap += v;
+    const int64_t m = n * T + t;
+    const float v = dH0[m * GHM_D + d];
+    const int tv = tok[m];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) at[c] += (tv == c) ? v : 0.f;
-    }
-    part_pos[(static_cast<int64_t>(blockIdx.x) * T + t) * GHM_D + d] = ap;
+    for (int c = 0; c < 16; ++c) at[c] += (tv == c) ? v : 0.f;
   }
 #pragma unroll
   for (int c = 0; c < 16; ++c)
-    if (c < V) part_tok[(static_cast<int64_t>(blockIdx.x) * V + c) * GHM_D + d] = at[c];
+    if (c < V) part_tok[(n * V + c) * GHM_D + d] = at[c];
 }
 
 // ---------------------------------------------------------------------------
@@ -451,15 +517,29 @@ struct SegDst {
   int n_seg;
 };
 
-__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ part, int n_split,
-                                                int64_t n, SegDst seg) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= n) return;
+// 1024 threads = 64 consecutive outputs x 16 split groups; group g sums splits
+// g, g+16, ... in order, then the 16 group sums are added in order: a fixed
+// summation tree independent of timing.
+__global__ __launch_bounds__(1024) void k_reduce(const float* __restrict__ part, int n_split,
+                                                 int64_t n, SegDst seg) {
+  __shared__ float red[16][64];
+  const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + e;
   float s = 0.f;
-  for (int k = 0; k < n_split; ++k) s += part[static_cast<int64_t>(k) * n + i];
-  int g = 0;
-  while (g + 1 < seg.n_seg && i >= seg.off[g + 1]) ++g;
-  seg.dst[g][i - seg.off[g]] = s;
+  if (i < n) {
+#pragma unroll 4
+    for (int k = g; k < n_split; k += 16) s += part[static_cast<int64_t>(k) * n + i];
+  }
+  red[g][e] = s;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][e];
+    int q = 0;
+    while (q + 1 < seg.n_seg && i >= seg.off[q + 1]) ++q;
+    seg.dst[q][i - seg.off[q]] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -521,7 +601,7 @@ extern "C" int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, in
   GHM_CHECK(A && B && part, "null pointer");
   GHM_CHECK(A_cols > 0 && B_cols > 0 && A_cols % 128 == 0 && B_cols % 128 == 0, "A_cols/B_cols % 128");
   GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
-  GHM_CHECK(tok_per_split > 0 && tok_per_split % 2 == 0, "tok_per_split must be positive and even");
+  GHM_CHECK(tok_per_split > 0 && tok_per_split % 32 == 0, "tok_per_split must be a positive multiple of 32");
   GHM_CHECK(b_mode >= 0 && b_mode <= 2, "b_mode");
   GHM_CHECK(b_mode != 2 || (stats && ln_w && ln_b), "layernorm mode needs stats/ln_w/ln_b");
   const int64_t nsplit = (M + tok_per_split - 1) / tok_per_split;
@@ -542,13 +622,11 @@ extern "C" int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, in
 }
 
 extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok,
-                             float* part_pos, int64_t n_seq, int T, int V, int D, int seq_per_chunk,
-                             void* stream) {
-  GHM_CHECK(dH0 && tokens && part_tok && part_pos, "null pointer");
-  GHM_CHECK(D == GHM_D && T >= 1 && V >= 1 && V <= 16 && n_seq >= 1 && seq_per_chunk >= 1, "shape");
-  const int64_t nchunk = (n_seq + seq_per_chunk - 1) / seq_per_chunk;
-  hipLaunchKernelGGL(k_embed_bwd, dim3(static_cast<unsigned>(nchunk)), dim3(128), 0, ghm_stream(stream), dH0,
-                     tokens, part_tok, part_pos, n_seq, T, V, seq_per_chunk);
+                             int64_t n_seq, int T, int V, int D, void* stream) {
+  GHM_CHECK(dH0 && tokens && part_tok, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && V >= 1 && V <= 16 && n_seq >= 1, "shape");
+  hipLaunchKernelGGL(k_embed_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0, ghm_stream(stream), dH0,
+                     tokens, part_tok, T, V);
   return ghm_launch_status();
 }
 
@@ -562,7 +640,7 @@ extern "C" int ghm_reduce_partials(const float* part, int n_split, int64_t n, in
   for (int k = 0; k < 5; ++k) seg.off[k] = k <= n_seg ? off[k] : n;
   GHM_CHECK(seg.off[0] == 0 && seg.off[n_seg] == n, "segment offsets");
   for (int k = 0; k < n_seg; ++k) GHM_CHECK(seg.dst[k] && seg.off[k] <= seg.off[k + 1], "segment");
-  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, ghm_stream(stream),
+  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(1024), 0, ghm_stream(stream),
                      part, n_split, n, seg);
   return ghm_launch_status();
 }

@@ -88,3 +88,33 @@ __device__ __forceinline__ void ln_stats64(const float* x, float eps, float& mea
   v += xhalf(v);
   rstd = 1.f / sqrtf(v * (1.f / 128.f) + eps);
 }
+
+// Register-staged global -> LDS copy of an R x C fp32 tile (row stride ld in
+// global, pitch P floats in LDS) by a 256-thread workgroup, split so the global
+// loads can be issued early (stage_load) and written to LDS after a barrier
+// (stage_store).  v must be a local array of stage_n<R, C>() float4.
+template <int R, int C>
+__device__ __forceinline__ constexpr int stage_n() { return R * (C / 4) / 256; }
+
+template <int R, int C>
+__device__ __forceinline__ void stage_load(float4* v, const float* __restrict__ g, int ld) {
+  constexpr int C4 = C / 4, N = R * C4 / 256;
+  static_assert(R * C4 % 256 == 0, "tile must be a multiple of 256 float4");
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    v[k] = *reinterpret_cast<const float4*>(g + static_cast<size_t>(idx / C4) * ld + 4 * (idx % C4));
+  }
+}
+
+template <int R, int C, int P>
+__device__ __forceinline__ void stage_store(const float4* v, float* lds) {
+  constexpr int C4 = C / 4, N = R * C4 / 256;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    *reinterpret_cast<float4*>(lds + (idx / C4) * P + 4 * (idx % C4)) = v[k];
+  }
+}
+
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }

@@ -41,15 +41,16 @@ __device__ __forceinline__ void ln_row(const float* __restrict__ row, const floa
   }
 }
 
-// Y^T tile (32 out features x 32 tokens) = W[o0:o0+32, :] . X^T, X in row layout.
-// A operand: lane (i=j, h) streams W[o0 + j][64h + s]; B operand: x[s].
-__device__ __forceinline__ f32x16 proj_tile(const float* __restrict__ W, int o0, int j, int h,
-                                            const float* x) {
-  const float4* wr = reinterpret_cast<const float4*>(W + static_cast<size_t>(o0 + j) * GHM_D + 64 * h);
+// Y^T tile (32 out features x 32 tokens) = W[o0:o0+32, :] . X^T, X in row layout,
+// W rows staged in LDS ([32][PW], PW = 132: the float4 reads of 16 lanes with
+// distinct rows hit 16 distinct 4-bank groups).  A operand: lane (i=j, h) reads
+// W[o0 + j][64h + s]; B operand: x[s].
+constexpr int PW = 132;
+__device__ __forceinline__ f32x16 proj_tile_lds(const float* wl, const float* x) {
   f32x16 acc = zero16();
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const float4 w = wr[q];
+    const float4 w = lds4(wl + 4 * q);
     acc = mfma32(w.x, x[4 * q + 0], acc);
     acc = mfma32(w.y, x[4 * q + 1], acc);
     acc = mfma32(w.z, x[4 * q + 2], acc);
@@ -60,33 +61,48 @@ __device__ __forceinline__ f32x16 proj_tile(const float* __restrict__ W, int o0,
 
 // ---------------------------------------------------------------------------
 // LN1 + Q/K/V projections                                       (model.py:772-775)
-// one wave = 32 tokens, 4 waves per workgroup
+// one wave = 32 tokens, 4 waves per workgroup; the 12 weight tiles (3 matrices
+// x 4 blocks of 32 output rows) stream through a double-buffered LDS ring, so
+// each weight byte is read from L2 once per 128 tokens.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd(
     const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const float* __restrict__ Wq, const float* __restrict__ Wk, const float* __restrict__ Wv,
     float* __restrict__ qkv, float2* __restrict__ stats, int64_t M, float eps) {
+  __shared__ __attribute__((aligned(16))) float sw[2][32 * PW];
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
-  if (m0 >= M) return;
+  const bool active = m0 < M;  // inactive waves still stage tiles and join barriers
   const int64_t m = m0 + j;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
-  float x[64], mean, rstd;
-  ln_row(H + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
-  if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  float x[64], mean = 0.f, rstd = 0.f;
+  if (active) {
+    ln_row(H + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
+    if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
+  float4 st[stage_n<32, GHM_D>()];
+  stage_load<32, GHM_D>(st, Wq, GHM_D);
+  stage_store<32, GHM_D, PW>(st, sw[0]);
+  __syncthreads();
 #pragma unroll 1
-  for (int mat = 0; mat < 3; ++mat) {
-    const float* W = mat == 0 ? Wq : (mat == 1 ? Wk : Wv);
-#pragma unroll 1
-    for (int ot = 0; ot < 4; ++ot) {
-      const f32x16 acc = proj_tile(W, ot * 32, j, h, x);
+  for (int b = 0; b < 12; ++b) {  // b = mat * 4 + output block
+    const int cur = b & 1;
+    {  // prefetch tile b+1 (the last iteration re-stages tile 11 into the idle buffer)
+      const int nb = b + 1 < 12 ? b + 1 : 11;
+      const float* Wn = nb < 4 ? Wq : (nb < 8 ? Wk : Wv);
+      stage_load<32, GHM_D>(st, Wn + (nb & 3) * 32 * GHM_D, GHM_D);
+    }
+    if (active) {
+      const f32x16 acc = proj_tile_lds(sw[cur] + j * PW + 64 * h, x);
       if (valid) {
-        float* o = qkv + m * (3 * GHM_D) + mat * GHM_D + ot * 32;
+        float* o = qkv + m * (3 * GHM_D) + (b >> 2) * GHM_D + (b & 3) * 32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[acc_row(r, h)] = acc[r];
       }
     }
+    stage_store<32, GHM_D, PW>(st, sw[cur ^ 1]);
+    __syncthreads();
   }
 }
 
@@ -190,51 +206,75 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
 // LN2 + MLP (128 -> 512 -> GELU -> 128) + residual             (model.py:784-788)
 // The 512-wide hidden activation never leaves registers: each 32-unit chunk of
 // U^T is GELU'd in place and is immediately the B operand of the down product.
-// U (pre-GELU) is stored for the backward pass.
+// Per chunk the workgroup stages W1[32c:32c+32, :] ([32][132]) and
+// W2[:, 32c:32c+32] ([128][36]: float4 reads conflict-free) in a double-buffered
+// LDS ring.  U (pre-GELU) is stored for the backward pass.
 // ---------------------------------------------------------------------------
+constexpr int PW2 = 36;
 __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Hout, float* __restrict__ U,
     float2* __restrict__ stats, int64_t M, float eps) {
+  __shared__ __attribute__((aligned(16))) float s1[2][32 * PW];
+  __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * PW2];
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
-  if (m0 >= M) return;
+  const bool active = m0 < M;
   const int64_t m = m0 + j;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
-  float x[64], mean, rstd;
-  ln_row(Hmid + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
-  if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  float x[64], mean = 0.f, rstd = 0.f;
+  if (active) {
+    ln_row(Hmid + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
+    if (h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
   f32x16 y[4];
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot) y[ot] = zero16();
+  float4 st1[stage_n<32, GHM_D>()], st2[stage_n<GHM_D, 32>()];
+  stage_load<32, GHM_D>(st1, W1, GHM_D);
+  stage_load<GHM_D, 32>(st2, W2, GHM_F);
+  stage_store<32, GHM_D, PW>(st1, s1[0]);
+  stage_store<GHM_D, 32, PW2>(st2, s2[0]);
+  __syncthreads();
 #pragma unroll 1
   for (int c = 0; c < GHM_F / 32; ++c) {
-    const f32x16 u = proj_tile(W1, 32 * c, j, h, x);
-    float g[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int hid = 32 * c + acc_row(r, h);
-      const float uu = u[r] + b1[hid];
-      if (valid) U[m * GHM_F + hid] = uu;
-      g[r] = gelu_f(uu);
+    const int cur = c & 1;
+    {
+      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
+      stage_load<32, GHM_D>(st1, W1 + static_cast<size_t>(nc) * 32 * GHM_D, GHM_D);
+      stage_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F);
     }
+    if (active) {
+      const f32x16 u = proj_tile_lds(s1[cur] + j * PW + 64 * h, x);
+      float g[16];
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      // A operand: W2[32ot + j][hid(r, h)], hid(4q+t, h) = 32c + 8q + 4h + t
-      const float* w2 = W2 + static_cast<size_t>(32 * ot + j) * GHM_F + 32 * c + 4 * h;
+      for (int r = 0; r < 16; ++r) {
+        const int hid = 32 * c + acc_row(r, h);
+        const float uu = u[r] + b1[hid];
+        if (valid) U[m * GHM_F + hid] = uu;
+        g[r] = gelu_f(uu);
+      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 w = *reinterpret_cast<const float4*>(w2 + 8 * q);
-        y[ot] = mfma32(w.x, g[4 * q + 0], y[ot]);
-        y[ot] = mfma32(w.y, g[4 * q + 1], y[ot]);
-        y[ot] = mfma32(w.z, g[4 * q + 2], y[ot]);
-        y[ot] = mfma32(w.w, g[4 * q + 3], y[ot]);
+      for (int ot = 0; ot < 4; ++ot) {
+        // A operand: W2[32ot + j][32c + 8q + 4h + t] = s2[(32ot + j) * PW2 + 8q + 4h + t]
+        const float* w2 = s2[cur] + (32 * ot + j) * PW2 + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 w = lds4(w2 + 8 * q);
+          y[ot] = mfma32(w.x, g[4 * q + 0], y[ot]);
+          y[ot] = mfma32(w.y, g[4 * q + 1], y[ot]);
+          y[ot] = mfma32(w.z, g[4 * q + 2], y[ot]);
+          y[ot] = mfma32(w.w, g[4 * q + 3], y[ot]);
+        }
       }
     }
+    stage_store<32, GHM_D, PW>(st1, s1[cur ^ 1]);
+    stage_store<GHM_D, 32, PW2>(st2, s2[cur ^ 1]);
+    __syncthreads();
   }
-  if (valid) {
+  if (active && valid) {
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot) {
 #pragma unroll

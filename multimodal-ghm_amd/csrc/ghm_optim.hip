@@ -95,7 +95,11 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     const float gg = __fmul_rn(g[i], coef);                                       // grads *= clip_coef
     const float mm = __fadd_rn(__fmul_rn(b1, m[i]), __fmul_rn(omb1, gg));         // beta1*m + (1-beta1)*g
     const float vv = __fadd_rn(__fmul_rn(b2, v[i]), __fmul_rn(omb2, __fmul_rn(gg, gg)));
-    const float upd = __fdiv_rn(__fmul_rn(lr_t, mm), __fadd_rn(__fsqrt_rn(vv), eps));
+    // sqrt and divide evaluated in f64 and rounded once to f32: correctly rounded
+    // f32 results (53 >= 2*24 + 2), unlike the f32 hardware sequences.
+    const float sq = static_cast<float>(sqrt(static_cast<double>(vv)));
+    const float upd = static_cast<float>(static_cast<double>(__fmul_rn(lr_t, mm)) /
+                                         static_cast<double>(__fadd_rn(sq, eps)));
     float pp = __fsub_rn(p[i], upd);                                              // p -= lr_t m/(sqrt v+eps)
     pp = __fsub_rn(pp, __fmul_rn(lr_wd, pp));                                     // p -= lr*wd*p
     p[i] = pp;

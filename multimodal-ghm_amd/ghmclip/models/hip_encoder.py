@@ -96,7 +96,7 @@ class EncoderPlan:
             tiles = (ac // 128) * (bc // 128)
             nsplit = max(1, min(int(round(wgrad_target_blocks / tiles)), (M + 1) // 2))
             tps = -(-M // nsplit)
-            tps += tps & 1
+            tps = -(-tps // 32) * 32  # multiple of the 32-token k-step
             nsplit = -(-M // tps)
             self.wg[key] = (tps, nsplit)
         max_part = max(ns * 128 * 512 if k != "qkv" else ns * 384 * 128 for k, (t, ns) in self.wg.items())
@@ -106,10 +106,7 @@ class EncoderPlan:
         self.part_bro = e(N * num_class)
         self.part_wout = e(N * T)
         self.part_bout = e(N)
-        self.spc = 8
-        self.nchunk = -(-N // self.spc)
-        self.part_tok = e(self.nchunk * vocab * D_MODEL)
-        self.part_pos = e(self.nchunk * T * D_MODEL)
+        self.part_tok = e(N * vocab * D_MODEL)
         self.d_emb = e(N, num_class)
         self._gen = 0
 
@@ -198,7 +195,6 @@ class EncoderPlan:
             self._reduce(self.part_ln, self.nblk, 2 * D_MODEL,
                          [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]], s)
             cur, nxt = nxt, cur  # cur = dH_l
-        c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), _ptr(self.part_pos), N, T, self.V,
-          D_MODEL, self.spc, s)
-        self._reduce(self.part_tok, self.nchunk, self.V * D_MODEL, [g["token_embeddings.weight"]], s)
-        self._reduce(self.part_pos, self.nchunk, T * D_MODEL, [g["position_embeddings.weight"]], s)
+        c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
+        self._reduce(self.part_tok, N, self.V * D_MODEL, [g["token_embeddings.weight"]], s)
+        self._reduce(cur, N, T * D_MODEL, [g["position_embeddings.weight"]], s)
