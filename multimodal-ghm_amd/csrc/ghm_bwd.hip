@@ -88,16 +88,27 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
   float4 st2[stage_n<GHM_D, 32>()], st1[stage_n<32, GHM_D>()];
   stage_load<GHM_D, 32>(st2, W2, GHM_F);
   stage_load<32, GHM_D>(st1, W1, GHM_D);
+  // U of the current chunk, prefetched one chunk ahead (row-scattered loads whose
+  // latency would otherwise sit between the dG and dX MFMA chains)
+  float un[16];
+  const float* urow = U + mc * GHM_F;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) un[r] = urow[acc_row(r, h)];
   stage_store<GHM_D, 32, 32>(st2, s2[0]);
   stage_store<32, GHM_D, GHM_D>(st1, s1[0]);
   __syncthreads();
 #pragma unroll 1
   for (int c = 0; c < GHM_F / 32; ++c) {
     const int cur = c & 1;
+    float uc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) uc[r] = un[r];
     {
       const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
       stage_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F);
       stage_load<32, GHM_D>(st1, W1 + static_cast<size_t>(nc) * 32 * GHM_D, GHM_D);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) un[r] = urow[32 * nc + acc_row(r, h)];
     }
     if (active) {
       // dG^T[hid][token] = sum_o W2[o][hid] dY[token][o]
@@ -109,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int hid = 32 * c + acc_row(r, h);
-        const float v = g[r] * gelu_grad_f(U[mc * GHM_F + hid]);
+        const float v = g[r] * gelu_grad_f(uc[r]);
         du[r] = v;
         if (valid) dU[m * GHM_F + hid] = v;
       }

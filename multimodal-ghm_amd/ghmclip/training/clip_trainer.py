@@ -90,18 +90,30 @@ class ClipTrainer:
         self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
         self.graphs = None
         self.steps_done = 0
+        self.side = torch.cuda.Stream(device=self.device)
 
     # -- the launch sequence -----------------------------------------------------
     def _fwd_bwd(self):
-        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        """Text tower on the current stream, image tower on a side stream (fork /
+        join through stream waits, which graph capture records as edges), so the
+        two towers' launches overlap and fill each other's tails."""
+        main = torch.cuda.current_stream()
+        side = self.side
         pt, pi = self.plans
         (tp, tg, _, _), (ip, ig, _, _) = self.views
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            pi.forward(ip)
         pt.forward(tp)
-        pi.forward(ip)
+        main.wait_stream(side)
+        s = ctypes.c_void_p(main.cuda_stream)
         _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            pi.backward(ip, ig)
         pt.backward(tp, tg)
-        pi.backward(ip, ig)
+        main.wait_stream(side)
 
     def _optim(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -117,7 +129,8 @@ class ClipTrainer:
 
     def set_tokens(self, t_tokens, i_tokens):
         """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
-        the plans' token buffers, async on the current stream."""
+        the plans' token buffers, async on the current stream (the side stream
+        is ordered after it by the fork in _fwd_bwd)."""
         self.plans[0].tokens.copy_(t_tokens, non_blocking=True)
         self.plans[1].tokens.copy_(i_tokens, non_blocking=True)
 

@@ -1,0 +1,100 @@
+"""Host sampler -> HBM pipeline: the native GHM sampler runs in a producer
+thread one or more batches ahead, writing uint8 leaves into a ring of pinned
+host buffers; the training stream copies a slot to the device with an async
+H2D copy and records an event that releases the slot back to the producer.
+(the sampler stays on the host, overlapped with compute.)
+"""
+import threading
+
+import numpy as np
+import torch
+
+
+def shard_rows(block_rows, n_blocks, rank, world):
+    """Row indices rank `rank` of `world` keeps from a CLIP batch laid out as
+    n_blocks blocks of block_rows rows: a contiguous slice of the within-block
+    index i in every block (the loss is a mean over i, model.py:906-907, and
+    each term only touches rows {b*B + i}), so shard losses / gradients average
+    to the full-batch ones."""
+    if block_rows % world:
+        raise ValueError("block rows must divide by the world size")
+    per = block_rows // world
+    return np.concatenate([np.arange(k * block_rows + rank * per, k * block_rows + (rank + 1) * per)
+                           for k in range(n_blocks)])
+
+
+class BatchPipeline:
+    def __init__(self, native_sampler, batch_size, n_slots=3, row_slice=None):
+        """native_sampler: data.NativeClipSampler whose MT state is already set.
+        row_slice: optional (block_rows, rank, world): keep this rank's shard of
+        every block (see shard_rows; data-parallel sharding)."""
+        self.s = native_sampler
+        self.B = batch_size
+        rows = batch_size * (native_sampler.K + 1)
+        T = native_sampler.T
+        self.full_rows, self.T = rows, T
+        self.slice = row_slice
+        self.slots = [(torch.empty(rows, T, dtype=torch.uint8).pin_memory(),
+                       torch.empty(rows, T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+        if row_slice is not None:
+            br, rank, world = row_slice
+            idx = shard_rows(br, rows // br, rank, world)
+            self.idx = torch.from_numpy(idx)
+            self.out = [(torch.empty(len(idx), T, dtype=torch.uint8).pin_memory(),
+                         torch.empty(len(idx), T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+        self.free = [threading.Event() for _ in range(n_slots)]
+        self.ready = [threading.Event() for _ in range(n_slots)]
+        self.copy_done = [None] * n_slots
+        for f in self.free:
+            f.set()
+        self.n = n_slots
+        self.stop = False
+        self.err = None
+        self.k_prod = 0
+        self.k_cons = 0
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _run(self):
+        try:
+            while not self.stop:
+                i = self.k_prod % self.n
+                self.free[i].wait()
+                if self.stop:
+                    return
+                ev = self.copy_done[i]
+                if ev is not None:
+                    ev.synchronize()  # the previous H2D copy out of this slot is done
+                self.free[i].clear()
+                t, im = self.slots[i]
+                self.s.next_into(self.B, t.numpy(), im.numpy())
+                if self.slice is not None:
+                    torch.index_select(t, 0, self.idx, out=self.out[i][0])
+                    torch.index_select(im, 0, self.idx, out=self.out[i][1])
+                self.ready[i].set()
+                self.k_prod += 1
+        except Exception as e:  # surfaced on the consumer side
+            self.err = e
+            for r in self.ready:
+                r.set()
+
+    def next_into(self, trainer):
+        """Wait for the next batch and enqueue its H2D copy on the current stream."""
+        i = self.k_cons % self.n
+        self.ready[i].wait()
+        if self.err is not None:
+            raise self.err
+        self.ready[i].clear()
+        t, im = self.out[i] if self.slice is not None else self.slots[i]
+        trainer.set_tokens(t, im)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.copy_done[i] = ev
+        self.free[i].set()
+        self.k_cons += 1
+
+    def close(self):
+        self.stop = True
+        for f in self.free:
+            f.set()
+        self.th.join(timeout=5)

@@ -1,0 +1,82 @@
+"""Data-parallel sharding on CPU (gloo, world_size 2): the product's row
+sharding (ghmclip.training.pipeline.shard_rows) + an AVG all-reduce of the
+per-rank gradients reproduce the full-batch loss and gradients.
+The per-rank forward/backward is the CPU oracle (no GPU here)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, B, K, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-ghm_amd")]
+    from ghmclip.training.pipeline import shard_rows
+    from oracle import ghm_oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    s = O.ClipSamplerOracle([3, 3], [3, 3], [0.2, 0.2], K=K, seedtree=42)
+    O.seed_everything(224)
+    tm, im = O.build_encoders(27, 1, 16)
+    batch = s.get_batch(B)  # every rank draws the same global batch
+    idx = shard_rows(B, K + 1, rank, world)
+    t = tm(torch.as_tensor(batch[0][idx]))[0]
+    i = im(torch.as_tensor(batch[2][idx]))[0]
+    loss = O.clip_loss(t, i, K, B // world)
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in list(tm.parameters()) + list(im.parameters())])
+    dist.all_reduce(g, op=dist.ReduceOp.SUM)
+    g /= world
+    lt = loss.detach().reshape(1).clone()
+    dist.all_reduce(lt, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        out.put((g.numpy(), float(lt.item() / world)))
+    dist.destroy_process_group()
+
+
+def test_sharded_grads_equal_full_batch():
+    from oracle import ghm_oracle as O
+    B, K, world = 8, 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, B, K, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    g_dp, loss_dp = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s = O.ClipSamplerOracle([3, 3], [3, 3], [0.2, 0.2], K=K, seedtree=42)
+    O.seed_everything(224)
+    tm, im = O.build_encoders(27, 1, 16)
+    batch = s.get_batch(B)
+    loss = O.clip_loss(tm(torch.as_tensor(batch[0]))[0], im(torch.as_tensor(batch[2]))[0], K, B)
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in list(tm.parameters()) + list(im.parameters())]).numpy()
+    assert abs(loss_dp - loss.item()) < 1e-6
+    np.testing.assert_allclose(g_dp, g, rtol=1e-4, atol=1e-7)
+
+
+def test_shard_rows_partition():
+    from ghmclip.training.pipeline import shard_rows
+    B, K = 16, 4
+    parts = [shard_rows(B, K + 1, r, 4) for r in range(4)]
+    allrows = np.sort(np.concatenate(parts))
+    np.testing.assert_array_equal(allrows, np.arange(B * (K + 1)))
+    # each shard keeps the block structure: block b of the shard = rows b*B + [r*B/4, (r+1)*B/4)
+    np.testing.assert_array_equal(parts[1][:4], [4, 5, 6, 7])
+    np.testing.assert_array_equal(parts[1][4:8], [20, 21, 22, 23])

@@ -1,0 +1,111 @@
+"""Per-kernel timing of the default CLIP config with HIP events (one process).
+
+    python tools/kbench.py [--reps 20] [--only name,name]
+
+Builds the default-config trainer, runs two real steps to populate every
+activation, then re-launches each kernel of encoder 0 / layer 0 `reps` times
+on the current stream between two events.  Prints us/launch and the f32 MFMA
+fraction for the GEMM-shaped kernels.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-ghm_amd"))
+sys.path.insert(0, ROOT)
+
+PEAK = 157.3e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    import bench
+    from ghmclip import _native
+    sampler, tr = bench.build(0, 128, 5, 0.2, 3000)
+    ring = bench.make_ring(sampler, 128, 2)
+    for k in range(2):
+        tr.set_tokens(ring[k, 0], ring[k, 1])
+        tr.step()
+    torch.cuda.synchronize()
+    plan, p = tr.plans[0], tr.views[0][0]
+    g = tr.views[0][1]
+    M, N, T = plan.M, plan.N, plan.T
+    s = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(s.cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    c = _native.call
+    l = 0
+    tps_w2, ns_w2 = plan.wg["w2"]
+    tps_w1, ns_w1 = plan.wg["w1"]
+    tps_q, ns_q = plan.wg["qkv"]
+    gf = lambda flop: flop / 1e9  # noqa: E731
+    kernels = {
+        "ln_qkv_fwd": (lambda: c("ghm_ln_qkv_fwd", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
+                                 P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
+                                 P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
+        "attn_fwd": (lambda: c("ghm_attn_fwd", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]), N, T,
+                               128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
+        "ln_mlp_fwd": (lambda: c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+                                 P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
+                                 P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.U[l]), P(plan.st2[l]), M, 128, 512,
+                                 plan.eps, sp), gf(4 * M * 128 * 512)),
+        "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]),
+                              P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.U[l]), P(plan.dU),
+                              P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
+        "wgrad_w2": (lambda: c("ghm_wgrad", P(plan.H[l + 1]), 128, 128, P(plan.U[l]), 512, 512, 1, None, None, None,
+                               P(plan.part_w), P(plan.part_b), M, tps_w2, sp), gf(2 * M * 128 * 512)),
+        "wgrad_w1": (lambda: c("ghm_wgrad", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2, P(plan.st2[l]),
+                               P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w), P(plan.part_b), M,
+                               tps_w1, sp), gf(2 * M * 128 * 512)),
+        "attn_bwd": (lambda: c("ghm_attn_bwd", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dqkv), N, T, 128,
+                               plan.scale_div, sp), gf(8 * N * T * T * 128)),
+        "wgrad_qkv": (lambda: c("ghm_wgrad", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2, P(plan.st1[l]),
+                                P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]), P(plan.part_w), None, M, tps_q, sp),
+                      gf(2 * M * 128 * 384)),
+        "qkv_bwd": (lambda: c("ghm_qkv_bwd", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]),
+                              P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
+                              P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, sp), gf(2 * M * 128 * 384)),
+        "reduce_w2": (lambda: plan._reduce(plan.part_w, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
+        "reduce_ln": (lambda: plan._reduce(plan.part_ln, plan.nblk, 256, [g["_lns_1.0.weight"], g["_lns_1.0.bias"]], sp),
+                      None),
+        "readout_bwd": (lambda: c("ghm_readout_bwd", P(plan.H[5]), P(p["_read_out.weight"]), P(p["_read_out.bias"]),
+                                  P(p["_out.weight"]), P(plan.d_emb), P(plan.dH[0]), P(plan.part_ro), P(plan.part_bro),
+                                  P(plan.part_wout), P(plan.part_bout), N, T, 128, 10, sp), None),
+        "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
+                      None),
+    }
+    only = set(a.only.split(",")) if a.only else None
+    res = {}
+    for name, (fn, gflop) in kernels.items():
+        if only and name not in only:
+            continue
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(a.reps):
+            fn()
+        e1.record(s)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / a.reps * 1e3
+        frac = (gflop * 1e9 / (us * 1e-6)) / PEAK if gflop else None
+        res[name] = {"us": round(us, 2), "gflop": gflop, "mfma_frac": round(frac, 4) if frac else None}
+        print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
+              flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
