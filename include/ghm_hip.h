@@ -39,7 +39,10 @@ int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln_b, const f
                    float eps, void* stream);
 
 /* H_mid = H + softmax(Q K^T / scale_div) V, single head over all D dims (no W_O);
- * P (compact [n_seq][T][T]) saved for backward  —  models/model.py:778-782. */
+ * the probabilities are saved for backward in the kernel's register-native
+ * layout P[n_seq][nkt][nkt][16][64] (nkt = ceil(T/32); element (q, key) with
+ * q = 32w + (l & 31), key = 32kt + 8(r>>2) + 4(l>>5) + (r&3) at [w][kt][r][l];
+ * padded keys are 0)  —  models/model.py:778-782. */
 int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                  int D, float scale_div, void* stream);
 
@@ -79,7 +82,8 @@ int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats, con
                 const float* W1, const float* W2, const float* U, float* dU, float* dH_mid,
                 float* part_ln, int64_t M, int D, int F, void* stream);
 
-/* Attention backward: dqkv[:, q|k|v] from dH_mid, qkv and P  —  backward of model.py:778-782. */
+/* Attention backward: dqkv[:, q|k|v] from dH_mid, qkv and P (native layout
+ * of ghm_attn_fwd)  —  backward of model.py:778-782. */
 int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dqkv,
                  int64_t n_seq, int T, int D, float scale_div, void* stream);
 

@@ -6,24 +6,33 @@
 #include "ghm_launch.h"
 
 // LayerNorm backward for one token held in accumulator layout (feature
-// f = 32*it + acc_row(r,h)); dy = dL/d(LN output).  Writes dH = dres + dx and,
-// reduced over the wave's 32 tokens, the (sum dy*xhat, sum dy) partials of
-// dgamma/dbeta into red_g/red_b[wave][f] (LDS).
+// f = 32*it + 8q + 4h + t for register 4q+t of tile it); dy = dL/d(LN output).
+// Writes dH = dres + dx (float4 per quad) and, reduced over the wave's 32
+// tokens, the (sum dy*xhat, sum dy) partials of dgamma/dbeta into red_g/red_b
+// (LDS, indexed by feature).  gam: LN weight staged in LDS.
 __device__ __forceinline__ void ln_bwd_acc(const f32x16* dy, const float* __restrict__ X,
-                                           float2 st, const float* __restrict__ lnw,
+                                           float2 st, const float* gam,
                                            const float* __restrict__ dres, float* __restrict__ dH,
                                            bool valid, int h, int j, float* red_g, float* red_b) {
   const float mean = st.x, rstd = st.y;
+  float xh[64];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int f = 32 * it + acc_row(r, h);
-      const float xhat = (X[f] - mean) * rstd;
-      const float dyg = dy[it][r] * lnw[f];
-      s1 += dyg;
-      s2 += dyg * xhat;
+    for (int q = 0; q < 4; ++q) {
+      const int f = 32 * it + quad_off(q, h);
+      const float4 xv = *reinterpret_cast<const float4*>(X + f);
+      const float4 gv = lds4(gam + f);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float xhat = (xs[t] - mean) * rstd;
+        xh[16 * it + 4 * q + t] = xhat;
+        const float dyg = dy[it][4 * q + t] * gs[t];
+        s1 += dyg;
+        s2 += dyg * xhat;
+      }
     }
   }
   s1 += xhalf(s1);
@@ -31,14 +40,30 @@ __device__ __forceinline__ void ln_bwd_acc(const f32x16* dy, const float* __rest
   const float m1 = s1 * (1.f / GHM_D), m2 = s2 * (1.f / GHM_D);
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
+    float4 dr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dr[q] = *reinterpret_cast<const float4*>(dres + 32 * it + quad_off(q, h));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 32 * it + quad_off(q, h);
+      const float4 gv = lds4(gam + f);
+      const float gs[4] = {gv.x, gv.y, gv.z, gv.w}, rs[4] = {dr[q].x, dr[q].y, dr[q].z, dr[q].w};
+      float o[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float xhat = xh[16 * it + 4 * q + t];
+        o[t] = rs[t] + rstd * (dy[it][4 * q + t] * gs[t] - m1 - xhat * m2);
+      }
+      if (valid) st4(dH + f, o[0], o[1], o[2], o[3]);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int f = 32 * it + acc_row(r, h);
-      const float xhat = (X[f] - mean) * rstd;
       const float dyv = dy[it][r];
-      const float dx = rstd * (dyv * lnw[f] - m1 - xhat * m2);
-      if (valid) dH[f] = dres[f] + dx;
-      const float sg = sum32(valid ? dyv * xhat : 0.f);
+      const float sg = sum32(valid ? dyv * xh[16 * it + r] : 0.f);
       const float sb = sum32(valid ? dyv : 0.f);
       if (j == 0) {
         red_g[f] = sg;
@@ -73,10 +98,12 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
   __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * 32];
   __shared__ __attribute__((aligned(16))) float s1[2][32 * GHM_D];
   __shared__ float red[2 * 4 * GHM_D];
+  __shared__ __attribute__((aligned(16))) float gam[GHM_D];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
   const bool active = m0 < M;  // inactive waves still stage tiles and join barriers
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
@@ -90,10 +117,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
   stage_load<32, GHM_D>(st1, W1, GHM_D);
   // U of the current chunk, prefetched one chunk ahead (row-scattered loads whose
   // latency would otherwise sit between the dG and dX MFMA chains)
-  float un[16];
+  float4 un[4];
   const float* urow = U + mc * GHM_F;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) un[r] = urow[acc_row(r, h)];
+  for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + quad_off(q, h));
   stage_store<GHM_D, 32, 32>(st2, s2[0]);
   stage_store<32, GHM_D, GHM_D>(st1, s1[0]);
   __syncthreads();
@@ -102,13 +129,15 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
     const int cur = c & 1;
     float uc[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) uc[r] = un[r];
+    for (int q = 0; q < 4; ++q) {
+      uc[4 * q] = un[q].x; uc[4 * q + 1] = un[q].y; uc[4 * q + 2] = un[q].z; uc[4 * q + 3] = un[q].w;
+    }
     {
       const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
       stage_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F);
       stage_load<32, GHM_D>(st1, W1 + static_cast<size_t>(nc) * 32 * GHM_D, GHM_D);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) un[r] = urow[32 * nc + acc_row(r, h)];
+      for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + 32 * nc + quad_off(q, h));
     }
     if (active) {
       // dG^T[hid][token] = sum_o W2[o][hid] dY[token][o]
@@ -118,11 +147,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
       for (int s = 0; s < 64; ++s) g = mfma32(w2[s * 32], dy[s], g);
       float du[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int hid = 32 * c + acc_row(r, h);
-        const float v = g[r] * gelu_grad_f(uc[r]);
-        du[r] = v;
-        if (valid) dU[m * GHM_F + hid] = v;
+      for (int r = 0; r < 16; ++r) du[r] = g[r] * gelu_grad_f(uc[r]);
+      if (valid) {
+        float* drow = dU + m * GHM_F + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st4(drow + quad_off(q, h), du[4 * q], du[4 * q + 1], du[4 * q + 2], du[4 * q + 3]);
       }
       // dX2^T[in][token] += sum_hid W1[hid][in] dU[token][hid]
       const float* w1 = s1[cur] + j;
@@ -137,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
     __syncthreads();
   }
   if (active)
-    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], lnw, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -155,10 +184,12 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd(
   // tile b = mat*4 + it: W_mat[:, 32it:32it+32] as [o][32] in a double-buffered LDS ring
   __shared__ __attribute__((aligned(16))) float sw[2][GHM_D * 32];
   __shared__ float red[2 * 4 * GHM_D];
+  __shared__ __attribute__((aligned(16))) float gam[GHM_D];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
   const bool active = m0 < M;
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
@@ -191,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd(
     }
   }
   if (active)
-    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], lnw, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -237,13 +268,14 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restric
       }
       dp[kt] = acc;
     }
+    // P in the register-native layout written by k_attn_fwd (padded keys are 0)
+    const float* pw = P + ((static_cast<int64_t>(blockIdx.x) * NKT + w) * NKT) * 16 * 64 + lane;
     float delta = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = 32 * kt + acc_row(r, h);
-        const float pv = (qv && key < T) ? P[(base + q) * T + key] : 0.f;
+        const float pv = qv ? pw[(kt * 16 + r) * 64] : 0.f;
         p[kt][r] = pv;
         delta += pv * dp[kt][r];
       }
@@ -276,7 +308,8 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restric
       if (qv) {
         float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[acc_row(r, h)] = acc[r];
+        for (int qd = 0; qd < 4; ++qd)
+          st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
       }
     }
   }
@@ -297,9 +330,9 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restric
       if (kv) {
         float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          o[2 * GHM_D + acc_row(r, h)] = aV[r];
-          o[GHM_D + acc_row(r, h)] = aK[r];
+        for (int qd = 0; qd < 4; ++qd) {
+          st4(o + 2 * GHM_D + quad_off(qd, h), aV[4 * qd], aV[4 * qd + 1], aV[4 * qd + 2], aV[4 * qd + 3]);
+          st4(o + GHM_D + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
         }
       }
     }

@@ -37,6 +37,14 @@ __device__ __forceinline__ constexpr int acc_row(int r, int h) {
   return (r & 3) + 8 * (r >> 2) + 4 * h;
 }
 
+// Accumulator registers 4q..4q+3 of a lane hold 4 consecutive features
+// 8q + 4h + t: epilogue loads/stores use one float4 per quad.
+__device__ __forceinline__ constexpr int quad_off(int q, int h) { return 8 * q + 4 * h; }
+
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+
 // lane-pair (l, l^32) exchange
 __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32, 64); }
 

@@ -98,7 +98,8 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd(
       if (valid) {
         float* o = qkv + m * (3 * GHM_D) + (b >> 2) * GHM_D + (b & 3) * 32;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[acc_row(r, h)] = acc[r];
+        for (int q = 0; q < 4; ++q)
+          st4(o + quad_off(q, h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
       }
     }
     stage_store<32, GHM_D, PW>(st, sw[cur ^ 1]);
@@ -168,13 +169,15 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
   }
   sum += xhalf(sum);
   const float inv = 1.f / sum;
+  // P in the register-native layout [seq][w][kt][r][lane]: fully coalesced,
+  // unconditional; padded keys hold exactly 0 (exp(-inf)).
+  float* pw = P + ((static_cast<int64_t>(blockIdx.x) * NKT + w) * NKT) * 16 * 64 + lane;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       s[kt][r] *= inv;
-      const int key = 32 * kt + acc_row(r, h);
-      if (qv && key < T) P[(base + q) * T + key] = s[kt][r];
+      pw[(kt * 16 + r) * 64] = s[kt][r];
     }
   }
   // O^T[d][q] = sum_key V[key][d] P[q][key]
@@ -193,11 +196,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
     }
     if (qv) {
       const int64_t row = (base + q) * GHM_D + 32 * dt;
+      float4 hv[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int d = acc_row(r, h);
-        Hmid[row + d] = H[row + d] + acc[r];
-      }
+      for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        st4(Hmid + row + quad_off(qd, h), hv[qd].x + acc[4 * qd], hv[qd].y + acc[4 * qd + 1],
+            hv[qd].z + acc[4 * qd + 2], hv[qd].w + acc[4 * qd + 3]);
     }
   }
 }
@@ -218,12 +223,14 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
     float2* __restrict__ stats, int64_t M, float eps) {
   __shared__ __attribute__((aligned(16))) float s1[2][32 * PW];
   __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * PW2];
+  __shared__ __attribute__((aligned(16))) float sb1[GHM_F];
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
   const bool active = m0 < M;
   const int64_t m = m0 + j;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
+  for (int i = threadIdx.x; i < GHM_F; i += 256) sb1[i] = b1[i];
   float x[64], mean = 0.f, rstd = 0.f;
   if (active) {
     ln_row(Hmid + mc * GHM_D, lnw, lnb, h, eps, x, mean, rstd);
@@ -250,12 +257,20 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
       const f32x16 u = proj_tile_lds(s1[cur] + j * PW + 64 * h, x);
       float g[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int hid = 32 * c + acc_row(r, h);
-        const float uu = u[r] + b1[hid];
-        if (valid) U[m * GHM_F + hid] = uu;
-        g[r] = gelu_f(uu);
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = lds4(sb1 + 32 * c + quad_off(q, h));
+        g[4 * q + 0] = u[4 * q + 0] + bb.x;
+        g[4 * q + 1] = u[4 * q + 1] + bb.y;
+        g[4 * q + 2] = u[4 * q + 2] + bb.z;
+        g[4 * q + 3] = u[4 * q + 3] + bb.w;
       }
+      if (valid) {
+        float* urow = U + m * GHM_F + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st4(urow + quad_off(q, h), g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g[r] = gelu_f(g[r]);
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot) {
         // A operand: W2[32ot + j][32c + 8q + 4h + t] = s2[(32ot + j) * PW2 + 8q + 4h + t]
@@ -277,11 +292,17 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
   if (active && valid) {
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot) {
+      float4 hv[4], bv[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = 32 * ot + acc_row(r, h);
-        Hout[m * GHM_D + o] = Hmid[m * GHM_D + o] + (y[ot][r] + b2[o]);
+      for (int q = 0; q < 4; ++q) {
+        hv[q] = *reinterpret_cast<const float4*>(Hmid + m * GHM_D + 32 * ot + quad_off(q, h));
+        bv[q] = *reinterpret_cast<const float4*>(b2 + 32 * ot + quad_off(q, h));
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(Hout + m * GHM_D + 32 * ot + quad_off(q, h), hv[q].x + (y[ot][4 * q] + bv[q].x),
+            hv[q].y + (y[ot][4 * q + 1] + bv[q].y), hv[q].z + (y[ot][4 * q + 2] + bv[q].z),
+            hv[q].w + (y[ot][4 * q + 3] + bv[q].w));
     }
   }
 }

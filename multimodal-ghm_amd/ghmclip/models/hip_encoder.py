@@ -8,7 +8,8 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   H    [L+1, M, 128]   residual stream entering each layer (+ final output)
   Hmid [L,   M, 128]   residual after attention
   qkv  [L,   M, 384]   Q | K | V
-  P    [L, n_seq, T, T] attention probabilities (backward input)
+  P    [L, n_seq, nkt, nkt, 16, 64] attention probabilities in the attention
+                       kernel's register-native layout (nkt = ceil(T/32)), backward input
   U    [L,   M, 512]   MLP pre-activation (backward input)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
@@ -77,7 +78,8 @@ class EncoderPlan:
         self.H = e(L + 1, M, D_MODEL)
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
-        self.P = e(L, N, T, T)
+        self.nkt = -(-T // 32)
+        self.P = e(L, N, self.nkt, self.nkt, 16, 64)
         self.U = e(L, M, D_HIDDEN)
         self.st1 = e(L, M, 2)
         self.st2 = e(L, M, 2)
@@ -109,6 +111,21 @@ class EncoderPlan:
         self.part_tok = e(N * vocab * D_MODEL)
         self.d_emb = e(N, num_class)
         self._gen = 0
+
+    def probs_dense(self, l):
+        """Layer l's attention probabilities as a dense [n_seq, T, T] tensor
+        (test / inspection helper; un-permutes the native layout)."""
+        nkt, T = self.nkt, self.T
+        lane = torch.arange(64, device=self.device)
+        r = torch.arange(16, device=self.device)
+        w = torch.arange(nkt, device=self.device)
+        kt = torch.arange(nkt, device=self.device)
+        q = (32 * w[:, None, None, None] + (lane & 31)[None, None, None, :]).expand(nkt, nkt, 16, 64)
+        key = (32 * kt[None, :, None, None] + 8 * (r >> 2)[None, None, :, None] + 4 * (lane >> 5)[None, None, None, :]
+               + (r & 3)[None, None, :, None]).expand(nkt, nkt, 16, 64)
+        dense = torch.zeros(self.N, 32 * nkt, 32 * nkt, device=self.device)
+        dense[:, q.reshape(-1), key.reshape(-1)] = self.P[l].reshape(self.N, -1)
+        return dense[:, :T, :T]
 
     # ------------------------------------------------------------------
     def forward(self, p, tokens=None):

@@ -93,7 +93,7 @@ def test_encoder_forward_stages(T, nseq):
     for l in range(2):
         assert _rel(plan.H[l].view(nseq, T, 128), want["H"][l]) < 2e-5, f"H[{l}]"
         assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < 2e-5, f"qkv[{l}]"
-        assert _rel(plan.P[l], want["P"][l]) < 2e-5, f"P[{l}]"
+        assert _rel(plan.probs_dense(l), want["P"][l]) < 2e-5, f"P[{l}]"
         assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < 2e-5, f"Hmid[{l}]"
         assert _rel(plan.U[l].view(nseq, T, 512), want["U"][l]) < 2e-5, f"U[{l}]"
     assert _rel(plan.H[2][:M].view(nseq, T, 128), want["H"][2]) < 2e-5, "H[L]"
