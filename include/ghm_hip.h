@@ -39,10 +39,8 @@ int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln_b, const f
                    float eps, void* stream);
 
 /* H_mid = H + softmax(Q K^T / scale_div) V, single head over all D dims (no W_O);
- * the probabilities are saved for backward in the kernel's register-native
- * layout P[n_seq][nkt][nkt][16][64] (nkt = ceil(T/32); element (q, key) with
- * q = 32w + (l & 31), key = 32kt + 8(r>>2) + 4(l>>5) + (r&3) at [w][kt][r][l];
- * padded keys are 0)  —  models/model.py:778-782. */
+ * the probabilities are saved for backward dense and padded, P[n_seq][96][96]
+ * (P[n][q][key]; keys >= T hold 0, rows q >= T are unused)  —  model.py:778-782. */
 int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                  int D, float scale_div, void* stream);
 
@@ -82,9 +80,9 @@ int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats, con
                 const float* W1, const float* W2, const float* U, float* dU, float* dH_mid,
                 float* part_ln, int64_t M, int D, int F, void* stream);
 
-/* Attention backward: dqkv[:, q|k|v] from dH_mid, qkv and P (native layout
- * of ghm_attn_fwd)  —  backward of model.py:778-782. */
-int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dqkv,
+/* Attention backward: dqkv[:, q|k|v] from dH_mid, qkv and P (layout of
+ * ghm_attn_fwd); dS: caller scratch [n_seq][96][96]  —  backward of model.py:778-782. */
+int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                  int64_t n_seq, int T, int D, float scale_div, void* stream);
 
 /* QKV + LN1 backward: dH = dH_mid + dLN1(dqkv W); part_ln as in ghm_mlp_bwd
@@ -114,6 +112,17 @@ int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, int6
  * outputs [off[k], off[k+1]) into dst[k] (off[0] = 0, off[n_seg] = n). */
 int ghm_reduce_partials(const float* part, int n_split, int64_t n, int n_seg,
                         float* const* dst, const int64_t* off, void* stream);
+
+/* Up to 8 independent partial reductions in one launch (same semantics). */
+typedef struct ghm_reduce_job {
+  const float* part;
+  int32_t n_split;
+  int32_t n_seg;
+  int64_t n;
+  float* dst[4];
+  int64_t off[5];
+} ghm_reduce_job;
+int ghm_reduce_batch(const ghm_reduce_job* jobs, int n_jobs, void* stream);
 
 /* ---- clip_grad_norm_ + AdamW (train_CLIP.py:163-167, optimizer.py:41-85) ---- */
 

@@ -229,111 +229,188 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd(
 }
 
 // ---------------------------------------------------------------------------
-// Attention backward, one workgroup per sequence               (model.py:778-782)
-// phase 1 (wave = query block): dP^T = V dO^T, dS = P (dP - rowsum(P dP)) / c,
-//          dQ^T = K^T dS^T; P and dS are staged to LDS as [query][key].
-// phase 2 (wave = key block):   dV^T = dO^T P, dK^T = Q^T dS  (sum over queries).
+// Attention backward                                            (model.py:778-782)
+// kernel 1 (workgroup = sequence, wave = query block): dP^T = V dO^T,
+//   dS = P (dP - rowsum(P dP)) / c, dQ^T = K^T dS^T; dS written dense/padded
+//   like P.  V (feature halves) and K (column blocks) staged in LDS.
+// kernel 2 (workgroup = sequence, wave = key block): dV^T = dO^T P and
+//   dK^T = Q^T dS, summing over queries; P and dS are read with the key on the
+//   lane (coalesced 128-B rows), dO and Q column blocks staged in LDS.
 // ---------------------------------------------------------------------------
+constexpr int AT_P = 96;
+constexpr int AK_PITCH = 68;
+
 template <int NKT>
-__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd(const float* __restrict__ qkv,
-                                                          const float* __restrict__ P,
-                                                          const float* __restrict__ dHmid,
-                                                          float* __restrict__ dqkv, int T,
-                                                          float scale_div) {
+__device__ __forceinline__ void stage_k_half_b(const float* __restrict__ seq, int T, int c, int col0, float* sk) {
+  // K/V[:, 64h + 32c + t] (h = 0,1; t < 32) of the sequence as [key][h][32] (pitch AK_PITCH);
+  // all global loads are issued before the first LDS write
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int key = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    const int kc = key < T ? key : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(kc) * (3 * GHM_D) + col0 + 64 * hh +
+                                            32 * c + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int key = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    *reinterpret_cast<float4*>(sk + key * AK_PITCH + 32 * hh + 4 * q4) = v[k];
+  }
+}
+
+template <int NKT>
+__device__ __forceinline__ void stage_cols32_b(const float* __restrict__ base_row, int ld, int T, int col,
+                                             float* sv) {
+  // X[:, col + t] (t < 32) of the sequence as [row][32]; rows >= T clamp
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 3, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(base_row + static_cast<int64_t>(rc) * ld + col + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    *reinterpret_cast<float4*>(sv + (idx >> 3) * 32 + 4 * (idx & 7)) = v[k];
+  }
+}
+
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q(const float* __restrict__ qkv,
+                                                            const float* __restrict__ P,
+                                                            const float* __restrict__ dHmid,
+                                                            float* __restrict__ dS_out,
+                                                            float* __restrict__ dqkv, int T,
+                                                            float scale_div) {
   constexpr int TP = NKT * 32;
-  __shared__ float sP[TP][TP + 1];
-  __shared__ float sdS[TP][TP + 1];
+  __shared__ __attribute__((aligned(16))) float sbuf[TP * AK_PITCH];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
-  {
-    const int q = 32 * w + j;
-    const bool qv = q < T;
-    const int qc = qv ? q : T - 1;
-    float go[64];
-    load64(dHmid + (base + qc) * GHM_D + 64 * h, go);
-    f32x16 dp[NKT], p[NKT];
+  const float* seq = qkv + base * (3 * GHM_D);
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  float go[64];
+  load64(dHmid + (base + qc) * GHM_D + 64 * h, go);  // dO[q][64h + s]
+  f32x16 dp[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) dp[kt] = zero16();
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    stage_k_half_b<NKT>(seq, T, c, 2 * GHM_D, sbuf);  // V halves
+    __syncthreads();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      const int key = 32 * kt + j;
-      const int kc = key < T ? key : T - 1;
-      const float4* vr = reinterpret_cast<const float4*>(qkv + (base + kc) * (3 * GHM_D) + 2 * GHM_D + 64 * h);
-      f32x16 acc = zero16();
+      const float* vr = sbuf + (32 * kt + j) * AK_PITCH + 32 * h;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float4 v = vr[i];
-        acc = mfma32(v.x, go[4 * i + 0], acc);
-        acc = mfma32(v.y, go[4 * i + 1], acc);
-        acc = mfma32(v.z, go[4 * i + 2], acc);
-        acc = mfma32(v.w, go[4 * i + 3], acc);
-      }
-      dp[kt] = acc;
-    }
-    // P in the register-native layout written by k_attn_fwd (padded keys are 0)
-    const float* pw = P + ((static_cast<int64_t>(blockIdx.x) * NKT + w) * NKT) * 16 * 64 + lane;
-    float delta = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = qv ? pw[(kt * 16 + r) * 64] : 0.f;
-        p[kt][r] = pv;
-        delta += pv * dp[kt][r];
+      for (int i = 0; i < 8; ++i) {
+        const float4 v = lds4(vr + 4 * i);
+        dp[kt] = mfma32(v.x, go[32 * c + 4 * i + 0], dp[kt]);
+        dp[kt] = mfma32(v.y, go[32 * c + 4 * i + 1], dp[kt]);
+        dp[kt] = mfma32(v.z, go[32 * c + 4 * i + 2], dp[kt]);
+        dp[kt] = mfma32(v.w, go[32 * c + 4 * i + 3], dp[kt]);
       }
     }
-    delta += xhalf(delta);
+    __syncthreads();
+  }
+  // P rows (dense, padded keys are 0); queries >= T contribute nothing
+  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
+  float delta = 0.f;
+  f32x16 p[NKT];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
+  for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = 32 * kt + acc_row(r, h);
-        const float ds = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
-        dp[kt][r] = ds;
-        sP[q][key] = p[kt][r];
-        sdS[q][key] = ds;
-      }
+    for (int qd = 0; qd < 4; ++qd) {
+      const float4 pv = *reinterpret_cast<const float4*>(prow + 32 * kt + quad_off(qd, h));
+      p[kt][4 * qd + 0] = qv ? pv.x : 0.f;
+      p[kt][4 * qd + 1] = qv ? pv.y : 0.f;
+      p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
+      p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
     }
-    // dQ^T[d][q] = sum_key K[key][d] dS[q][key]
+#pragma unroll
+    for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+  }
+  delta += xhalf(delta);
+  float* srow = dS_out + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[kt][r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(srow + 32 * kt + quad_off(qd, h), dp[kt][4 * qd], dp[kt][4 * qd + 1], dp[kt][4 * qd + 2],
+          dp[kt][4 * qd + 3]);
+  }
+  // dQ^T[d][q] = sum_key K[key][d] dS[q][key], K column block [key][32] in LDS
 #pragma unroll 1
-    for (int dt = 0; dt < 4; ++dt) {
-      f32x16 acc = zero16();
+  for (int dt = 0; dt < 4; ++dt) {
+    stage_cols32_b<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * dt, sbuf);
+    __syncthreads();
+    f32x16 acc = zero16();
 #pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = 32 * kt + acc_row(r, h);
-          const int kc = key < T ? key : T - 1;
-          acc = mfma32(qkv[(base + kc) * (3 * GHM_D) + GHM_D + 32 * dt + j], dp[kt][r], acc);
-        }
-      }
-      if (qv) {
-        float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
+      for (int r = 0; r < 16; ++r) acc = mfma32(sbuf[(32 * kt + acc_row(r, h)) * 32 + j], dp[kt][r], acc);
+    }
+    __syncthreads();
+    if (qv) {
+      float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
 #pragma unroll
-        for (int qd = 0; qd < 4; ++qd)
-          st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
-      }
+      for (int qd = 0; qd < 4; ++qd)
+        st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
     }
   }
-  __syncthreads();
-  {
-    const int key = 32 * w + j;
-    const bool kv = key < T;
-#pragma unroll 1
-    for (int dt = 0; dt < 4; ++dt) {
-      f32x16 aV = zero16(), aK = zero16();
-#pragma unroll 8
-      for (int s = 0; s < TP / 2; ++s) {
-        const int qq = 2 * s + h;
-        const int qc = qq < T ? qq : T - 1;
-        aV = mfma32(dHmid[(base + qc) * GHM_D + 32 * dt + j], sP[qq][key], aV);
-        aK = mfma32(qkv[(base + qc) * (3 * GHM_D) + 32 * dt + j], sdS[qq][key], aK);
-      }
-      if (kv) {
-        float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
+}
+
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv(const float* __restrict__ qkv,
+                                                             const float* __restrict__ P,
+                                                             const float* __restrict__ dS,
+                                                             const float* __restrict__ dHmid,
+                                                             float* __restrict__ dqkv, int T) {
+  constexpr int TP = NKT * 32;
+  __shared__ __attribute__((aligned(16))) float sdo[TP * 32];
+  __shared__ __attribute__((aligned(16))) float sq[TP * 32];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const int key = 32 * w + j;
+  const bool kv = key < T;
+  // this lane's column of P and dS (queries 2st + h), loaded once and reused by
+  // all four column blocks; rows >= T of P / dS are 0
+  const float* pc = P + static_cast<int64_t>(blockIdx.x) * AT_P * AT_P + key;
+  const float* sc = dS + static_cast<int64_t>(blockIdx.x) * AT_P * AT_P + key;
+  float pb[TP / 2], sb[TP / 2];
 #pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-          st4(o + 2 * GHM_D + quad_off(qd, h), aV[4 * qd], aV[4 * qd + 1], aV[4 * qd + 2], aV[4 * qd + 3]);
-          st4(o + GHM_D + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
-        }
+  for (int st = 0; st < TP / 2; ++st) {
+    pb[st] = pc[(2 * st + h) * AT_P];
+    sb[st] = sc[(2 * st + h) * AT_P];
+  }
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    stage_cols32_b<NKT>(dHmid + base * GHM_D, GHM_D, T, 32 * dt, sdo);
+    stage_cols32_b<NKT>(qkv + base * (3 * GHM_D), 3 * GHM_D, T, 32 * dt, sq);
+    __syncthreads();
+    f32x16 aV = zero16(), aK = zero16();
+#pragma unroll
+    for (int st = 0; st < TP / 2; ++st) {
+      const int qq = 2 * st + h;
+      aV = mfma32(sdo[qq * 32 + j], pb[st], aV);
+      aK = mfma32(sq[qq * 32 + j], sb[st], aK);
+    }
+    __syncthreads();
+    if (kv) {
+      float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        st4(o + 2 * GHM_D + quad_off(qd, h), aV[4 * qd], aV[4 * qd + 1], aV[4 * qd + 2], aV[4 * qd + 3]);
+        st4(o + GHM_D + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
       }
     }
   }
@@ -452,78 +529,102 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, i
 
 // ---------------------------------------------------------------------------
 // Readout backward, one workgroup per sequence                 (model.py:802-805)
+// The sequence's rows of H are staged once into LDS (coalesced float4 loads);
+// every later access (P recompute, dW_ro partial, dH) reads LDS.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void k_readout_bwd(
+constexpr int RO_PITCH = GHM_D + 4;  // 16-B aligned rows; float4 reads of distinct rows conflict-free
+template <int NC>
+__global__ __launch_bounds__(256) void k_readout_bwd(
     const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
     const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
     float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
-    float* __restrict__ part_bout, int T, int C) {
-  __shared__ float sW[16 * GHM_D];
-  __shared__ float sdP[128][17];
-  const int t = threadIdx.x, n = blockIdx.x;
+    float* __restrict__ part_bout, int T) {
+  __shared__ __attribute__((aligned(16))) float sW[NC * GHM_D];
+  __shared__ __attribute__((aligned(16))) float sH[GHM_MAXT * RO_PITCH];
+  __shared__ float sdP[GHM_MAXT][NC + 1];
+  const int tid = threadIdx.x, n = blockIdx.x;
   const int64_t base = static_cast<int64_t>(n) * T;
-  for (int i = t; i < C * GHM_D; i += 128) sW[i] = Wro[i];
-  float de[16];
+  for (int i = tid; i < NC * GHM_D; i += 256) sW[i] = Wro[i];
+  {  // coalesced staging of the sequence's rows: all loads issued before any LDS write
+    constexpr int NIT = GHM_MAXT * (GHM_D / 4) / 256;
+    float4 v[NIT];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) de[c] = c < C ? demb[static_cast<int64_t>(n) * C + c] : 0.f;
+    for (int k = 0; k < NIT; ++k) {
+      const int i = tid + 256 * k;
+      const int tt = i >> 5, c4 = i & 31;
+      const int tc = tt < T ? tt : T - 1;
+      v[k] = *reinterpret_cast<const float4*>(H + (base + tc) * GHM_D + 4 * c4);
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int i = tid + 256 * k;
+      *reinterpret_cast<float4*>(sH + (i >> 5) * RO_PITCH + 4 * (i & 31)) = v[k];
+    }
+  }
+  float de[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
   __syncthreads();
-  if (t < T) {
-    float p[16];
+  if (tid < T) {  // thread = token: recompute P[t][c], dP, dw_out partial
+    const int t = tid;
+    float p[NC];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) p[c] = 0.f;
-    const float4* row = reinterpret_cast<const float4*>(H + (base + t) * GHM_D);
+    for (int c = 0; c < NC; ++c) p[c] = 0.f;
+#pragma unroll 4
     for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
-      const float4 hv = row[d4];
+      const float4 hv = lds4(sH + t * RO_PITCH + 4 * d4);
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (c < C) {
-          const float* wc = sW + c * GHM_D + 4 * d4;
-          p[c] += hv.x * wc[0] + hv.y * wc[1] + hv.z * wc[2] + hv.w * wc[3];
-        }
+      for (int c = 0; c < NC; ++c) {
+        const float4 wv = lds4(sW + c * GHM_D + 4 * d4);
+        p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
       }
     }
     float dw = 0.f;
     const float wt = wout[t];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (c < C) {
-        dw += de[c] * (p[c] + bro[c]);
-        sdP[t][c] = de[c] * wt;
-      }
+    for (int c = 0; c < NC; ++c) {
+      dw += de[c] * (p[c] + bro[c]);
+      sdP[t][c] = de[c] * wt;
     }
     part_wout[base + t] = dw;
   }
   __syncthreads();
-  // thread = feature d: dH[t][d] and the partial dW_ro[c][d]
-  const int d = t;
-  float aw[16];
+  if (tid < GHM_D) {  // thread = feature d: partial dW_ro[c][d]
+    const int d = tid;
+    float aw[NC];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) aw[c] = 0.f;
-  for (int tt = 0; tt < T; ++tt) {
-    const float hv = H[(base + tt) * GHM_D + d];
-    float dh = 0.f;
+    for (int c = 0; c < NC; ++c) aw[c] = 0.f;
+#pragma unroll 3
+    for (int t = 0; t < T; ++t) {
+      const float hv = sH[t * RO_PITCH + d];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (c < C) {
-        const float dpv = sdP[tt][c];
-        aw[c] += dpv * hv;
-        dh += dpv * sW[c * GHM_D + d];
-      }
+      for (int c = 0; c < NC; ++c) aw[c] += sdP[t][c] * hv;
     }
-    dH[(base + tt) * GHM_D + d] = dh;
-  }
 #pragma unroll
-  for (int c = 0; c < 16; ++c)
-    if (c < C) part_wro[(static_cast<int64_t>(n) * C + c) * GHM_D + d] = aw[c];
-  if (t < C) {
-    float s = 0.f;
-    for (int tt = 0; tt < T; ++tt) s += sdP[tt][t];
-    part_bro[static_cast<int64_t>(n) * C + t] = s;
+    for (int c = 0; c < NC; ++c) part_wro[(static_cast<int64_t>(n) * NC + c) * GHM_D + d] = aw[c];
+  } else if (tid < GHM_D + NC) {
+    const int c = tid - GHM_D;
+    float sacc = 0.f;
+    for (int t = 0; t < T; ++t) sacc += sdP[t][c];
+    part_bro[static_cast<int64_t>(n) * NC + c] = sacc;
+    if (c == 0) {
+      float sbo = 0.f;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) sbo += de[k];
+      part_bout[n] = sbo;
+    }
   }
-  if (t == 0) {
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s += de[c];
-    part_bout[n] = s;
+  // dH[t][d] = sum_c dP[t][c] W_ro[c][d]: float4 per thread, coalesced rows
+  for (int i = tid; i < T * (GHM_D / 4); i += 256) {
+    const int t = i >> 5, c4 = i & 31;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float dpv = sdP[t][c];
+      const float4 wv = lds4(sW + c * GHM_D + 4 * c4);
+      o.x += dpv * wv.x; o.y += dpv * wv.y; o.z += dpv * wv.z; o.w += dpv * wv.w;
+    }
+    *reinterpret_cast<float4*>(dH + (base + t) * GHM_D + 4 * c4) = o;
   }
 }
 
@@ -540,6 +641,7 @@ __global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0
   float at[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) at[c] = 0.f;
+#pragma unroll 9
   for (int t = 0; t < T; ++t) {
     const int64_t m = n * T + t;
     const float v = dH0[m * GHM_D + d];
@@ -553,26 +655,32 @@ __global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0
 }
 
 // ---------------------------------------------------------------------------
-// Deterministic partial reduction into up to 4 destination segments
-// ---------------------------------------------------------------------------
-struct SegDst {
-  float* dst[4];
-  int64_t off[5];
-  int n_seg;
-};
-
+// Deterministic partial reductions, several jobs per launch.
 // 1024 threads = 64 consecutive outputs x 16 split groups; group g sums splits
 // g, g+16, ... in order, then the 16 group sums are added in order: a fixed
-// summation tree independent of timing.
-__global__ __launch_bounds__(1024) void k_reduce(const float* __restrict__ part, int n_split,
-                                                 int64_t n, SegDst seg) {
+// summation tree independent of timing.  Block b serves the job whose block
+// range contains b.
+// ---------------------------------------------------------------------------
+#define GHM_MAX_JOBS 8
+struct ReduceJobs {
+  ghm_reduce_job job[GHM_MAX_JOBS];
+  int64_t blk_end[GHM_MAX_JOBS];  // cumulative block counts
+  int n_jobs;
+};
+
+__global__ __launch_bounds__(1024) void k_reduce(ReduceJobs J) {
   __shared__ float red[16][64];
+  int q = 0;
+  while (q + 1 < J.n_jobs && static_cast<int64_t>(blockIdx.x) >= J.blk_end[q]) ++q;
+  const ghm_reduce_job& jb = J.job[q];
+  const int64_t blk = static_cast<int64_t>(blockIdx.x) - (q ? J.blk_end[q - 1] : 0);
   const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + e;
+  const int64_t i = blk * 64 + e;
+  const int64_t n = jb.n;
   float s = 0.f;
   if (i < n) {
 #pragma unroll 4
-    for (int k = g; k < n_split; k += 16) s += part[static_cast<int64_t>(k) * n + i];
+    for (int k = g; k < jb.n_split; k += 16) s += jb.part[static_cast<int64_t>(k) * n + i];
   }
   red[g][e] = s;
   __syncthreads();
@@ -580,9 +688,9 @@ __global__ __launch_bounds__(1024) void k_reduce(const float* __restrict__ part,
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) t += red[k][e];
-    int q = 0;
-    while (q + 1 < seg.n_seg && i >= seg.off[q + 1]) ++q;
-    seg.dst[q][i - seg.off[q]] = t;
+    int d = 0;
+    while (d + 1 < jb.n_seg && i >= jb.off[d + 1]) ++d;
+    jb.dst[d][i - jb.off[d]] = t;
   }
 }
 
@@ -595,9 +703,10 @@ extern "C" int ghm_readout_bwd(const float* H, const float* W_ro, const float* b
                                int T, int D, int C, void* stream) {
   GHM_CHECK(H && W_ro && b_ro && w_out && d_emb && dH && part_wro && part_bro && part_wout && part_bout,
             "null pointer");
-  GHM_CHECK(D == GHM_D && T >= 1 && T <= 128 && C >= 1 && C <= 16 && n_seq >= 1, "shape");
-  hipLaunchKernelGGL(k_readout_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0, ghm_stream(stream),
-                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T, C);
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
+  GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
+  hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
+                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T);
   return ghm_launch_status();
 }
 
@@ -613,18 +722,22 @@ extern "C" int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float*
   return ghm_launch_status();
 }
 
-extern "C" int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dqkv,
+extern "C" int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                             int64_t n_seq, int T, int D, float scale_div, void* stream) {
-  GHM_CHECK(qkv && P && dH_mid && dqkv, "null pointer");
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
   const unsigned g = static_cast<unsigned>(n_seq);
   hipStream_t s = ghm_stream(stream);
-  if (T <= 32)
-    hipLaunchKernelGGL(k_attn_bwd<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
-  else if (T <= 64)
-    hipLaunchKernelGGL(k_attn_bwd<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
-  else
-    hipLaunchKernelGGL(k_attn_bwd<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+  if (T <= 32) {
+    hipLaunchKernelGGL(k_attn_bwd_q<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv<1>, dim3(g), dim3(64), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else if (T <= 64) {
+    hipLaunchKernelGGL(k_attn_bwd_q<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv<2>, dim3(g), dim3(128), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_q<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv<3>, dim3(g), dim3(192), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  }
   return ghm_launch_status();
 }
 
@@ -674,17 +787,44 @@ extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* par
   return ghm_launch_status();
 }
 
+static int validate_job(const ghm_reduce_job& j) {
+  GHM_CHECK(j.part, "null partials");
+  GHM_CHECK(j.n_split >= 1 && j.n >= 1 && j.n_seg >= 1 && j.n_seg <= 4, "job shape");
+  GHM_CHECK(j.off[0] == 0 && j.off[j.n_seg] == j.n, "segment offsets");
+  for (int k = 0; k < j.n_seg; ++k) GHM_CHECK(j.dst[k] && j.off[k] <= j.off[k + 1], "segment");
+  return 0;
+}
+
+extern "C" int ghm_reduce_batch(const ghm_reduce_job* jobs, int n_jobs, void* stream) {
+  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= GHM_MAX_JOBS, "1..8 jobs");
+  ReduceJobs J;
+  J.n_jobs = n_jobs;
+  int64_t blocks = 0;
+  for (int q = 0; q < GHM_MAX_JOBS; ++q) {
+    if (q < n_jobs) {
+      const int rc = validate_job(jobs[q]);
+      if (rc) return rc;
+      J.job[q] = jobs[q];
+      blocks += (jobs[q].n + 63) / 64;
+    } else {
+      J.job[q] = jobs[n_jobs - 1];
+    }
+    J.blk_end[q] = blocks;
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>(blocks)), dim3(1024), 0, ghm_stream(stream), J);
+  return ghm_launch_status();
+}
+
 extern "C" int ghm_reduce_partials(const float* part, int n_split, int64_t n, int n_seg,
                                    float* const* dst, const int64_t* off, void* stream) {
-  GHM_CHECK(part && dst && off, "null pointer");
-  GHM_CHECK(n_split >= 1 && n >= 1 && n_seg >= 1 && n_seg <= 4, "shape");
-  SegDst seg;
-  seg.n_seg = n_seg;
-  for (int k = 0; k < 4; ++k) seg.dst[k] = k < n_seg ? dst[k] : nullptr;
-  for (int k = 0; k < 5; ++k) seg.off[k] = k <= n_seg ? off[k] : n;
-  GHM_CHECK(seg.off[0] == 0 && seg.off[n_seg] == n, "segment offsets");
-  for (int k = 0; k < n_seg; ++k) GHM_CHECK(seg.dst[k] && seg.off[k] <= seg.off[k + 1], "segment");
-  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(1024), 0, ghm_stream(stream),
-                     part, n_split, n, seg);
-  return ghm_launch_status();
+  GHM_CHECK(dst && off, "null pointer");
+  GHM_CHECK(n_seg >= 1 && n_seg <= 4, "segments");
+  ghm_reduce_job j;
+  j.part = part;
+  j.n_split = n_split;
+  j.n = n;
+  j.n_seg = n_seg;
+  for (int k = 0; k < 4; ++k) j.dst[k] = k < n_seg ? dst[k] : nullptr;
+  for (int k = 0; k < 5; ++k) j.off[k] = k <= n_seg ? off[k] : n;
+  return ghm_reduce_batch(&j, 1, stream);
 }

@@ -112,37 +112,95 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd(
 // one workgroup = one sequence; wave w = query block [32w, 32w+32).
 // S^T = K Q^T keeps the query on the lane, so the softmax row lives in the
 // lane's registers (+ one lane-pair exchange) and the probabilities are the B
-// operand of O^T = V^T P^T without leaving registers.
+// operand of O^T = V^T P^T without leaving registers.  K (two halves of the
+// feature dim) and V (four 32-column blocks) pass through one LDS buffer
+// shared by the workgroup's waves.  P is written dense and padded,
+// [seq][96][96] (float4 per quad, unconditional; padded keys and padded
+// query rows hold 0).
 // ---------------------------------------------------------------------------
+constexpr int AT_P = 96;          // padded sequence length of the P / dS layouts
+constexpr int AK_PITCH = 68;      // K half-chunk row: [h][32] + 4 pad -> conflict-free float4
+__device__ __forceinline__ int kchunk_elems(int tp) { return tp * AK_PITCH; }
+
+// stage K[:, 64h + 32c + t] (h = 0,1; t < 32) of the sequence as [key][h][32]
+template <int NKT>
+__device__ __forceinline__ void stage_k_half(const float* __restrict__ seq, int T, int c, int col0, float* sk) {
+  // K/V[:, 64h + 32c + t] (h = 0,1; t < 32) of the sequence as [key][h][32] (pitch AK_PITCH);
+  // all global loads are issued before the first LDS write
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int key = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    const int kc = key < T ? key : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(kc) * (3 * GHM_D) + col0 + 64 * hh +
+                                            32 * c + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int key = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    *reinterpret_cast<float4*>(sk + key * AK_PITCH + 32 * hh + 4 * q4) = v[k];
+  }
+}
+
+template <int NKT>
+__device__ __forceinline__ void stage_cols32(const float* __restrict__ base_row, int ld, int T, int col,
+                                             float* sv) {
+  // X[:, col + t] (t < 32) of the sequence as [row][32]; rows >= T clamp
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 3, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(base_row + static_cast<int64_t>(rc) * ld + col + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    *reinterpret_cast<float4*>(sv + (idx >> 3) * 32 + 4 * (idx & 7)) = v[k];
+  }
+}
+
 template <int NKT>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restrict__ qkv,
                                                           const float* __restrict__ H,
                                                           float* __restrict__ Hmid,
                                                           float* __restrict__ P, int T,
                                                           float scale_div) {
+  constexpr int TP = NKT * 32;
+  __shared__ __attribute__((aligned(16))) float sbuf[TP * AK_PITCH];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * (3 * GHM_D);
   const int q = 32 * w + j;
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
   float xq[64];
-  load64(qkv + (base + qc) * (3 * GHM_D) + 64 * h, xq);
+  load64(seq + static_cast<int64_t>(qc) * (3 * GHM_D) + 64 * h, xq);  // Q[q][64h + s]
   f32x16 s[NKT];
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    const int key = 32 * kt + j;
-    const int kc = key < T ? key : T - 1;
-    const float4* kr = reinterpret_cast<const float4*>(qkv + (base + kc) * (3 * GHM_D) + GHM_D + 64 * h);
-    f32x16 acc = zero16();
+  for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float4 kv = kr[i];
-      acc = mfma32(kv.x, xq[4 * i + 0], acc);
-      acc = mfma32(kv.y, xq[4 * i + 1], acc);
-      acc = mfma32(kv.z, xq[4 * i + 2], acc);
-      acc = mfma32(kv.w, xq[4 * i + 3], acc);
+  for (int c = 0; c < 2; ++c) {
+    stage_k_half<NKT>(seq, T, c, GHM_D, sbuf);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const float* kr = sbuf + (32 * kt + j) * AK_PITCH + 32 * h;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 kv = lds4(kr + 4 * i);
+        s[kt] = mfma32(kv.x, xq[32 * c + 4 * i + 0], s[kt]);
+        s[kt] = mfma32(kv.y, xq[32 * c + 4 * i + 1], s[kt]);
+        s[kt] = mfma32(kv.z, xq[32 * c + 4 * i + 2], s[kt]);
+        s[kt] = mfma32(kv.w, xq[32 * c + 4 * i + 3], s[kt]);
+      }
     }
-    s[kt] = acc;
+    __syncthreads();
   }
   // softmax over keys for query q (= this lane's column)
   float mx = -INFINITY;
@@ -168,32 +226,30 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
     }
   }
   sum += xhalf(sum);
-  const float inv = 1.f / sum;
-  // P in the register-native layout [seq][w][kt][r][lane]: fully coalesced,
-  // unconditional; padded keys hold exactly 0 (exp(-inf)).
-  float* pw = P + ((static_cast<int64_t>(blockIdx.x) * NKT + w) * NKT) * 16 * 64 + lane;
+  // rows of padded queries (q >= T) are stored as 0: the key-block backward
+  // kernel sums P over all 96 rows
+  const float inv = qv ? 1.f / sum : 0.f;
+  float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[kt][r] *= inv;
-      pw[(kt * 16 + r) * 64] = s[kt][r];
-    }
+    for (int r = 0; r < 16; ++r) s[kt][r] *= inv;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(prow + 32 * kt + quad_off(qd, h), s[kt][4 * qd], s[kt][4 * qd + 1], s[kt][4 * qd + 2], s[kt][4 * qd + 3]);
   }
-  // O^T[d][q] = sum_key V[key][d] P[q][key]
+  // O^T[d][q] = sum_key V[key][d] P[q][key], V block [key][32] in LDS
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
+    stage_cols32<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D + 32 * dt, sbuf);
+    __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = 32 * kt + acc_row(r, h);
-        const int kc = key < T ? key : T - 1;
-        const float a = qkv[(base + kc) * (3 * GHM_D) + 2 * GHM_D + 32 * dt + j];
-        acc = mfma32(a, s[kt][r], acc);
-      }
+      for (int r = 0; r < 16; ++r) acc = mfma32(sbuf[(32 * kt + acc_row(r, h)) * 32 + j], s[kt][r], acc);
     }
+    __syncthreads();
     if (qv) {
       const int64_t row = (base + q) * GHM_D + 32 * dt;
       float4 hv[4];
@@ -311,49 +367,67 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
 // Readout: Linear(D->C) over every token, then Linear(T->1) over the token axis
 // (model.py:802-805).  One workgroup per sequence, thread = token.
 // ---------------------------------------------------------------------------
+constexpr int RO_PITCH = GHM_D + 4;  // 16-B aligned rows; float4 reads of distinct rows conflict-free
+template <int NC>
 __global__ __launch_bounds__(128) void k_readout_fwd(const float* __restrict__ H,
                                                      const float* __restrict__ Wro,
                                                      const float* __restrict__ bro,
                                                      const float* __restrict__ wout,
                                                      const float* __restrict__ bout,
-                                                     float* __restrict__ emb, int T, int C) {
-  __shared__ float sW[16 * GHM_D];
-  __shared__ float red[2][16];
+                                                     float* __restrict__ emb, int T) {
+  __shared__ __attribute__((aligned(16))) float sW[NC * GHM_D];
+  __shared__ __attribute__((aligned(16))) float sH[GHM_MAXT * RO_PITCH];
+  __shared__ float red[2][NC];
   const int t = threadIdx.x, n = blockIdx.x;
-  for (int i = t; i < C * GHM_D; i += 128) sW[i] = Wro[i];
+  const int64_t base = static_cast<int64_t>(n) * T;
+  for (int i = t; i < NC * GHM_D; i += 128) sW[i] = Wro[i];
+  {  // coalesced staging of the sequence's rows: all loads issued before any LDS write
+    constexpr int NIT = GHM_MAXT * (GHM_D / 4) / 128;
+    float4 v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int i = t + 128 * k;
+      const int tt = i >> 5, c4 = i & 31;
+      const int tc = tt < T ? tt : T - 1;
+      v[k] = *reinterpret_cast<const float4*>(H + (base + tc) * GHM_D + 4 * c4);
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int i = t + 128 * k;
+      *reinterpret_cast<float4*>(sH + (i >> 5) * RO_PITCH + 4 * (i & 31)) = v[k];
+    }
+  }
   __syncthreads();
-  float p[16];
+  float p[NC];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) p[c] = 0.f;
+  for (int c = 0; c < NC; ++c) p[c] = 0.f;
   if (t < T) {
-    const float4* row = reinterpret_cast<const float4*>(H + (static_cast<int64_t>(n) * T + t) * GHM_D);
+#pragma unroll 4
     for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
-      const float4 hv = row[d4];
+      const float4 hv = lds4(sH + t * RO_PITCH + 4 * d4);
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (c < C) {
-          const float* wc = sW + c * GHM_D + 4 * d4;
-          p[c] += hv.x * wc[0] + hv.y * wc[1] + hv.z * wc[2] + hv.w * wc[3];
-        }
+      for (int c = 0; c < NC; ++c) {
+        const float4 wv = lds4(sW + c * GHM_D + 4 * d4);
+        p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
       }
     }
     const float wt = wout[t];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) p[c] = c < C ? (p[c] + bro[c]) * wt : 0.f;
+    for (int c = 0; c < NC; ++c) p[c] = (p[c] + bro[c]) * wt;
   }
   const int lane = t & 63, wv = t >> 6;
   // deterministic wave reduction: 32-lane butterfly, then the lane-pair exchange
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const float v = sum32(p[c]);
     p[c] = v + __shfl_xor(v, 32, 64);
   }
   if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) red[wv][c] = p[c];
+    for (int c = 0; c < NC; ++c) red[wv][c] = p[c];
   }
   __syncthreads();
-  if (t < C) emb[static_cast<int64_t>(n) * C + t] = red[0][t] + red[1][t] + bout[0];
+  if (t < NC) emb[static_cast<int64_t>(n) * NC + t] = red[0][t] + red[1][t] + bout[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -491,9 +565,10 @@ extern "C" int ghm_readout_fwd(const float* H, const float* W_ro, const float* b
                                const float* w_out, const float* b_out, float* emb, int64_t n_seq,
                                int T, int D, int C, void* stream) {
   GHM_CHECK(H && W_ro && b_ro && w_out && b_out && emb, "null pointer");
-  GHM_CHECK(D == GHM_D && T >= 1 && T <= 128 && C >= 1 && C <= 16 && n_seq >= 1, "shape");
-  hipLaunchKernelGGL(k_readout_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0,
-                     ghm_stream(stream), H, W_ro, b_ro, w_out, b_out, emb, T, C);
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
+  GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
+  hipLaunchKernelGGL(k_readout_fwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0,
+                     ghm_stream(stream), H, W_ro, b_ro, w_out, b_out, emb, T);
   return ghm_launch_status();
 }
 

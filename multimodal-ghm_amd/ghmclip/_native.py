@@ -14,6 +14,12 @@ HIP_LIB = os.path.join(_LIBDIR, "libghm_hip.so")
 HOST_LIB = os.path.join(_LIBDIR, "libghm_host.so")
 
 _p = ctypes.c_void_p
+
+
+class ReduceJob(ctypes.Structure):
+    """ghm_reduce_job (include/ghm_hip.h)."""
+    _fields_ = [("part", ctypes.c_void_p), ("n_split", ctypes.c_int32), ("n_seg", ctypes.c_int32),
+                ("n", ctypes.c_int64), ("dst", ctypes.c_void_p * 4), ("off", ctypes.c_int64 * 5)]
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _f = ctypes.c_float
@@ -32,11 +38,12 @@ HIP_SIGNATURES = {
     "ghm_clip_loss": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p],
     "ghm_readout_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_mlp_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
-    "ghm_attn_bwd": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_attn_bwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_qkv_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_wgrad": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_embed_bwd": [_p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_reduce_partials": [_p, _i, _i64, _i, _p, _p, _p],
+    "ghm_reduce_batch": [_p, _i, _p],
     "ghm_clip_prepare": [_p, _i64, _f, _p, _i, _p, _p, _p, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }

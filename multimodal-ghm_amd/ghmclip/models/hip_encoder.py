@@ -8,8 +8,7 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   H    [L+1, M, 128]   residual stream entering each layer (+ final output)
   Hmid [L,   M, 128]   residual after attention
   qkv  [L,   M, 384]   Q | K | V
-  P    [L, n_seq, nkt, nkt, 16, 64] attention probabilities in the attention
-                       kernel's register-native layout (nkt = ceil(T/32)), backward input
+  P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input)
   U    [L,   M, 512]   MLP pre-activation (backward input)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
@@ -59,13 +58,13 @@ def require_hip(t):
 
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", wgrad_target_blocks=1024):
+                 normalize_attn=True, device="cuda", wgrad_target_blocks=512):
         if n_embd != D_MODEL:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
         if n_token > 96:
             raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
-        if num_class > 16 or vocab > 16:
-            raise ValueError("num_class / vocabulary must be <= 16")
+        if num_class != 10 or vocab > 16:
+            raise ValueError("the HIP readout is built for num_class == 10 and a vocabulary <= 16")
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -78,8 +77,7 @@ class EncoderPlan:
         self.H = e(L + 1, M, D_MODEL)
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
-        self.nkt = -(-T // 32)
-        self.P = e(L, N, self.nkt, self.nkt, 16, 64)
+        self.P = torch.zeros(L, N, 96, 96, dtype=f32, device=dev)
         self.U = e(L, M, D_HIDDEN)
         self.st1 = e(L, M, 2)
         self.st2 = e(L, M, 2)
@@ -89,8 +87,10 @@ class EncoderPlan:
         self.dH = e(2, M, D_MODEL)
         self.dqkv = e(M, 3 * D_MODEL)
         self.dU = e(M, D_HIDDEN)
+        self.dS = torch.zeros(N, 96, 96, dtype=f32, device=dev)
         self.nblk = int(_native.hip_lib().ghm_token_blocks(M))
         self.part_ln = e(self.nblk, 2, D_MODEL)
+        self.part_ln2 = e(self.nblk, 2, D_MODEL)
         # split-K plans (A_cols x B_cols output tiles of 128x128)
         self.wg = {}
         for key, (ac, bc) in {"w2": (D_MODEL, D_HIDDEN), "w1": (D_HIDDEN, D_MODEL),
@@ -101,9 +101,14 @@ class EncoderPlan:
             tps = -(-tps // 32) * 32  # multiple of the 32-token k-step
             nsplit = -(-M // tps)
             self.wg[key] = (tps, nsplit)
-        max_part = max(ns * 128 * 512 if k != "qkv" else ns * 384 * 128 for k, (t, ns) in self.wg.items())
-        self.part_w = e(max_part)
-        self.part_b = e(max(ns * 512 for (_, ns) in self.wg.values()))
+        # one partial buffer per pending reduction job of a layer (flushed once per layer)
+        self.part_w2 = e(self.wg["w2"][1] * D_MODEL * D_HIDDEN)
+        self.part_w1 = e(self.wg["w1"][1] * D_HIDDEN * D_MODEL)
+        self.part_wq = e(self.wg["qkv"][1] * 3 * D_MODEL * D_MODEL)
+        self.part_b2 = e(self.wg["w2"][1] * D_MODEL)
+        self.part_b1 = e(self.wg["w1"][1] * D_HIDDEN)
+        self.part_w = self.part_w2  # (kbench / legacy name)
+        self.part_b = self.part_b1
         self.part_ro = e(N * num_class * D_MODEL)
         self.part_bro = e(N * num_class)
         self.part_wout = e(N * T)
@@ -113,19 +118,8 @@ class EncoderPlan:
         self._gen = 0
 
     def probs_dense(self, l):
-        """Layer l's attention probabilities as a dense [n_seq, T, T] tensor
-        (test / inspection helper; un-permutes the native layout)."""
-        nkt, T = self.nkt, self.T
-        lane = torch.arange(64, device=self.device)
-        r = torch.arange(16, device=self.device)
-        w = torch.arange(nkt, device=self.device)
-        kt = torch.arange(nkt, device=self.device)
-        q = (32 * w[:, None, None, None] + (lane & 31)[None, None, None, :]).expand(nkt, nkt, 16, 64)
-        key = (32 * kt[None, :, None, None] + 8 * (r >> 2)[None, None, :, None] + 4 * (lane >> 5)[None, None, None, :]
-               + (r & 3)[None, None, :, None]).expand(nkt, nkt, 16, 64)
-        dense = torch.zeros(self.N, 32 * nkt, 32 * nkt, device=self.device)
-        dense[:, q.reshape(-1), key.reshape(-1)] = self.P[l].reshape(self.N, -1)
-        return dense[:, :T, :T]
+        """Layer l's attention probabilities [n_seq, T, T] (inspection helper)."""
+        return self.P[l, :, :self.T, :self.T]
 
     # ------------------------------------------------------------------
     def forward(self, p, tokens=None):
@@ -153,65 +147,81 @@ class EncoderPlan:
         return self.emb
 
     # ------------------------------------------------------------------
-    def _reduce(self, part, n_split, n, dsts, s):
-        n_seg = len(dsts)
-        arr = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in dsts], *([0] * (4 - n_seg)))
+    @staticmethod
+    def _job(part, n_split, dsts):
+        j = _native.ReduceJob()
+        j.part = part.data_ptr()
+        j.n_split = n_split
+        j.n_seg = len(dsts)
         offs = [0]
         for t in dsts:
             offs.append(offs[-1] + t.numel())
-        assert offs[-1] == n, (offs, n)
-        off = (ctypes.c_int64 * 5)(*offs, *([n] * (5 - len(offs))))
-        _native.call("ghm_reduce_partials", _ptr(part), n_split, n, n_seg, arr, off, s)
+        j.n = offs[-1]
+        for k, t in enumerate(dsts):
+            j.dst[k] = t.data_ptr()
+        for k in range(5):
+            j.off[k] = offs[min(k, len(dsts))]
+        return j
+
+    def _flush(self, jobs, s):
+        for a in range(0, len(jobs), 8):
+            chunk = jobs[a:a + 8]
+            arr = (_native.ReduceJob * len(chunk))(*chunk)
+            _native.call("ghm_reduce_batch", arr, len(chunk), s)
+        jobs.clear()
+
+    def _reduce(self, part, n_split, n, dsts, s):
+        j = self._job(part, n_split, dsts)
+        assert j.n == n
+        self._flush([j], s)
 
     def backward(self, p, g, d_emb=None, tokens=None):
         """Accumulate nothing: writes d(loss)/d(param) into g[name] (fp32 device
-        tensors, same keys as p).  d_emb: [n_seq, C] (defaults to self.d_emb)."""
+        tensors, same keys as p).  d_emb: [n_seq, C] (defaults to self.d_emb).
+        Parameter-gradient partials are reduced by one batched launch per layer."""
         tok = self.tokens if tokens is None else tokens
         de = self.d_emb if d_emb is None else d_emb
         s = _stream()
         c = _native.call
+        J = self._job
         M, T, N, L, C = self.M, self.T, self.N, self.L, self.C
         cur, nxt = self.dH[0], self.dH[1]
+        jobs = []
         c("ghm_readout_bwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(p["_out.weight"]), _ptr(de), _ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro),
           _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, s)
-        self._reduce(self.part_ro, N, C * D_MODEL, [g["_read_out.weight"]], s)
-        self._reduce(self.part_bro, N, C, [g["_read_out.bias"]], s)
-        self._reduce(self.part_wout, N, T, [g["_out.weight"]], s)
-        self._reduce(self.part_bout, N, 1, [g["_out.bias"]], s)
+        jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
+                 J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
         for l in reversed(range(L)):
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
             c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.U[l]), _ptr(self.dU),
-              _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, D_HIDDEN, s)
-            self._reduce(self.part_ln, self.nblk, 2 * D_MODEL,
-                         [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]], s)
+              _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
+            jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] GELU(U)[m][hid]; db2 = sum dY
             c("ghm_wgrad", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.U[l]), D_HIDDEN, D_HIDDEN, 1,
-              None, None, None, _ptr(self.part_w), _ptr(self.part_b), M, tps, s)
-            self._reduce(self.part_w, ns, D_MODEL * D_HIDDEN, [g[f"_mlps.{l}.2.weight"]], s)
-            self._reduce(self.part_b, ns, D_MODEL, [g[f"_mlps.{l}.2.bias"]], s)
+              None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)
+            jobs += [J(self.part_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(self.part_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU
             c("ghm_wgrad", _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
-              _ptr(self.part_w), _ptr(self.part_b), M, tps, s)
-            self._reduce(self.part_w, ns, D_HIDDEN * D_MODEL, [g[f"_mlps.{l}.0.weight"]], s)
-            self._reduce(self.part_b, ns, D_HIDDEN, [g[f"_mlps.{l}.0.bias"]], s)
+              _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
+            jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            c("ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,
-              self.scale_div, s)
+            c("ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
+              D_MODEL, self.scale_div, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
             c("ghm_wgrad", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-              _ptr(self.part_w), None, M, tps, s)
-            self._reduce(self.part_w, ns, 3 * D_MODEL * D_MODEL,
-                         [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"]], s)
+              _ptr(self.part_wq), None, M, tps, s)
+            jobs.append(J(self.part_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
+                                             g[f"_values.{l}.weight"]]))
             c("ghm_qkv_bwd", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, s)
-            self._reduce(self.part_ln, self.nblk, 2 * D_MODEL,
-                         [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]], s)
+            jobs.append(J(self.part_ln, self.nblk, [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]]))
+            self._flush(jobs, s)  # every partial buffer is reused by the next layer
             cur, nxt = nxt, cur  # cur = dH_l
         c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
-        self._reduce(self.part_tok, N, self.V * D_MODEL, [g["token_embeddings.weight"]], s)
-        self._reduce(cur, N, T * D_MODEL, [g["position_embeddings.weight"]], s)
+        jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
+        self._flush(jobs, s)

@@ -67,8 +67,8 @@ def main():
         "wgrad_w1": (lambda: c("ghm_wgrad", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2, P(plan.st2[l]),
                                P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w), P(plan.part_b), M,
                                tps_w1, sp), gf(2 * M * 128 * 512)),
-        "attn_bwd": (lambda: c("ghm_attn_bwd", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dqkv), N, T, 128,
-                               plan.scale_div, sp), gf(8 * N * T * T * 128)),
+        "attn_bwd": (lambda: c("ghm_attn_bwd", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS), P(plan.dqkv),
+                               N, T, 128, plan.scale_div, sp), gf(8 * N * T * T * 128)),
         "wgrad_qkv": (lambda: c("ghm_wgrad", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2, P(plan.st1[l]),
                                 P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]), P(plan.part_w), None, M, tps_q, sp),
                       gf(2 * M * 128 * 384)),
