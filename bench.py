@@ -87,7 +87,7 @@ def time_dominant_kernel(trainer, reps=20):
     def launch():
         _native.call("ghm_ln_mlp_fwd", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                      ptr(pd["_mlps.0.0.weight"]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.weight"]),
-                     ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.U[0]), ptr(plan.st2[0]),
+                     ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]),
                      plan.M, 128, 512, plan.eps, sp)
     launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -44,11 +44,12 @@ int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln_b, const f
 int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                  int D, float scale_div, void* stream);
 
-/* H_out = H_mid + W2 GELU(W1 LN2(H_mid) + b1) + b2; U = pre-GELU [M][F] saved;
- * stats = LN2 (mean, rstd)  —  models/model.py:741-747,784-788. */
+/* H_out = H_mid + W2 GELU(W1 LN2(H_mid) + b1) + b2, U = W1 LN2(H_mid) + b1; saves
+ * G = GELU(U) and Dg = GELU'(U) [M][F] for backward; stats = LN2 (mean, rstd)
+ * —  models/model.py:741-747,784-788. */
 int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float* ln_b, const float* W1,
-                   const float* b1, const float* W2, const float* b2, float* H_out, float* U,
-                   float* stats, int64_t M, int D, int F, float eps, void* stream);
+                   const float* b1, const float* W2, const float* b2, float* H_out, float* G,
+                   float* Dg, float* stats, int64_t M, int D, int F, float eps, void* stream);
 
 /* emb[n][c] = b_out + sum_t w_out[t] (b_ro[c] + H[n,t,:] . W_ro[c,:])
  * —  models/model.py:802-805 (_read_out, transpose, _out). */
@@ -73,7 +74,8 @@ int ghm_readout_bwd(const float* H, const float* W_ro, const float* b_ro, const 
                     float* part_wout, float* part_bout, int64_t n_seq, int T, int D, int C,
                     void* stream);
 
-/* MLP + LN2 backward for one layer: writes dU [M][F] and dH_mid = dH_out + dLN2;
+/* MLP + LN2 backward for one layer (Dg = GELU'(U) from ghm_ln_mlp_fwd, passed as U):
+ * writes dU [M][F] and dH_mid = dH_out + dLN2;
  * part_ln [n_blocks][2][D] = partial (dgamma, dbeta) of LN2 where
  * n_blocks = ghm_token_blocks(M)  —  backward of model.py:784-788. */
 int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,

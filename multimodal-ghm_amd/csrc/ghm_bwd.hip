@@ -57,18 +57,22 @@ __device__ __forceinline__ void ln_bwd_acc(const f32x16* dy, const float* __rest
       if (valid) st4(dH + f, o[0], o[1], o[2], o[3]);
     }
   }
+  // dgamma / dbeta partials over the wave's 32 tokens, 16 features at a time:
+  // butterfly reduce-scatter, lane j ends with feature r = j >> 1 of the group
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
+    float vg[16], vb[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int f = 32 * it + acc_row(r, h);
-      const float dyv = dy[it][r];
-      const float sg = sum32(valid ? dyv * xh[16 * it + r] : 0.f);
-      const float sb = sum32(valid ? dyv : 0.f);
-      if (j == 0) {
-        red_g[f] = sg;
-        red_b[f] = sb;
-      }
+      vb[r] = valid ? dy[it][r] : 0.f;
+      vg[r] = vb[r] * xh[16 * it + r];
+    }
+    const float sg = reduce_scatter16(vg, j);
+    const float sb = reduce_scatter16(vb, j);
+    if ((j & 1) == 0) {
+      const int f = 32 * it + acc_row(j >> 1, h);
+      red_g[f] = sg;
+      red_b[f] = sb;
     }
   }
 }
@@ -93,6 +97,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
     const float* __restrict__ lnw, const float* __restrict__ W1, const float* __restrict__ W2,
     const float* __restrict__ U, float* __restrict__ dU, float* __restrict__ dHmid,
     float* __restrict__ part_ln, int64_t M) {
+  // U here is D = GELU'(pre-activation), written by k_ln_mlp_fwd.
   // per 32-unit chunk c: W2[:, 32c:32c+32] as [o][32] and W1[32c:32c+32, :] as [32][in]
   // in a double-buffered LDS ring; every MFMA A operand is a conflict-free ds_read_b32
   __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * 32];
@@ -147,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
       for (int s = 0; s < 64; ++s) g = mfma32(w2[s * 32], dy[s], g);
       float du[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) du[r] = g[r] * gelu_grad_f(uc[r]);
+      for (int r = 0; r < 16; ++r) du[r] = g[r] * uc[r];
       if (valid) {
         float* drow = dU + m * GHM_F + 32 * c;
 #pragma unroll

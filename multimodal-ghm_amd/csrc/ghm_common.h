@@ -72,11 +72,41 @@ __device__ __forceinline__ void load64(const float* __restrict__ p, float* x) {
 __device__ __forceinline__ float gelu_f(float x) {
   return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
 }
+// GELU and its derivative from one erf evaluation (same formulas as torch's
+// forward and GeluBackward, approximate='none')
+__device__ __forceinline__ void gelu_and_grad(float x, float& g, float& d) {
+  const float e = erff(x * 0.70710678118654752440f);
+  g = x * 0.5f * (1.f + e);
+  const float cdf = 0.5f * (1.f + e);
+  const float pdf = 0.39894228040143267794f * expf(-0.5f * x * x);
+  d = cdf + x * pdf;
+}
 // torch GeluBackward (approximate='none'): dy * (cdf + x * pdf)
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
   const float pdf = 0.39894228040143267794f * expf(-0.5f * x * x);
   return cdf + x * pdf;
+}
+
+// Reduce-scatter of 16 values over the 32 lanes of a half (j = lane & 31):
+// lanes j and j^1 both return the 32-lane sum of element j >> 1.  Four
+// halving butterfly levels plus one pairwise sum: 16 exchanges instead of
+// 16 x 5.  Fixed exchange/sum order -> deterministic.
+__device__ __forceinline__ float reduce_scatter16(float* v, int j) {
+#pragma unroll
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    const int half = 8 >> lvl;  // live values 16 >> lvl
+    const int d = 16 >> lvl;
+    const bool upper = (j & d) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float lo = v[i], hi = v[i + half];
+      const float send = upper ? lo : hi;
+      const float keep = upper ? hi : lo;
+      v[i] = keep + __shfl_xor(send, d, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
 }
 
 // Row LayerNorm statistics for a token held in row layout by lane pair (j,h):

@@ -269,14 +269,15 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
 // U^T is GELU'd in place and is immediately the B operand of the down product.
 // Per chunk the workgroup stages W1[32c:32c+32, :] ([32][132]) and
 // W2[:, 32c:32c+32] ([128][36]: float4 reads conflict-free) in a double-buffered
-// LDS ring.  U (pre-GELU) is stored for the backward pass.
+// LDS ring.  G = GELU(U) and D = GELU'(U) are stored for the backward pass
+// (one erf evaluation serves both; the backward needs no transcendentals).
 // ---------------------------------------------------------------------------
 constexpr int PW2 = 36;
 __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
-    const float* __restrict__ b2, float* __restrict__ Hout, float* __restrict__ U,
-    float2* __restrict__ stats, int64_t M, float eps) {
+    const float* __restrict__ b2, float* __restrict__ Hout, float* __restrict__ G,
+    float* __restrict__ Dg, float2* __restrict__ stats, int64_t M, float eps) {
   __shared__ __attribute__((aligned(16))) float s1[2][32 * PW];
   __shared__ __attribute__((aligned(16))) float s2[2][GHM_D * PW2];
   __shared__ __attribute__((aligned(16))) float sb1[GHM_F];
@@ -320,13 +321,18 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
         g[4 * q + 2] = u[4 * q + 2] + bb.z;
         g[4 * q + 3] = u[4 * q + 3] + bb.w;
       }
-      if (valid) {
-        float* urow = U + m * GHM_F + 32 * c;
+      float dg[16];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) st4(urow + quad_off(q, h), g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+      for (int r = 0; r < 16; ++r) gelu_and_grad(g[r], g[r], dg[r]);
+      if (valid) {  // G = GELU(U) for dW2, D = GELU'(U) for the backward
+        float* grow = G + m * GHM_F + 32 * c;
+        float* drow = Dg + m * GHM_F + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          st4(grow + quad_off(q, h), g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+          st4(drow + quad_off(q, h), dg[4 * q], dg[4 * q + 1], dg[4 * q + 2], dg[4 * q + 3]);
+        }
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) g[r] = gelu_f(g[r]);
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot) {
         // A operand: W2[32ot + j][32c + 8q + 4h + t] = s2[(32ot + j) * PW2 + 8q + 4h + t]
@@ -551,12 +557,12 @@ extern "C" int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, floa
 
 extern "C" int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float* ln_b,
                               const float* W1, const float* b1, const float* W2, const float* b2,
-                              float* H_out, float* U, float* stats, int64_t M, int D, int F,
+                              float* H_out, float* G, float* Dg, float* stats, int64_t M, int D, int F,
                               float eps, void* stream) {
-  GHM_CHECK(H_mid && ln_w && ln_b && W1 && b1 && W2 && b2 && H_out && U && stats, "null pointer");
+  GHM_CHECK(H_mid && ln_w && ln_b && W1 && b1 && W2 && b2 && H_out && G && Dg && stats, "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   hipLaunchKernelGGL(k_ln_mlp_fwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2, b2, H_out, U,
+                     ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2, b2, H_out, G, Dg,
                      reinterpret_cast<float2*>(stats), M, eps);
   return ghm_launch_status();
 }

@@ -33,7 +33,7 @@ HIP_SIGNATURES = {
     "ghm_embed_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ln_qkv_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_attn_fwd": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
-    "ghm_ln_mlp_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_ln_mlp_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_readout_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_clip_loss": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p],
     "ghm_readout_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],

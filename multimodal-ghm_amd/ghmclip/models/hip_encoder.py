@@ -9,7 +9,7 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   Hmid [L,   M, 128]   residual after attention
   qkv  [L,   M, 384]   Q | K | V
   P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input)
-  U    [L,   M, 512]   MLP pre-activation (backward input)
+  G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (backward inputs)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
 [M, 384], dU [M, 512], and split-K / per-block partial buffers.
@@ -78,7 +78,8 @@ class EncoderPlan:
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
         self.P = torch.zeros(L, N, 96, 96, dtype=f32, device=dev)
-        self.U = e(L, M, D_HIDDEN)
+        self.G = e(L, M, D_HIDDEN)
+        self.Dg = e(L, M, D_HIDDEN)
         self.st1 = e(L, M, 2)
         self.st2 = e(L, M, 2)
         self.emb = e(N, num_class)
@@ -139,8 +140,8 @@ class EncoderPlan:
               N, T, D_MODEL, self.scale_div, s)
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
-              _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.U[l]), _ptr(self.st2[l]),
-              M, D_MODEL, D_HIDDEN, self.eps, s)
+              _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
+              _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
         c("ghm_readout_fwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, s)
         self._gen += 1
@@ -195,11 +196,11 @@ class EncoderPlan:
         for l in reversed(range(L)):
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
             c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-              _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.U[l]), _ptr(self.dU),
+              _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
               _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
             jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
-            tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] GELU(U)[m][hid]; db2 = sum dY
-            c("ghm_wgrad", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.U[l]), D_HIDDEN, D_HIDDEN, 1,
+            tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
+            c("ghm_wgrad", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G[l]), D_HIDDEN, D_HIDDEN, 0,
               None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)
             jobs += [J(self.part_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(self.part_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU

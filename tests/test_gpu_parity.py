@@ -61,7 +61,7 @@ def _pair(L=2, T=81, seed=7):
 def _oracle_intermediates(ref, x):
     """Oracle forward that records the per-layer tensors the HIP plan stores."""
     B, T = x.shape
-    out = {"H": [], "Hmid": [], "qkv": [], "P": [], "U": []}
+    out = {"H": [], "Hmid": [], "qkv": [], "P": [], "G": [], "Dg": []}
     H = ref.token_embeddings(x) + ref.position_embeddings(torch.arange(T).expand(B, T))
     for q, k, v, mlp, ln1, ln2 in zip(ref._queries, ref._keys, ref._values, ref._mlps, ref._lns_1, ref._lns_2):
         out["H"].append(H)
@@ -73,7 +73,9 @@ def _oracle_intermediates(ref, x):
         H = H + A @ V
         out["Hmid"].append(H)
         U = mlp[0](ln2(H))
-        out["U"].append(U)
+        out["G"].append(torch.nn.functional.gelu(U))
+        cdf = 0.5 * (1 + torch.erf(U / np.sqrt(2.0)))
+        out["Dg"].append(cdf + U * torch.exp(-0.5 * U * U) / np.sqrt(2 * np.pi))
         H = H + mlp[2](mlp[1](U))
     out["H"].append(H)
     return out
@@ -95,7 +97,8 @@ def test_encoder_forward_stages(T, nseq):
         assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < 2e-5, f"qkv[{l}]"
         assert _rel(plan.probs_dense(l), want["P"][l]) < 2e-5, f"P[{l}]"
         assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < 2e-5, f"Hmid[{l}]"
-        assert _rel(plan.U[l].view(nseq, T, 512), want["U"][l]) < 2e-5, f"U[{l}]"
+        assert _rel(plan.G[l].view(nseq, T, 512), want["G"][l]) < 2e-5, f"G[{l}]"
+        assert _rel(plan.Dg[l].view(nseq, T, 512), want["Dg"][l]) < 2e-5, f"Dg[{l}]"
     assert _rel(plan.H[2][:M].view(nseq, T, 128), want["H"][2]) < 2e-5, "H[L]"
     ref_emb = ref(x)[0]
     assert _rel(emb, ref_emb) < 2e-5

@@ -57,12 +57,12 @@ def main():
                                128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
         "ln_mlp_fwd": (lambda: c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
                                  P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
-                                 P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.U[l]), P(plan.st2[l]), M, 128, 512,
+                                 P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
                                  plan.eps, sp), gf(4 * M * 128 * 512)),
         "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]),
-                              P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.U[l]), P(plan.dU),
+                              P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.Dg[l]), P(plan.dU),
                               P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
-        "wgrad_w2": (lambda: c("ghm_wgrad", P(plan.H[l + 1]), 128, 128, P(plan.U[l]), 512, 512, 1, None, None, None,
+        "wgrad_w2": (lambda: c("ghm_wgrad", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None, None, None,
                                P(plan.part_w), P(plan.part_b), M, tps_w2, sp), gf(2 * M * 128 * 512)),
         "wgrad_w1": (lambda: c("ghm_wgrad", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2, P(plan.st2[l]),
                                P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w), P(plan.part_b), M,
