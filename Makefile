@@ -6,8 +6,8 @@ CXX ?= g++
 LIBDIR := multimodal-ghm_amd/ghmclip/_lib
 SRC := multimodal-ghm_amd/csrc
 HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result
-HIP_SRCS := $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_optim.hip
-HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h include/ghm_hip.h
+HIP_SRCS := $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_x3.hip $(SRC)/ghm_optim.hip
+HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h $(SRC)/ghm_split.h $(SRC)/ghm_ln.h include/ghm_hip.h
 
 all: $(LIBDIR)/libghm_hip.so $(LIBDIR)/libghm_host.so
 
@@ -22,6 +22,7 @@ $(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h
 resource-usage: $(HIP_SRCS) $(HIP_HDRS)
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_fwd.hip -o /tmp/ghm_fwd.o
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_bwd.hip -o /tmp/ghm_bwd.o
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_x3.hip -o /tmp/ghm_x3.o
 
 clean:
 	rm -f $(LIBDIR)/*.so

@@ -47,7 +47,7 @@ def setup_dist(n_gpus):
     return ws, rank, local
 
 
-def build(rank, B, L, p, total_iters):
+def build(rank, B, L, p, total_iters, precision=None):
     from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
     from ghmclip.training.clip_trainer import ClipTrainer
     p_y = np.ones(10) / 10
@@ -56,7 +56,7 @@ def build(rank, B, L, p, total_iters):
     tm = EncoderTransformer(81, 10, 128, L).cuda()
     im = EncoderTransformer(81, 10, 128, L).cuda()
     sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, total_iters) for s in range(total_iters + 1)]
-    trainer = ClipTrainer(tm, im, 4, B, sched, device="cuda")
+    trainer = ClipTrainer(tm, im, 4, B, sched, device="cuda", precision=precision)
     sampler.native.seed(224 + 1000 * rank)  # each rank draws its own shard of the global batch
     return sampler, trainer
 
@@ -125,11 +125,13 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ring", type=int, default=16)
+    ap.add_argument("--precision", default=None, choices=["f32", "x3"],
+                    help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or f32)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
     total_iters = max(3000, a.steps + a.warmup + 1)
-    sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters)
+    sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision)
     ring = make_ring(sampler, a.batch, a.ring)
 
     def one(k):
@@ -183,7 +185,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
         "config": {"workload": "clip_default: 2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW",
                    "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,

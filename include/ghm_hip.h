@@ -141,6 +141,41 @@ int ghm_adamw(float* param, const float* grad, float* m, float* v, int64_t n, co
               float b1, float one_minus_b1, float b2, float one_minus_b2, float eps,
               void* stream);
 
+/* ---- split-bf16 ("x3") path ------------------------------------------------
+ * Same semantics and buffers as the f32 entry points above; every product is
+ * evaluated as hi*hi + hi*lo + lo*hi with the operands split into bf16
+ * hi = bf16(x), lo = bf16(x - hi) and f32 accumulation (v_mfma_f32_32x32x16_bf16):
+ * ~2^-16 relative error per product instead of exact-f32 MFMA, at 5.3x the
+ * matrix-core rate.  Weights come from a per-layer "pack" of pre-split bf16
+ * planes written by ghm_split_weights (GHM_SPLIT_PACK_ELEMS bf16 per layer,
+ * 16-byte aligned); re-split after every parameter update. */
+#define GHM_SPLIT_PACK_ELEMS 720896
+#define GHM_SPLIT_MAX_JOBS 16
+typedef struct ghm_split_job {
+  const float* Wq;  /* [128][128] each, nn.Linear layout [out][in] */
+  const float* Wk;
+  const float* Wv;
+  const float* W1;  /* [512][128] */
+  const float* W2;  /* [128][512] */
+  void* pack;       /* GHM_SPLIT_PACK_ELEMS bf16 */
+} ghm_split_job;
+/* Split one layer's Q/K/V/MLP weights per job into its pack (up to 16 jobs). */
+int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream);
+/* As ghm_ln_qkv_fwd (model.py:772-775). */
+int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, const void* pack, float* qkv,
+                      float* stats, int64_t M, int D, float eps, void* stream);
+/* As ghm_ln_mlp_fwd (model.py:741-747,784-788); b1 [512], b2 [128] stay f32. */
+int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                      const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
+                      int64_t M, int D, int F, float eps, void* stream);
+/* As ghm_mlp_bwd (backward of model.py:784-788); Dg = GELU'(U) from the forward. */
+int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
+                   const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln, int64_t M,
+                   int D, int F, void* stream);
+/* As ghm_qkv_bwd (backward of model.py:772-775). */
+int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
+                   const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

@@ -3,6 +3,7 @@
 // and :877-907 (GuidedClipLoss, guide=False).  See ghm_common.h for the
 // "tokens on lanes" register layout shared by all token-parallel kernels.
 #include "ghm_common.h"
+#include "ghm_ln.h"
 
 // ---------------------------------------------------------------------------
 // H0[m] = tok_w[tokens[m]] + pos_w[m % T]                      (model.py:764-765)
@@ -21,24 +22,6 @@ __global__ __launch_bounds__(256) void k_embed_fwd(const uint8_t* __restrict__ t
   const float4 a = reinterpret_cast<const float4*>(tok_w + v * GHM_D)[c4];
   const float4 b = reinterpret_cast<const float4*>(pos_w + t * GHM_D)[c4];
   reinterpret_cast<float4*>(H + m * GHM_D)[c4] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-
-// Load one token row (row layout), LayerNorm it in place; returns stats.
-__device__ __forceinline__ void ln_row(const float* __restrict__ row, const float* __restrict__ lnw,
-                                       const float* __restrict__ lnb, int h, float eps, float* x,
-                                       float& mean, float& rstd) {
-  load64(row + 64 * h, x);
-  ln_stats64(x, eps, mean, rstd);
-  const float4* g4 = reinterpret_cast<const float4*>(lnw + 64 * h);
-  const float4* b4 = reinterpret_cast<const float4*>(lnb + 64 * h);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const float4 g = g4[q], b = b4[q];
-    x[4 * q + 0] = (x[4 * q + 0] - mean) * rstd * g.x + b.x;
-    x[4 * q + 1] = (x[4 * q + 1] - mean) * rstd * g.y + b.y;
-    x[4 * q + 2] = (x[4 * q + 2] - mean) * rstd * g.z + b.z;
-    x[4 * q + 3] = (x[4 * q + 3] - mean) * rstd * g.w + b.w;
-  }
 }
 
 // Y^T tile (32 out features x 32 tokens) = W[o0:o0+32, :] . X^T, X in row layout,

@@ -1,0 +1,504 @@
+// Split-bf16 ("x3") token-parallel kernels of the GHM CLIP encoder step (gfx950).
+//
+// Same data flow, buffers and outputs as the exact-f32 kernels of ghm_fwd.hip /
+// ghm_bwd.hip, with every product evaluated as three bf16 MFMAs
+// (ghm_split.h).  Weights enter through a per-layer "pack" of pre-split bf16
+// planes in the layouts the kernels read (written once per step by
+// ghm_split_weights), so the LDS staging of a weight tile is a plain 16-byte
+// copy.  Activations are split in registers where they become MFMA operands.
+// Reference semantics: src/ghmclip/models/model.py:772-788 (LN1 + Q/K/V,
+// LN2 + MLP) and their autograd backward (train_CLIP.py:158).
+#include "ghm_common.h"
+#include "ghm_ln.h"
+#include "ghm_split.h"
+#include "ghm_launch.h"
+
+// ---------------------------------------------------------------------------
+// Weight pack (bf16 elements per layer; each region = hi plane then lo plane)
+// ---------------------------------------------------------------------------
+constexpr int PK_QKV = 3 * GHM_D * GHM_D;  // 49152 elements per plane
+constexpr int PK_W = GHM_F * GHM_D;        // 65536
+constexpr int PK_QKV_N = 0;                // [384][128]: row 128*mat + o, col d   = W_mat[o][d]
+constexpr int PK_QKV_T = 2 * PK_QKV;       // [128][384]: row d, col 128*mat + o   = W_mat[o][d]
+constexpr int PK_W1_N = 4 * PK_QKV;        // [512][128]: W1[f][d]
+constexpr int PK_W1_T = PK_W1_N + 2 * PK_W;  // [128][512]: row d, col q           = W1[perm(q)][d]
+constexpr int PK_W2_P = PK_W1_T + 2 * PK_W;  // [128][512]: row o, col q           = W2[o][perm(q)]
+constexpr int PK_W2_T = PK_W2_P + 2 * PK_W;  // [512][128]: row f, col o           = W2[o][f]
+constexpr int PK_ELEMS = PK_W2_T + 2 * PK_W;  // 720896
+static_assert(PK_ELEMS == GHM_SPLIT_PACK_ELEMS, "pack layout mismatch with include/ghm_hip.h");
+
+// column permutation inside each 16-group for operands met by an accumulator
+// tile (ghm_split.h): position q holds original column perm_col(q)
+__device__ __forceinline__ constexpr int perm_col(int q) {
+  return (q & ~15) + (q & 3) + 8 * ((q >> 2) & 1) + 4 * ((q >> 3) & 1);
+}
+
+struct SplitJobs {
+  ghm_split_job job[GHM_SPLIT_MAX_JOBS];
+};
+
+__global__ __launch_bounds__(256) void k_split_weights(SplitJobs J) {
+  const ghm_split_job& jb = J.job[blockIdx.y];
+  const int e = 4 * (static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x));
+  if (e >= PK_ELEMS / 2) return;
+  float v[4];
+  int base, n, idx;
+  if (e < PK_QKV) {
+    idx = e; base = PK_QKV_N; n = PK_QKV;
+    const int row = e >> 7, col = e & 127;
+    const float* W = row < 128 ? jb.Wq : (row < 256 ? jb.Wk : jb.Wv);
+    const float4 f = *reinterpret_cast<const float4*>(W + (row & 127) * GHM_D + col);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  } else if (e < 2 * PK_QKV) {
+    idx = e - PK_QKV; base = PK_QKV_T; n = PK_QKV;
+    const int d = idx / 384, c = idx % 384, mat = c >> 7, o = c & 127;
+    const float* W = mat == 0 ? jb.Wq : (mat == 1 ? jb.Wk : jb.Wv);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = W[(o + t) * GHM_D + d];
+  } else if (e < 2 * PK_QKV + PK_W) {
+    idx = e - 2 * PK_QKV; base = PK_W1_N; n = PK_W;
+    const float4 f = *reinterpret_cast<const float4*>(jb.W1 + idx);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  } else if (e < 2 * PK_QKV + 2 * PK_W) {
+    idx = e - 2 * PK_QKV - PK_W; base = PK_W1_T; n = PK_W;
+    const int d = idx >> 9, q = idx & 511;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = jb.W1[perm_col(q + t) * GHM_D + d];
+  } else if (e < 2 * PK_QKV + 3 * PK_W) {
+    idx = e - 2 * PK_QKV - 2 * PK_W; base = PK_W2_P; n = PK_W;
+    const int o = idx >> 9, q = idx & 511;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = jb.W2[o * GHM_F + perm_col(q + t)];
+  } else {
+    idx = e - 2 * PK_QKV - 3 * PK_W; base = PK_W2_T; n = PK_W;
+    const int f = idx >> 7, o = idx & 127;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = jb.W2[(o + t) * GHM_F + f];
+  }
+  bf16x4 hi, lo;
+  split4(make_float4(v[0], v[1], v[2], v[3]), hi, lo);
+  __bf16* pk = reinterpret_cast<__bf16*>(jb.pack);
+  stb4(pk + base + idx, hi);
+  stb4(pk + base + n + idx, lo);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 tile staging: R x C elements (global row pitch ldg) -> LDS pitch P,
+// 16 bytes per thread-load, 256 threads; both planes (lo plane at +plane).
+// ---------------------------------------------------------------------------
+template <int R, int C>
+__device__ __forceinline__ constexpr int stage_bf_n() { return R * (C / 8) / 256; }
+
+template <int R, int C>
+__device__ __forceinline__ void stage_bf_load(uint4* v, const __bf16* __restrict__ g, int ldg, int plane) {
+  constexpr int C8 = C / 8, N = R * C8 / 256;
+  static_assert(R * C8 % 256 == 0, "tile must be a multiple of 256 x 16 B");
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    const __bf16* p = g + static_cast<size_t>(idx / C8) * ldg + 8 * (idx % C8);
+    v[k] = *reinterpret_cast<const uint4*>(p);
+    v[N + k] = *reinterpret_cast<const uint4*>(p + plane);
+  }
+}
+
+template <int R, int C, int P>
+__device__ __forceinline__ void stage_bf_store(const uint4* v, __bf16* hi, __bf16* lo) {
+  constexpr int C8 = C / 8, N = R * C8 / 256;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    const int off = (idx / C8) * P + 8 * (idx % C8);
+    *reinterpret_cast<uint4*>(hi + off) = v[k];
+    *reinterpret_cast<uint4*>(lo + off) = v[N + k];
+  }
+}
+
+constexpr int PB1 = GHM_D + 8;  // [32][128] tile row pitch (bf16): 272 B
+constexpr int PB2 = 32 + 8;     // [128][32] tile row pitch (bf16): 80 B
+
+// Y^T tile (32 rows x 32 tokens) = A[32][128] . X^T with A rows in LDS
+// (pitch PB1) and X a row-layout token split into 8 k-steps (k = 64h + 8t + i)
+__device__ __forceinline__ f32x16 proj_x3(const __bf16* ah, const __bf16* al, const bf16x8* xh,
+                                          const bf16x8* xl, f32x16 acc) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc = mfma_x3(ldsb8(ah + 8 * t), ldsb8(al + 8 * t), xh[t], xl[t], acc);
+  return acc;
+}
+
+// LN a token row (row layout) and split it into the 8 k-step fragments
+__device__ __forceinline__ void ln_row_split(const float* __restrict__ row, const float* __restrict__ lnw,
+                                             const float* __restrict__ lnb, int h, float eps, bool active,
+                                             bf16x8* xh, bf16x8* xl, float& mean, float& rstd) {
+  float x[64];
+  if (active) {
+    ln_row(row, lnw, lnb, h, eps, x, mean, rstd);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x[k] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
+}
+
+// load a row-layout token vector (64 floats at p) and split it
+__device__ __forceinline__ void load_split64(const float* __restrict__ p, bool active, bf16x8* xh, bf16x8* xl) {
+  float x[64];
+  if (active) {
+    load64(p, x);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x[k] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
+}
+
+// ---------------------------------------------------------------------------
+// LN1 + Q/K/V projections                                       (model.py:772-775)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
+    const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* __restrict__ pack, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
+    float eps) {
+  __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const bool active = m0 < M;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  bf16x8 xh[8], xl[8];
+  {
+    float mean = 0.f, rstd = 0.f;
+    ln_row_split(H + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
+    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
+  const __bf16* W = pack + PK_QKV_N;
+  uint4 st[2 * stage_bf_n<32, GHM_D>()];
+  stage_bf_load<32, GHM_D>(st, W, GHM_D, PK_QKV);
+  stage_bf_store<32, GHM_D, PB1>(st, swh[0], swl[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
+    const int cur = b & 1;
+    stage_bf_load<32, GHM_D>(st, W + (b + 1 < 12 ? b + 1 : 11) * 32 * GHM_D, GHM_D, PK_QKV);
+    if (active) {
+      const f32x16 acc = proj_x3(swh[cur] + j * PB1 + 64 * h, swl[cur] + j * PB1 + 64 * h, xh, xl, zero16());
+      if (valid) {
+        float* o = qkv + m * (3 * GHM_D) + 32 * b;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          st4(o + quad_off(q, h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+      }
+    }
+    stage_bf_store<32, GHM_D, PB1>(st, swh[cur ^ 1], swl[cur ^ 1]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LN2 + MLP (128 -> 512 -> GELU -> 128) + residual             (model.py:784-788)
+// Per 32-unit chunk: W1 rows [32][128] and W2 columns [128][32] (k-permuted)
+// through a double-buffered LDS ring; the hidden chunk stays in registers.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd_x3(
+    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* __restrict__ pack, const float* __restrict__ b1, const float* __restrict__ b2,
+    float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
+    int64_t M, float eps) {
+  __shared__ __attribute__((aligned(16))) __bf16 s1h[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 s1l[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 s2h[2][GHM_D * PB2];
+  __shared__ __attribute__((aligned(16))) __bf16 s2l[2][GHM_D * PB2];
+  __shared__ __attribute__((aligned(16))) float sb1[GHM_F];
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const bool active = m0 < M;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  for (int i = threadIdx.x; i < GHM_F; i += 256) sb1[i] = b1[i];
+  bf16x8 xh[8], xl[8];
+  {
+    float mean = 0.f, rstd = 0.f;
+    ln_row_split(Hmid + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
+    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
+  f32x16 y[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) y[ot] = zero16();
+  const __bf16* W1 = pack + PK_W1_N;
+  const __bf16* W2 = pack + PK_W2_P;
+  uint4 st1[2 * stage_bf_n<32, GHM_D>()], st2[2 * stage_bf_n<GHM_D, 32>()];
+  stage_bf_load<32, GHM_D>(st1, W1, GHM_D, PK_W);
+  stage_bf_load<GHM_D, 32>(st2, W2, GHM_F, PK_W);
+  stage_bf_store<32, GHM_D, PB1>(st1, s1h[0], s1l[0]);
+  stage_bf_store<GHM_D, 32, PB2>(st2, s2h[0], s2l[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < GHM_F / 32; ++c) {
+    const int cur = c & 1;
+    {
+      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
+      stage_bf_load<32, GHM_D>(st1, W1 + nc * 32 * GHM_D, GHM_D, PK_W);
+      stage_bf_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F, PK_W);
+    }
+    if (active) {
+      const f32x16 u = proj_x3(s1h[cur] + j * PB1 + 64 * h, s1l[cur] + j * PB1 + 64 * h, xh, xl, zero16());
+      float g[16], dg[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 bb = lds4(sb1 + 32 * c + quad_off(q, h));
+        g[4 * q + 0] = u[4 * q + 0] + bb.x;
+        g[4 * q + 1] = u[4 * q + 1] + bb.y;
+        g[4 * q + 2] = u[4 * q + 2] + bb.z;
+        g[4 * q + 3] = u[4 * q + 3] + bb.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gelu_fast(g[r], g[r], dg[r]);
+      if (valid) {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward
+        float* grow = G + m * GHM_F + 32 * c;
+        float* drow = Dg + m * GHM_F + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          st4(grow + quad_off(q, h), g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+          st4(drow + quad_off(q, h), dg[4 * q], dg[4 * q + 1], dg[4 * q + 2], dg[4 * q + 3]);
+        }
+      }
+      bf16x8 gh[2], gl[2];
+      split_acc(g, 0, gh[0], gl[0]);
+      split_acc(g, 1, gh[1], gl[1]);
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        const __bf16* w2h = s2h[cur] + (32 * ot + j) * PB2 + 8 * h;
+        const __bf16* w2l = s2l[cur] + (32 * ot + j) * PB2 + 8 * h;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          y[ot] = mfma_x3(ldsb8(w2h + 16 * s), ldsb8(w2l + 16 * s), gh[s], gl[s], y[ot]);
+      }
+    }
+    stage_bf_store<32, GHM_D, PB1>(st1, s1h[cur ^ 1], s1l[cur ^ 1]);
+    stage_bf_store<GHM_D, 32, PB2>(st2, s2h[cur ^ 1], s2l[cur ^ 1]);
+    __syncthreads();
+  }
+  if (active && valid) {
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      float4 hv[4], bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        hv[q] = *reinterpret_cast<const float4*>(Hmid + m * GHM_D + 32 * ot + quad_off(q, h));
+        bv[q] = *reinterpret_cast<const float4*>(b2 + 32 * ot + quad_off(q, h));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(Hout + m * GHM_D + 32 * ot + quad_off(q, h), hv[q].x + (y[ot][4 * q] + bv[q].x),
+            hv[q].y + (y[ot][4 * q + 1] + bv[q].y), hv[q].z + (y[ot][4 * q + 2] + bv[q].z),
+            hv[q].w + (y[ot][4 * q + 3] + bv[q].w));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MLP + LN2 backward                                          (model.py:784-788)
+//   dG^T = W2^T dY^T (per chunk), dU = dG * GELU'(U) (stored),
+//   dX2^T += W1^T dU^T (registers), then LN2 backward + residual.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
+    const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const __bf16* __restrict__ pack, const float* __restrict__ Dg,
+    float* __restrict__ dU, float* __restrict__ dHmid, float* __restrict__ part_ln, int64_t M) {
+  // the LN partial buffer `red` aliases the first ring buffer after the loop
+  __shared__ __attribute__((aligned(16))) __bf16 sah[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 sal[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 sbh[2][GHM_D * PB2];
+  __shared__ __attribute__((aligned(16))) __bf16 sbl[2][GHM_D * PB2];
+  __shared__ __attribute__((aligned(16))) float gam[GHM_D];
+  static_assert(sizeof(sah) >= 2 * 4 * GHM_D * sizeof(float), "red alias");
+  float* red = reinterpret_cast<float*>(&sah[0][0]);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
+  const bool active = m0 < M;
+  if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
+  const int64_t m = m0 + j;
+  const bool valid = active && m < M;
+  const int64_t mc = m < M ? m : M - 1;
+  f32x16 dx[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) dx[it] = zero16();
+  bf16x8 yh[8], yl[8];
+  load_split64(dHout + mc * GHM_D + 64 * h, active, yh, yl);  // dY[token][o = 64h + 8t + i]
+  const __bf16* WA = pack + PK_W2_T;  // rows = hidden unit, cols = o
+  const __bf16* WB = pack + PK_W1_T;  // rows = d, cols = hidden (permuted)
+  uint4 sta[2 * stage_bf_n<32, GHM_D>()], stb[2 * stage_bf_n<GHM_D, 32>()];
+  stage_bf_load<32, GHM_D>(sta, WA, GHM_D, PK_W);
+  stage_bf_load<GHM_D, 32>(stb, WB, GHM_F, PK_W);
+  float4 un[4];
+  const float* urow = Dg + mc * GHM_F;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + quad_off(q, h));
+  stage_bf_store<32, GHM_D, PB1>(sta, sah[0], sal[0]);
+  stage_bf_store<GHM_D, 32, PB2>(stb, sbh[0], sbl[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < GHM_F / 32; ++c) {
+    const int cur = c & 1;
+    float uc[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uc[4 * q] = un[q].x; uc[4 * q + 1] = un[q].y; uc[4 * q + 2] = un[q].z; uc[4 * q + 3] = un[q].w;
+    }
+    {
+      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
+      stage_bf_load<32, GHM_D>(sta, WA + nc * 32 * GHM_D, GHM_D, PK_W);
+      stage_bf_load<GHM_D, 32>(stb, WB + nc * 32, GHM_F, PK_W);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + 32 * nc + quad_off(q, h));
+    }
+    if (active) {
+      const f32x16 g = proj_x3(sah[cur] + j * PB1 + 64 * h, sal[cur] + j * PB1 + 64 * h, yh, yl, zero16());
+      float du[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) du[r] = g[r] * uc[r];
+      if (valid) {
+        float* drow = dU + m * GHM_F + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) st4(drow + quad_off(q, h), du[4 * q], du[4 * q + 1], du[4 * q + 2], du[4 * q + 3]);
+      }
+      bf16x8 dh[2], dl[2];
+      split_acc(du, 0, dh[0], dl[0]);
+      split_acc(du, 1, dh[1], dl[1]);
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const __bf16* wh = sbh[cur] + (32 * it + j) * PB2 + 8 * h;
+        const __bf16* wl = sbl[cur] + (32 * it + j) * PB2 + 8 * h;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) dx[it] = mfma_x3(ldsb8(wh + 16 * s), ldsb8(wl + 16 * s), dh[s], dl[s], dx[it]);
+      }
+    }
+    stage_bf_store<32, GHM_D, PB1>(sta, sah[cur ^ 1], sal[cur ^ 1]);
+    stage_bf_store<GHM_D, 32, PB2>(stb, sbh[cur ^ 1], sbl[cur ^ 1]);
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  __syncthreads();
+  if (active)
+    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
+               red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
+  __syncthreads();
+  ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
+}
+
+// ---------------------------------------------------------------------------
+// QKV + LN1 backward                                          (model.py:772-775)
+//   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
+    const float* __restrict__ dqkv, const float* __restrict__ H, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const __bf16* __restrict__ pack, const float* __restrict__ dHmid,
+    float* __restrict__ dH, float* __restrict__ part_ln, int64_t M) {
+  __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
+  __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
+  __shared__ float red[2 * 4 * GHM_D];
+  __shared__ __attribute__((aligned(16))) float gam[GHM_D];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
+  const bool active = m0 < M;
+  for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
+  if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
+  const int64_t m = m0 + j;
+  const bool valid = active && m < M;
+  const int64_t mc = m < M ? m : M - 1;
+  f32x16 dx[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) dx[it] = zero16();
+  const __bf16* W = pack + PK_QKV_T;  // [128 d][384]
+  uint4 st[2 * stage_bf_n<32, GHM_D>()];
+  stage_bf_load<32, GHM_D>(st, W, 3 * GHM_D, PK_QKV);
+  stage_bf_store<32, GHM_D, PB1>(st, swh[0], swl[0]);
+  __syncthreads();
+#pragma unroll 1
+  for (int mat = 0; mat < 3; ++mat) {
+    bf16x8 gh[8], gl[8];
+    load_split64(dqkv + mc * (3 * GHM_D) + mat * GHM_D + 64 * h, active, gh, gl);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int b = mat * 4 + it, cur = b & 1;
+      {
+        const int nb = b + 1 < 12 ? b + 1 : 11;  // tile nb: rows 32*(nb&3).., columns 128*(nb>>2)..
+        stage_bf_load<32, GHM_D>(st, W + (nb & 3) * 32 * (3 * GHM_D) + (nb >> 2) * GHM_D, 3 * GHM_D, PK_QKV);
+      }
+      if (active) dx[it] = proj_x3(swh[cur] + j * PB1 + 64 * h, swl[cur] + j * PB1 + 64 * h, gh, gl, dx[it]);
+      stage_bf_store<32, GHM_D, PB1>(st, swh[cur ^ 1], swl[cur ^ 1]);
+      __syncthreads();
+    }
+  }
+  if (active)
+    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
+               red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
+  __syncthreads();
+  ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI launchers
+// ---------------------------------------------------------------------------
+extern "C" int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream) {
+  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= GHM_SPLIT_MAX_JOBS, "jobs");
+  SplitJobs J;
+  for (int i = 0; i < n_jobs; ++i) {
+    const ghm_split_job& jb = jobs[i];
+    GHM_CHECK(jb.Wq && jb.Wk && jb.Wv && jb.W1 && jb.W2 && jb.pack, "null pointer in job");
+    GHM_CHECK((reinterpret_cast<uintptr_t>(jb.pack) & 15) == 0, "pack must be 16-byte aligned");
+    J.job[i] = jb;
+  }
+  const unsigned nblk = (PK_ELEMS / 2 / 4 + 255) / 256;
+  hipLaunchKernelGGL(k_split_weights, dim3(nblk, static_cast<unsigned>(n_jobs)), dim3(256), 0,
+                     ghm_stream(stream), J);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, const void* pack,
+                                 float* qkv, float* stats, int64_t M, int D, float eps, void* stream) {
+  GHM_CHECK(H && ln_w && ln_b && pack && qkv && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), qkv,
+                     reinterpret_cast<float2*>(stats), M, eps);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                                 const float* b1, const float* b2, float* H_out, float* G, float* Dg,
+                                 float* stats, int64_t M, int D, int F, float eps, void* stream) {
+  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && G && Dg && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  hipLaunchKernelGGL(k_ln_mlp_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1, b2,
+                     H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
+                              const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln,
+                              int64_t M, int D, int F, void* stream) {
+  GHM_CHECK(dH_out && H_mid && stats && ln_w && pack && Dg && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  hipLaunchKernelGGL(k_mlp_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w,
+                     reinterpret_cast<const __bf16*>(pack), Dg, dU, dH_mid, part_ln, M);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w,
+                              const void* pack, const float* dH_mid, float* dH, float* part_ln, int64_t M,
+                              int D, void* stream) {
+  GHM_CHECK(dqkv && H && stats && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  hipLaunchKernelGGL(k_qkv_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dqkv, H, reinterpret_cast<const float2*>(stats), ln_w,
+                     reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln, M);
+  return ghm_launch_status();
+}

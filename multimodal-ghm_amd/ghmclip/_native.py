@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
-HIP_LIB = os.path.join(_LIBDIR, "libghm_hip.so")
+HIP_LIB = os.environ.get("GHM_HIP_LIB") or os.path.join(_LIBDIR, "libghm_hip.so")
 HOST_LIB = os.path.join(_LIBDIR, "libghm_host.so")
 
 _p = ctypes.c_void_p
@@ -20,6 +20,16 @@ class ReduceJob(ctypes.Structure):
     """ghm_reduce_job (include/ghm_hip.h)."""
     _fields_ = [("part", ctypes.c_void_p), ("n_split", ctypes.c_int32), ("n_seg", ctypes.c_int32),
                 ("n", ctypes.c_int64), ("dst", ctypes.c_void_p * 4), ("off", ctypes.c_int64 * 5)]
+
+
+class SplitJob(ctypes.Structure):
+    """ghm_split_job (include/ghm_hip.h)."""
+    _fields_ = [("Wq", ctypes.c_void_p), ("Wk", ctypes.c_void_p), ("Wv", ctypes.c_void_p),
+                ("W1", ctypes.c_void_p), ("W2", ctypes.c_void_p), ("pack", ctypes.c_void_p)]
+
+
+GHM_SPLIT_PACK_ELEMS = 720896  # include/ghm_hip.h
+
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _f = ctypes.c_float
@@ -45,6 +55,11 @@ HIP_SIGNATURES = {
     "ghm_reduce_partials": [_p, _i, _i64, _i, _p, _p, _p],
     "ghm_reduce_batch": [_p, _i, _p],
     "ghm_clip_prepare": [_p, _i64, _f, _p, _i, _p, _p, _p, _p],
+    "ghm_split_weights": [_p, _i, _p],
+    "ghm_ln_qkv_fwd_x3": [_p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
+    "ghm_ln_mlp_fwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_mlp_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
+    "ghm_qkv_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64}

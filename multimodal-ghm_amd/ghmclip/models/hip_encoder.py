@@ -11,11 +11,13 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input)
   G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (backward inputs)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
+  pack [L, 720896] bf16 (precision "x3" only): per-layer pre-split weight planes
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
 [M, 384], dU [M, 512], and split-K / per-block partial buffers.
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -50,6 +52,17 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+PRECISIONS = ("f32", "x3")
+
+
+def default_precision():
+    """GHM_PRECISION env var: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA)."""
+    p = os.environ.get("GHM_PRECISION", "f32")
+    if p not in PRECISIONS:
+        raise ValueError(f"GHM_PRECISION must be one of {PRECISIONS} (got {p!r})")
+    return p
+
+
 def require_hip(t):
     if not (isinstance(t, torch.Tensor) and t.is_cuda and torch.version.hip):
         raise RuntimeError("ghmclip (MI355X build) runs on a HIP device only; "
@@ -58,13 +71,16 @@ def require_hip(t):
 
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", wgrad_target_blocks=512):
+                 normalize_attn=True, device="cuda", wgrad_target_blocks=512, precision=None):
         if n_embd != D_MODEL:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
         if n_token > 96:
             raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
         if num_class != 10 or vocab > 16:
             raise ValueError("the HIP readout is built for num_class == 10 and a vocabulary <= 16")
+        self.precision = default_precision() if precision is None else precision
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}")
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -116,6 +132,10 @@ class EncoderPlan:
         self.part_bout = e(N)
         self.part_tok = e(N * vocab * D_MODEL)
         self.d_emb = e(N, num_class)
+        self.pack = None
+        if self.precision == "x3":
+            npk = int(_native.GHM_SPLIT_PACK_ELEMS)
+            self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
         self._gen = 0
 
     def probs_dense(self, l):
@@ -130,9 +150,23 @@ class EncoderPlan:
         s = _stream()
         c = _native.call
         M, T, N, L = self.M, self.T, self.N, self.L
+        x3 = self.precision == "x3"
+        if x3:
+            self.split_weights(p, s)
         c("ghm_embed_fwd", _ptr(tok), _ptr(p["token_embeddings.weight"]),
           _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), N, T, self.V, D_MODEL, s)
         for l in range(L):
+            if x3:
+                pk = _ptr(self.pack[l])
+                c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+                  pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
+                c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                  N, T, D_MODEL, self.scale_div, s)
+                c("ghm_ln_mlp_fwd_x3", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                  _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
+                  _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL,
+                  D_HIDDEN, self.eps, s)
+                continue
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
@@ -146,6 +180,23 @@ class EncoderPlan:
           _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, s)
         self._gen += 1
         return self.emb
+
+    def split_weights(self, p, s=None):
+        """Write every layer's pre-split bf16 weight pack (precision "x3")."""
+        s = _stream() if s is None else s
+        jobs = []
+        for l in range(self.L):
+            j = _native.SplitJob()
+            j.Wq = p[f"_queries.{l}.weight"].data_ptr()
+            j.Wk = p[f"_keys.{l}.weight"].data_ptr()
+            j.Wv = p[f"_values.{l}.weight"].data_ptr()
+            j.W1 = p[f"_mlps.{l}.0.weight"].data_ptr()
+            j.W2 = p[f"_mlps.{l}.2.weight"].data_ptr()
+            j.pack = self.pack[l].data_ptr()
+            jobs.append(j)
+        for a in range(0, len(jobs), 16):
+            chunk = jobs[a:a + 16]
+            _native.call("ghm_split_weights", (_native.SplitJob * len(chunk))(*chunk), len(chunk), s)
 
     # ------------------------------------------------------------------
     @staticmethod
@@ -193,11 +244,17 @@ class EncoderPlan:
           _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, s)
         jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
                  J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
+        x3 = self.precision == "x3"
         for l in reversed(range(L)):
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
-            c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-              _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
-              _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
+            if x3:
+                c("ghm_mlp_bwd_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                  _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL,
+                  D_HIDDEN, s)
+            else:
+                c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                  _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
+                  _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
             jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
             c("ghm_wgrad", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G[l]), D_HIDDEN, D_HIDDEN, 0,
@@ -217,9 +274,14 @@ class EncoderPlan:
               _ptr(self.part_wq), None, M, tps, s)
             jobs.append(J(self.part_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
                                              g[f"_values.{l}.weight"]]))
-            c("ghm_qkv_bwd", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-              _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
-              _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, s)
+            if x3:
+                c("ghm_qkv_bwd_x3", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]),
+                  _ptr(p[f"_lns_1.{l}.weight"]), _ptr(self.pack[l]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M,
+                  D_MODEL, s)
+            else:
+                c("ghm_qkv_bwd", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+                  _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
+                  _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, s)
             jobs.append(J(self.part_ln, self.nblk, [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]]))
             self._flush(jobs, s)  # every partial buffer is reused by the next layer
             cur, nxt = nxt, cur  # cur = dH_l

@@ -116,14 +116,18 @@ class EncoderTransformer(nn.Module):
         self._out = nn.Linear(n_token, 1)
         self._names = param_names(n_layer)
         self._plans = {}
+        # matrix-product mode of the HIP kernels: None -> $GHM_PRECISION or "f32";
+        # "f32" exact-f32 MFMA, "x3" split-bf16 MFMA (hip_encoder.py)
+        self.precision = None
 
     def _plan(self, n_seq, T, device):
-        key = (n_seq, T, str(device))
+        key = (n_seq, T, str(device), self.precision)
         if key not in self._plans:
             self._plans.clear()  # keep one workspace set alive per module
             self._plans[key] = EncoderPlan(self.n_layer, T, n_seq, num_class=self.vocab_size,
                                            vocab=self.vocab_size, n_embd=self.n_embd,
-                                           normalize_attn=self.normalize_attn, device=device)
+                                           normalize_attn=self.normalize_attn, device=device,
+                                           precision=self.precision)
         return self._plans[key]
 
     def forward(self, x):

@@ -32,9 +32,12 @@ def _p(t):
 
 class ClipTrainer:
     def __init__(self, tmodel, imodel, K, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
-                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None):
+                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
+                 precision=None):
         """lr_schedule: sequence of python-float learning rates, one per step
-        (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1))."""
+        (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
+        precision: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA); None ->
+        $GHM_PRECISION or "f32"."""
         self.device = torch.device(device)
         self.tm, self.im = tmodel, imodel
         self.K, self.B = K, batch_size
@@ -68,8 +71,10 @@ class ClipTrainer:
         T = tmodel.n_token
         n_seq = batch_size * (K + 1)
         self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
-                                  n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device)
+                                  n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
+                                  precision=precision)
                       for m in self.models]
+        self.precision = self.plans[0].precision
         self.T, self.n_seq = T, n_seq
         self.C = tmodel.vocab_size
         # optimizer constants and the per-step schedule table

@@ -7,6 +7,9 @@ throughout; reductions run in a different order than PyTorch-CPU BLAS):
   parameter gradients              : 1e-4 relative to the tensor's max-abs
   AdamW update                     : bit-exact
   loss curves                      : |delta| <= 1e-4 (BASELINE.json north_star)
+Split-bf16 ("x3") matrix products carry ~2^-16 relative error per product, so
+the per-tensor bounds of that mode are wider (FWD_TOL / GRAD_TOL below); the
+loss-curve bound is the same 1e-4 for both modes.
 """
 import os
 
@@ -20,6 +23,9 @@ from oracle import ghm_oracle as O
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
+PRECISIONS = ["f32", "x3"]
+FWD_TOL = {"f32": 2e-5, "x3": 1e-4}
+GRAD_TOL = {"f32": 1e-4, "x3": 5e-4}
 
 
 def _rel(a, b):
@@ -37,7 +43,7 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-def _pair(L=2, T=81, seed=7):
+def _pair(L=2, T=81, seed=7, precision="f32"):
     """Product encoder on the GPU + oracle encoder on the CPU with equal weights."""
     from ghmclip import EncoderTransformer
     torch.manual_seed(seed)
@@ -55,6 +61,7 @@ def _pair(L=2, T=81, seed=7):
                 d = 0.1 * torch.randn(vp.shape, generator=g)
                 vp.add_(d)
                 vr.add_(d)
+    prod.precision = precision
     return prod.to(DEV), ref
 
 
@@ -81,9 +88,11 @@ def _oracle_intermediates(ref, x):
     return out
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("T,nseq", [(81, 20), (81, 7), (27, 33), (9, 5)])
-def test_encoder_forward_stages(T, nseq):
-    prod, ref = _pair(L=2, T=T)
+def test_encoder_forward_stages(T, nseq, precision):
+    prod, ref = _pair(L=2, T=T, precision=precision)
+    tol = FWD_TOL[precision]
     g = torch.Generator().manual_seed(3)
     x = torch.randint(0, 10, (nseq, T), generator=g)
     emb, gl = prod(x.to(DEV))
@@ -93,20 +102,21 @@ def test_encoder_forward_stages(T, nseq):
     want = _oracle_intermediates(ref, x)
     M = nseq * T
     for l in range(2):
-        assert _rel(plan.H[l].view(nseq, T, 128), want["H"][l]) < 2e-5, f"H[{l}]"
-        assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < 2e-5, f"qkv[{l}]"
-        assert _rel(plan.probs_dense(l), want["P"][l]) < 2e-5, f"P[{l}]"
-        assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < 2e-5, f"Hmid[{l}]"
-        assert _rel(plan.G[l].view(nseq, T, 512), want["G"][l]) < 2e-5, f"G[{l}]"
-        assert _rel(plan.Dg[l].view(nseq, T, 512), want["Dg"][l]) < 2e-5, f"Dg[{l}]"
-    assert _rel(plan.H[2][:M].view(nseq, T, 128), want["H"][2]) < 2e-5, "H[L]"
+        assert _rel(plan.H[l].view(nseq, T, 128), want["H"][l]) < tol, f"H[{l}]"
+        assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < tol, f"qkv[{l}]"
+        assert _rel(plan.probs_dense(l), want["P"][l]) < tol, f"P[{l}]"
+        assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < tol, f"Hmid[{l}]"
+        assert _rel(plan.G[l].view(nseq, T, 512), want["G"][l]) < tol, f"G[{l}]"
+        assert _rel(plan.Dg[l].view(nseq, T, 512), want["Dg"][l]) < tol, f"Dg[{l}]"
+    assert _rel(plan.H[2][:M].view(nseq, T, 128), want["H"][2]) < tol, "H[L]"
     ref_emb = ref(x)[0]
-    assert _rel(emb, ref_emb) < 2e-5
+    assert _rel(emb, ref_emb) < tol
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("T,nseq", [(81, 20), (81, 7), (27, 33)])
-def test_encoder_backward(T, nseq):
-    prod, ref = _pair(L=2, T=T)
+def test_encoder_backward(T, nseq, precision):
+    prod, ref = _pair(L=2, T=T, precision=precision)
     g = torch.Generator().manual_seed(5)
     x = torch.randint(0, 10, (nseq, T), generator=g)
     R = torch.randn(nseq, 10, generator=g)
@@ -115,7 +125,7 @@ def test_encoder_backward(T, nseq):
     (ref(x)[0] * R).sum().backward()
     torch.cuda.synchronize()
     for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
-        assert _rel(pp.grad, pr.grad) < 1e-4, k
+        assert _rel(pp.grad, pr.grad) < GRAD_TOL[precision], k
 
 
 def test_clip_loss_and_grad():
@@ -180,7 +190,7 @@ def test_adamw_bit_exact():
         assert ulp.max() <= 2, ulp.max()
 
 
-def _trainer(L, B, p, total_iters=3000, graph=False):
+def _trainer(L, B, p, total_iters=3000, precision="f32"):
     from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
     from ghmclip.training.clip_trainer import ClipTrainer
     p_y = np.ones(10) / 10
@@ -189,7 +199,7 @@ def _trainer(L, B, p, total_iters=3000, graph=False):
     tm = EncoderTransformer(81, 10, 128, L).to(DEV)
     im = EncoderTransformer(81, 10, 128, L).to(DEV)
     sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, total_iters) for s in range(total_iters + 1)]
-    tr = ClipTrainer(tm, im, 4, B, sched, device=DEV)
+    tr = ClipTrainer(tm, im, 4, B, sched, device=DEV, precision=precision)
     return sampler, tr
 
 
@@ -204,11 +214,12 @@ def _run(sampler, tr, B, steps, graph_after=None):
     return tr.loss_history()
 
 
-def test_train_steps_vs_reference_fixture():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_train_steps_vs_reference_fixture(precision):
     """Two full steps of the d=128, L=2, B=8 config against the reference's own
     numbers (tests/golden/clip_d128.npz)."""
     gfx = np.load(os.path.join(GOLDEN, "clip_d128.npz"))
-    sampler, tr = _trainer(2, 8, 0.2)
+    sampler, tr = _trainer(2, 8, 0.2, precision=precision)
     hist = _run(sampler, tr, 8, 2)
     for it in range(2):
         assert abs(hist[it] - float(gfx[f"s{it}.loss"])) < 1e-5
@@ -222,25 +233,27 @@ def test_train_steps_vs_reference_fixture():
                 assert abs(got - ck[1]) <= 1e-5 * ck[1] + 1e-9, k
 
 
-def test_graph_replay_matches_eager():
-    s1, t1 = _trainer(1, 4, 0.2)
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_graph_replay_matches_eager(precision):
+    s1, t1 = _trainer(1, 4, 0.2, precision=precision)
     h1 = _run(s1, t1, 4, 6)
-    s2, t2 = _trainer(1, 4, 0.2)
+    s2, t2 = _trainer(1, 4, 0.2, precision=precision)
     h2 = _run(s2, t2, 4, 6, graph_after=2)
     np.testing.assert_array_equal(h1, h2)
     for a, b in zip(t1.tm.parameters(), t2.tm.parameters()):
         assert torch.equal(a, b)
 
 
-def test_default_config_curve_vs_reference():
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_default_config_curve_vs_reference(precision):
     """North-star parity: the default CLIP config (p=0.2, L=5, d=128, B=128)
     loss_history vs the reference PyTorch-CPU run on identical GHM draws."""
     path = os.path.join(GOLDEN, "clip_default_curve.npz")
     g = np.load(path)
     ref = g["loss_history"]
     n = len(ref)
-    sampler, tr = _trainer(5, 128, 0.2)
+    sampler, tr = _trainer(5, 128, 0.2, precision=precision)
     hist = _run(sampler, tr, 128, n, graph_after=3)
     dev = np.abs(hist - ref)
-    print(f"default-config curve: {n} steps, max |dloss| = {dev.max():.3e}, final {hist[-1]:.6f} vs {ref[-1]:.6f}")
+    print(f"default-config curve [{precision}]: {n} steps, max |dloss| = {dev.max():.3e}, final {hist[-1]:.6f} vs {ref[-1]:.6f}")
     assert dev.max() <= 1e-4

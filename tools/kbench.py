@@ -49,6 +49,8 @@ def main():
     tps_w1, ns_w1 = plan.wg["w1"]
     tps_q, ns_q = plan.wg["qkv"]
     gf = lambda flop: flop / 1e9  # noqa: E731
+    xo = {"H": torch.empty_like(plan.H[l + 1]), "G": torch.empty_like(plan.G[l]), "Dg": torch.empty_like(plan.Dg[l]),
+          "st": torch.empty_like(plan.st2[l])}
     kernels = {
         "ln_qkv_fwd": (lambda: c("ghm_ln_qkv_fwd", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                  P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
@@ -59,6 +61,10 @@ def main():
                                  P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
                                  P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
                                  plan.eps, sp), gf(4 * M * 128 * 512)),
+        "ln_mlp_fwd_x3": (lambda: c("ghm_ln_mlp_fwd_x3", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+                                    P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
+                                    P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["G"]), P(xo["Dg"]), P(xo["st"]), M, 128, 512,
+                                    plan.eps, sp), gf(4 * M * 128 * 512)),
         "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]),
                               P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.Dg[l]), P(plan.dU),
                               P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
@@ -102,6 +108,16 @@ def main():
         res[name] = {"us": round(us, 2), "gflop": gflop, "mfma_frac": round(frac, 4) if frac else None}
         print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
               flush=True)
+    if "ln_mlp_fwd_x3" in res:  # split-bf16 vs exact-f32 MLP forward on the same inputs
+        c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+          P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
+          P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
+          plan.eps, sp)
+        torch.cuda.synchronize()
+        for k, ref in (("H", plan.H[l + 1]), ("G", plan.G[l]), ("Dg", plan.Dg[l])):
+            d = (xo[k] - ref).abs().max().item() / ref.abs().max().item()
+            print(f"x3 vs f32 {k}: max rel-to-maxabs diff {d:.3e}", flush=True)
+            res["ln_mlp_fwd_x3"]["diff_" + k] = d
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
