@@ -28,6 +28,10 @@ sys.path.insert(0, os.path.join(ROOT, "multimodal-ghm_amd"))
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 STEP_GFLOP = 625.87            # algorithmic work per step at B=128
 MLP_FWD_GFLOP_PER_LAUNCH = 4 * 51840 * 128 * 512 / 1e9  # one encoder-layer MLP: 2 GEMMs
+# algorithmic HBM bytes of one LN2+MLP forward launch (fp32): Hmid in + H out
+# ([M,128] each) + G and GELU'(U) out ([M,512] each), M = 51,840 tokens
+MLP_FWD_BYTES_PER_LAUNCH = 4 * 51840 * (128 + 128 + 512 + 512)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
 def log(*a):
@@ -73,22 +77,35 @@ def make_ring(sampler, B, R):
     return ring.cuda()
 
 
-def time_dominant_kernel(trainer, reps=20):
-    """Average duration of the dominant kernel (encoder-layer LN2+MLP forward,
-    k_ln_mlp_fwd) launched on the current stream, bracketed by HIP events."""
+def dominant_kernel(trainer):
+    """(name, launch) of the step's dominant kernel — the encoder-layer LN2+MLP
+    forward (k_ln_mlp_fwd / k_ln_mlp_fwd_x3) of layer 0 — launched on the
+    current stream with the trainer's own buffers."""
     from ghmclip import _native
     import ctypes
     plan = trainer.plans[0]
     pd = trainer.views[0][0]
-    s = torch.cuda.current_stream()
-    sp = ctypes.c_void_p(s.cuda_stream)
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    if plan.precision == "x3":
+        def launch():
+            _native.call("ghm_ln_mlp_fwd_x3", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
+                         ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]),
+                         ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
+        return "k_ln_mlp_fwd_x3", launch
 
     def launch():
         _native.call("ghm_ln_mlp_fwd", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                      ptr(pd["_mlps.0.0.weight"]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.weight"]),
                      ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]),
                      plan.M, 128, 512, plan.eps, sp)
+    return "k_ln_mlp_fwd", launch
+
+
+def time_kernel(launch, reps=20):
+    """Average duration (ms) of `launch` on the current stream, bracketed by HIP
+    events recorded on that same stream."""
+    s = torch.cuda.current_stream()
     launch()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -96,10 +113,22 @@ def time_dominant_kernel(trainer, reps=20):
         launch()
     e1.record(s)
     e1.synchronize()
-    return e0.elapsed_time(e1) / reps  # ms
+    return e0.elapsed_time(e1) / reps
 
 
-def cpu_baseline(B, L, steps=3):
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE, tools/traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    k = t.get("kernels", {}).get(kernel)
+    return None if k is None else k["hbm_bytes"]
+
+
+def cpu_baseline(B, L, steps=8):
     from oracle import ghm_oracle as O
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
@@ -163,7 +192,8 @@ def main():
 
     losses = tr.loss_history()
     finite = bool(np.isfinite(losses).all())
-    kern_ms = time_dominant_kernel(tr)
+    kname, klaunch = dominant_kernel(tr)
+    kern_ms = time_kernel(klaunch)
     if rank != 0:
         if ws > 1:
             dist.destroy_process_group()
@@ -173,7 +203,25 @@ def main():
     steps_per_s = a.steps / elapsed
     samples = a.batch * ws * a.steps
     step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
-    achieved = MLP_FWD_GFLOP_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e3
+    if tr.precision == "x3":
+        # split-bf16 products run at 5.3x the exact-f32 rate: the kernel's roof is
+        # HBM (algorithmic bytes: Hmid in, H out, G and GELU' out, fp32)
+        traffic = pmc_traffic(kname)
+        achieved = MLP_FWD_BYTES_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None if traffic is None else round(traffic * (a.batch / 128)),
+                    "algorithmic_bytes": round(MLP_FWD_BYTES_PER_LAUNCH * (a.batch / 128)),
+                    "kernel_ms": round(kern_ms, 4)}
+    else:
+        traffic = pmc_traffic(kname)
+        achieved = MLP_FWD_GFLOP_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e3
+        roofline = {"bound": "mfma", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
+                    "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": None if traffic is None else round(traffic * (a.batch / 128)),
+                    "kernel_ms": round(kern_ms, 4)}
     out = {
         "metric": "GHM training samples/sec (CLIP default config)",
         "value": round(samples / elapsed, 2),
@@ -191,10 +239,7 @@ def main():
                    "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,
                    "global_batch_rows": a.batch * ws, "n_layer": a.layers, "parallelism": f"dp{ws}",
                    "hip_graph": not a.no_graph},
-        "roofline": {"bound": "mfma", "kernel": "k_ln_mlp_fwd (LN2+MLP fwd, one encoder-layer)",
-                     "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel_ms": round(kern_ms, 4)},
+        "roofline": roofline,
         "steps_per_s": round(steps_per_s, 3),
         "sequences_per_s": round(samples * 10 / elapsed, 1),
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),

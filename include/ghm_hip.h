@@ -176,6 +176,11 @@ int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, 
 int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
                    const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, void* stream);
 
+/* As ghm_wgrad (b_mode 0 plain or 2 layernorm). */
+int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
+                 const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,
+                 int tok_per_split, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

@@ -443,6 +443,129 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 }
 
 // ---------------------------------------------------------------------------
+// Split-K weight gradient, split-bf16                 (nn.Linear weight/bias grads)
+//   part[z][a][b] = sum_{m in chunk z} A[m][a] op(B)[m][b],  op = id | LayerNorm
+// Tokens are the MFMA k dimension.  Per 32-token step each thread loads ONE
+// column of A and of op(B) for 16 tokens (dword loads, coalesced across the
+// wave), splits them and writes [column][token] bf16 images (64-B rows, 16-B
+// chunks XOR-swizzled by row so the operand reads are conflict-free), so a
+// lane's 8-token operand fragment is one ds_read_b128.  Workgroup = 128 x 128
+// output tile, 4 waves as 2 x 2 of 64 x 64.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (ch ^ ((row >> 2) & 3)); }
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A, int lda,
+                                                     const float* __restrict__ Bs, int ldb,
+                                                     const float2* __restrict__ stats,
+                                                     const float* __restrict__ lnw,
+                                                     const float* __restrict__ lnb,
+                                                     float* __restrict__ part,
+                                                     float* __restrict__ bias_part, int64_t M,
+                                                     int tok_per_split, int Acols, int Bcols) {
+  constexpr int KT = 32, IMG = 128 * 32;
+  __shared__ __attribute__((aligned(16))) __bf16 sAh[2][IMG];
+  __shared__ __attribute__((aligned(16))) __bf16 sAl[2][IMG];
+  __shared__ __attribute__((aligned(16))) __bf16 sBh[2][IMG];
+  __shared__ __attribute__((aligned(16))) __bf16 sBl[2][IMG];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+  const int a_blk = blockIdx.x * 128, b_blk = blockIdx.y * 128;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * tok_per_split;
+  int64_t m_end = m_begin + tok_per_split;
+  if (m_end > M) m_end = M;
+  const int nsteps = static_cast<int>((m_end - m_begin + KT - 1) / KT);
+  // staging role: column c of the tile, tokens 16*th .. 16*th + 15 of the step
+  const int c = threadIdx.x & 127, th = threadIdx.x >> 7;
+  float gam = 1.f, bet = 0.f;
+  if (MODE == 2) {
+    gam = lnw[b_blk + c];
+    bet = lnb[b_blk + c];
+  }
+  float va[16], vb[16];
+  float bsum = 0.f;
+  auto load = [&](int step) {
+    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t mt = mb + i;
+      const bool ok = mt < m_end;
+      const int64_t mcl = ok ? mt : m_begin;
+      const float a = A[mcl * lda + a_blk + c];
+      float b = Bs[mcl * ldb + b_blk + c];
+      if (MODE == 2) {
+        const float2 sv = stats[mcl];
+        b = (b - sv.x) * sv.y * gam + bet;
+      }
+      va[i] = ok ? a : 0.f;
+      vb[i] = b;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 ah, al, bh, bl;
+      split8(va + 8 * half, ah, al);
+      split8(vb + 8 * half, bh, bl);
+      const int off = wg_img(c, 2 * th + half);
+      *reinterpret_cast<bf16x8*>(sAh[buf] + off) = ah;
+      *reinterpret_cast<bf16x8*>(sAl[buf] + off) = al;
+      *reinterpret_cast<bf16x8*>(sBh[buf] + off) = bh;
+      *reinterpret_cast<bf16x8*>(sBl[buf] + off) = bl;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bsum += va[i];
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) acc[i][k] = zero16();
+  load(0);
+  store(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nsteps) load(st + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int oa = wg_img(wa + 32 * i + j, 2 * s + h), ob = wg_img(wb + 32 * i + j, 2 * s + h);
+        ah[i] = ldsb8(sAh[cur] + oa);
+        al[i] = ldsb8(sAl[cur] + oa);
+        bh[i] = ldsb8(sBh[cur] + ob);
+        bl[i] = ldsb8(sBl[cur] + ob);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) acc[i][k] = mfma_x3(ah[i], al[i], bh[k], bl[k], acc[i][k]);
+    }
+    if (st + 1 < nsteps) store(cur ^ 1);
+    __syncthreads();
+  }
+  float* pz = part + static_cast<int64_t>(blockIdx.z) * Acols * Bcols;
+  const int a_base = a_blk + wa, b_base = b_blk + wb;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t ra = a_base + acc_row(r, h);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) pz[(ra + 32 * i) * Bcols + b_base + 32 * k + j] = acc[i][k][r];
+  }
+  if (bias_part && blockIdx.y == 0) {
+    float* red = reinterpret_cast<float*>(&sAh[0][0]);  // the ring is idle after the last barrier
+    red[th * 128 + c] = bsum;
+    __syncthreads();
+    if (th == 0) bias_part[static_cast<int64_t>(blockIdx.z) * Acols + a_blk + c] = red[c] + red[128 + c];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C-ABI launchers
 // ---------------------------------------------------------------------------
 extern "C" int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream) {
@@ -500,5 +623,28 @@ extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* st
   hipLaunchKernelGGL(k_qkv_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), dqkv, H, reinterpret_cast<const float2*>(stats), ln_w,
                      reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln, M);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
+                            const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part,
+                            int64_t M, int tok_per_split, void* stream) {
+  GHM_CHECK(A && B && part, "null pointer");
+  GHM_CHECK(A_cols > 0 && B_cols > 0 && A_cols % 128 == 0 && B_cols % 128 == 0, "A_cols/B_cols % 128");
+  GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
+  GHM_CHECK(tok_per_split > 0 && tok_per_split % 32 == 0, "tok_per_split must be a positive multiple of 32");
+  GHM_CHECK(b_mode == 0 || b_mode == 2, "b_mode (split path: 0 plain, 2 layernorm)");
+  GHM_CHECK(b_mode != 2 || (stats && ln_w && ln_b), "layernorm mode needs stats/ln_w/ln_b");
+  const int64_t nsplit = (M + tok_per_split - 1) / tok_per_split;
+  GHM_CHECK(nsplit <= 65535, "too many splits");
+  dim3 grid(A_cols / 128, B_cols / 128, static_cast<unsigned>(nsplit));
+  hipStream_t s = ghm_stream(stream);
+  const float2* st = reinterpret_cast<const float2*>(stats);
+  if (b_mode == 0)
+    hipLaunchKernelGGL(k_wgrad_x3<0>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                       tok_per_split, A_cols, B_cols);
+  else
+    hipLaunchKernelGGL(k_wgrad_x3<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                       tok_per_split, A_cols, B_cols);
   return ghm_launch_status();
 }

@@ -245,6 +245,7 @@ class EncoderPlan:
         jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
                  J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
         x3 = self.precision == "x3"
+        wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
         for l in reversed(range(L)):
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
             if x3:
@@ -257,11 +258,11 @@ class EncoderPlan:
                   _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
             jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
-            c("ghm_wgrad", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G[l]), D_HIDDEN, D_HIDDEN, 0,
+            c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G[l]), D_HIDDEN, D_HIDDEN, 0,
               None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)
             jobs += [J(self.part_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(self.part_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU
-            c("ghm_wgrad", _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
+            c(wgrad, _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
             jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
@@ -269,7 +270,7 @@ class EncoderPlan:
             c("ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
               D_MODEL, self.scale_div, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
-            c("ghm_wgrad", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
+            c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(self.part_wq), None, M, tps, s)
             jobs.append(J(self.part_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],

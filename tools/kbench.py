@@ -28,10 +28,12 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--precision", default="x3", choices=["f32", "x3"],
+                    help="trainer precision; x3 also enables the *_x3 kernel entries")
     a = ap.parse_args()
     import bench
     from ghmclip import _native
-    sampler, tr = bench.build(0, 128, 5, 0.2, 3000)
+    sampler, tr = bench.build(0, 128, 5, 0.2, 3000, a.precision)
     ring = bench.make_ring(sampler, 128, 2)
     for k in range(2):
         tr.set_tokens(ring[k, 0], ring[k, 1])
@@ -49,8 +51,6 @@ def main():
     tps_w1, ns_w1 = plan.wg["w1"]
     tps_q, ns_q = plan.wg["qkv"]
     gf = lambda flop: flop / 1e9  # noqa: E731
-    xo = {"H": torch.empty_like(plan.H[l + 1]), "G": torch.empty_like(plan.G[l]), "Dg": torch.empty_like(plan.Dg[l]),
-          "st": torch.empty_like(plan.st2[l])}
     kernels = {
         "ln_qkv_fwd": (lambda: c("ghm_ln_qkv_fwd", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                  P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
@@ -61,27 +61,23 @@ def main():
                                  P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
                                  P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
                                  plan.eps, sp), gf(4 * M * 128 * 512)),
-        "ln_mlp_fwd_x3": (lambda: c("ghm_ln_mlp_fwd_x3", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
-                                    P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
-                                    P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["G"]), P(xo["Dg"]), P(xo["st"]), M, 128, 512,
-                                    plan.eps, sp), gf(4 * M * 128 * 512)),
         "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]),
                               P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.Dg[l]), P(plan.dU),
                               P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
         "wgrad_w2": (lambda: c("ghm_wgrad", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None, None, None,
-                               P(plan.part_w), P(plan.part_b), M, tps_w2, sp), gf(2 * M * 128 * 512)),
+                               P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp), gf(2 * M * 128 * 512)),
         "wgrad_w1": (lambda: c("ghm_wgrad", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2, P(plan.st2[l]),
-                               P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w), P(plan.part_b), M,
+                               P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w1), P(plan.part_b1), M,
                                tps_w1, sp), gf(2 * M * 128 * 512)),
         "attn_bwd": (lambda: c("ghm_attn_bwd", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS), P(plan.dqkv),
                                N, T, 128, plan.scale_div, sp), gf(8 * N * T * T * 128)),
         "wgrad_qkv": (lambda: c("ghm_wgrad", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2, P(plan.st1[l]),
-                                P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]), P(plan.part_w), None, M, tps_q, sp),
+                                P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]), P(plan.part_wq), None, M, tps_q, sp),
                       gf(2 * M * 128 * 384)),
         "qkv_bwd": (lambda: c("ghm_qkv_bwd", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]),
                               P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
                               P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, sp), gf(2 * M * 128 * 384)),
-        "reduce_w2": (lambda: plan._reduce(plan.part_w, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
+        "reduce_w2": (lambda: plan._reduce(plan.part_w2, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
         "reduce_ln": (lambda: plan._reduce(plan.part_ln, plan.nblk, 256, [g["_lns_1.0.weight"], g["_lns_1.0.bias"]], sp),
                       None),
         "readout_bwd": (lambda: c("ghm_readout_bwd", P(plan.H[5]), P(p["_read_out.weight"]), P(p["_read_out.bias"]),
@@ -90,6 +86,31 @@ def main():
         "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
                       None),
     }
+    if plan.pack is not None:
+        pk = P(plan.pack[l])
+        kernels.update({
+            "ln_qkv_fwd_x3": (lambda: c("ghm_ln_qkv_fwd_x3", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
+                                        pk, P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
+            "ln_mlp_fwd_x3": (lambda: c("ghm_ln_mlp_fwd_x3", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                        P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
+                                        P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
+                                        plan.eps, sp), gf(4 * M * 128 * 512)),
+            "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
+                                     P(p["_lns_2.0.weight"]), pk, P(plan.Dg[l]), P(plan.dU), P(plan.dH[1]),
+                                     P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
+            "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]),
+                                     P(p["_lns_1.0.weight"]), pk, P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M,
+                                     128, sp), gf(2 * M * 128 * 384)),
+            "wgrad_w2_x3": (lambda: c("ghm_wgrad_x3", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None,
+                                      None, None, P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp),
+                            gf(2 * M * 128 * 512)),
+            "wgrad_w1_x3": (lambda: c("ghm_wgrad_x3", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2,
+                                      P(plan.st2[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+                                      P(plan.part_w1), P(plan.part_b1), M, tps_w1, sp), gf(2 * M * 128 * 512)),
+            "wgrad_qkv_x3": (lambda: c("ghm_wgrad_x3", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2,
+                                       P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
+                                       P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
+        })
     only = set(a.only.split(",")) if a.only else None
     res = {}
     for name, (fn, gflop) in kernels.items():
@@ -108,16 +129,6 @@ def main():
         res[name] = {"us": round(us, 2), "gflop": gflop, "mfma_frac": round(frac, 4) if frac else None}
         print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
               flush=True)
-    if "ln_mlp_fwd_x3" in res:  # split-bf16 vs exact-f32 MLP forward on the same inputs
-        c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
-          P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
-          P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
-          plan.eps, sp)
-        torch.cuda.synchronize()
-        for k, ref in (("H", plan.H[l + 1]), ("G", plan.G[l]), ("Dg", plan.Dg[l])):
-            d = (xo[k] - ref).abs().max().item() / ref.abs().max().item()
-            print(f"x3 vs f32 {k}: max rel-to-maxabs diff {d:.3e}", flush=True)
-            res["ln_mlp_fwd_x3"]["diff_" + k] = d
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

@@ -9,8 +9,18 @@ it is doubled here; WRITE_SIZE is exact for 16-B-per-lane stores.
 import csv
 import glob
 import json
+import re
 import sys
 from collections import defaultdict
+
+
+def kname(raw):
+    """Plain kernel name: 'void k_x<3>(...)' -> 'k_x<3>', '_Z15k_ln_mlp_fwd_x3PKf...' -> 'k_ln_mlp_fwd_x3'."""
+    m = re.match(r"_Z(\d+)(\w+)", raw)
+    if m:
+        return m.group(2)[:int(m.group(1))]
+    name = raw.split("(")[0]
+    return name[5:] if name.startswith("void ") else name
 
 
 def load(d, counter):
@@ -18,7 +28,7 @@ def load(d, counter):
     acc = defaultdict(list)
     for r in csv.DictReader(open(f[0])):
         if r["Counter_Name"] == counter:
-            acc[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)
+            acc[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
@@ -32,7 +42,10 @@ def main():
         out[k] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr}
         print(f"{k[:40]:40s} read {rd/1e6:9.2f} MB  write {wr/1e6:9.2f} MB  total {(rd+wr)/1e6:9.2f} MB")
     if "--json" in sys.argv:
-        json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+        doc = {"source": f"rocprofv3 --pmc FETCH_SIZE ({sys.argv[1]}) and --pmc WRITE_SIZE ({sys.argv[2]}) "
+                         "over tools/kbench.py; bytes per dispatch, FETCH_SIZE doubled (gfx950 correction)",
+               "kernels": out}
+        json.dump(doc, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
 
 if __name__ == "__main__":
