@@ -176,6 +176,12 @@ int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, 
 int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
                    const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, void* stream);
 
+/* As ghm_attn_fwd / ghm_attn_bwd (model.py:778-782 and its backward); P and dS
+ * are stored fp32 in the same dense padded layout. */
+int ghm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T, int D,
+                    float scale_div, void* stream);
+int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
+                    int T, int D, float scale_div, void* stream);
 /* As ghm_wgrad (b_mode 0 plain or 2 layernorm). */
 int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
                  const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,

@@ -566,6 +566,344 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
 }
 
 // ---------------------------------------------------------------------------
+// Attention, split-bf16                                         (model.py:778-782)
+// Same decomposition as the f32 kernels (workgroup = sequence; forward and the
+// dQ kernel: wave = query block with the query on the lane; dK/dV kernel: wave
+// = key block with the key on the lane).  Operands that are read along the
+// feature axis use [row][h][32] half images read with ds_read_b128; operands
+// that are read along the token axis (V^T, K^T, dO^T, Q^T) use [token][32]
+// column-block images read with ds_read_b64_tr_b16, the hardware transpose:
+// one 8-token fragment = two transposed reads of 4 rows.
+// ---------------------------------------------------------------------------
+constexpr int AT_PAD = 96;         // padded sequence length of the P / dS layouts
+constexpr int AH_PITCH = 64 + 8;   // [row][h][32] half image row (bf16): 144 B, b128 reads conflict-free
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 ldtr(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+}
+// 8-row transposed fragment from a [row][32] image (pitch 32 bf16 = 64 B: the
+// 2 x 4 rows x 32 B a 32-lane half reads fall on 64 distinct banks).  Lane l of
+// group g = l >> 4 receives column 16(g & 1) + (l & 15) of rows r0, r0 + 1,
+// r0 + 2, r0 + 3 (first read) and rows r1 .. r1 + 3 (second read).
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int r0, int r1, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = 16 * (g & 1) + 4 * p;
+  const bf16x4 a = ldtr(img + (r0 + q) * 32 + col);
+  const bf16x4 b = ldtr(img + (r1 + q) * 32 + col);
+  bf16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return v;
+}
+
+// stage the feature half c of a [T][384]-strided operand (columns col0 + 64hh +
+// 32c + 0..31, hh = 0,1) as a split [row][hh][32] image; rows >= T clamp
+template <int NKT>
+__device__ __forceinline__ void stage_half_x3(const float* __restrict__ seq, int T, int c, int col0,
+                                              __bf16* ih, __bf16* il) {
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * (3 * GHM_D) + col0 + 64 * hh +
+                                            32 * c + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    bf16x4 a, b;
+    split4(v[k], a, b);
+    stb4(ih + row * AH_PITCH + 32 * hh + 4 * q4, a);
+    stb4(il + row * AH_PITCH + 32 * hh + 4 * q4, b);
+  }
+}
+
+// stage columns col .. col+31 of rows 0..TP-1 (row pitch ld floats) as a split
+// [row][32] image for transposed reads; rows >= T clamp
+template <int NKT>
+__device__ __forceinline__ void stage_cols_x3(const float* __restrict__ base, int ld, int T, int col,
+                                              __bf16* ih, __bf16* il) {
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 3, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(base + static_cast<int64_t>(rc) * ld + col + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    bf16x4 a, b;
+    split4(v[k], a, b);
+    stb4(ih + idx * 4, a);  // row * 32 + 4 * q4 == 4 * idx
+    stb4(il + idx * 4, b);
+  }
+}
+
+// S^T tiles (keys on rows, this wave's queries on lanes) += X_half . Y^T where
+// X rows come from a [row][h][32] half image (feature half c) and Y is the
+// lane's row-layout token split into 8 k-steps (k-steps 4c .. 4c+3 used)
+template <int NKT>
+__device__ __forceinline__ void rows_dot_half(const __bf16* ih, const __bf16* il, const bf16x8* yh,
+                                              const bf16x8* yl, int c, int j, int h, f32x16* acc) {
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int off = (32 * kt + j) * AH_PITCH + 32 * h;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+      acc[kt] = mfma_x3(ldsb8(ih + off + 8 * tt), ldsb8(il + off + 8 * tt), yh[4 * c + tt], yl[4 * c + tt], acc[kt]);
+  }
+}
+
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __restrict__ qkv,
+                                                             const float* __restrict__ H,
+                                                             float* __restrict__ Hmid,
+                                                             float* __restrict__ P, int T,
+                                                             float scale_div) {
+  constexpr int TP = NKT * 32;
+  __shared__ __attribute__((aligned(16))) __bf16 sh[TP * AH_PITCH];
+  __shared__ __attribute__((aligned(16))) __bf16 sl[TP * AH_PITCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * (3 * GHM_D);
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  bf16x8 qh[8], ql[8];
+  load_split64(seq + static_cast<int64_t>(qc) * (3 * GHM_D) + 64 * h, true, qh, ql);  // Q[q][64h + 8t + i]
+  f32x16 s[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    stage_half_x3<NKT>(seq, T, c, GHM_D, sh, sl);  // K
+    __syncthreads();
+    rows_dot_half<NKT>(sh, sl, qh, ql, c, j, h, s);
+    __syncthreads();
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * kt + acc_row(r, h);
+      const float v = key < T ? s[kt][r] / scale_div : -INFINITY;
+      s[kt][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  }
+  mx = fmaxf(mx, xhalf(mx));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kt][r] - mx);
+      s[kt][r] = e;
+      sum += e;
+    }
+  }
+  sum += xhalf(sum);
+  const float inv = qv ? 1.f / sum : 0.f;
+  float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
+  bf16x8 ph[2 * NKT], pl[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kt][r] *= inv;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(prow + 32 * kt + quad_off(qd, h), s[kt][4 * qd], s[kt][4 * qd + 1], s[kt][4 * qd + 2], s[kt][4 * qd + 3]);
+    float pv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pv[r] = s[kt][r];
+    split_acc(pv, 0, ph[2 * kt], pl[2 * kt]);
+    split_acc(pv, 1, ph[2 * kt + 1], pl[2 * kt + 1]);
+  }
+  // O^T[d][q] = sum_key V[key][d] P[q][key]: V column block [key][32] in LDS,
+  // A fragment of k-step (kt, s) = keys 32kt + 16s + 4h + 0..3 and + 8
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    stage_cols_x3<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D + 32 * dt, sh, sl);
+    __syncthreads();
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 32 * kt + 16 * ss + 4 * h;
+        acc = mfma_x3(tr_frag(sh, r0, r0 + 8, lane), tr_frag(sl, r0, r0 + 8, lane), ph[2 * kt + ss],
+                      pl[2 * kt + ss], acc);
+      }
+    }
+    __syncthreads();
+    if (qv) {
+      const int64_t row = (base + q) * GHM_D + 32 * dt;
+      float4 hv[4];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        st4(Hmid + row + quad_off(qd, h), hv[qd].x + acc[4 * qd], hv[qd].y + acc[4 * qd + 1],
+            hv[qd].z + acc[4 * qd + 2], hv[qd].w + acc[4 * qd + 3]);
+    }
+  }
+}
+
+// dP^T = V dO^T, dS = P (dP - rowsum(P dP)) / c (stored, dense/padded), dQ^T = K^T dS^T
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __restrict__ qkv,
+                                                               const float* __restrict__ P,
+                                                               const float* __restrict__ dHmid,
+                                                               float* __restrict__ dS_out,
+                                                               float* __restrict__ dqkv, int T,
+                                                               float scale_div) {
+  constexpr int TP = NKT * 32;
+  __shared__ __attribute__((aligned(16))) __bf16 sh[TP * AH_PITCH];
+  __shared__ __attribute__((aligned(16))) __bf16 sl[TP * AH_PITCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * (3 * GHM_D);
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  f32x16 dp[NKT];
+  {
+    bf16x8 oh[8], ol[8];
+    load_split64(dHmid + (base + qc) * GHM_D + 64 * h, true, oh, ol);  // dO[q][64h + 8t + i]
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) dp[kt] = zero16();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      stage_half_x3<NKT>(seq, T, c, 2 * GHM_D, sh, sl);  // V
+      __syncthreads();
+      rows_dot_half<NKT>(sh, sl, oh, ol, c, j, h, dp);
+      __syncthreads();
+    }
+  }
+  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
+  float delta = 0.f;
+  f32x16 p[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const float4 pv = *reinterpret_cast<const float4*>(prow + 32 * kt + quad_off(qd, h));
+      p[kt][4 * qd + 0] = qv ? pv.x : 0.f;
+      p[kt][4 * qd + 1] = qv ? pv.y : 0.f;
+      p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
+      p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+  }
+  delta += xhalf(delta);
+  float* srow = dS_out + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
+  bf16x8 dh[2 * NKT], dl[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    float dv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+    split_acc(dv, 0, dh[2 * kt], dl[2 * kt]);
+    split_acc(dv, 1, dh[2 * kt + 1], dl[2 * kt + 1]);
+  }
+  // dQ^T[d][q] = sum_key K[key][d] dS[q][key], K column block [key][32] in LDS
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    stage_cols_x3<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * dt, sh, sl);
+    __syncthreads();
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 32 * kt + 16 * ss + 4 * h;
+        acc = mfma_x3(tr_frag(sh, r0, r0 + 8, lane), tr_frag(sl, r0, r0 + 8, lane), dh[2 * kt + ss],
+                      dl[2 * kt + ss], acc);
+      }
+    }
+    __syncthreads();
+    if (qv) {
+      float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
+    }
+  }
+}
+
+// dV^T = dO^T P and dK^T = Q^T dS, summing over queries; wave = key block, the
+// key on the lane.  P / dS columns of the lane's key are read from HBM (rows >=
+// T are 0) and split once; dO^T / Q^T fragments come from [query][32] column
+// blocks through transposed reads.
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __restrict__ qkv,
+                                                                const float* __restrict__ P,
+                                                                const float* __restrict__ dS,
+                                                                const float* __restrict__ dHmid,
+                                                                float* __restrict__ dqkv, int T) {
+  constexpr int TP = NKT * 32, KS = TP / 16;  // k-steps over queries
+  __shared__ __attribute__((aligned(16))) __bf16 soh[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sol[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sqh[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sql[TP * 32];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const int key = 32 * w + j;
+  const bool kv = key < T;
+  // B fragments: P[16s + 8h + i][key] and dS[...][key], i = 0..7
+  const float* pc = P + static_cast<int64_t>(blockIdx.x) * AT_PAD * AT_PAD + key;
+  const float* sc = dS + static_cast<int64_t>(blockIdx.x) * AT_PAD * AT_PAD + key;
+  bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    float pv[8], sv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int qq = 16 * st + 8 * h + i;
+      pv[i] = pc[qq * AT_PAD];
+      sv[i] = sc[qq * AT_PAD];
+    }
+    split8(pv, pbh[st], pbl[st]);
+    split8(sv, sbh[st], sbl[st]);
+  }
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    stage_cols_x3<NKT>(dHmid + base * GHM_D, GHM_D, T, 32 * dt, soh, sol);
+    stage_cols_x3<NKT>(qkv + base * (3 * GHM_D), 3 * GHM_D, T, 32 * dt, sqh, sql);
+    __syncthreads();
+    f32x16 aV = zero16(), aK = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int r0 = 16 * st + 8 * h;
+      aV = mfma_x3(tr_frag(soh, r0, r0 + 4, lane), tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
+      aK = mfma_x3(tr_frag(sqh, r0, r0 + 4, lane), tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
+    }
+    __syncthreads();
+    if (kv) {
+      float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        st4(o + 2 * GHM_D + quad_off(qd, h), aV[4 * qd], aV[4 * qd + 1], aV[4 * qd + 2], aV[4 * qd + 3]);
+        st4(o + GHM_D + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C-ABI launchers
 // ---------------------------------------------------------------------------
 extern "C" int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream) {
@@ -646,5 +984,39 @@ extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B,
   else
     hipLaunchKernelGGL(k_wgrad_x3<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
                        tok_per_split, A_cols, B_cols);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
+                               int D, float scale_div, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  hipStream_t s = ghm_stream(stream);
+  if (T <= 32)
+    hipLaunchKernelGGL(k_attn_fwd_x3<1>, dim3(g), dim3(64), 0, s, qkv, H, H_mid, P, T, scale_div);
+  else if (T <= 64)
+    hipLaunchKernelGGL(k_attn_fwd_x3<2>, dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div);
+  else
+    hipLaunchKernelGGL(k_attn_fwd_x3<3>, dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
+                               int64_t n_seq, int T, int D, float scale_div, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  hipStream_t s = ghm_stream(stream);
+  if (T <= 32) {
+    hipLaunchKernelGGL(k_attn_bwd_q_x3<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv_x3<1>, dim3(g), dim3(64), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else if (T <= 64) {
+    hipLaunchKernelGGL(k_attn_bwd_q_x3<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv_x3<2>, dim3(g), dim3(128), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_q_x3<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
+    hipLaunchKernelGGL(k_attn_bwd_kv_x3<3>, dim3(g), dim3(192), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  }
   return ghm_launch_status();
 }

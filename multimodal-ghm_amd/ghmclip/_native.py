@@ -61,6 +61,8 @@ HIP_SIGNATURES = {
     "ghm_mlp_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_qkv_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_wgrad_x3": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
+    "ghm_attn_fwd_x3": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64}

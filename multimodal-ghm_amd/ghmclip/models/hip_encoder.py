@@ -160,7 +160,7 @@ class EncoderPlan:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
                   pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-                c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   N, T, D_MODEL, self.scale_div, s)
                 c("ghm_ln_mlp_fwd_x3", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
@@ -267,7 +267,7 @@ class EncoderPlan:
               _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
             jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            c("ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
+            c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
               D_MODEL, self.scale_div, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
             c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,

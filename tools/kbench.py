@@ -101,6 +101,10 @@ def main():
             "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]),
                                      P(p["_lns_1.0.weight"]), pk, P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M,
                                      128, sp), gf(2 * M * 128 * 384)),
+            "attn_fwd_x3": (lambda: c("ghm_attn_fwd_x3", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]),
+                                      N, T, 128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
+            "attn_bwd_x3": (lambda: c("ghm_attn_bwd_x3", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS),
+                                      P(plan.dqkv), N, T, 128, plan.scale_div, sp), gf(8 * N * T * T * 128)),
             "wgrad_w2_x3": (lambda: c("ghm_wgrad_x3", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None,
                                       None, None, P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp),
                             gf(2 * M * 128 * 512)),
