@@ -155,7 +155,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
-                    help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or f32)")
+                    help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)

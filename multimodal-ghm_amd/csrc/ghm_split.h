@@ -65,6 +65,11 @@ __device__ __forceinline__ void split_acc(const float* g, int s, bf16x8& hi, bf1
 // the 4-column groups 1 and 2 swap.
 __device__ __forceinline__ constexpr int perm16_group(int g4) { return g4 == 1 ? 2 : (g4 == 2 ? 1 : g4); }
 
+// Keep prefetch loads where they are written: without it the compiler sinks a
+// next-tile global load down to its first use (the LDS store after the compute),
+// which serialises its full latency into every loop iteration.
+__device__ __forceinline__ void issue_fence() { asm volatile("" ::: "memory"); }
+
 __device__ __forceinline__ bf16x8 ldsb8(const __bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void stb4(__bf16* p, bf16x4 v) { *reinterpret_cast<bf16x4*>(p) = v; }
 

@@ -482,26 +482,35 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
     gam = lnw[b_blk + c];
     bet = lnb[b_blk + c];
   }
+  // MODE 0: raw prefetch registers, the token mask applied in store(), so the
+  // loads stay in flight across the compute.  MODE 2: the LayerNorm transform
+  // is applied at load time (its per-token statistics would otherwise hold 32
+  // more registers across the compute, which measured slower).
   float va[16], vb[16];
+  int nvalid = 0;
   float bsum = 0.f;
   auto load = [&](int step) {
     const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;
+    const int64_t left = m_end - mb;
+    nvalid = left < 0 ? 0 : (left > 16 ? 16 : static_cast<int>(left));
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int64_t mt = mb + i;
-      const bool ok = mt < m_end;
-      const int64_t mcl = ok ? mt : m_begin;
-      const float a = A[mcl * lda + a_blk + c];
+      const int64_t mcl = mt < m_end ? mt : m_begin;
+      va[i] = A[mcl * lda + a_blk + c];
       float b = Bs[mcl * ldb + b_blk + c];
       if (MODE == 2) {
         const float2 sv = stats[mcl];
         b = (b - sv.x) * sv.y * gam + bet;
       }
-      va[i] = ok ? a : 0.f;
       vb[i] = b;
     }
+    if (MODE == 0) issue_fence();
   };
   auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i >= nvalid) va[i] = 0.f;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       bf16x8 ah, al, bh, bl;

@@ -56,8 +56,10 @@ PRECISIONS = ("f32", "x3")
 
 
 def default_precision():
-    """GHM_PRECISION env var: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA)."""
-    p = os.environ.get("GHM_PRECISION", "f32")
+    """GHM_PRECISION env var: "x3" (default: split-bf16 MFMA, fp32-accurate to
+    ~1e-5 relative per product, the reference's 200-step loss curve within
+    3e-6) or "f32" (exact-f32 MFMA, the curve within 5e-7)."""
+    p = os.environ.get("GHM_PRECISION", "x3")
     if p not in PRECISIONS:
         raise ValueError(f"GHM_PRECISION must be one of {PRECISIONS} (got {p!r})")
     return p

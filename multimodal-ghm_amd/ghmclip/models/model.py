@@ -116,7 +116,7 @@ class EncoderTransformer(nn.Module):
         self._out = nn.Linear(n_token, 1)
         self._names = param_names(n_layer)
         self._plans = {}
-        # matrix-product mode of the HIP kernels: None -> $GHM_PRECISION or "f32";
+        # matrix-product mode of the HIP kernels: None -> $GHM_PRECISION or "x3";
         # "f32" exact-f32 MFMA, "x3" split-bf16 MFMA (hip_encoder.py)
         self.precision = None
 

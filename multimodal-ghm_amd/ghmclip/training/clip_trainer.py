@@ -37,7 +37,7 @@ class ClipTrainer:
         """lr_schedule: sequence of python-float learning rates, one per step
         (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
         precision: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA); None ->
-        $GHM_PRECISION or "f32"."""
+        $GHM_PRECISION or "x3"."""
         self.device = torch.device(device)
         self.tm, self.im = tmodel, imodel
         self.K, self.B = K, batch_size
