@@ -51,16 +51,20 @@ def setup_dist(n_gpus):
     return ws, rank, local
 
 
-def build(rank, B, L, p, total_iters, precision=None):
+def build(rank, B, L, p, total_iters, precision=None, guide=False):
+    """Default CLIP config (exp_clip_standardTF.sh); guide=True: the guided config
+    (exp_clip_guidedTF.sh: BP guide targets on 4 layers, penalty 1e-3, lr 1e-3)."""
     from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
     from ghmclip.training.clip_trainer import ClipTrainer
     p_y = np.ones(10) / 10
     sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [p, p], K=4, seedtree=42)
     seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
-    tm = EncoderTransformer(81, 10, 128, L).cuda()
-    im = EncoderTransformer(81, 10, 128, L).cuda()
-    sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, total_iters) for s in range(total_iters + 1)]
-    trainer = ClipTrainer(tm, im, 4, B, sched, device="cuda", precision=precision)
+    tm = EncoderTransformer(81, 10, 128, L, n_guided_layer=4, guide=guide).cuda()
+    im = EncoderTransformer(81, 10, 128, L, n_guided_layer=4, guide=guide).cuda()
+    lr_max, lr_min = (1e-3, 1e-6) if guide else (3e-4, 3e-7)
+    sched = [get_lr_cosine_schedule(s, lr_max, lr_min, 0, total_iters) for s in range(total_iters + 1)]
+    trainer = ClipTrainer(tm, im, 4, B, sched, device="cuda", precision=precision, penalty=1e-3,
+                          guide_trans=(sampler.t_templ, sampler.i_templ) if guide else None)
     sampler.native.seed(224 + 1000 * rank)  # each rank draws its own shard of the global batch
     return sampler, trainer
 
@@ -128,18 +132,19 @@ def pmc_traffic(kernel):
     return None if k is None else k["hbm_bytes"]
 
 
-def cpu_baseline(B, L, steps=8):
+def cpu_baseline(B, L, steps=8, guide=False):
     from oracle import ghm_oracle as O
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
-    tr = O.OracleTrainer(p=0.2, B=B, L=L)
+    tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
+          else O.OracleTrainer(p=0.2, B=B, L=L))
     tr.step()  # warm-up
     t0 = time.time()
     for _ in range(steps):
         tr.step()
     dt = (time.time() - t0) / steps
     return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} steps (after 1 warm-up) of the default CLIP config, B={B}, fp32 "
+            "sample": f"{steps} steps (after 1 warm-up) of the {'guided' if guide else 'default'} CLIP config, B={B}, fp32 "
                       f"PyTorch-CPU restatement of the reference (oracle/ghm_oracle.py); "
                       f"{dt:.3f} s/step"}
 
@@ -154,13 +159,15 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ring", type=int, default=16)
+    ap.add_argument("--guide", action="store_true",
+                    help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
     total_iters = max(3000, a.steps + a.warmup + 1)
-    sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision)
+    sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
     ring = make_ring(sampler, a.batch, a.ring)
 
     def one(k):
@@ -235,7 +242,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
-        "config": {"workload": "clip_default: 2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW",
+        "config": {"workload": ("clip_guided: " if a.guide else "clip_default: ")
+                   + "2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW"
+                   + (" + on-device BP guide targets and penalty on 4 layers" if a.guide else ""),
                    "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,
                    "global_batch_rows": a.batch * ws, "n_layer": a.layers, "parallelism": f"dp{ws}",
                    "hip_graph": not a.no_graph},
@@ -248,7 +257,7 @@ def main():
         "last_loss": float(losses[-1]) if len(losses) else None,
     }
     if ws == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.batch, a.layers)
+        out["cpu_baseline"] = cpu_baseline(a.batch, a.layers, guide=a.guide)
     print(json.dumps(out), flush=True)
     if ws > 1:
         dist.destroy_process_group()

@@ -187,6 +187,33 @@ int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, i
                  const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,
                  int tok_per_split, void* stream);
 
+/* ---- guided CLIP (clip_guide=True) ------------------------------------------
+ * Exact BP_CLS messages of each sequence's GHM tree (data_random_GHM.py:185-208,
+ * guided_info :526-549) from its leaves: trans = [L][C][V][V] f64 templates
+ * (parent value, child value); msgs = [n_seq][n_total][V] f32 with
+ * n_total = (C^L - 1)/(C - 1), levels in guided-target order (depth L-1 first,
+ * root last), log-domain, max-shifted per node. */
+int ghm_bp_cls(const double* trans, const uint8_t* tokens, float* msgs, int64_t n_seq, int L, int C, int V,
+               void* stream);
+/* part[n] = sum_{t,c<V} (H[n,t,c] - msgs[n][node_level(t)][c])^2 for guided target
+ * `level` (model.py:790-800, 909-924); H is a [n_seq*T][128] residual stream. */
+int ghm_guide_fwd(const float* H, const float* msgs, float* part, int64_t n_seq, int L, int C, int V, int level,
+                  void* stream);
+/* dH[n,t,c] += scale * (H[n,t,c] - msgs[...][c]) for c < V (scale = 2*penalty/n_seq). */
+int ghm_guide_bwd(const float* H, const float* msgs, float* dH, int64_t n_seq, int L, int C, int V, int level,
+                  float scale, void* stream);
+/* loss_io[1] = loss_io[0] + penalty * mean_n sum_k part[k][n]; loss_io[2] = that mean / penalty;
+ * phist[*step] = loss_io[1] if phist.  part: [n_parts][n_seq]. */
+int ghm_guide_total(const float* part, int n_parts, int64_t n_seq, float penalty, float* loss_io, float* phist,
+                    const int32_t* step, void* stream);
+
+/* Module-API helpers (dense guided targets): out[r] = sum_e (a - b)^2 over rows of
+ * row_len; out = scale[0]*alpha*(a - b); dst[m][c] += src[m][c] for c < V (dst [M][128]). */
+int ghm_sqdiff_rows(const float* a, const float* b, float* out, int64_t rows, int64_t row_len, void* stream);
+int ghm_scaled_diff(const float* a, const float* b, const float* scale, float alpha, float* out, int64_t n,
+                    void* stream);
+int ghm_add_cols(float* dst, const float* src, int64_t M, int V, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

@@ -1,0 +1,269 @@
+// Guided CLIP (clip_guide=True) on the device: exact BP_CLS messages of the GHM
+// trees behind each sequence, and the layer-wise Frobenius penalty that pulls a
+// guided layer's first V hidden features toward them.
+// Reference: src/ghmclip/data/data_random_GHM.py:185-221 (GHMTree.BP_CLS),
+// :526-549 (guided_info), models/model.py:790-800 (guided layers: H[:, :, 0:V]
+// after each flagged layer) and :909-924 (GuidedClipLoss guide branch).
+#include "ghm_common.h"
+#include "ghm_launch.h"
+
+constexpr int BP_MAXV = 16;
+constexpr int BP_MAXN = 32;  // nodes at depth L-1 (T / C <= 96 / 3)
+
+// One 64-thread workgroup per sequence, f64 arithmetic like the reference's
+// numpy.  Messages are log-domain and max-shifted per node (:196, :208).
+// trans: [L][C][V][V] (parent value v, child value u) of the translation-
+// invariant templates; msgs: [N][n_total][V] f32, levels in guided-target order
+// (depth L-1 first, root last), nodes in breadth-first order within a level.
+__global__ __launch_bounds__(64) void k_bp_cls(const double* __restrict__ trans, const uint8_t* __restrict__ tok,
+                                               float* __restrict__ msgs, int L, int C, int V, int T,
+                                               int n_total) {
+  __shared__ double cur[BP_MAXN * BP_MAXV];
+  __shared__ double nxt[BP_MAXN * BP_MAXV];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* x = tok + static_cast<int64_t>(n) * T;
+  float* out = msgs + static_cast<int64_t>(n) * n_total * V;
+  int nodes = T / C;
+  // depth L-1: sum_c log T_{L-1,c}[v][x_child]                        (:191-195)
+  for (int e = tid; e < nodes * V; e += 64) {
+    const int node = e / V, v = e % V;
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) {
+      int xv = x[node * C + c];
+      xv = xv < V ? xv : V - 1;
+      s += log(trans[((L - 1) * C + c) * V * V + v * V + xv]);
+    }
+    cur[e] = s;
+  }
+  __syncthreads();
+  int off = 0;
+  for (int d = L - 1;; --d) {
+    // max shift per node (:196 / :208) and emit the level
+    for (int node = tid; node < nodes; node += 64) {
+      double mx = cur[node * V];
+      for (int v = 1; v < V; ++v) mx = fmax(mx, cur[node * V + v]);
+      for (int v = 0; v < V; ++v) {
+        cur[node * V + v] -= mx;
+        out[(off + node) * V + v] = static_cast<float>(cur[node * V + v]);
+      }
+    }
+    __syncthreads();
+    off += nodes;
+    if (d == 0) break;
+    // depth d-1: sum_c log(T_{d-1,c} @ exp(child message))              (:201-207)
+    const int np = nodes / C;
+    for (int e = tid; e < np * V; e += 64) {
+      const int node = e / V, v = e % V;
+      double s = 0.0;
+      for (int c = 0; c < C; ++c) {
+        const double* tr = trans + ((d - 1) * C + c) * V * V + v * V;
+        const double* ch = cur + (node * C + c) * V;
+        double a = 0.0;
+        for (int u = 0; u < V; ++u) a += tr[u] * exp(ch[u]);
+        s += log(a);
+      }
+      nxt[e] = s;
+    }
+    __syncthreads();
+    for (int e = tid; e < np * V; e += 64) cur[e] = nxt[e];
+    __syncthreads();
+    nodes = np;
+  }
+}
+
+// Per-sequence penalty partial of one guided layer:
+//   part[n] = sum_{t<T, c<V} (H[n, t, c] - msg[n][lvl_off + t / ext][c])^2
+// One 128-thread workgroup per sequence, thread = token, fixed reduction tree.
+__global__ __launch_bounds__(128) void k_guide_fwd(const float* __restrict__ H, const float* __restrict__ msgs,
+                                                   float* __restrict__ part, int T, int V, int n_total,
+                                                   int lvl_off, int ext) {
+  __shared__ float red[2];
+  const int n = blockIdx.x, t = threadIdx.x;
+  float s = 0.f;
+  if (t < T) {
+    const float* h = H + (static_cast<int64_t>(n) * T + t) * GHM_D;
+    const float* m = msgs + (static_cast<int64_t>(n) * n_total + lvl_off + t / ext) * V;
+    for (int c = 0; c < V; ++c) {
+      const float dd = h[c] - m[c];
+      s += dd * dd;
+    }
+  }
+  s = sum32(s);
+  s += __shfl_xor(s, 32, 64);
+  if ((t & 63) == 0) red[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) part[n] = red[0] + red[1];
+}
+
+// dH[n, t, c] += scale * (H[n, t, c] - msg[...][c]) for c < V   (scale = 2 penalty / N)
+__global__ __launch_bounds__(256) void k_guide_bwd(const float* __restrict__ H, const float* __restrict__ msgs,
+                                                   float* __restrict__ dH, int64_t M, int T, int V, int n_total,
+                                                   int lvl_off, int ext, float scale) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= M * V) return;
+  const int64_t m = i / V;
+  const int c = static_cast<int>(i % V);
+  const int64_t n = m / T;
+  const int t = static_cast<int>(m % T);
+  const float target = msgs[(n * n_total + lvl_off + t / ext) * V + c];
+  dH[m * GHM_D + c] += scale * (H[m * GHM_D + c] - target);
+}
+
+// ploss = loss_nop + penalty * mean_n sum_k part[k][n]; also the logged
+// penalty value mean / penalty (GuidedClipLoss returns loss3.mean()/penalty).
+// loss_io[0] holds loss_nop on entry; loss_io[1] <- ploss, loss_io[2] <- pen.
+// If phist is non-NULL: phist[*step] = ploss.  One 256-thread workgroup.
+__global__ __launch_bounds__(256) void k_guide_total(const float* __restrict__ part, int n_parts, int N,
+                                                     float penalty, float* __restrict__ loss_io,
+                                                     float* __restrict__ phist, const int32_t* __restrict__ step) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float r = 0.f;
+    for (int k = 0; k < n_parts; ++k) r += part[static_cast<int64_t>(k) * N + n];
+    s += r;
+  }
+  s = sum32(s);
+  s += __shfl_xor(s, 32, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float mean = penalty * (((red[0] + red[1]) + (red[2] + red[3])) / static_cast<float>(N));
+    const float ploss = loss_io[0] + mean;
+    loss_io[1] = ploss;
+    loss_io[2] = mean / penalty;
+    if (phist) phist[*step] = ploss;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI launchers
+// ---------------------------------------------------------------------------
+extern "C" int ghm_bp_cls(const double* trans, const uint8_t* tokens, float* msgs, int64_t n_seq, int L, int C,
+                          int V, void* stream) {
+  GHM_CHECK(trans && tokens && msgs, "null pointer");
+  GHM_CHECK(L >= 1 && C >= 2 && V >= 2 && V <= BP_MAXV && n_seq >= 1, "shape");
+  int T = 1, n_total = 0;
+  for (int d = 0; d < L; ++d) {
+    n_total += T;
+    T *= C;
+  }
+  GHM_CHECK(T <= GHM_MAXT && T / C <= BP_MAXN, "tree too large (leaves <= 96)");
+  hipLaunchKernelGGL(k_bp_cls, dim3(static_cast<unsigned>(n_seq)), dim3(64), 0, ghm_stream(stream), trans, tokens,
+                     msgs, L, C, V, T, n_total);
+  return ghm_launch_status();
+}
+
+static int guide_level(int L, int C, int level, int& off, int& ext, int& n_total, int& T) {
+  T = 1;
+  n_total = 0;
+  for (int d = 0; d < L; ++d) {
+    n_total += T;
+    T *= C;
+  }
+  off = 0;
+  int nodes = T / C;
+  ext = C;
+  for (int k = 0; k < level; ++k) {
+    off += nodes;
+    nodes /= C;
+    ext *= C;
+  }
+  return 0;
+}
+
+extern "C" int ghm_guide_fwd(const float* H, const float* msgs, float* part, int64_t n_seq, int L, int C, int V,
+                             int level, void* stream) {
+  GHM_CHECK(H && msgs && part, "null pointer");
+  GHM_CHECK(level >= 0 && level < L && V >= 1 && V <= GHM_D && n_seq >= 1, "shape");
+  int off, ext, n_total, T;
+  guide_level(L, C, level, off, ext, n_total, T);
+  GHM_CHECK(T <= 128, "sequence too long");
+  hipLaunchKernelGGL(k_guide_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0, ghm_stream(stream), H, msgs,
+                     part, T, V, n_total, off, ext);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_bwd(const float* H, const float* msgs, float* dH, int64_t n_seq, int L, int C, int V,
+                             int level, float scale, void* stream) {
+  GHM_CHECK(H && msgs && dH, "null pointer");
+  GHM_CHECK(level >= 0 && level < L && V >= 1 && V <= GHM_D && n_seq >= 1, "shape");
+  int off, ext, n_total, T;
+  guide_level(L, C, level, off, ext, n_total, T);
+  const int64_t M = n_seq * T;
+  hipLaunchKernelGGL(k_guide_bwd, dim3(static_cast<unsigned>((M * V + 255) / 256)), dim3(256), 0,
+                     ghm_stream(stream), H, msgs, dH, M, T, V, n_total, off, ext, scale);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_total(const float* part, int n_parts, int64_t n_seq, float penalty, float* loss_io,
+                               float* phist, const int32_t* step, void* stream) {
+  GHM_CHECK(part && loss_io, "null pointer");
+  GHM_CHECK(!phist || step, "phist needs step");
+  GHM_CHECK(n_parts >= 1 && n_seq >= 1 && penalty > 0.f, "shape");
+  hipLaunchKernelGGL(k_guide_total, dim3(1), dim3(256), 0, ghm_stream(stream), part, n_parts,
+                     static_cast<int>(n_seq), penalty, loss_io, phist, step);
+  return ghm_launch_status();
+}
+
+// ---------------------------------------------------------------------------
+// Dense-target helpers for the module API (GuidedClipLoss(guide=True) on the
+// guided-layer tensors EncoderTransformer.forward returns)
+// ---------------------------------------------------------------------------
+// out[r] = sum_{e<E} (a[r*E+e] - b[r*E+e])^2, one 256-thread workgroup per row
+__global__ __launch_bounds__(256) void k_sqdiff_rows(const float* __restrict__ a, const float* __restrict__ b,
+                                                     float* __restrict__ out, int64_t E) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  float s = 0.f;
+  for (int64_t e = threadIdx.x; e < E; e += 256) {
+    const float d = a[r * E + e] - b[r * E + e];
+    s += d * d;
+  }
+  s = sum32(s);
+  s += __shfl_xor(s, 32, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[r] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// out[i] = scale[0] * alpha * (a[i] - b[i])   (scale: device scalar, e.g. the upstream gradient)
+__global__ __launch_bounds__(256) void k_scaled_diff(const float* __restrict__ a, const float* __restrict__ b,
+                                                     const float* __restrict__ scale, float alpha,
+                                                     float* __restrict__ out, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) out[i] = (scale[0] * alpha) * (a[i] - b[i]);
+}
+
+// dst[m*128 + c] += src[m*V + c], c < V: a guided layer's gradient into the residual stream
+__global__ __launch_bounds__(256) void k_add_cols(float* __restrict__ dst, const float* __restrict__ src,
+                                                  int64_t M, int V) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= M * V) return;
+  const int64_t m = i / V;
+  const int c = static_cast<int>(i % V);
+  dst[m * GHM_D + c] += src[i];
+}
+
+extern "C" int ghm_sqdiff_rows(const float* a, const float* b, float* out, int64_t rows, int64_t row_len,
+                               void* stream) {
+  GHM_CHECK(a && b && out && rows >= 1 && row_len >= 1, "shape");
+  hipLaunchKernelGGL(k_sqdiff_rows, dim3(static_cast<unsigned>(rows)), dim3(256), 0, ghm_stream(stream), a, b, out,
+                     row_len);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_scaled_diff(const float* a, const float* b, const float* scale, float alpha, float* out,
+                               int64_t n, void* stream) {
+  GHM_CHECK(a && b && scale && out && n >= 1, "shape");
+  hipLaunchKernelGGL(k_scaled_diff, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, ghm_stream(stream),
+                     a, b, scale, alpha, out, n);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_add_cols(float* dst, const float* src, int64_t M, int V, void* stream) {
+  GHM_CHECK(dst && src && M >= 1 && V >= 1 && V <= GHM_D, "shape");
+  hipLaunchKernelGGL(k_add_cols, dim3(static_cast<unsigned>((M * V + 255) / 256)), dim3(256), 0, ghm_stream(stream),
+                     dst, src, M, V);
+  return ghm_launch_status();
+}

@@ -63,6 +63,13 @@ HIP_SIGNATURES = {
     "ghm_wgrad_x3": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_attn_fwd_x3": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_bp_cls": [_p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_guide_fwd": [_p, _p, _p, _i64, _i, _i, _i, _i, _p],
+    "ghm_guide_bwd": [_p, _p, _p, _i64, _i, _i, _i, _i, _f, _p],
+    "ghm_guide_total": [_p, _i, _i64, _f, _p, _p, _p, _p],
+    "ghm_sqdiff_rows": [_p, _p, _p, _i64, _i64, _p],
+    "ghm_scaled_diff": [_p, _p, _p, _f, _p, _i64, _p],
+    "ghm_add_cols": [_p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64}

@@ -17,7 +17,7 @@ import torch
 
 from .. import _native
 
-__all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior",
+__all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior", "guided_targets",
            "NativeClipSampler"]
 
 
@@ -127,17 +127,18 @@ def _native_check(rc):
         raise RuntimeError(f"native sampler call failed ({rc})")
 
 
-def bp_cls_posterior(templ, leaves, p_y):
-    """BP_CLS (data_random_GHM.py:185-221), vectorised over the nodes of a layer
-    (translation invariance makes their matrices equal per child slot).
-    templ [n_layer, n_child, V, V]; leaves [B, T] -> p(root | leaves) [B, V]."""
+def _bp_levels(templ, leaves):
+    """BP_CLS messages (data_random_GHM.py:185-208), vectorised over the nodes of a
+    layer (translation invariance makes their matrices equal per child slot).
+    Returns the per-level messages [n_nodes, V, B], depth L-1 first, root last."""
     n_layer, n_child, V, _ = templ.shape
-    lv = np.asarray(leaves).T
+    lv = np.asarray(leaves).astype(np.int64).T
     n_par = lv.shape[0] // n_child
     msg = np.zeros((n_par, V, lv.shape[1]))
     for c in range(n_child):
         msg += np.log(templ[-1, c][:, lv[c::n_child]].transpose(1, 0, 2))
     msg -= msg.max(axis=1, keepdims=True)
+    levels = [msg]
     for layer in range(n_layer - 2, -1, -1):
         n_par = msg.shape[0] // n_child
         new = np.zeros((n_par, V, msg.shape[2]))
@@ -145,6 +146,45 @@ def bp_cls_posterior(templ, leaves, p_y):
             new += np.log(np.einsum("ij,njb->nib", templ[layer, c], np.exp(msg[c::n_child])))
         new -= new.max(axis=1, keepdims=True)
         msg = new
+        levels.append(msg)
+    return levels
+
+
+def guided_targets(templ, leaves, device="cpu"):
+    """GHMTree.guided_info for classification (data_random_GHM.py:526-539): one
+    float32 [B, T, V] tensor per tree level (depth L-1 first, root last), every
+    leaf position carrying its ancestor's BP message.  On a HIP device the
+    messages come from the ghm_bp_cls kernel (the path ClipTrainer uses);
+    otherwise from the host BP above."""
+    templ = np.ascontiguousarray(templ, dtype=np.float64)
+    L, C, V, _ = templ.shape
+    leaves = np.asarray(leaves)
+    B, T = leaves.shape
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        n_total = (C ** L - 1) // (C - 1)
+        tok = torch.from_numpy(np.ascontiguousarray(leaves, dtype=np.uint8)).to(dev)
+        tr = torch.from_numpy(templ).to(dev)
+        msgs = torch.empty(B, n_total, V, dtype=torch.float32, device=dev)
+        _native.call("ghm_bp_cls", tr.data_ptr(), tok.data_ptr(), msgs.data_ptr(), B, L, C, V,
+                     torch.cuda.current_stream().cuda_stream)
+        out, off, nodes = [], 0, T // C
+        for _ in range(L):
+            out.append(msgs[:, off:off + nodes].repeat_interleave(T // nodes, dim=1))
+            off += nodes
+            nodes //= C
+        return out
+    out = []
+    for m in _bp_levels(templ, leaves):
+        ext = T // m.shape[0]
+        out.append(torch.from_numpy(np.repeat(m.transpose(2, 0, 1), ext, axis=1).astype(np.float32)))
+    return out
+
+
+def bp_cls_posterior(templ, leaves, p_y):
+    """BP_CLS (data_random_GHM.py:185-221): p(root | leaves) [B, V].
+    templ [n_layer, n_child, V, V]; leaves [B, T]."""
+    msg = _bp_levels(templ, leaves)[-1]
     h0 = msg[0] + np.log(p_y).reshape(-1, 1)
     h0 -= h0.max(axis=0)
     return (np.exp(h0) / np.exp(h0).sum(axis=0)).T
@@ -211,13 +251,21 @@ class ClipSampler(DoubleSampler):
         return tl, tr, il, ir
 
     def get_batch(self, device="cpu", batch_size=128, guide=False):
-        """:753-784.  Returns [text_leaves, text_root, None, None], [image ...]
-        with leaves as int64 [B(K+1), T] on ``device``."""
-        if guide:
-            raise NotImplementedError("guide=True (BP guide targets) is not part of the HIP path yet")
+        """:753-784.  Returns [text_leaves, text_root, guided_info, t_pp],
+        [image ...] with leaves as int64 [B(K+1), T] on ``device``; with guide=True
+        guided_info is the list of per-level BP guide targets (float32 [B(K+1),
+        T, V] on ``device``) and t_pp the BP_CLS posteriors [B(K+1), V] (numpy),
+        else both are None."""
         tl, tr, il, ir = self.draw_numpy(batch_size)
         to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
-        return [to(tl), to(tr), None, None], [to(il), to(ir), None, None]
+        tg = ig = tp = ip = None
+        if guide:
+            tg = guided_targets(self.t_templ, tl, device)
+            ig = guided_targets(self.i_templ, il, device)
+            p_y = np.ones(self.variable_type) / self.variable_type
+            tp = bp_cls_posterior(self.t_templ, tl, p_y)
+            ip = bp_cls_posterior(self.i_templ, il, p_y)
+        return [to(tl), to(tr), tg, tp], [to(il), to(ir), ig, ip]
 
     def get_Bayes(self, n_eval=10000):
         """:786-817 — exact Bayes CLIP loss from BP posteriors (host, once per run)."""

@@ -229,9 +229,12 @@ class EncoderPlan:
         assert j.n == n
         self._flush([j], s)
 
-    def backward(self, p, g, d_emb=None, tokens=None):
+    def backward(self, p, g, d_emb=None, tokens=None, layer_grad=None):
         """Accumulate nothing: writes d(loss)/d(param) into g[name] (fp32 device
         tensors, same keys as p).  d_emb: [n_seq, C] (defaults to self.d_emb).
+        layer_grad: optional {layer l: fn(dH, stream)} — adds a loss term's gradient
+        w.r.t. the residual stream H[l+1] leaving layer l (guided layers,
+        model.py:790-800) before that layer's backward runs.
         Parameter-gradient partials are reduced by one batched launch per layer."""
         tok = self.tokens if tokens is None else tokens
         de = self.d_emb if d_emb is None else d_emb
@@ -249,6 +252,8 @@ class EncoderPlan:
         x3 = self.precision == "x3"
         wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
         for l in reversed(range(L)):
+            if layer_grad and l in layer_grad:
+                layer_grad[l](cur, s)
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
             if x3:
                 c("ghm_mlp_bwd_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),

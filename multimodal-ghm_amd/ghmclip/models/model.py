@@ -40,6 +40,9 @@ def get_activation(activation="softmax"):
 
 
 class _EncoderFn(torch.autograd.Function):
+    """Outputs: the embedding [N, C] and, for a guided encoder, H_{l+1}[:, :, 0:V]
+    of every flagged layer l (model.py:790-800) as [N, T, V] tensors."""
+
     @staticmethod
     def forward(ctx, module, tokens, *params):
         plan = module._plan(tokens.shape[0], tokens.shape[1], tokens.device)
@@ -47,10 +50,12 @@ class _EncoderFn(torch.autograd.Function):
         emb = plan.forward(pd, tokens).clone()
         ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
         ctx.save_for_backward(tokens, *params)
-        return emb
+        N, T, V = tokens.shape[0], tokens.shape[1], module.vocab_size
+        guided = [plan.H[l + 1].view(N, T, -1)[:, :, :V].contiguous() for l in module._guided_layers()]
+        return (emb, *guided)
 
     @staticmethod
-    def backward(ctx, d_emb):
+    def backward(ctx, d_emb, *d_guided):
         plan = ctx.plan
         if plan._gen != ctx.gen:
             raise RuntimeError("EncoderTransformer: another forward of this module overwrote the "
@@ -58,7 +63,18 @@ class _EncoderFn(torch.autograd.Function):
         tokens, *params = ctx.saved_tensors
         names = ctx.module._names
         grads = {n: torch.empty_like(p) for n, p in zip(names, params)}
-        plan.backward(dict(zip(names, params)), grads, d_emb=d_emb.contiguous().float(), tokens=tokens)
+        hooks = {}
+        V = ctx.module.vocab_size
+        for l, dg in zip(ctx.module._guided_layers(), d_guided):
+            if dg is None:
+                continue
+            dg = dg.contiguous().float()
+
+            def fn(dH, s, dg=dg):
+                _native.call("ghm_add_cols", dH.data_ptr(), dg.data_ptr(), plan.M, V, s)
+            hooks[l] = fn
+        plan.backward(dict(zip(names, params)), grads, d_emb=d_emb.contiguous().float(), tokens=tokens,
+                      layer_grad=hooks)
         return (None, None, *[grads[n] for n in names])
 
 
@@ -130,11 +146,14 @@ class EncoderTransformer(nn.Module):
                                            precision=self.precision)
         return self._plans[key]
 
+    def _guided_layers(self):
+        """Indices of the guided layers (model.py:751-755 flags)."""
+        return [l for l, f in enumerate(self.guided_layer_flag) if f] if self.guide else []
+
     def forward(self, x):
-        """x: LongTensor [B, n_token] on the HIP device -> (prediction [B, num_class], [])."""
+        """x: LongTensor [B, n_token] on the HIP device -> (prediction [B, num_class],
+        guided layers: [H_{l+1}[:, :, 0:num_class] for each flagged layer l])."""
         require_hip(x)
-        if self.guide:
-            raise NotImplementedError("guided CLIP (clip_guide=True) has no HIP kernels yet")
         B, T = x.shape
         if T != self.n_token:
             raise ValueError(f"expected {self.n_token} tokens, got {T}")
@@ -146,7 +165,8 @@ class EncoderTransformer(nn.Module):
         for prm in params:
             if prm.dtype != torch.float32 or not prm.is_contiguous():
                 raise RuntimeError("HIP encoder parameters must be contiguous fp32")
-        return _EncoderFn.apply(self, tokens, *params), []
+        out = _EncoderFn.apply(self, tokens, *params)
+        return out[0], list(out[1:])
 
 
 class _ClipLossFn(torch.autograd.Function):
@@ -171,6 +191,43 @@ class _ClipLossFn(torch.autograd.Function):
         return dt * g, di * g, None, None
 
 
+class _GuidePenaltyFn(torch.autograd.Function):
+    """mean_n sum_k penalty * ||g_k[n] - t_k[n]||_F^2 (model.py:913-924) with the
+    squared differences and their gradient in libghm_hip (ghm_sqdiff_rows,
+    ghm_scaled_diff)."""
+
+    @staticmethod
+    def forward(ctx, penalty, n, *gt):
+        g = [x.contiguous().float() for x in gt[:n]]
+        t = [x.to(g[0].device).contiguous().float() for x in gt[n:]]
+        N = g[0].shape[0]
+        s = torch.cuda.current_stream().cuda_stream
+        rows = torch.empty(n, N, dtype=torch.float32, device=g[0].device)
+        for k in range(n):
+            if g[k].shape != t[k].shape:
+                raise ValueError(f"guided layer {k}: {tuple(g[k].shape)} vs target {tuple(t[k].shape)}")
+            _native.call("ghm_sqdiff_rows", g[k].data_ptr(), t[k].data_ptr(), rows[k].data_ptr(), N,
+                         g[k].numel() // N, s)
+        ctx.save_for_backward(*g, *t)
+        ctx.penalty, ctx.n = penalty, n
+        return (rows.sum(0) * penalty).mean()
+
+    @staticmethod
+    def backward(ctx, up):
+        saved = ctx.saved_tensors
+        n = ctx.n
+        g, t = saved[:n], saved[n:]
+        up = up.contiguous().float()
+        s = torch.cuda.current_stream().cuda_stream
+        out = []
+        for k in range(n):
+            d = torch.empty_like(g[k])
+            _native.call("ghm_scaled_diff", g[k].data_ptr(), t[k].data_ptr(), up.data_ptr(),
+                         2.0 * ctx.penalty / g[k].shape[0], d.data_ptr(), d.numel(), s)
+            out.append(d)
+        return (None, None, *out, *[None] * n)
+
+
 class GuidedClipLoss(nn.Module):
     """Reference: models/model.py:867-926.  Returns (loss, guided_penalty)."""
 
@@ -182,10 +239,17 @@ class GuidedClipLoss(nn.Module):
         self.guide = guide
 
     def forward(self, tmodel_outputs, imodel_outputs, targets):
-        if self.guide:
-            raise NotImplementedError("guided CLIP penalty has no HIP kernel yet")
         loss = _ClipLossFn.apply(tmodel_outputs[0], imodel_outputs[0], self.K, self.batch_size)
-        return loss, 0
+        if not self.guide:
+            return loss, 0
+        # :909-924 — per-sample sum of penalty * ||guided - target||_F^2 over both
+        # towers' guided layers, averaged over samples
+        g = list(tmodel_outputs[1]) + list(imodel_outputs[1])
+        t = list(targets[0]) + list(targets[1])
+        if len(g) != len(t):
+            raise ValueError(f"{len(g)} guided layers but {len(t)} targets")
+        loss3 = _GuidePenaltyFn.apply(self.penalty, len(g), *g, *t)
+        return loss + loss3, loss3.item() / self.penalty
 
 
 class ClipLoss(nn.Module):

@@ -33,11 +33,15 @@ def _p(t):
 class ClipTrainer:
     def __init__(self, tmodel, imodel, K, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
                  betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
-                 precision=None):
+                 precision=None, penalty=1e-3, guide_trans=None):
         """lr_schedule: sequence of python-float learning rates, one per step
         (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
         precision: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA); None ->
-        $GHM_PRECISION or "x3"."""
+        $GHM_PRECISION or "x3".
+        Guided CLIP (train_CLIP.py --clip_guide=True) is on when the encoders were
+        built with guide=True: guide_trans = (text, image) transition templates
+        [L][C][V][V] (ClipSampler.t_templ / i_templ) for the on-device BP guide
+        targets, penalty = GuidedClipLoss's penalty."""
         self.device = torch.device(device)
         self.tm, self.im = tmodel, imodel
         self.K, self.B = K, batch_size
@@ -91,11 +95,72 @@ class ClipTrainer:
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.hyper = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.work = torch.zeros(1024, dtype=torch.float32, device=self.device)
-        self.loss_out = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
         self.graphs = None
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
+        self._setup_guide(penalty, guide_trans)
+
+    def _setup_guide(self, penalty, guide_trans):
+        """Buffers of the guided objective (model.py:909-924): per-tower BP
+        messages [N][n_nodes][V], per-(tower, guided layer) penalty partials, and
+        the penalised loss history (train_CLIP.py ploss_history)."""
+        flags = [getattr(m, "guide", False) for m in self.models]
+        self.guide = all(flags)
+        if any(flags) and not self.guide:
+            raise ValueError("both encoders must be built with the same guide setting")
+        self.loss_out = torch.zeros(3, dtype=torch.float32, device=self.device)
+        self.phist = None
+        if not self.guide:
+            return
+        if guide_trans is None:
+            raise ValueError("guided CLIP needs guide_trans=(sampler.t_templ, sampler.i_templ)")
+        self.penalty = float(penalty)
+        self.glayers, self.gtrans, self.gmsgs, self.gtree = [], [], [], []
+        for m, tr in zip(self.models, guide_trans):
+            tr = np.ascontiguousarray(tr, dtype=np.float64)
+            L, C, V = tr.shape[0], tr.shape[1], tr.shape[2]
+            if C ** L != m.n_token or V != m.vocab_size:
+                raise ValueError("guide transitions do not match the encoder's token count / vocabulary")
+            layers = [l for l, f in enumerate(m.guided_layer_flag) if f]
+            if len(layers) > L:
+                raise ValueError("more guided layers than tree levels")
+            n_total = (C ** L - 1) // (C - 1)
+            self.glayers.append(layers)
+            self.gtree.append((L, C, V))
+            self.gtrans.append(torch.from_numpy(tr).to(self.device))
+            self.gmsgs.append(torch.zeros(self.n_seq, n_total, V, dtype=torch.float32, device=self.device))
+        self.n_gparts = sum(len(x) for x in self.glayers)
+        self.gpart = torch.zeros(max(1, self.n_gparts), self.n_seq, dtype=torch.float32, device=self.device)
+        self.phist = torch.zeros_like(self.hist)
+
+    def _guide_fwd(self, tower, s):
+        """BP guide targets from the staged tokens, then the penalty partials of
+        the tower's guided layers (after its forward)."""
+        L, C, V = self.gtree[tower]
+        plan = self.plans[tower]
+        base = sum(len(x) for x in self.glayers[:tower])
+        _native.call("ghm_bp_cls", _p(self.gtrans[tower]), _p(plan.tokens), _p(self.gmsgs[tower]), self.n_seq,
+                     L, C, V, s)
+        for k, l in enumerate(self.glayers[tower]):
+            _native.call("ghm_guide_fwd", _p(plan.H[l + 1]), _p(self.gmsgs[tower]), _p(self.gpart[base + k]),
+                         self.n_seq, L, C, V, k, s)
+
+    def _guide_hooks(self, tower):
+        """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / N."""
+        if not self.guide:
+            return None
+        L, C, V = self.gtree[tower]
+        plan = self.plans[tower]
+        msgs = self.gmsgs[tower]
+        scale = 2.0 * self.penalty / self.n_seq
+        hooks = {}
+        for k, l in enumerate(self.glayers[tower]):
+            def fn(dH, s, l=l, k=k):
+                _native.call("ghm_guide_bwd", _p(plan.H[l + 1]), _p(msgs), _p(dH), self.n_seq, L, C, V, k,
+                             scale, s)
+            hooks[l] = fn
+        return hooks
 
     # -- the launch sequence -----------------------------------------------------
     def _fwd_bwd(self):
@@ -109,15 +174,22 @@ class ClipTrainer:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             pi.forward(ip)
+            if self.guide:
+                self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
         pt.forward(tp)
-        main.wait_stream(side)
         s = ctypes.c_void_p(main.cuda_stream)
+        if self.guide:
+            self._guide_fwd(0, s)
+        main.wait_stream(side)
         _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
+        if self.guide:
+            _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.n_seq, self.penalty,
+                         _p(self.loss_out), _p(self.phist), _p(self.step_ctr), s)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            pi.backward(ip, ig)
-        pt.backward(tp, tg)
+            pi.backward(ip, ig, layer_grad=self._guide_hooks(1))
+        pt.backward(tp, tg, layer_grad=self._guide_hooks(0))
         main.wait_stream(side)
 
     def _optim(self):
@@ -171,8 +243,17 @@ class ClipTrainer:
 
     # -- host-side views -----------------------------------------------------------
     def loss_history(self, upto=None):
+        """Plain CLIP loss per step (train_CLIP.py loss_history, from loss_nop)."""
         n = self.steps_done if upto is None else upto
         return self.hist[:n].double().cpu().numpy()
+
+    def ploss_history(self, upto=None):
+        """Loss including the guided penalty (train_CLIP.py ploss_history); equals
+        loss_history without guidance."""
+        if self.phist is None:
+            return self.loss_history(upto)
+        n = self.steps_done if upto is None else upto
+        return self.phist[:n].double().cpu().numpy()
 
     def fill_optimizer_state(self, optimizer):
         """Expose the flat moments as the reference AdamW's per-parameter state

@@ -7,7 +7,8 @@ and figures/eval-clip-*.py work unchanged.  The hot loop (:139-201) runs as the
 fused, HIP-graph-replayed ClipTrainer step with the native sampler overlapped
 in a producer thread.  Differences, by design:
   * --device must be a HIP device (there is no CPU path);
-  * clip_guide=True is not implemented on the HIP path (raises);
+  * clip_guide=True computes the BP guide targets on the device from the staged
+    leaves (ghm_bp_cls) inside the captured step instead of in the sampler;
   * resume (--init_from=<checkpoint.pth>) actually resumes: weights, AdamW
     moments, step count and loss histories (the reference's resume is broken,
     :126-137);
@@ -68,8 +69,6 @@ def run_names(c):
 
 def main(argv=None):
     c = parse(argv)
-    if c.clip_guide:
-        raise NotImplementedError("clip_guide=True: the guided penalty has no HIP kernels yet")
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if ws > 1:
@@ -138,7 +137,9 @@ def main(argv=None):
         ploss_history[:start] = ck['ploss_history'][:start]
     sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters) for i in range(start, total)]
     B_local = c.batch_size // ws
-    trainer = ClipTrainer(tmodel, imodel, c.K, B_local, sched, max_norm=c.max_norm, device=device, t_offset=start)
+    trainer = ClipTrainer(tmodel, imodel, c.K, B_local, sched, max_norm=c.max_norm, device=device, t_offset=start,
+                          penalty=c.penalty,
+                          guide_trans=(sampler.t_templ, sampler.i_templ) if c.clip_guide else None)
     if start:
         trainer.load_optimizer_state(optimizer)
 
@@ -161,13 +162,18 @@ def main(argv=None):
 
     def sync_hist(upto):
         h = trainer.loss_history(upto - start)
+        ph = trainer.ploss_history(upto - start)  # == h without guidance
         if ws > 1:
             import torch.distributed as dist
-            t = torch.from_numpy(h).to(device)
+            t = torch.from_numpy(np.stack([h, ph])).to(device)
             dist.all_reduce(t, op=dist.ReduceOp.AVG)
-            h = t.cpu().numpy()
+            h, ph = t.cpu().numpy()
         loss_history[start:upto] = h
-        ploss_history[start:upto] = h  # guide=False: penalty-free loss == training loss
+        ploss_history[start:upto] = ph
+
+    def guided_penalty(i):
+        """GuidedClipLoss's second output at step i: loss3.mean() / penalty."""
+        return (ploss_history[i] - loss_history[i]) / c.penalty if c.clip_guide else 0.0
 
     curr_time = time.time()
     lr = sched[0]
@@ -184,7 +190,7 @@ def main(argv=None):
                 logger.info((f'Iter: {iter_num}, '
                              f'Penalty train loss: {np.mean(ploss_history[iter_num//2:iter_num]):.4f}, '
                              f'Train loss: {np.mean(loss_history[iter_num//2:iter_num]):.4f}, '
-                             f'Guided penalty: [{0:.4f}],'
+                             f'Guided penalty: [{guided_penalty(iter_num):.4f}],'
                              f'Bayes: {Bayes_loss:.4f}, '
                              f'LR: {lr:.6f}, '
                              f'Time: {(finish_time - curr_time):.2f}s'))

@@ -144,6 +144,36 @@ def bp_cls_posterior(trans, leaves, p_y):
     return pp.T
 
 
+def bp_cls_messages(trans, leaves):
+    """Per-level BP_CLS messages (data_random_GHM.py:185-208) as GHMTree.guided_info
+    returns them (:526-549), compactly: one entry per tree node instead of one per
+    descendant leaf.  Returns [msg_depth_{L-1}, ..., msg_root], each float64
+    [B, n_nodes, V] (n_nodes = 27, 9, 3, 1 for L=4, C=3), node order BFS."""
+    n_layer, n_child, V, _ = trans.shape
+    lv = leaves.T  # [n_leaves, B]
+    n_par = lv.shape[0] // n_child
+    msg = np.zeros((n_par, V, lv.shape[1]))
+    for c in range(n_child):
+        msg += np.log(trans[-1, c][:, lv[c::n_child]].transpose(1, 0, 2))
+    msg -= msg.max(axis=1, keepdims=True)
+    out = [msg]
+    for layer in range(n_layer - 2, -1, -1):
+        n_par = msg.shape[0] // n_child
+        new = np.zeros((n_par, V, msg.shape[2]))
+        for c in range(n_child):
+            new += np.log(np.einsum("ij,njb->nib", trans[layer, c], np.exp(msg[c::n_child])))
+        new -= new.max(axis=1, keepdims=True)
+        msg = new
+        out.append(msg)
+    return [m.transpose(2, 0, 1) for m in out]
+
+
+def expand_messages(msgs, n_leaves):
+    """[B, n_nodes, V] per level -> the reference's guided targets [B, n_leaves, V]
+    (float32, torch.tensor(..., dtype=torch.float) in guided_info)."""
+    return [torch.from_numpy(np.repeat(m, n_leaves // m.shape[1], axis=1).astype(np.float32)) for m in msgs]
+
+
 def clip_bayes(sampler, n_eval=10000):
     """ClipSampler.get_Bayes (data_random_GHM.py:786-817) without the dense kron."""
     t_l, _, i_l, _ = sampler.get_batch(n_eval)
@@ -172,9 +202,17 @@ class OracleEncoder(nn.Module):
     identical initial weights and identical state_dict keys (model.py:725-758)."""
 
     def __init__(self, n_token, num_class, n_embd=128, n_layer=12, n_mlp_multiplier=4,
-                 normalize_attn=True):
+                 normalize_attn=True, guide=False, n_guided_layer=4):
         super().__init__()
         self.n_embd, self.normalize_attn = n_embd, normalize_attn
+        self.vocab_size = num_class
+        # guided layer flags, model.py:716-718,751-755
+        gap = max(1, n_layer // n_guided_layer)
+        self.guided_layer_flag, cnt = [False] * n_layer, 0
+        for i in range(n_layer):
+            if guide and cnt < n_guided_layer and (i + 1) % gap == 0:
+                self.guided_layer_flag[i] = True
+                cnt += 1
         self.token_embeddings = nn.Embedding(num_class, n_embd)
         self.position_embeddings = nn.Embedding(n_token, n_embd)
         self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -194,8 +232,10 @@ class OracleEncoder(nn.Module):
         B, T = x.shape
         pos = torch.arange(T, device=x.device).expand(B, T)
         H = self.token_embeddings(x) + self.position_embeddings(pos)  # :765
-        for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values,
-                                          self._mlps, self._lns_1, self._lns_2):
+        guided = []
+        for q, k, v, mlp, ln1, ln2, flag in zip(self._queries, self._keys, self._values,
+                                                self._mlps, self._lns_1, self._lns_2,
+                                                self.guided_layer_flag):
             H1 = ln1(H)  # :772
             S = torch.matmul(q(H1), k(H1).transpose(-2, -1))  # :778
             if self.normalize_attn:
@@ -203,8 +243,10 @@ class OracleEncoder(nn.Module):
             A = F.softmax(S, dim=-1)  # :781
             H = H + torch.einsum("bij,bjd->bid", A, v(H1))  # :782
             H = H + mlp(ln2(H))  # :784-788
+            if flag:  # :790-800 — the slice index never advances (_layer_count stays 0)
+                guided.append(H[:, :, 0:self.vocab_size])
         P = self._read_out(H).transpose(1, 2)  # :802-804
-        return self._out(P)[:, :, 0], []  # :805-808
+        return self._out(P)[:, :, 0], guided  # :805-808
 
 
 def clip_loss(t, i, K, B):
@@ -222,6 +264,19 @@ def clip_loss(t, i, K, B):
     Si = fold(torch.exp((ii * torch.cat([tm] * (K - 1), 0)).sum(1)))
     l2 = -torch.log(Sm / (Sm + Si))
     return (l1 + l2).mean()
+
+
+def guide_penalty(t_guided, i_guided, t_targets, i_targets, penalty):
+    """GuidedClipLoss guide branch (model.py:909-924): per-sample sum over guided
+    layers of penalty * ||H_l[:, :, :V] - target_l||_F^2 for both towers; returns
+    (the mean over samples, which is added to the loss, and mean / penalty)."""
+    loss3 = 0
+    for g, t in zip(t_guided, t_targets):
+        loss3 = loss3 + penalty * torch.pow(torch.linalg.norm(g - t, dim=(1, 2), ord="fro"), 2)
+    for g, t in zip(i_guided, i_targets):
+        loss3 = loss3 + penalty * torch.pow(torch.linalg.norm(g - t, dim=(1, 2), ord="fro"), 2)
+    m = loss3.mean()
+    return m, m.item() / penalty
 
 
 # ----------------------------------------------------------------------------
@@ -270,19 +325,21 @@ def lr_cosine(t, lr_max, lr_min, warmup_iters, total_iters):
 # ----------------------------------------------------------------------------
 # training loop — training/train_CLIP.py:62-201 (raw=True, guide=False)
 # ----------------------------------------------------------------------------
-def build_encoders(T=81, L=5, d=128, V=10):
-    return OracleEncoder(T, V, d, L), OracleEncoder(T, V, d, L)
+def build_encoders(T=81, L=5, d=128, V=10, guide=False):
+    return (OracleEncoder(T, V, d, L, guide=guide), OracleEncoder(T, V, d, L, guide=guide))
 
 
 class OracleTrainer:
     def __init__(self, p=0.2, B=128, L=5, d=128, K=4, lr_max=3e-4, lr_min=3e-7, warmup=0,
                  total_iters=3000, max_norm=1.0, seed=224, seedtree=42, n_layer_tree=4,
-                 n_child=3):
+                 n_child=3, guide=False, penalty=1e-3):
         self.sampler = ClipSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], K=K,
                                          seedtree=seedtree)
         seed_everything(seed)  # :83
         T = n_child ** n_layer_tree
-        self.tm, self.im = build_encoders(T, L, d)
+        self.tm, self.im = build_encoders(T, L, d, guide=guide)
+        self.guide, self.penalty = guide, penalty
+        self.last_penalty = 0.0
         self.params = list(self.tm.parameters()) + list(self.im.parameters())
         self.opt = OracleAdamW(self.params)
         self.B, self.K = B, K
@@ -296,9 +353,16 @@ class OracleTrainer:
         if batch is None:
             batch = self.sampler.get_batch(self.B)
         t_l, _, i_l, _ = batch
-        t = self.tm(torch.as_tensor(t_l, dtype=torch.long))[0]
-        i = self.im(torch.as_tensor(i_l, dtype=torch.long))[0]
+        t, tg = self.tm(torch.as_tensor(t_l, dtype=torch.long))
+        i, ig = self.im(torch.as_tensor(i_l, dtype=torch.long))
         loss = clip_loss(t, i, self.K, self.B)
+        self.last_loss_nop = float(loss.item())
+        if self.guide:  # train_CLIP.py:145-158 with clip_guide=True
+            T = t_l.shape[1]
+            tt = expand_messages(bp_cls_messages(self.sampler.t_trans, t_l), T)
+            it = expand_messages(bp_cls_messages(self.sampler.i_trans, i_l), T)
+            pen, self.last_penalty = guide_penalty(tg, ig, tt, it, self.penalty)
+            loss = loss + pen
         loss.backward()
         norm = torch.nn.utils.clip_grad_norm_(self.params, self.max_norm, norm_type=2)
         lr = lr_cosine(self.it, *self.sched)

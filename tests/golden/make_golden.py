@@ -20,6 +20,15 @@ clip_d128.npz       d=128, L=2, B=8 single step: embeddings, loss, grad checksum
 clip_default_curve.npz  the default CLIP config (p=0.2, L=5, d=128, B=128) loss_history
                     for the first --curve-steps steps of the 3001-step schedule.
 bayes.json          the 20 published Bayes CLIP risks (figures/data/ghm-data/clip-risk.json:90-110).
+guide_bp.npz        get_batch(guide=True) at B=8 (p=0.2) after seed_everything(224): leaves,
+                    the 4 guided targets per tower stored compactly per tree node
+                    (GHMTree.guided_info, data_random_GHM.py:526-549, repeats checked
+                    here) and the BP_CLS posteriors (:185-221).
+guide_tiny.npz      guided CLIP (clip_guide=True, exp_clip_guidedTF.sh: lr 1e-3 -> 1e-6,
+                    penalty 1e-3) at L=5, d=16, B=4 for 2 steps: loss, loss_nop, penalty,
+                    raw grads, weights after each step.
+guide_curve.npz     the guided default config (L=5, d=128, B=128) ploss/loss history
+                    for the first --guide-steps steps.
 """
 import argparse
 import json
@@ -164,6 +173,113 @@ def curve_fixture(steps, p=0.2, B=128, total_iters=3000):
     print("wrote clip_default_curve.npz")
 
 
+def build_guided(T, L, d):
+    kw = dict(n_token=T, num_class=10, n_embd=d, n_layer=L, n_guided_layer=4, n_head=4,
+              n_mlp_multiplier=4, activation="softmax", mlp=True, normalize_attn=True,
+              layernorm=True, guide=True)
+    return EncoderTransformer(**kw), EncoderTransformer(**kw)
+
+
+def compact_targets(gl):
+    """[N,81,10] guided target k (ancestor at depth 3-k repeated over its 3^(k+1)
+    leaves) -> [N, 81/3^(k+1), 10], checking the repeats are exact."""
+    out = []
+    for k, g in enumerate(gl):
+        g = g.numpy()
+        ext = 3 ** (k + 1)
+        c = g[:, ::ext, :]
+        assert np.array_equal(np.repeat(c, ext, axis=1), g)
+        out.append(c.astype(np.float32))
+    return out
+
+
+def guide_bp_fixture(B=8, p=0.2):
+    s = make_sampler(p)
+    seed_everything(224)
+    rt, ri = s.get_batch(device="cpu", batch_size=B, guide=True)
+    out = {"p": p, "B": B, "t_transition": distinct_transitions(s.t_transition),
+           "i_transition": distinct_transitions(s.i_transition),
+           "t_leaves": rt[0].numpy().astype(np.uint8), "i_leaves": ri[0].numpy().astype(np.uint8),
+           "t_pp": np.asarray(rt[3], dtype=np.float64), "i_pp": np.asarray(ri[3], dtype=np.float64)}
+    for pref, r in (("t", rt), ("i", ri)):
+        for k, c in enumerate(compact_targets(r[2])):
+            out[f"{pref}_msg{k}"] = c
+    np.savez_compressed(os.path.join(HERE, "guide_bp.npz"), **out)
+    print("wrote guide_bp.npz")
+
+
+def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, penalty=1e-3,
+                       lr_max=1e-3, lr_min=1e-6):
+    """train_CLIP.py:83-167 with clip_guide=True (exp_clip_guidedTF.sh)."""
+    s = make_sampler(p)
+    seed_everything(224)
+    tm, im = build_guided(81, L, d)
+    loss = GuidedClipLoss(4, B, penalty=penalty, guide=True)
+    loss_nop = GuidedClipLoss(4, B, penalty=0, guide=False)
+    params = list(tm.parameters()) + list(im.parameters())
+    opt = AdamW(params=params, lr=None)
+    out = {}
+    out.update({"init." + k: v for k, v in flat_state(tm, "t").items()})
+    out.update({"init." + k: v for k, v in flat_state(im, "i").items()})
+    for it in range(nsteps):
+        opt.zero_grad()
+        rt, ri = s.get_batch(device="cpu", batch_size=B, guide=True)
+        to = tm(rt[0]); io = im(ri[0])
+        o = loss(to, io, [rt[2], ri[2]])
+        onop = loss_nop(to, io, [rt[2], ri[2]])
+        o[0].backward()
+        out[f"s{it}.t_leaves"] = rt[0].numpy().astype(np.uint8)
+        out[f"s{it}.i_leaves"] = ri[0].numpy().astype(np.uint8)
+        out[f"s{it}.loss"] = np.float64(o[0].item())
+        out[f"s{it}.loss_nop"] = np.float64(onop[0].item())
+        out[f"s{it}.penalty"] = np.float64(o[1])
+        for pref, m in (("t", tm), ("i", im)):
+            for k, prm in m.named_parameters():
+                out[f"s{it}.grad.{pref}.{k}"] = prm.grad.detach().clone().numpy()
+        tot = torch.nn.utils.clip_grad_norm_(params, 1.0, norm_type=2)
+        out[f"s{it}.total_norm"] = np.float64(tot.item())
+        lr = get_lr_cosine_schedule(it, lr_max, lr_min, 0, total_iters)
+        opt.set_lr(lr)
+        opt.step()
+        out.update({f"s{it}.post.{k}": v for k, v in flat_state(tm, "t").items()})
+        out.update({f"s{it}.post.{k}": v for k, v in flat_state(im, "i").items()})
+    out["meta"] = np.array([L, d, B, nsteps, total_iters], dtype=np.int64)
+    out["hyper"] = np.array([p, penalty, lr_max, lr_min])
+    np.savez_compressed(os.path.join(HERE, name), **out)
+    print("wrote", name)
+
+
+def guide_curve_fixture(steps, p=0.2, B=128, total_iters=3000, penalty=1e-3, lr_max=1e-3, lr_min=1e-6):
+    """Guided default config (exp_clip_guidedTF.sh) ploss/loss history."""
+    s = make_sampler(p)
+    seed_everything(224)
+    tm, im = build_guided(81, 5, 128)
+    loss = GuidedClipLoss(4, B, penalty=penalty, guide=True)
+    loss_nop = GuidedClipLoss(4, B, penalty=0, guide=False)
+    params = list(tm.parameters()) + list(im.parameters())
+    opt = AdamW(params=params, lr=None)
+    hist, phist, pen = np.zeros(steps), np.zeros(steps), np.zeros(steps)
+    t0 = time.time()
+    for it in range(steps):
+        opt.zero_grad()
+        rt, ri = s.get_batch(device="cpu", batch_size=B, guide=True)
+        to = tm(rt[0]); io = im(ri[0])
+        o = loss(to, io, [rt[2], ri[2]])
+        onop = loss_nop(to, io, [rt[2], ri[2]])
+        o[0].backward()
+        phist[it], hist[it], pen[it] = o[0].item(), onop[0].item(), o[1]
+        torch.nn.utils.clip_grad_norm_(params, 1.0, norm_type=2)
+        opt.set_lr(get_lr_cosine_schedule(it, lr_max, lr_min, 0, total_iters))
+        opt.step()
+        if it % 20 == 0:
+            print(f"guide curve step {it} ploss {phist[it]:.6f} loss {hist[it]:.6f} ({time.time()-t0:.0f}s)",
+                  flush=True)
+    np.savez_compressed(os.path.join(HERE, "guide_curve.npz"), loss_history=hist, ploss_history=phist,
+                        penalty=pen, p=p, B=B, total_iters=total_iters,
+                        hyper=np.array([penalty, lr_max, lr_min]), threads=torch.get_num_threads())
+    print("wrote guide_curve.npz")
+
+
 def bayes_fixture():
     with open(os.path.join(REF, "figures/data/ghm-data/clip-risk.json")) as f:
         d = json.load(f)
@@ -179,6 +295,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--curve-steps", type=int, default=200)
     ap.add_argument("--only", default="")
+    ap.add_argument("--guide-steps", type=int, default=100)
     a = ap.parse_args()
     jobs = a.only.split(",") if a.only else ["sampler", "tiny", "d128", "bayes", "curve"]
     if "sampler" in jobs:
@@ -192,3 +309,9 @@ if __name__ == "__main__":
         bayes_fixture()
     if "curve" in jobs:
         curve_fixture(a.curve_steps)
+    if "guide_bp" in jobs:
+        guide_bp_fixture()
+    if "guide_tiny" in jobs:
+        guide_step_fixture("guide_tiny.npz")
+    if "guide_curve" in jobs:
+        guide_curve_fixture(a.guide_steps)

@@ -257,3 +257,120 @@ def test_default_config_curve_vs_reference(precision):
     dev = np.abs(hist - ref)
     print(f"default-config curve [{precision}]: {n} steps, max |dloss| = {dev.max():.3e}, final {hist[-1]:.6f} vs {ref[-1]:.6f}")
     assert dev.max() <= 1e-4
+
+
+# ----------------------------------------------------------------------------
+# guided CLIP (clip_guide=True)
+# ----------------------------------------------------------------------------
+def test_bp_cls_kernel_matches_reference():
+    """ghm_bp_cls == the reference's BP_CLS + guided_info messages (guide_bp.npz)."""
+    from ghmclip import _native
+    g = np.load(os.path.join(GOLDEN, "guide_bp.npz"))
+    for pref in ("t", "i"):
+        trans = torch.from_numpy(np.ascontiguousarray(g[f"{pref}_transition"])).to(DEV)
+        leaves = torch.from_numpy(np.ascontiguousarray(g[f"{pref}_leaves"])).to(DEV)  # stored Fortran-order
+        N = leaves.shape[0]
+        msgs = torch.empty(N, 40, 10, dtype=torch.float32, device=DEV)
+        _native.call("ghm_bp_cls", trans.data_ptr(), leaves.data_ptr(), msgs.data_ptr(), N, 4, 3, 10,
+                     torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        off = 0
+        for k in range(4):
+            want = g[f"{pref}_msg{k}"]
+            got = msgs[:, off:off + want.shape[1]].cpu().numpy()
+            np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-6)
+            off += want.shape[1]
+
+
+def _guided_trainer(L, B, precision, total_iters=3000):
+    from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
+    from ghmclip.training.clip_trainer import ClipTrainer
+    p_y = np.ones(10) / 10
+    sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    seed_everything(224)
+    mk = lambda: EncoderTransformer(81, 10, 128, L, n_guided_layer=4, guide=True)  # noqa: E731
+    tm, im = mk().to(DEV), mk().to(DEV)
+    sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters + 1)]
+    tr = ClipTrainer(tm, im, 4, B, sched, device=DEV, precision=precision, penalty=1e-3,
+                     guide_trans=(sampler.t_templ, sampler.i_templ))
+    return sampler, tr
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_guided_steps_vs_oracle(precision):
+    """Fused guided step (on-device BP targets + penalty) == the oracle's guided
+    step (itself pinned to the reference by tests/golden/guide_tiny.npz)."""
+    sampler, tr = _guided_trainer(5, 4, precision)
+    ref = O.OracleTrainer(p=0.2, B=4, L=5, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3)
+    gpu_params = list(tr.tm.parameters()) + list(tr.im.parameters())
+    for it in range(2):
+        tl, _, il, _ = sampler.draw_numpy(4)
+        tr.set_tokens(torch.from_numpy(tl), torch.from_numpy(il))
+        tr.step()
+        ploss, _ = ref.step(batch=(tl.astype(np.int64), None, il.astype(np.int64), None))
+        torch.cuda.synchronize()
+        assert abs(tr.loss_history()[it] - ref.last_loss_nop) < 1e-5
+        assert abs(tr.ploss_history()[it] - ploss) <= 1e-5 * abs(ploss)
+        # gradients of this step: the oracle's are clipped in place, the trainer's
+        # stay raw with the clip coefficient in hyper[1] (ghm_clip_prepare)
+        coef = tr.hyper[1].item()
+        for p_gpu, p_ref in zip(gpu_params, ref.params):
+            assert _rel(p_gpu.grad * coef, p_ref.grad) < GRAD_TOL[precision]
+    if precision == "f32":
+        # (x3: Adam turns noise-level gradient differences of near-zero entries
+        # into +-lr steps at the guided lr of 1e-3, so parameters are not compared)
+        for p_gpu, p_ref in zip(gpu_params, ref.params):
+            assert _rel(p_gpu, p_ref) < 1e-4
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_guided_curve_vs_reference(precision):
+    """Guided default config (exp_clip_guidedTF.sh) vs the reference's own run on
+    identical GHM draws: penalty-free loss within 1e-4, penalised loss within 1e-4
+    relative (it starts at ~650)."""
+    g = np.load(os.path.join(GOLDEN, "guide_curve.npz"))
+    ref, pref = g["loss_history"], g["ploss_history"]
+    n = len(ref)
+    sampler, tr = _guided_trainer(5, 128, precision)
+    hist = _run(sampler, tr, 128, n, graph_after=3)
+    ph = tr.ploss_history()
+    dev = np.abs(hist - ref)
+    pdev = np.abs(ph - pref) / np.abs(pref)
+    print(f"guided curve [{precision}]: {n} steps, max |dloss| = {dev.max():.3e}, "
+          f"max rel |dploss| = {pdev.max():.3e}")
+    assert dev.max() <= 1e-4
+    assert pdev.max() <= 1e-4
+
+
+def test_guided_module_api():
+    """EncoderTransformer(guide=True) returns H_{l+1}[:, :, :10] of the flagged
+    layers, and GuidedClipLoss(guide=True) matches the oracle's value and grads."""
+    from ghmclip import EncoderTransformer, GuidedClipLoss
+    B, K, L = 4, 4, 5
+    N = B * (K + 1)
+    torch.manual_seed(3)
+    tp = EncoderTransformer(81, 10, 128, L, n_guided_layer=4, guide=True)
+    ip = EncoderTransformer(81, 10, 128, L, n_guided_layer=4, guide=True)
+    torch.manual_seed(3)
+    tr_, ir_ = O.OracleEncoder(81, 10, 128, L, guide=True), O.OracleEncoder(81, 10, 128, L, guide=True)
+    tp.precision = ip.precision = "f32"
+    tp, ip = tp.to(DEV), ip.to(DEV)
+    gen = torch.Generator().manual_seed(4)
+    xt = torch.randint(0, 10, (N, 81), generator=gen)
+    xi = torch.randint(0, 10, (N, 81), generator=gen)
+    targets = [[torch.randn(N, 81, 10, generator=gen) for _ in range(4)] for _ in range(2)]
+    to, io = tp(xt.to(DEV)), ip(xi.to(DEV))
+    assert len(to[1]) == 4
+    lossf = GuidedClipLoss(K, B, penalty=1e-3, guide=True)
+    loss, pen = lossf(to, io, [[t.to(DEV) for t in targets[0]], [t.to(DEV) for t in targets[1]]])
+    loss.backward()
+    rt, ri = tr_(xt), ir_(xi)
+    for a, b in zip(to[1], rt[1]):
+        assert _rel(a, b) < 2e-5
+    rl = O.clip_loss(rt[0], ri[0], K, B)
+    rpen, rpen_v = O.guide_penalty(rt[1], ri[1], targets[0], targets[1], 1e-3)
+    (rl + rpen).backward()
+    assert abs(loss.item() - (rl + rpen).item()) <= 1e-5 * abs((rl + rpen).item())
+    assert abs(pen - rpen_v) <= 1e-5 * abs(rpen_v)
+    for (k, a), (_, b) in zip(tp.named_parameters(), tr_.named_parameters()):
+        assert _rel(a.grad, b.grad) < 1e-4, k

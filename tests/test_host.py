@@ -129,3 +129,21 @@ def test_bayes_product_matches_published():
     s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
     bayes, _ = s.get_Bayes(10000)
     np.testing.assert_allclose(bayes, d["Bayes"][9], rtol=1e-12)
+
+
+def test_guided_targets_host_match_reference():
+    """ClipSampler.get_batch(guide=True)'s host BP targets == the reference's
+    guided_info on its own draws (tests/golden/guide_bp.npz)."""
+    import numpy as np
+    from ghmclip.data.data_random_GHM import bp_cls_posterior, guided_targets
+    g = np.load(os.path.join(GOLDEN, "guide_bp.npz"))
+    for pref in ("t", "i"):
+        leaves = g[f"{pref}_leaves"]
+        tg = guided_targets(g[f"{pref}_transition"], leaves, "cpu")
+        assert len(tg) == 4
+        for k, t in enumerate(tg):
+            want = g[f"{pref}_msg{k}"]
+            ext = 81 // want.shape[1]
+            np.testing.assert_allclose(t.numpy(), np.repeat(want, ext, axis=1), rtol=1e-6, atol=1e-6)
+        pp = bp_cls_posterior(g[f"{pref}_transition"], leaves, np.ones(10) / 10)
+        np.testing.assert_allclose(pp, g[f"{pref}_pp"], rtol=1e-10, atol=1e-12)

@@ -116,3 +116,47 @@ def test_default_curve_prefix():
     for it in range(3):
         loss, _ = tr.step()
         assert abs(loss - g["loss_history"][it]) < 1e-5
+
+
+# ----------------------------------------------------------------------------
+# guided CLIP (clip_guide=True): BP guide targets and the Frobenius penalty
+# ----------------------------------------------------------------------------
+def test_guide_bp_messages_match_reference():
+    """bp_cls_messages == GHMTree.BP_CLS + guided_info (data_random_GHM.py:185-221,
+    526-549) on the reference's own draws, and the posteriors match BP_CLS."""
+    g = _load("guide_bp.npz")
+    for pref in ("t", "i"):
+        trans = g[f"{pref}_transition"]
+        leaves = g[f"{pref}_leaves"].astype(np.int64)
+        msgs = O.bp_cls_messages(trans, leaves)
+        assert len(msgs) == 4
+        for k, m in enumerate(msgs):
+            want = g[f"{pref}_msg{k}"]
+            assert m.shape == want.shape
+            np.testing.assert_allclose(m.astype(np.float32), want, rtol=1e-6, atol=1e-6)
+        pp = O.bp_cls_posterior(trans, leaves, np.ones(10) / 10)
+        np.testing.assert_allclose(pp, g[f"{pref}_pp"], rtol=1e-10, atol=1e-12)
+
+
+def test_guided_training_steps():
+    """Two guided CLIP steps (exp_clip_guidedTF.sh hyper-parameters, L=5, d=16, B=4)."""
+    g = _load("guide_tiny.npz")
+    L, d, B, nsteps, total = [int(x) for x in g["meta"]]
+    p, penalty, lr_max, lr_min = [float(x) for x in g["hyper"]]
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    tr = O.OracleTrainer(p=p, B=B, L=L, d=d, total_iters=total, lr_max=lr_max, lr_min=lr_min,
+                         guide=True, penalty=penalty)
+    assert tr.tm.guided_layer_flag == [True, True, True, True, False]
+    for pref, m in (("t", tr.tm), ("i", tr.im)):
+        for k, v in m.state_dict().items():
+            np.testing.assert_array_equal(v.numpy(), g[f"init.{pref}.{k}"])
+    for it in range(nsteps):
+        batch = tr.sampler.get_batch(B)
+        np.testing.assert_array_equal(batch[0], g[f"s{it}.t_leaves"])
+        ploss, _ = tr.step(batch=batch)
+        np.testing.assert_allclose(tr.last_loss_nop, float(g[f"s{it}.loss_nop"]), rtol=1e-6)
+        np.testing.assert_allclose(ploss, float(g[f"s{it}.loss"]), rtol=1e-6)
+        np.testing.assert_allclose(tr.last_penalty, float(g[f"s{it}.penalty"]), rtol=1e-5)
+        for pref, m in (("t", tr.tm), ("i", tr.im)):
+            for k, v in m.state_dict().items():
+                np.testing.assert_allclose(v.numpy(), g[f"s{it}.post.{pref}.{k}"], rtol=1e-5, atol=1e-7)
