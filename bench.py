@@ -83,7 +83,7 @@ def make_ring(sampler, B, R):
 
 def dominant_kernel(trainer):
     """(name, launch) of the step's dominant kernel — the encoder-layer LN2+MLP
-    forward (k_ln_mlp_fwd / k_ln_mlp_fwd_x3) of layer 0 — launched on the
+    forward (k_ln_mlp_fwd / k_ln_mlp_fwd_x3b) of layer 0 — launched on the
     current stream with the trainer's own buffers."""
     from ghmclip import _native
     import ctypes
@@ -93,10 +93,10 @@ def dominant_kernel(trainer):
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     if plan.precision == "x3":
         def launch():
-            _native.call("ghm_ln_mlp_fwd_x3", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
+            _native.call("ghm_ln_mlp_fwd_x3b", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                          ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]),
                          ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
-        return "k_ln_mlp_fwd_x3", launch
+        return "k_ln_mlp_fwd_x3b", launch
 
     def launch():
         _native.call("ghm_ln_mlp_fwd", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),

@@ -149,7 +149,7 @@ int ghm_adamw(float* param, const float* grad, float* m, float* v, int64_t n, co
  * matrix-core rate.  Weights come from a per-layer "pack" of pre-split bf16
  * planes written by ghm_split_weights (GHM_SPLIT_PACK_ELEMS bf16 per layer,
  * 16-byte aligned); re-split after every parameter update. */
-#define GHM_SPLIT_PACK_ELEMS 720896
+#define GHM_SPLIT_PACK_ELEMS 983040
 #define GHM_SPLIT_MAX_JOBS 16
 typedef struct ghm_split_job {
   const float* Wq;  /* [128][128] each, nn.Linear layout [out][in] */

@@ -31,6 +31,24 @@ __device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x
   return mfma_bf(ah, bh, c);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16x16x32 bf16: lane l holds A[row l&15][k = 8(l>>4) + i], B[k = 8(l>>4) + i][col l&15];
+// C/D: col = l&15, row = 4(l>>4) + r
+__device__ __forceinline__ f32x4 mfma16_bf(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl, f32x4 c) {
+  c = mfma16_bf(al, bh, c);
+  c = mfma16_bf(ah, bl, c);
+  return mfma16_bf(ah, bh, c);
+}
+__device__ __forceinline__ f32x4 zero4() {
+  f32x4 z;
+  z[0] = z[1] = z[2] = z[3] = 0.f;
+  return z;
+}
+
 __device__ __forceinline__ void split1(float x, __bf16& hi, __bf16& lo) {
   hi = static_cast<__bf16>(x);
   lo = static_cast<__bf16>(x - static_cast<float>(hi));

@@ -24,13 +24,21 @@ constexpr int PK_W1_N = 4 * PK_QKV;        // [512][128]: W1[f][d]
 constexpr int PK_W1_T = PK_W1_N + 2 * PK_W;  // [128][512]: row d, col q           = W1[perm(q)][d]
 constexpr int PK_W2_P = PK_W1_T + 2 * PK_W;  // [128][512]: row o, col q           = W2[o][perm(q)]
 constexpr int PK_W2_T = PK_W2_P + 2 * PK_W;  // [512][128]: row f, col o           = W2[o][f]
-constexpr int PK_ELEMS = PK_W2_T + 2 * PK_W;  // 720896
+constexpr int PK_W1_T32 = PK_W2_T + 2 * PK_W;   // [128][512]: row d, col q          = W1[perm32(q)][d]
+constexpr int PK_W2_P32 = PK_W1_T32 + 2 * PK_W;  // [128][512]: row o, col q          = W2[o][perm32(q)]
+constexpr int PK_ELEMS = PK_W2_P32 + 2 * PK_W;   // 983040
 static_assert(PK_ELEMS == GHM_SPLIT_PACK_ELEMS, "pack layout mismatch with include/ghm_hip.h");
 
 // column permutation inside each 16-group for operands met by an accumulator
 // tile (ghm_split.h): position q holds original column perm_col(q)
 __device__ __forceinline__ constexpr int perm_col(int q) {
   return (q & ~15) + (q & 3) + 8 * ((q >> 2) & 1) + 4 * ((q >> 3) & 1);
+}
+
+// the same for 16x16x32 accumulator operands (ghm_split.h, 16-token tiles):
+// k-slot 8g + i of a 32-group holds unit 4g + i (i < 4) or 16 + 4g + i - 4
+__device__ __forceinline__ constexpr int perm32(int q) {
+  return (q & ~31) + ((q & 7) < 4 ? 4 * ((q >> 3) & 3) + (q & 3) : 16 + 4 * ((q >> 3) & 3) + (q & 3));
 }
 
 struct SplitJobs {
@@ -69,11 +77,21 @@ __global__ __launch_bounds__(256) void k_split_weights(SplitJobs J) {
     const int o = idx >> 9, q = idx & 511;
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = jb.W2[o * GHM_F + perm_col(q + t)];
-  } else {
+  } else if (e < 2 * PK_QKV + 4 * PK_W) {
     idx = e - 2 * PK_QKV - 3 * PK_W; base = PK_W2_T; n = PK_W;
     const int f = idx >> 7, o = idx & 127;
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = jb.W2[(o + t) * GHM_F + f];
+  } else if (e < 2 * PK_QKV + 5 * PK_W) {
+    idx = e - 2 * PK_QKV - 4 * PK_W; base = PK_W1_T32; n = PK_W;
+    const int d = idx >> 9, q = idx & 511;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = jb.W1[perm32(q + t) * GHM_D + d];
+  } else {
+    idx = e - 2 * PK_QKV - 5 * PK_W; base = PK_W2_P32; n = PK_W;
+    const int o = idx >> 9, q = idx & 511;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = jb.W2[o * GHM_F + perm32(q + t)];
   }
   bf16x4 hi, lo;
   split4(make_float4(v[0], v[1], v[2], v[3]), hi, lo);
@@ -297,6 +315,180 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd_x3(
         st4(Hout + m * GHM_D + 32 * ot + quad_off(q, h), hv[q].x + (y[ot][4 * q] + bv[q].x),
             hv[q].y + (y[ot][4 * q + 1] + bv[q].y), hv[q].z + (y[ot][4 * q + 2] + bv[q].z),
             hv[q].w + (y[ot][4 * q + 3] + bv[q].w));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA (global_load_lds_dwordx4) weight tiles: one wave-instruction writes
+// 64 x 16 B lane-linearly, so images are unpadded and XOR-swizzled on 16-byte
+// chunks; the swizzle goes on each lane's SOURCE address and again on the read
+// (conflict-free ds_read_b128):
+//   R32  [32 rows][128] (256-B rows):  chunk c of row r at c ^ (r & 15)
+//   R128 [128 rows][32] (64-B rows):   chunk c of row r at c ^ ((r >> 2) & 3)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void glds16(const __bf16* src, __bf16* lds_base) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
+                                   (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
+}
+constexpr int PLANE = 32 * GHM_D;  // bf16 elements of one tile plane (8 KB)
+__device__ __forceinline__ int r32_off(int row, int lc) { return row * 128 + 8 * (lc ^ (row & 15)); }
+__device__ __forceinline__ int r128_off(int row, int lc) { return row * 32 + 8 * (lc ^ ((row >> 2) & 3)); }
+
+// ---------------------------------------------------------------------------
+// 16-token-per-wave variant of LN2 + MLP (v_mfma_f32_16x16x32_bf16).
+// Lane l = (token t = l & 15, group g = l >> 4); a wave owns 16 tokens, a
+// 512-thread workgroup 128.  The token row enters as the B operand in 4 k-steps
+// of 32 features (lane holds features 32s + 8g + i); accumulators hold 4
+// consecutive features 4g + r of a 16-row tile, and a 32-unit hidden chunk
+// (two tiles) is the B operand of the down-projection with the perm32 k order
+// (weights pre-permuted in the pack).  Weight tiles arrive by LDS-DMA (one
+// instruction per wave per plane); the barrier waits only for them (counted
+// vmcnt), every lane stores to a real row (lanes past M recompute row M-1), so
+// each wave has exactly 4 stores in flight per chunk.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fill_r32_w8(const __bf16* g, int ldg, int lo_off, __bf16* ih, __bf16* il) {
+  const int b = threadIdx.x >> 6, L = threadIdx.x & 63;
+  const int row = 4 * b + (L >> 4), lc = (L & 15) ^ (row & 15);
+  const __bf16* src = g + row * ldg + 8 * lc;
+  glds16(src, ih + 512 * b);
+  glds16(src + lo_off, il + 512 * b);
+}
+__device__ __forceinline__ void fill_r128_w8(const __bf16* g, int ldg, int lo_off, __bf16* ih, __bf16* il) {
+  const int b = threadIdx.x >> 6, L = threadIdx.x & 63;
+  const int row = 16 * b + (L >> 2), lc = (L & 3) ^ ((row >> 2) & 3);
+  const __bf16* src = g + row * ldg + 8 * lc;
+  glds16(src, ih + 512 * b);
+  glds16(src + lo_off, il + 512 * b);
+}
+
+// pick element 4g + r of a wave-uniform 16-float group (scalar registers)
+__device__ __forceinline__ float pick16(const float4* b4, int g, int r) {
+  const float v0 = (&b4[0].x)[r], v1 = (&b4[1].x)[r], v2 = (&b4[2].x)[r], v3 = (&b4[3].x)[r];
+  return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+}
+
+__global__ __launch_bounds__(512, 2) void k_ln_mlp_fwd_x3b(
+    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
+    float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
+    int64_t M, float eps) {
+  // ONE __shared__ object: [W1 hi|lo][W2 hi|lo] x 2 buffers
+  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE];
+  auto s1h = [&](int buf) { return lds + 4 * PLANE * buf; };
+  auto s1l = [&](int buf) { return lds + 4 * PLANE * buf + PLANE; };
+  auto s2h = [&](int buf) { return lds + 4 * PLANE * buf + 2 * PLANE; };
+  auto s2l = [&](int buf) { return lds + 4 * PLANE * buf + 3 * PLANE; };
+  constexpr int NC = GHM_F / 32;
+  const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * 8 + (threadIdx.x >> 6)) * 16 + t;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W1 = pack + PK_W1_N;
+  const __bf16* W2 = pack + PK_W2_P32;
+  fill_r32_w8(W1, GHM_D, PK_W, s1h(0), s1l(0));
+  fill_r128_w8(W2, GHM_F, PK_W, s2h(0), s2l(0));
+  // LN2 of the token row, lane holds features 32s + 8g + i
+  bf16x8 xh[4], xl[4];
+  {
+    const float* row = Hmid + mc * GHM_D;
+    float x[32];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const float4 a = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g);
+      const float4 b = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g + 4);
+      x[8 * s2 + 0] = a.x; x[8 * s2 + 1] = a.y; x[8 * s2 + 2] = a.z; x[8 * s2 + 3] = a.w;
+      x[8 * s2 + 4] = b.x; x[8 * s2 + 5] = b.y; x[8 * s2 + 6] = b.z; x[8 * s2 + 7] = b.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) sm += x[k];
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    const float mean = sm * (1.f / 128.f);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float d = x[k] - mean;
+      v += d * d;
+    }
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const float rstd = 1.f / sqrtf(v * (1.f / 128.f) + eps);
+    if (g == 0 && valid) stats[m] = make_float2(mean, rstd);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int f = 32 * s2 + 8 * g + i;
+        x[8 * s2 + i] = (x[8 * s2 + i] - mean) * rstd * lnw[f] + lnb[f];
+      }
+      split8(x + 8 * s2, xh[s2], xl[s2]);
+    }
+  }
+  f32x4 y[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = zero4();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const int cur = c & 1;
+    {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
+      const int cn = c + 1 < NC ? c + 1 : NC - 1;
+      fill_r32_w8(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
+      fill_r128_w8(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
+    }
+    f32x4 u[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      u[jt] = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int o = r32_off(16 * jt + t, 4 * s2 + g);
+        u[jt] = mfma16_x3(ldsb8(s1h(cur) + o), ldsb8(s1l(cur) + o), xh[s2], xl[s2], u[jt]);
+      }
+    }
+    float gv[8], dg[8];
+    {  // + b1 (wave-uniform scalar loads: no ordinary load beside the LDS-DMA)
+      const float4* bc = reinterpret_cast<const float4*>(b1 + 32 * c);
+      float4 bv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bv[k] = bc[k];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gv[4 * jt + r] = u[jt][r] + pick16(bv + 4 * jt, g, r);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) gelu_fast(gv[r], gv[r], dg[r]);
+    {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward: 4 stores per wave
+      float* grow = G + mc * GHM_F + 32 * c + 4 * g;
+      float* drow = Dg + mc * GHM_F + 32 * c + 4 * g;
+      st4(grow, gv[0], gv[1], gv[2], gv[3]);
+      st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
+      st4(drow, dg[0], dg[1], dg[2], dg[3]);
+      st4(drow + 16, dg[4], dg[5], dg[6], dg[7]);
+    }
+    bf16x8 gh, gl;
+    split8(gv, gh, gl);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = r128_off(16 * j + t, g);
+      y[j] = mfma16_x3(ldsb8(s2h(cur) + o), ldsb8(s2l(cur) + o), gh, gl, y[j]);
+    }
+    // retire this iteration's 4 LDS-DMA fills (issued before the 4 stores)
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (valid) {
+    const float* hr = Hmid + m * GHM_D;
+    float* orow = Hout + m * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
+      st4(orow + f, hv.x + (y[j][0] + bv.x), hv.y + (y[j][1] + bv.y), hv.z + (y[j][2] + bv.z),
+          hv.w + (y[j][3] + bv.w));
     }
   }
 }
@@ -1027,5 +1219,16 @@ extern "C" int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH
     hipLaunchKernelGGL(k_attn_bwd_q_x3<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
     hipLaunchKernelGGL(k_attn_bwd_kv_x3<3>, dim3(g), dim3(192), 0, s, qkv, P, dS, dH_mid, dqkv, T);
   }
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                                  const float* b1, const float* b2, float* H_out, float* G, float* Dg,
+                                  float* stats, int64_t M, int D, int F, float eps, void* stream) {
+  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && G && Dg && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  hipLaunchKernelGGL(k_ln_mlp_fwd_x3b, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
+                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1, b2,
+                     H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
   return ghm_launch_status();
 }

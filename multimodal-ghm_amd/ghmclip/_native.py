@@ -28,7 +28,7 @@ class SplitJob(ctypes.Structure):
                 ("W1", ctypes.c_void_p), ("W2", ctypes.c_void_p), ("pack", ctypes.c_void_p)]
 
 
-GHM_SPLIT_PACK_ELEMS = 720896  # include/ghm_hip.h
+GHM_SPLIT_PACK_ELEMS = 983040  # include/ghm_hip.h
 
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -58,6 +58,7 @@ HIP_SIGNATURES = {
     "ghm_split_weights": [_p, _i, _p],
     "ghm_ln_qkv_fwd_x3": [_p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_mlp_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_qkv_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_wgrad_x3": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],

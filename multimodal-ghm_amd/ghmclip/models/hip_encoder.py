@@ -11,7 +11,7 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input)
   G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (backward inputs)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
-  pack [L, 720896] bf16 (precision "x3" only): per-layer pre-split weight planes
+  pack [L, 983040] bf16 (precision "x3" only): per-layer pre-split weight planes
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
 [M, 384], dU [M, 512], and split-K / per-block partial buffers.
 """
@@ -164,7 +164,7 @@ class EncoderPlan:
                   pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
                 c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   N, T, D_MODEL, self.scale_div, s)
-                c("ghm_ln_mlp_fwd_x3", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
                   _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL,
                   D_HIDDEN, self.eps, s)

@@ -86,6 +86,8 @@ def main():
         "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
                       None),
     }
+    xo = {"H": torch.empty_like(plan.H[l + 1]), "G": torch.empty_like(plan.G[l]), "Dg": torch.empty_like(plan.Dg[l]),
+          "st": torch.empty_like(plan.st2[l])}
     if plan.pack is not None:
         pk = P(plan.pack[l])
         kernels.update({
@@ -95,6 +97,10 @@ def main():
                                         P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
                                         P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
                                         plan.eps, sp), gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3b": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                         P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
+                                         P(xo["H"]), P(xo["G"]), P(xo["Dg"]), P(xo["st"]), M, 128, 512,
+                                         plan.eps, sp), gf(4 * M * 128 * 512)),
             "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                      P(p["_lns_2.0.weight"]), pk, P(plan.Dg[l]), P(plan.dU), P(plan.dH[1]),
                                      P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
@@ -133,6 +139,13 @@ def main():
         res[name] = {"us": round(us, 2), "gflop": gflop, "mfma_frac": round(frac, 4) if frac else None}
         print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
               flush=True)
+    if "ln_mlp_fwd_x3b" in res:  # variant vs the production kernel on the same inputs
+        kernels["ln_mlp_fwd_x3"][0]()
+        torch.cuda.synchronize()
+        for k, ref in (("H", plan.H[l + 1]), ("G", plan.G[l]), ("Dg", plan.Dg[l]), ("st", plan.st2[l])):
+            d = (xo[k] - ref).abs().max().item() / ref.abs().max().item()
+            print(f"x3b vs x3 {k}: max rel-to-maxabs diff {d:.3e}", flush=True)
+            res["ln_mlp_fwd_x3b"]["diff_" + k] = d
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
