@@ -168,6 +168,11 @@ int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, cons
 int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                       const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
                       int64_t M, int D, int F, float eps, void* stream);
+/* Same contract and results as ghm_ln_mlp_fwd_x3 (model.py:741-747,784-788), 16 tokens per
+   wave on v_mfma_f32_16x16x32_bf16 (the variant the trainer launches). */
+int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                       const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
+                       int64_t M, int D, int F, float eps, void* stream);
 /* As ghm_mlp_bwd (backward of model.py:784-788); Dg = GELU'(U) from the forward. */
 int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                    const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln, int64_t M,

@@ -140,6 +140,7 @@ def main():
         print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
               flush=True)
     if "ln_mlp_fwd_x3b" in res:  # variant vs the production kernel on the same inputs
+        kernels["ln_mlp_fwd_x3b"][0]()  # both on the current Hmid (later kernels rewrote it)
         kernels["ln_mlp_fwd_x3"][0]()
         torch.cuda.synchronize()
         for k, ref in (("H", plan.H[l + 1]), ("G", plan.G[l]), ("Dg", plan.Dg[l]), ("st", plan.st2[l])):
