@@ -43,6 +43,21 @@ int ghm_sampler_get_state(const ghm_sampler* s, uint32_t* key, int* pos);
 int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves,
                      uint8_t* t_root, uint8_t* i_root);
 
+/* One ConditionalDenoiseSampler.get_batch(batch_size=B) draw
+ * (data_random_GHM.py:854-869; replaces the per-node Python loop and np.random.randn):
+ *   t_leaves, i_leaves : [B][n_child**n_layer] uint8 (trees sharing one root per row)
+ *   root               : [B] uint8 (may be NULL)
+ *   z                  : [B][n_child**n_layer] float64 noisy image observations
+ *                        randn * sigma + leaf (the reference's image_tree_noise, transposed)
+ * Stream order: choice(V, B), text tree, image tree, randn(T, B) leaf-major. */
+int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t* t_leaves, uint8_t* i_leaves,
+                         uint8_t* root, double* z);
+/* numpy legacy Gaussian cache (RandomState.get_state()[3:5]): import / export. */
+int ghm_sampler_set_gauss(ghm_sampler* s, int has_gauss, double gauss);
+int ghm_sampler_get_gauss(const ghm_sampler* s, int* has_gauss, double* gauss);
+/* n draws of numpy.random.randn() (legacy polar method, cached second deviate). */
+int ghm_sampler_randn(ghm_sampler* s, double* out, int64_t n);
+
 /* Raw stream access for tests: n doubles of numpy.random.random_sample(). */
 int ghm_sampler_random_sample(ghm_sampler* s, double* out, int64_t n);
 /* n draws of numpy.random.choice(V) (legacy masked rejection). */

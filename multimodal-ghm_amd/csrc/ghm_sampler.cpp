@@ -1,12 +1,14 @@
 // Native host GHM sampler: numpy-legacy-compatible MT19937 stream + inverse-CDF
-// tree sampling.  Behaviour follows the reference producer
-//   ClipSampler.get_batch  src/ghmclip/data/data_random_GHM.py:753-784
-//   GHMTree.gen_values     src/ghmclip/data/data_random_GHM.py:145-165
+// tree sampling.  Behaviour follows the reference producers
+//   ClipSampler.get_batch                src/ghmclip/data/data_random_GHM.py:753-784
+//   ConditionalDenoiseSampler.get_batch  src/ghmclip/data/data_random_GHM.py:854-869
+//   GHMTree.gen_values                   src/ghmclip/data/data_random_GHM.py:145-165
 // The per-node Python loop of the reference becomes one pass per (layer, child
 // slot) over a contiguous uint8 value plane; the RNG stream is consumed in the
 // reference's exact order (BFS parent, child slot, batch element).
 #include "../../include/ghm_sampler.h"
 
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -79,8 +81,31 @@ struct ghm_sampler {
   // cdf[tree][layer][child][row][col], cumulative sums in the reference's order
   std::vector<double> cdf;
   MT19937 mt;
+  int has_gauss = 0;  // numpy legacy Gaussian cache (RandomState state[3], state[4])
+  double gauss = 0.0;
   std::vector<uint8_t> plane_a, plane_b;  // [n_nodes][rows] value planes
 };
+
+// numpy legacy_gauss: polar Box-Muller on random_sample pairs, the second
+// deviate cached for the next call (randn / normal consume this stream).
+static double legacy_gauss(ghm_sampler* s) {
+  if (s->has_gauss) {
+    s->has_gauss = 0;
+    const double g = s->gauss;
+    s->gauss = 0.0;
+    return g;
+  }
+  double x1, x2, r2;
+  do {
+    x1 = 2.0 * s->mt.next_double() - 1.0;
+    x2 = 2.0 * s->mt.next_double() - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+  } while (r2 >= 1.0 || r2 == 0.0);
+  const double f = std::sqrt(-2.0 * std::log(r2) / r2);
+  s->gauss = f * x1;
+  s->has_gauss = 1;
+  return f * x2;
+}
 
 static void build_cdf(const double* trans, int n_layer, int n_child, int V, double* out) {
   const int nm = n_layer * n_child;
@@ -196,5 +221,48 @@ extern "C" int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_
   sample_tree(s, s->cdf.data() + per, ir.data(), rows, i_leaves);
   if (t_root) std::memcpy(t_root, tr.data(), rows);
   if (i_root) std::memcpy(i_root, ir.data(), rows);
+  return 0;
+}
+
+extern "C" int ghm_sampler_set_gauss(ghm_sampler* s, int has_gauss, double gauss) {
+  if (!s) return -1;
+  s->has_gauss = has_gauss ? 1 : 0;
+  s->gauss = gauss;
+  return 0;
+}
+
+extern "C" int ghm_sampler_get_gauss(const ghm_sampler* s, int* has_gauss, double* gauss) {
+  if (!s || !has_gauss || !gauss) return -1;
+  *has_gauss = s->has_gauss;
+  *gauss = s->gauss;
+  return 0;
+}
+
+extern "C" int ghm_sampler_randn(ghm_sampler* s, double* out, int64_t n) {
+  if (!s || (!out && n)) return -1;
+  for (int64_t i = 0; i < n; ++i) out[i] = legacy_gauss(s);
+  return 0;
+}
+
+// ConditionalDenoiseSampler.get_batch (guide=False) draws, in the reference's
+// stream order: choice(V, B) shared roots (:863), the text tree (:865), the image
+// tree (:866), then np.random.randn(T, B) * sigma + leaves (:869) — drawn
+// leaf-major ([T][B] C order) and written transposed as z[b][t] (the .T at :882).
+extern "C" int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t* t_leaves,
+                                    uint8_t* i_leaves, uint8_t* root, double* z) {
+  if (!s || B < 1 || !t_leaves || !i_leaves || !z) return -1;
+  const int V = s->V, T = s->T;
+  std::vector<uint8_t> r(B);
+  for (int b = 0; b < B; ++b) r[b] = static_cast<uint8_t>(s->mt.bounded(V - 1));
+  const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * V * V;
+  sample_tree(s, s->cdf.data(), r.data(), B, t_leaves);
+  sample_tree(s, s->cdf.data() + per, r.data(), B, i_leaves);
+  for (int t = 0; t < T; ++t) {
+    for (int b = 0; b < B; ++b) {
+      const double g = legacy_gauss(s);
+      z[static_cast<size_t>(b) * T + t] = g * sigma + static_cast<double>(i_leaves[static_cast<size_t>(b) * T + t]);
+    }
+  }
+  if (root) std::memcpy(root, r.data(), B);
   return 0;
 }

@@ -84,6 +84,10 @@ HOST_SIGNATURES = {
     "ghm_sampler_next": [_p, _i, _p, _p, _p, _p],
     "ghm_sampler_random_sample": [_p, _p, _i64],
     "ghm_sampler_choice": [_p, _i, _i64, _p],
+    "ghm_sampler_next_cdm": [_p, _i, ctypes.c_double, _p, _p, _p, _p],
+    "ghm_sampler_set_gauss": [_p, _i, ctypes.c_double],
+    "ghm_sampler_get_gauss": [_p, _p, _p],
+    "ghm_sampler_randn": [_p, _p, _i64],
 }
 _HOST_RESTYPE = {"ghm_sampler_create": ctypes.c_void_p, "ghm_sampler_destroy": None}
 

@@ -18,7 +18,7 @@ import torch
 from .. import _native
 
 __all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior", "guided_targets",
-           "NativeClipSampler"]
+           "NativeClipSampler", "ConditionalDenoiseSampler", "bp_dns_posterior", "bp_cls_root_message"]
 
 
 def _softmax_row(x):
@@ -103,16 +103,31 @@ class NativeClipSampler:
         _native_check(rc)
 
     # numpy global-state bridge -------------------------------------------------
+    def next_cdm_into(self, B, sigma, t_leaves, i_leaves, z, root=None):
+        """ConditionalDenoiseSampler draw into caller-owned buffers: uint8 [B, T]
+        leaves, float64 [B, T] noisy observations z, optional uint8 [B] roots."""
+        rc = self._lib.ghm_sampler_next_cdm(self._h, B, float(sigma), _addr(t_leaves), _addr(i_leaves),
+                                            _addr(root) if root is not None else None, _addr(z))
+        _native_check(rc)
+
+    def set_gauss(self, has_gauss, gauss):
+        _native_check(self._lib.ghm_sampler_set_gauss(self._h, int(has_gauss), float(gauss)))
+
+    def get_gauss(self):
+        h, g = ctypes.c_int(0), ctypes.c_double(0.0)
+        _native_check(self._lib.ghm_sampler_get_gauss(self._h, ctypes.byref(h), ctypes.byref(g)))
+        return h.value, g.value
+
     def pull_numpy_state(self):
         st = np.random.get_state()
         if st[0] != "MT19937":
             raise RuntimeError("unexpected numpy RNG")
-        self._np_extra = (st[3], st[4])
         self.set_state(st[1], st[2])
+        self.set_gauss(st[3], st[4])
 
     def push_numpy_state(self):
         key, pos = self.get_state()
-        has_gauss, cached = getattr(self, "_np_extra", (0, 0.0))
+        has_gauss, cached = self.get_gauss()
         np.random.set_state(("MT19937", key, pos, has_gauss, cached))
 
 
@@ -274,3 +289,101 @@ class ClipSampler(DoubleSampler):
         tp = bp_cls_posterior(self.t_templ, tl, p_y).T
         ip = bp_cls_posterior(self.i_templ, il, p_y).T
         return PPCLIPLoss(tp, ip, n_eval, self.K, self.variable_type)
+
+
+def bp_cls_root_message(templ, leaves):
+    """The max-shifted BP_CLS root message [V, B] (data_random_GHM.py:201-208) — the
+    text tree's evidence the conditional denoiser's image BP receives (:875-877)."""
+    return _bp_levels(templ, leaves)[-1][0]
+
+
+def bp_dns_posterior(templ, z, sigma, ext):
+    """BP_DNS (data_random_GHM.py:467-523) on the host, vectorised over the nodes of a
+    layer (translation invariance: node n uses its child-slot matrix n % C).
+    z: noisy leaf observations [n_leaves, B] float64; ext: external root message
+    [V, B].  Returns the posterior means [n_leaves, B]."""
+    n_layer, C, V, _ = templ.shape
+    vt = np.linspace(0, V - 1, V).reshape(1, V, 1)
+
+    def up(msg, mats, transpose=False):
+        out = np.empty_like(msg)
+        eq = "ji,njb->nib" if transpose else "ij,njb->nib"
+        for c in range(C):
+            out[c::C] = np.log(np.einsum(eq, mats[c], np.exp(msg[c::C])))
+        return out
+
+    def children_sum(q):  # sum(child.qd for child in children), children in slot order
+        acc = q[0::C].copy()
+        for c in range(1, C):
+            acc += q[c::C]
+        return acc
+
+    hd = {n_layer: -0.5 * (np.asarray(z, dtype=np.float64)[:, None, :] - vt) ** 2 / (sigma ** 2)}
+    qd = {n_layer: up(hd[n_layer], templ[-1])}
+    for layer in range(n_layer - 1, 0, -1):  # leaves -> root (:489-495)
+        h = children_sum(qd[layer + 1])
+        h -= h.max(axis=1, keepdims=True)
+        hd[layer], qd[layer] = h, up(h, templ[layer - 1])
+    bu = children_sum(qd[1])  # root (:499-504)
+    bu -= bu.max(axis=1, keepdims=True)
+    bu = bu + np.asarray(ext)[None]
+    for layer in range(1, n_layer + 1):  # root -> leaves (:507-512)
+        b = hd[layer] + up(np.repeat(bu, C, axis=0) - qd[layer], templ[layer - 1], transpose=True)
+        bu = b - b.max(axis=1, keepdims=True)
+    w = np.exp(bu)
+    return ((vt * w).sum(axis=1) / w.sum(axis=1))
+
+
+class ConditionalDenoiseSampler(DoubleSampler):
+    """data_random_GHM.py:846-894 with the per-step draw (trees + Gaussian noise) in
+    native code.  The BP posteriors of get_batch run vectorised on the host; the
+    CDM trainer computes them on the device instead (ghm_bp_dns)."""
+
+    def __init__(self, n_layers, n_childs, p_ys, p_flips, sigma=1, flip_scale=1, variable_type=10,
+                 translation_invariance=True, seedtree=42):
+        super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
+                         translation_invariance, seedtree)
+        self.sigma = sigma
+        self.t_templ = _templates(self.t_transition, n_childs[0])
+        self.i_templ = _templates(self.i_transition, n_childs[1])
+        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, 2)
+        self.T = self.native.T
+
+    def draw_numpy(self, batch_size):
+        """One reference-identical draw from numpy's global state: (text leaves uint8
+        [B, T], roots uint8 [B], z float64 [B, T], image leaves uint8 [B, T])."""
+        B, T = batch_size, self.T
+        tl = np.empty((B, T), np.uint8)
+        il = np.empty((B, T), np.uint8)
+        root = np.empty(B, np.uint8)
+        z = np.empty((B, T), np.float64)
+        self.native.pull_numpy_state()
+        self.native.next_cdm_into(B, self.sigma, tl, il, z, root)
+        self.native.push_numpy_state()
+        return tl, root, z, il
+
+    def posterior(self, tl, z):
+        """(text BP_CLS posteriors [V, B], image BP_DNS posterior means [B, T])."""
+        p_y = np.ones(self.variable_type) / self.variable_type
+        t_pp = bp_cls_posterior(self.t_templ, tl, p_y).T
+        ext = bp_cls_root_message(self.t_templ, tl)
+        return t_pp, bp_dns_posterior(self.i_templ, np.asarray(z).T, self.sigma, ext).T
+
+    def get_batch(self, batch_size=128, device="cpu", guide=False):
+        """:854-884.  Returns (text_leaves int64 [B, T], text_root int64 [B], None,
+        t_pp [V, B]), (z float32 [B, T], image_leaves int64 [B, T], None,
+        posterior means float64 [B, T])."""
+        if guide:
+            raise NotImplementedError("guided CDM (guided_info targets) is not built yet")
+        tl, root, z, il = self.draw_numpy(batch_size)
+        t_pp, post = self.posterior(tl, z)
+        to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
+        return ((to(tl), to(root), None, t_pp),
+                (torch.from_numpy(z.astype(np.float32)).to(device), to(il), None, post))
+
+    def get_Bayes(self, n_eval=30000):
+        """:886-894 — mean and standard error of the Bayes (posterior-mean) squared error."""
+        tl, _, z, il = self.draw_numpy(n_eval)
+        _, post = self.posterior(tl, z)
+        loss = np.sum(np.power(post - il.astype(np.int64), 2), 1)
+        return np.mean(loss), np.std(loss) / np.sqrt(n_eval)

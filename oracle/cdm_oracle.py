@@ -1,0 +1,190 @@
+"""ORACLE — CPU restatement of the reference's sequential conditional-denoising (CDM)
+training path (BASELINE config 4: scripts/experiments/exp_cdm_standardTF.sh).
+
+TEST INFRASTRUCTURE ONLY, like ghm_oracle.py: only tests/, __graft_entry__.smoke()
+and bench.py's ``cpu_baseline`` leg may import it, as the checker / the timed CPU
+baseline.  Nothing in multimodal-ghm_amd/ imports it.
+
+Parity pinning: checked against fixtures produced by importing the real reference
+(tests/golden/make_golden_cdm.py): the sampler draws, the BP_DNS posteriors and the
+Bayes risk (cdm_sampler.npz), two full training steps at L=1 (cdm_tiny.npz) and the
+first 100 steps of the default config (cdm_curve.npz).
+
+Reference file:line it follows (relative to src/ghmclip/):
+  sampler    data/data_random_GHM.py:641-658 (DoubleSampler), :854-884
+             (ConditionalDenoiseSampler.get_batch), :886-894 (get_Bayes)
+  BP         data/data_random_GHM.py:185-215 (BP_CLS root message), :467-523 (BP_DNS)
+  model      models/model.py:337-532 (ConditionalDenoiseEncoderTransformer, sequential=True)
+  loss       models/model.py:989-1041 (ConditionalGuidedLsLoss, guide=False), :1152-1160 (LsLoss)
+  loop       training/train_sequential_DNS.py:62-168
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .ghm_oracle import (OracleAdamW, OracleEncoder, bp_cls_messages, gen_leaves, gen_transition, lr_cosine,
+                         seed_everything)
+
+
+def bp_dns_posterior(trans, z, sigma, ext):
+    """BP_DNS (data_random_GHM.py:467-523), vectorised over the nodes of a layer
+    (translation invariance: node n of a layer uses its child-slot matrix n % C).
+    z: noisy leaf observations [n_leaves, B]; ext: the text tree's BP_CLS root
+    message [V, B] (:875-877).  Returns the posterior means [n_leaves, B]."""
+    n_layer, C, V, _ = trans.shape
+    vt = np.linspace(0, V - 1, V).reshape(1, V, 1)
+
+    def up(msg, mats):  # log(T_slot @ exp(msg)) per node
+        out = np.empty_like(msg)
+        for c in range(C):
+            out[c::C] = np.log(np.einsum("ij,njb->nib", mats[c], np.exp(msg[c::C])))
+        return out
+
+    def children_sum(q):  # python sum(child.qd for child in children): 0 + q0 + q1 + ...
+        acc = 0
+        for c in range(C):
+            acc = acc + q[c::C]
+        return acc
+
+    hd = {n_layer: -0.5 * (z[:, None, :] - vt) ** 2 / (sigma ** 2)}  # :481-486
+    qd = {n_layer: up(hd[n_layer], trans[-1])}
+    for layer in range(n_layer - 1, 0, -1):  # downward pass :489-495
+        h = children_sum(qd[layer + 1])
+        h = h - h.max(axis=1, keepdims=True)
+        hd[layer] = h
+        qd[layer] = up(h, trans[layer - 1])
+    root = children_sum(qd[1])  # :499-504
+    root = root - root.max(axis=1, keepdims=True)
+    bu = root + ext[None]
+    for layer in range(1, n_layer + 1):  # upward pass :507-512
+        parent = np.repeat(bu, C, axis=0)
+        diff = parent - qd[layer]
+        out = np.empty_like(diff)
+        for c in range(C):
+            out[c::C] = np.log(np.einsum("ji,njb->nib", trans[layer - 1, c], np.exp(diff[c::C])))
+        b = hd[layer] + out
+        bu = b - b.max(axis=1, keepdims=True)
+    w = np.exp(bu)  # :514-518
+    return (vt * w).sum(axis=1) / w.sum(axis=1)
+
+
+class CdmSamplerOracle:
+    """ConditionalDenoiseSampler (data_random_GHM.py:846-894), translation-invariant trees."""
+
+    def __init__(self, n_layers, n_childs, p_flips, sigma=1.0, flip_scale=1, variable_type=10, seedtree=42):
+        self.V, self.sigma = variable_type, sigma
+        np.random.seed(seedtree)  # DoubleSampler.__init__ :654
+        self.t_trans = gen_transition(n_layers[0], n_childs[0], variable_type, p_flips[0], flip_scale)
+        self.i_trans = gen_transition(n_layers[1], n_childs[1], variable_type, p_flips[1], flip_scale)
+
+    def get_batch(self, batch_size=128):
+        """:854-884.  Returns (t_leaves [B,T], root [B], z float32 [B,T], i_leaves [B,T],
+        posterior means float64 [B,T])."""
+        B = batch_size
+        root = np.random.choice(self.V, size=B)
+        t_leaves = gen_leaves(self.t_trans, root)
+        i_leaves = gen_leaves(self.i_trans, root)
+        noise = np.random.randn(i_leaves.shape[1], B) * self.sigma + i_leaves.T  # :869
+        ext = bp_cls_messages(self.t_trans, t_leaves)[-1][:, 0, :].T  # text root hd_message [V, B]
+        post = bp_dns_posterior(self.i_trans, noise, self.sigma, ext)
+        return t_leaves, root, noise.T.astype(np.float32), i_leaves, post.T
+
+    def get_Bayes(self, n_eval=30000):
+        """:886-894 — mean and standard error of the posterior-mean squared error."""
+        _, _, _, leaves, post = self.get_batch(n_eval)
+        loss = np.sum(np.power(post - leaves, 2), 1)
+        return float(np.mean(loss)), float(np.std(loss) / np.sqrt(n_eval))
+
+
+class OracleCdm(nn.Module):
+    """ConditionalDenoiseEncoderTransformer, sequential=True, guide=False
+    (model.py:337-532).  Construction order as the reference: position embedding,
+    the (then empty) ModuleLists, t_embedding, per layer q, k, v, ln1, mlp, ln2,
+    then _read_out Linear(d -> 1) and the unused _out Linear(n_token -> 1)."""
+
+    def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512):
+        super().__init__()
+        self.V, self.n_i_token, self.n_embd = num_class, n_i_token, n_embd
+        self.position_embeddings = nn.Embedding(n_token, n_embd)
+        self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        self._mlps, self._lns_1, self._lns_2 = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
+        self.t_embedding = nn.Embedding(num_class, n_embd)
+        for _ in range(n_layer):
+            self._queries.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._keys.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._values.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._lns_1.append(nn.LayerNorm([n_embd]))
+            self._mlps.append(nn.Sequential(nn.Linear(n_embd, n_mlp_hidden), nn.GELU(),
+                                            nn.Linear(n_mlp_hidden, n_embd)))
+            self._lns_2.append(nn.LayerNorm([n_embd]))
+        self._read_out = nn.Linear(n_embd, 1)
+        self._out = nn.Linear(n_token, 1)
+
+    def forward(self, xt, zi):
+        """xt: CLIP text features [B, T1, V]; zi: noisy image observations [B, T2]."""
+        B, T2 = zi.shape
+        T1 = xt.shape[1]
+        emb = torch.zeros(B, T1 + T2, self.n_embd)
+        opts = torch.arange(0, self.V).unsqueeze(0).unsqueeze(0).expand(B, T2, self.V)
+        emb[:, :T2, :self.V] = -torch.pow(opts - zi.unsqueeze(-1), 2) / 2  # :412-416
+        emb[:, T2:, :] = torch.cat([xt, torch.zeros(B, T1, self.n_embd - self.V)], dim=2)  # :418-423
+        pos = torch.arange(T1 + T2).expand(B, T1 + T2)
+        H = emb + self.position_embeddings(pos)  # :437
+        for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
+                                          self._lns_2):
+            H1 = ln1(H)
+            S = torch.einsum("bid,bjd->bij", q(H1), k(H1)) / np.sqrt(H.shape[2])  # :461-463
+            H = H + torch.einsum("bij,bjd->bid", F.softmax(S, dim=-1), v(H1))  # :466-467
+            H = H + mlp(ln2(H))  # :470-475
+        return self._read_out(H)[:, :T2, 0]  # :527-531
+
+
+def ls_loss(pred, target):
+    """LsLoss / ConditionalGuidedLsLoss(guide=False): mean over samples of the
+    per-sample sum of squared errors (model.py:998, :1159)."""
+    return torch.sum(torch.pow(pred - target, 2), dim=1).mean()
+
+
+class OracleCdmTrainer:
+    """train_sequential_DNS.py:62-168 (raw=True, guide=False) with the frozen CLIP text
+    encoder at its seeded initial weights (see make_golden_cdm.py)."""
+
+    def __init__(self, p=0.2, B=128, L=9, d=128, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
+                 max_norm=1.0, seed=224, seedtree=42, sigma=1.0, n_bayes=10000, n_layer_tree=4, n_child=3):
+        seed_everything(seed)
+        self.sampler = CdmSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], sigma=sigma, seedtree=seedtree)
+        self.bayes = self.sampler.get_Bayes(n_bayes) if n_bayes else None
+        T = n_child ** n_layer_tree
+        self.clip = OracleEncoder(T, 10, 128, 5)
+        self.model = OracleCdm(T + 1, T, 10, d, L, 4 * d)
+        self.params = list(self.model.parameters())
+        self.opt = OracleAdamW(self.params)
+        self.B = B
+        self.sched = (lr_max, lr_min, warmup, total_iters)
+        self.max_norm = max_norm
+        self.it = 0
+
+    def step(self, batch=None):
+        """Returns (ploss, loss, compare)."""
+        for p in self.params:
+            p.grad = None
+        if batch is None:
+            batch = self.sampler.get_batch(self.B)
+        t_l, _, z, i_l, post = batch[:5]
+        with torch.no_grad():
+            feat = self.clip(torch.as_tensor(t_l, dtype=torch.long))[0].unsqueeze(1)
+        self.last_feat = feat
+        pred = self.model(feat, torch.as_tensor(z, dtype=torch.float32))
+        self.last_pred = pred.detach()
+        target = torch.as_tensor(np.asarray(i_l), dtype=torch.long)
+        loss = ls_loss(pred, target)
+        loss.backward()
+        with torch.no_grad():
+            cmp = ls_loss(pred, torch.tensor(np.asarray(post), dtype=torch.float32))
+        with_grad = [p for p in self.params if p.grad is not None]
+        torch.nn.utils.clip_grad_norm_(with_grad, self.max_norm, norm_type=2)
+        self.opt.set_lr(lr_cosine(self.it, *self.sched))
+        self.opt.step()
+        self.it += 1
+        return float(loss.item()), float(loss.item()), float(cmp.item())
