@@ -81,14 +81,48 @@ def make_ring(sampler, B, R):
     return ring.cuda()
 
 
+def build_cdm(rank, B, L, p, total_iters, precision=None):
+    """BASELINE config 4 (exp_cdm_standardTF.sh): sequential CDM, L=9, d=128,
+    lr 1e-3 -> 1e-6, sigma 1, frozen CLIP text encoder (random init: no checkpoint
+    travels to the box; the step's work does not depend on the weights)."""
+    from ghmclip import (ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, EncoderTransformer,
+                         get_lr_cosine_schedule, seed_everything)
+    from ghmclip.training.cdm_trainer import CdmTrainer
+    p_y = np.ones(10) / 10
+    seed_everything(224)
+    sampler = ConditionalDenoiseSampler([4, 4], [3, 3], [p_y, p_y], [p, p], sigma=1)
+    clip = EncoderTransformer(81, 10, 128, 5).cuda()
+    model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True).cuda()
+    sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
+    trainer = CdmTrainer(model, clip, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0, device="cuda",
+                         precision=precision)
+    sampler.native.seed(224 + 1000 * rank)
+    return sampler, trainer
+
+
+def make_cdm_ring(sampler, B, R):
+    T = sampler.T
+    t = np.empty((B, T), np.uint8)
+    i = np.empty((B, T), np.uint8)
+    z = np.empty((B, T), np.float64)
+    ring = []
+    for _ in range(R):
+        sampler.native.next_cdm_into(B, 1.0, t, i, z)
+        ring.append((torch.from_numpy(t.copy()).cuda(), torch.from_numpy(i.copy()).cuda(),
+                     torch.from_numpy(z.copy()).cuda()))
+    return ring
+
+
 def dominant_kernel(trainer):
     """(name, launch) of the step's dominant kernel — the encoder-layer LN2+MLP
     forward (k_ln_mlp_fwd / k_ln_mlp_fwd_x3b) of layer 0 — launched on the
     current stream with the trainer's own buffers."""
     from ghmclip import _native
     import ctypes
-    plan = trainer.plans[0]
-    pd = trainer.views[0][0]
+    if hasattr(trainer, "plans"):
+        plan, pd = trainer.plans[0], trainer.views[0][0]
+    else:  # CdmTrainer
+        plan, pd = trainer.plan, trainer.pd
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     if plan.precision == "x3":
@@ -132,10 +166,22 @@ def pmc_traffic(kernel):
     return None if k is None else k["hbm_bytes"]
 
 
-def cpu_baseline(B, L, steps=8, guide=False):
+def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     from oracle import ghm_oracle as O
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
+    if workload == "cdm":
+        from oracle import cdm_oracle as CO
+        tr = CO.OracleCdmTrainer(B=B, L=L, n_bayes=0)
+        tr.step()
+        t0 = time.time()
+        for _ in range(steps):
+            tr.step()
+        dt = (time.time() - t0) / steps
+        return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+                "sample": f"{steps} steps (after 1 warm-up) of the sequential CDM config, B={B}, L={L}, fp32 "
+                          f"PyTorch-CPU restatement of the reference (oracle/cdm_oracle.py, frozen CLIP "
+                          f"forward + BP_DNS posterior included); {dt:.3f} s/step"}
     tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
           else O.OracleTrainer(p=0.2, B=B, L=L))
     tr.step()  # warm-up
@@ -161,11 +207,15 @@ def main():
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
+    ap.add_argument("--workload", default="clip", choices=["clip", "cdm"],
+                    help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
+    if a.workload == "cdm":
+        return main_cdm(a, ws, rank)
     total_iters = max(3000, a.steps + a.warmup + 1)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
     ring = make_ring(sampler, a.batch, a.ring)
@@ -174,35 +224,14 @@ def main():
         tr.set_tokens(ring[k % a.ring, 0], ring[k % a.ring, 1])
         tr.step()
 
-    for k in range(a.warmup):
-        one(k)
-        if k == 1 and not a.no_graph:
-            tr.capture()
-    if a.warmup < 2 and not a.no_graph:
-        tr.capture()
-
-    if ws > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        one(a.warmup + k)
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-
+    elapsed = timed_steps(a, ws, tr, one)
     losses = tr.loss_history()
     finite = bool(np.isfinite(losses).all())
     kname, klaunch = dominant_kernel(tr)
     kern_ms = time_kernel(klaunch)
     if rank != 0:
         if ws > 1:
+            import torch.distributed as dist
             dist.destroy_process_group()
         return
 
@@ -260,6 +289,86 @@ def main():
         out["cpu_baseline"] = cpu_baseline(a.batch, a.layers, guide=a.guide)
     print(json.dumps(out), flush=True)
     if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def timed_steps(a, ws, tr, one):
+    """W warm-up steps (graph captured after step 2), then K timed steps bracketed
+    by barrier + synchronize; returns the max-over-ranks elapsed seconds."""
+    for k in range(a.warmup):
+        one(k)
+        if k == 1 and not a.no_graph:
+            tr.capture()
+    if a.warmup < 2 and not a.no_graph:
+        tr.capture()
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        one(a.warmup + k)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+def main_cdm(a, ws, rank):
+    """Sequential CDM (BASELINE config 4) throughput: samples/s, B rows per rank."""
+    L = 9 if a.layers == 5 else a.layers  # exp_cdm_standardTF.sh: n_model_layer=9
+    total_iters = max(30000, a.steps + a.warmup + 1)
+    sampler, tr = build_cdm(rank, a.batch, L, 0.2, total_iters, a.precision)
+    ring = make_cdm_ring(sampler, a.batch, a.ring)
+
+    def one(k):
+        t, i, z = ring[k % a.ring]
+        tr.set_batch(t, i, z)
+        tr.step()
+
+    elapsed = timed_steps(a, ws, tr, one)
+    losses = tr.loss_history()
+    kname, klaunch = dominant_kernel(tr)
+    kern_ms = time_kernel(klaunch)
+    if rank != 0:
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    M = a.batch * 82
+    mlp_bytes = 4 * M * (128 + 128 + 512 + 512)
+    achieved = mlp_bytes / (kern_ms * 1e-3) / 1e9
+    out = {
+        "metric": "GHM training samples/sec (sequential CDM config)",
+        "value": round(a.batch * ws * a.steps / elapsed, 2),
+        "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
+        "data": f"synthetic GHM draws (native ConditionalDenoiseSampler, p=0.2, sigma=1), ring of {a.ring} "
+                f"batches resident in HBM",
+        "config": {"workload": f"cdm_sequential: ConditionalDenoiseEncoderTransformer(L={L}, d=128, T=82) + frozen "
+                               f"CLIP text EncoderTransformer(L=5) forward + on-device BP_DNS compare, fwd+bwd+clip+AdamW",
+                   "batch_rows_per_rank": a.batch, "global_batch_rows": a.batch * ws, "n_layer": L,
+                   "parallelism": f"dp{ws}", "hip_graph": not a.no_graph},
+        "roofline": {"bound": "hbm", "kernel": f"{kname} (LN2+MLP fwd, one CDM layer, M={M})",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": mlp_bytes,
+                     "kernel_ms": round(kern_ms, 4)},
+        "loss_finite": bool(np.isfinite(losses).all()),
+        "last_loss": float(losses[-1]) if len(losses) else None,
+    }
+    if ws == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=8, workload="cdm")
+    print(json.dumps(out), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -219,6 +219,41 @@ int ghm_scaled_diff(const float* a, const float* b, const float* scale, float al
                     void* stream);
 int ghm_add_cols(float* dst, const float* src, int64_t M, int V, void* stream);
 
+/* ---- sequential conditional denoising (CDM, train_sequential_DNS.py) ---------
+ * ConditionalDenoiseEncoderTransformer (models/model.py:337-532, sequential=True)
+ * runs the encoder layer kernels above at T = T_img + n_cond tokens; only the
+ * embedding, the readout, the loss and the BP posterior differ. */
+/* H0 = token embedding + position embedding (model.py:404-423, :437): image token
+ * t < T_img gets -((d - z[n,t])^2)/2 in features d < V, conditioning token
+ * j = t - T_img gets cond[n, j, d] (row stride cond_ld) in d < V; all else 0.
+ * z: f32 [n_seq][T_img]; cond: f32 [n_seq][T - T_img][cond_ld]; pos_w [T][128]. */
+int ghm_cdm_embed_fwd(const float* z, const float* cond, int cond_ld, const float* pos_w, float* H0,
+                      int64_t n_seq, int T, int T_img, int V, int D, void* stream);
+/* Exact BP, f64, one workgroup per sample: the text tree's BP_CLS root message
+ * (data_random_GHM.py:185-208) conditions BP_DNS of the image tree (:467-523,
+ * external message :875-877).  trans: [L][C][V][V] templates; t_tokens uint8
+ * [n_seq][C_t^L_t]; z f64 [n_seq][C_i^L_i] noisy observations.  Writes the
+ * posterior means post (f32, the "Compare" target, train_sequential_DNS.py:145)
+ * and z32 = (float)z, the model input (torch.tensor(noise, float32), :882). */
+int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
+               double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i, int V,
+               void* stream);
+/* pred[n, t] = H[n, t, :] . w_ro + b_ro for t < T_img (_read_out Linear(128, 1),
+ * model.py:527-531).  H [n_seq][T][128]. */
+int ghm_cdm_readout_fwd(const float* H, const float* w_ro, const float* b_ro, float* pred, int64_t n_seq, int T,
+                        int T_img, int D, void* stream);
+/* loss = mean_n sum_t (pred - target)^2 (ConditionalGuidedLsLoss guide=False and
+ * LsLoss, model.py:997-998, :1152-1160); compare = the same against post (may be
+ * NULL); dpred = 2 (pred - target) / n_seq (may be NULL).  loss_out[0..1] <- loss,
+ * compare; hist / chist [*step] likewise when non-NULL.  Deterministic. */
+int ghm_ls_loss(const float* pred, const uint8_t* target, const float* post, float* dpred, float* loss_out,
+                float* hist, float* chist, const int32_t* step, int64_t n_seq, int T_img, void* stream);
+/* Readout backward: dH[n, t, :] = dpred[n, t] w_ro (t < T_img; 0 for the
+ * conditioning tokens), per-sequence partials part_w [n_seq][128] and part_b
+ * [n_seq] of d_read_out.weight / .bias (reduce with ghm_reduce_batch). */
+int ghm_cdm_readout_bwd(const float* H, const float* w_ro, const float* dpred, float* dH, float* part_w,
+                        float* part_b, int64_t n_seq, int T, int T_img, int D, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

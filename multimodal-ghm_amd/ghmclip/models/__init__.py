@@ -1,3 +1,4 @@
 """Model, loss and optimizer exports (reference: src/ghmclip/models)."""
 from .model import *  # noqa: F401,F403
 from .optimizer import *  # noqa: F401,F403
+from .cdm import *  # noqa: F401,F403

@@ -1,0 +1,253 @@
+"""Sequential conditional denoiser (CDM, BASELINE config 4) on the HIP path.
+
+Reference: models/model.py:337-532 (ConditionalDenoiseEncoderTransformer),
+:989-1041 (ConditionalGuidedLsLoss), :1152-1160 (LsLoss); trained by
+training/train_sequential_DNS.py with a frozen CLIP text encoder supplying the
+one conditioning token.
+
+The denoiser is the CLIP encoder's layer stack at T = 81 image + 1 conditioning
+token, so ``CdmPlan`` reuses EncoderPlan's layer kernels and adds the CDM
+embedding (continuous leaf features), the Linear(d -> 1) readout and the
+position-embedding gradient (csrc/ghm_cdm.hip).
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from .. import _native
+from .hip_encoder import D_MODEL, EncoderPlan, require_hip
+
+__all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
+           "cdm_param_names", "CDM_UNTRAINED"]
+
+# parameters the reference never gives a gradient in sequential mode (the
+# conditioning token bypasses t_embedding, _out is unused by forward): AdamW and
+# clip_grad_norm_ skip them (optimizer.py:55-56)
+CDM_UNTRAINED = ("t_embedding.weight", "_out.weight", "_out.bias")
+
+
+def cdm_param_names(n_layer):
+    """state_dict keys of ConditionalDenoiseEncoderTransformer in registration order
+    (model.py:382-402: the ModuleLists are registered before t_embedding)."""
+    names = ["position_embeddings.weight"]
+    names += [f"_queries.{l}.weight" for l in range(n_layer)]
+    names += [f"_keys.{l}.weight" for l in range(n_layer)]
+    names += [f"_values.{l}.weight" for l in range(n_layer)]
+    for l in range(n_layer):
+        names += [f"_mlps.{l}.0.weight", f"_mlps.{l}.0.bias", f"_mlps.{l}.2.weight", f"_mlps.{l}.2.bias"]
+    for l in range(n_layer):
+        names += [f"_lns_1.{l}.weight", f"_lns_1.{l}.bias"]
+    for l in range(n_layer):
+        names += [f"_lns_2.{l}.weight", f"_lns_2.{l}.bias"]
+    names += ["t_embedding.weight", "_read_out.weight", "_read_out.bias", "_out.weight", "_out.bias"]
+    return names
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class CdmPlan(EncoderPlan):
+    """Device workspaces of one ConditionalDenoiseEncoderTransformer at one batch
+    shape: the EncoderPlan layer buffers at T = n_token plus the readout/loss ones.
+    HBM layout: H [L+1][N*T][128] etc. as EncoderPlan; pred, dpred [N][T_img];
+    readout partials part_rw [N][128], part_rb [N] (distinct from EncoderPlan's
+    split-K buffers part_w1 / part_b1)."""
+
+    def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
+                 normalize_attn=True, device="cuda", precision=None):
+        super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
+                         normalize_attn=normalize_attn, device=device, precision=precision)
+        if not 1 <= n_i_token <= n_token:
+            raise ValueError("n_i_token must be in [1, n_token]")
+        self.Ti = n_i_token
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.pred = e(n_seq, n_i_token)
+        self.dpred = e(n_seq, n_i_token)
+        self.part_rw = e(n_seq, D_MODEL)
+        self.part_rb = e(n_seq)
+
+    def forward(self, p, z, cond, cond_ld, split=True):
+        """z: f32 [N, T_img] noisy observations; cond: f32 [N, T - T_img, cond_ld]
+        conditioning features (first V used).  Returns self.pred [N, T_img]."""
+        s = _stream()
+        if self.precision == "x3" and split:
+            self.split_weights(p, s)
+        _native.call("ghm_cdm_embed_fwd", _ptr(z), _ptr(cond) if cond is not None else None, cond_ld,
+                     _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), self.N, self.T, self.Ti, self.C,
+                     D_MODEL, s)
+        self.layers_fwd(p, s)
+        _native.call("ghm_cdm_readout_fwd", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]),
+                     _ptr(p["_read_out.bias"]), _ptr(self.pred), self.N, self.T, self.Ti, D_MODEL, s)
+        self._gen += 1
+        return self.pred
+
+    def backward(self, p, g, dpred=None, layer_grad=None):
+        """Writes d(loss)/d(param) into g[name] for every trained parameter (not
+        CDM_UNTRAINED); dpred [N, T_img] defaults to self.dpred.  Returns dL/dH_0
+        [N*T, 128] (its conditioning rows give the gradient of cond)."""
+        s = _stream()
+        J = self._job
+        dp = self.dpred if dpred is None else dpred
+        cur = self.dH[0]
+        _native.call("ghm_cdm_readout_bwd", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]), _ptr(dp), _ptr(cur),
+                     _ptr(self.part_rw), _ptr(self.part_rb), self.N, self.T, self.Ti, D_MODEL, s)
+        jobs = [J(self.part_rw, self.N, [g["_read_out.weight"]]), J(self.part_rb, self.N, [g["_read_out.bias"]])]
+        cur = self.layers_bwd(p, g, jobs, s, layer_grad)
+        jobs.append(J(cur, self.N, [g["position_embeddings.weight"]]))
+        self._flush(jobs, s)
+        return cur
+
+
+class _CdmFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, module, xt, zi, *params):
+        N, T2 = zi.shape
+        T1 = xt.shape[1]
+        plan = module._plan(N, T1 + T2, T2, zi.device)
+        pd = dict(zip(module._names, params))
+        z = zi.contiguous().float()
+        cond = xt.contiguous().float()
+        pred = plan.forward(pd, z, cond, cond.shape[2]).clone()
+        ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
+        ctx.T1 = T1
+        ctx.save_for_backward(*params)
+        return pred
+
+    @staticmethod
+    def backward(ctx, dpred):
+        plan = ctx.plan
+        if plan._gen != ctx.gen:
+            raise RuntimeError("ConditionalDenoiseEncoderTransformer: another forward of this module "
+                               "overwrote the activations saved for backward")
+        params = ctx.saved_tensors
+        names = ctx.module._names
+        trained = [n not in CDM_UNTRAINED for n in names]
+        grads = {n: torch.empty_like(p) for n, p, t in zip(names, params, trained) if t}
+        dH0 = plan.backward(dict(zip(names, params)), grads, dpred=dpred.contiguous().float())
+        d_xt = None
+        if ctx.needs_input_grad[1]:
+            V = ctx.module.vocab_size
+            d_xt = torch.zeros(plan.N, ctx.T1, ctx.module.vocab_size, dtype=torch.float32, device=dH0.device)
+            d_xt.copy_(dH0.view(plan.N, plan.T, D_MODEL)[:, plan.Ti:, :V])
+        return (None, d_xt, None, *[grads.get(n) for n in names])
+
+
+class ConditionalDenoiseEncoderTransformer(nn.Module):
+    """Reference: models/model.py:337-532.  Same constructor, parameter creation
+    order (so torch.manual_seed gives identical weights) and state_dict keys.
+    The HIP path covers the sequential configuration the CDM experiments train
+    (scripts/experiments/exp_cdm_{standard,shallow}TF.sh): a frozen-CLIP feature
+    token, softmax attention, LayerNorm, MLP, no guide, no causal mask, n_embd 128."""
+
+    def __init__(self, n_token, n_i_token, num_class, n_embd=128, n_layer=12, n_guided_layers=(3, 3), n_head=4,
+                 n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True, auto_regressive=False,
+                 sequential=False, layernorm=True, maxnorm=False, guide=False, sigma=1):
+        super().__init__()
+        self.name = f"EncoderTF_embd={n_embd}_layer={n_layer}_head={n_head}"
+        self.vocab_size = num_class
+        self.context_length = n_token
+        self.n_token = n_token
+        self.n_i_token = n_i_token
+        self.n_embd = n_embd
+        self.n_head = n_head
+        self.n_layer = n_layer
+        self.n_mlp_hidden = n_mlp_hidden
+        self.sequential = sequential
+        self.activation = activation
+        self.mlp = mlp
+        self.normalize_attn = normalize_attn
+        self.layernorm = layernorm
+        self.maxnorm = maxnorm
+        self.auto_regressive = auto_regressive
+        self.guide = guide
+        self.n_t_guided_layer = n_guided_layers[0]
+        self.n_i_guided_layer = n_guided_layers[1]
+        self.guided_layer_gap = n_layer // (n_guided_layers[1] * 2 + 1)
+        self.sigma = sigma
+        if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive or guide:
+            raise NotImplementedError("HIP CDM: softmax attention, mlp=True, layernorm=True, maxnorm=False, "
+                                      "auto_regressive=False, guide=False")
+        if not sequential:
+            raise NotImplementedError("HIP CDM: sequential=True (frozen-CLIP conditioning token); the joint "
+                                      "model's 162-token sequences exceed the 96-token attention kernels")
+        if n_mlp_hidden != 4 * n_embd:
+            raise NotImplementedError("HIP CDM: n_mlp_hidden = 4 * n_embd")
+        # construction (RNG) order of the reference, model.py:382-402
+        self.position_embeddings = nn.Embedding(self.context_length, self.n_embd)
+        self._queries = nn.ModuleList()
+        self._keys = nn.ModuleList()
+        self._values = nn.ModuleList()
+        self._mlps = nn.ModuleList()
+        self._lns_1 = nn.ModuleList()
+        self._lns_2 = nn.ModuleList()
+        self.t_guided_layer_flag = [False] * n_layer
+        self.i_guided_layer_flag = [False] * n_layer
+        self.t_embedding = nn.Embedding(self.vocab_size, self.n_embd)
+        for _ in range(n_layer):
+            self._queries.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._keys.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._values.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._lns_1.append(nn.LayerNorm([self.n_embd]))
+            self._mlps.append(nn.Sequential(nn.Linear(n_embd, n_mlp_hidden), nn.GELU(),
+                                            nn.Linear(n_mlp_hidden, n_embd)))
+            self._lns_2.append(nn.LayerNorm([self.n_embd]))
+        self._read_out = nn.Linear(n_embd, 1)
+        self._out = nn.Linear(n_token, 1)
+        self._names = cdm_param_names(n_layer)
+        self._plans = {}
+        self.precision = None  # None -> $GHM_PRECISION or "x3" (hip_encoder.py)
+
+    def _plan(self, n_seq, T, T_img, device):
+        key = (n_seq, T, T_img, str(device), self.precision)
+        if key not in self._plans:
+            self._plans.clear()
+            self._plans[key] = CdmPlan(self.n_layer, T, T_img, n_seq, num_class=self.vocab_size,
+                                       n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
+                                       precision=self.precision)
+        return self._plans[key]
+
+    def forward(self, xt, zi):
+        """xt: conditioning features [B, T1, num_class] (the frozen CLIP text
+        embedding, unsqueezed); zi: noisy image observations [B, T2] (float).
+        Returns (denoised predictions [B, T2], guided layers [[], []])."""
+        require_hip(zi)
+        B, T2 = zi.shape
+        if xt.dim() != 3 or xt.shape[0] != B or xt.shape[2] != self.vocab_size:
+            raise ValueError(f"expected xt of shape [{B}, T1, {self.vocab_size}], got {tuple(xt.shape)}")
+        if T2 != self.n_i_token or xt.shape[1] + T2 != self.n_token:
+            raise ValueError(f"expected {self.n_i_token} image + {self.n_token - self.n_i_token} conditioning tokens")
+        sd = dict(self.named_parameters())
+        params = [sd[n] for n in self._names]
+        for prm in params:
+            if prm.dtype != torch.float32 or not prm.is_contiguous():
+                raise RuntimeError("HIP CDM parameters must be contiguous fp32")
+        pred = _CdmFn.apply(self, xt, zi, *params)
+        return pred, [[], []]
+
+
+class LsLoss(nn.Module):
+    """models/model.py:1152-1160: mean over samples of the summed squared error."""
+
+    def forward(self, inputs, targets):
+        return torch.sum(torch.pow(inputs - targets, 2), dim=1).mean()
+
+
+class ConditionalGuidedLsLoss(nn.Module):
+    """models/model.py:989-1041 (guide=False): returns (loss, 0, 0, 0, 0)."""
+
+    def __init__(self, penalty=1e-4, guide=False):
+        super().__init__()
+        self.penalty = penalty
+        self.guide = guide
+        if guide:
+            raise NotImplementedError("guided CDM penalties are not built yet")
+
+    def forward(self, inputs, targets, verbose=False):
+        loss = torch.sum(torch.pow(inputs[0] - targets[0], 2), dim=1)
+        return loss.mean(), 0, 0, 0, 0

@@ -145,19 +145,31 @@ class EncoderPlan:
         return self.P[l, :, :self.T, :self.T]
 
     # ------------------------------------------------------------------
-    def forward(self, p, tokens=None):
+    def forward(self, p, tokens=None, split=True):
         """p: dict name -> fp32 device tensor (state_dict keys).  tokens: uint8
-        [n_seq, T] on the device (defaults to self.tokens).  Returns self.emb."""
+        [n_seq, T] on the device (defaults to self.tokens).  Returns self.emb.
+        split=False reuses the weight packs of the previous forward (frozen weights)."""
         tok = self.tokens if tokens is None else tokens
         s = _stream()
         c = _native.call
-        M, T, N, L = self.M, self.T, self.N, self.L
-        x3 = self.precision == "x3"
-        if x3:
+        T, N, L = self.T, self.N, self.L
+        if self.precision == "x3" and split:
             self.split_weights(p, s)
         c("ghm_embed_fwd", _ptr(tok), _ptr(p["token_embeddings.weight"]),
           _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), N, T, self.V, D_MODEL, s)
-        for l in range(L):
+        self.layers_fwd(p, s)
+        c("ghm_readout_fwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
+          _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, s)
+        self._gen += 1
+        return self.emb
+
+    def layers_fwd(self, p, s):
+        """The n_layer encoder layers (model.py:769-800) from H[0] to H[L]:
+        LN1+QKV, attention+residual, LN2+MLP+residual per layer."""
+        c = _native.call
+        M, T, N = self.M, self.T, self.N
+        x3 = self.precision == "x3"
+        for l in range(self.L):
             if x3:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
@@ -178,10 +190,6 @@ class EncoderPlan:
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
               _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
               _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
-        c("ghm_readout_fwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
-          _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, s)
-        self._gen += 1
-        return self.emb
 
     def split_weights(self, p, s=None):
         """Write every layer's pre-split bf16 weight pack (precision "x3")."""
@@ -241,17 +249,31 @@ class EncoderPlan:
         s = _stream()
         c = _native.call
         J = self._job
-        M, T, N, L, C = self.M, self.T, self.N, self.L, self.C
-        cur, nxt = self.dH[0], self.dH[1]
+        T, N, L, C = self.T, self.N, self.L, self.C
+        cur = self.dH[0]
         jobs = []
         c("ghm_readout_bwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(p["_out.weight"]), _ptr(de), _ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro),
           _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, s)
         jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
                  J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
+        cur = self.layers_bwd(p, g, jobs, s, layer_grad)
+        c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
+        jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
+        self._flush(jobs, s)
+
+    def layers_bwd(self, p, g, jobs, s, layer_grad=None):
+        """Backward of the n_layer encoder layers from dH[0] (= dL/dH_L, written by
+        the caller's readout backward) down to dL/dH_0, which is returned (one of
+        the dH ping-pong buffers).  Parameter-gradient partials are reduced by one
+        batched launch per layer (pending jobs in `jobs` are flushed with them)."""
+        c = _native.call
+        J = self._job
+        M, T, N = self.M, self.T, self.N
+        cur, nxt = self.dH[0], self.dH[1]
         x3 = self.precision == "x3"
         wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
-        for l in reversed(range(L)):
+        for l in reversed(range(self.L)):
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
@@ -293,6 +315,4 @@ class EncoderPlan:
             jobs.append(J(self.part_ln, self.nblk, [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]]))
             self._flush(jobs, s)  # every partial buffer is reused by the next layer
             cur, nxt = nxt, cur  # cur = dH_l
-        c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
-        jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
-        self._flush(jobs, s)
+        return cur

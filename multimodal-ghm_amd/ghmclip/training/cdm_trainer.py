@@ -1,0 +1,218 @@
+"""Fused sequential-CDM training step on the HIP path — the hot loop of
+src/ghmclip/training/train_sequential_DNS.py:141-168 (zero_grad, sample, frozen
+CLIP text encoder, denoiser forward, ConditionalGuidedLsLoss / LsLoss / Compare,
+backward, clip_grad_norm_, cosine LR, AdamW).
+
+Per step, on the device (one captured graph + one optimizer graph):
+  side stream: ghm_bp_dns — exact BP posterior means from the staged text leaves
+               and the f64 noisy observations (the "Compare" target), and the f32
+               model input z (the reference computes both on the host, :145,
+               data_random_GHM.py:871-882)
+  main stream: frozen CLIP text EncoderPlan forward -> [B, 10] features,
+               CdmPlan forward, ghm_ls_loss (loss, compare, dpred, histories),
+               CdmPlan backward
+  optimizer:   ghm_clip_prepare + ghm_adamw over the flat buffer of the trained
+               parameters (t_embedding and _out get no gradient in the reference,
+               so AdamW and the clip skip them, optimizer.py:55-56).
+Data parallel (optional): the loss is a mean over samples, so ranks take equal
+row shards and average gradients with one RCCL all-reduce.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.cdm import CDM_UNTRAINED, CdmPlan
+from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.optimizer import adam_consts, adam_lr_t
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class CdmTrainer:
+    def __init__(self, model, clip_model, batch_size, lr_schedule, t_templ, i_templ, sigma=1.0, max_norm=1.0,
+                 weight_decay=0.001, betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
+                 precision=None):
+        """model: ConditionalDenoiseEncoderTransformer (sequential); clip_model: the
+        frozen CLIP text EncoderTransformer; lr_schedule: one learning rate per step;
+        t_templ / i_templ: the sampler's transition templates [L][C][V][V]."""
+        self.device = torch.device(device)
+        self.model, self.clip = model, clip_model
+        self.B = batch_size
+        self.max_norm = float(max_norm)
+        self.pg = process_group
+        self.sigma = float(sigma)
+        self.names = list(model._names)
+        sd = dict(model.named_parameters())
+        for p in list(sd.values()) + list(clip_model.parameters()):
+            require_hip(p)
+        trained = [n for n in self.names if n not in CDM_UNTRAINED]
+        n = sum(sd[k].numel() for k in trained)
+        self.n_params = n
+        self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.gflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.pd, self.gd, self.md, self.vd = {}, {}, {}, {}
+        off = 0
+        with torch.no_grad():
+            for k in trained:
+                p = sd[k]
+                c = p.numel()
+                self.pflat[off:off + c].copy_(p.data.reshape(-1))
+                p.data = self.pflat[off:off + c].view(p.shape)
+                p.grad = self.gflat[off:off + c].view(p.shape)
+                self.pd[k], self.gd[k] = p.data, p.grad
+                self.md[k] = self.mflat[off:off + c].view(p.shape)
+                self.vd[k] = self.vflat[off:off + c].view(p.shape)
+                off += c
+            for k in CDM_UNTRAINED:
+                self.pd[k] = sd[k].data
+        self.clip_p = {k: v.data for k, v in clip_model.named_parameters()}
+        T, Ti = model.n_token, model.n_i_token
+        self.T, self.Ti = T, Ti
+        self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,
+                            normalize_attn=model.normalize_attn, device=self.device, precision=precision)
+        self.precision = self.plan.precision
+        self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+                                     num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
+                                     n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
+                                     device=self.device, precision=self.precision)
+        if self.precision == "x3":
+            self.clip_plan.split_weights(self.clip_p)  # frozen: split once
+        t_templ = np.ascontiguousarray(t_templ, dtype=np.float64)
+        i_templ = np.ascontiguousarray(i_templ, dtype=np.float64)
+        if i_templ.shape[1] ** i_templ.shape[0] != Ti or t_templ.shape[1] ** t_templ.shape[0] != clip_model.n_token:
+            raise ValueError("transition templates do not match the token counts")
+        self.tree = (t_templ.shape[0], t_templ.shape[1], i_templ.shape[0], i_templ.shape[1], t_templ.shape[2])
+        self.t_trans = torch.from_numpy(t_templ).to(self.device)
+        self.i_trans = torch.from_numpy(i_templ).to(self.device)
+        # staged inputs (text leaves live in the CLIP plan's token buffer)
+        self.i_tok = torch.empty(batch_size, Ti, dtype=torch.uint8, device=self.device)
+        self.z64 = torch.empty(batch_size, Ti, dtype=torch.float64, device=self.device)
+        self.z32 = torch.empty(batch_size, Ti, dtype=torch.float32, device=self.device)
+        self.post = torch.empty(batch_size, Ti, dtype=torch.float32, device=self.device)
+        # optimizer constants and the per-step schedule table (as ClipTrainer)
+        self.betas, self.wd = betas, weight_decay
+        self.consts = adam_consts(betas, eps)
+        self.t_offset = t_offset
+        sched = np.zeros((len(lr_schedule), 2), dtype=np.float32)
+        for s, lr in enumerate(lr_schedule):
+            sched[s, 0] = adam_lr_t(lr, s + 1 + t_offset, betas)
+            sched[s, 1] = lr * weight_decay
+        self.sched = torch.from_numpy(sched.reshape(-1)).to(self.device)
+        self.n_sched = len(lr_schedule)
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.work = torch.zeros(1024, dtype=torch.float32, device=self.device)
+        self.loss_out = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
+        self.chist = torch.zeros_like(self.hist)
+        self.graphs = None
+        self.steps_done = 0
+        self.side = torch.cuda.Stream(device=self.device)
+
+    # -- the launch sequence -----------------------------------------------------
+    def _fwd_bwd(self):
+        main = torch.cuda.current_stream()
+        side = self.side
+        Lt, Ct, Li, Ci, V = self.tree
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.clip_plan.tokens), _p(self.z64),
+                         self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V,
+                         ctypes.c_void_p(side.cuda_stream))
+        emb = self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_DNS.py:141
+        main.wait_stream(side)
+        s = ctypes.c_void_p(main.cuda_stream)
+        self.plan.forward(self.pd, self.z32, emb, emb.shape[1])
+        _native.call("ghm_ls_loss", _p(self.plan.pred), _p(self.i_tok), _p(self.post), _p(self.plan.dpred),
+                     _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.Ti, s)
+        self.plan.backward(self.pd, self.gd)
+
+    def _optim(self):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        b1, omb1, b2, omb2, eps = self.consts
+        _native.call("ghm_clip_prepare", _p(self.gflat), self.n_params, self.max_norm, _p(self.sched),
+                     self.n_sched, _p(self.step_ctr), _p(self.hyper), _p(self.work), s)
+        _native.call("ghm_adamw", _p(self.pflat), _p(self.gflat), _p(self.mflat), _p(self.vflat),
+                     self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
+
+    def _allreduce(self):
+        import torch.distributed as dist
+        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+
+    def set_batch(self, t_tokens, i_tokens, z):
+        """Stage one batch: text / image leaves uint8 [B, 81] and the noisy image
+        observations z float64 [B, 81] (host-pinned or device), async."""
+        self.clip_plan.tokens.copy_(t_tokens, non_blocking=True)
+        self.i_tok.copy_(i_tokens, non_blocking=True)
+        self.z64.copy_(z, non_blocking=True)
+
+    def step(self):
+        """One training step on the staged batch (async; no host sync)."""
+        if self.steps_done >= self.n_sched:
+            raise RuntimeError("schedule exhausted")
+        dp = self.pg is not None or _dist_on()
+        if self.graphs is not None:
+            self.graphs[0].replay()
+            if dp:
+                self._allreduce()
+            self.graphs[1].replay()
+        else:
+            self._fwd_bwd()
+            if dp:
+                self._allreduce()
+            self._optim()
+        self.steps_done += 1
+
+    def capture(self):
+        """Capture the step into HIP graphs (after >= 1 eager step)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._fwd_bwd()
+            with torch.cuda.graph(g2, stream=s):
+                self._optim()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graphs = (g1, g2)
+
+    # -- host-side views -----------------------------------------------------------
+    def loss_history(self, upto=None):
+        """Denoising loss per step (train_sequential_DNS.py loss_history; equals
+        ploss_history without guidance)."""
+        n = self.steps_done if upto is None else upto
+        return self.hist[:n].double().cpu().numpy()
+
+    ploss_history = loss_history
+
+    def compare_history(self, upto=None):
+        """Squared error against the BP posterior means per step (compare_history)."""
+        n = self.steps_done if upto is None else upto
+        return self.chist[:n].double().cpu().numpy()
+
+    def fill_optimizer_state(self, optimizer):
+        """Expose the flat moments as the reference AdamW's per-parameter state."""
+        t = self.steps_done + self.t_offset
+        for name, p in self.model.named_parameters():
+            if name in self.md:
+                optimizer.state[p] = {"t": t, "m": self.md[name], "v": self.vd[name]}
+
+    def load_optimizer_state(self, optimizer):
+        """Copy a loaded reference-format AdamW state ('m', 'v') into the flat moments."""
+        with torch.no_grad():
+            for name, p in self.model.named_parameters():
+                st = optimizer.state.get(p)
+                if st and name in self.md:
+                    self.md[name].copy_(st["m"])
+                    self.vd[name].copy_(st["v"])
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1

@@ -30,18 +30,8 @@ class BatchPipeline:
         every block (see shard_rows; data-parallel sharding)."""
         self.s = native_sampler
         self.B = batch_size
-        rows = batch_size * (native_sampler.K + 1)
-        T = native_sampler.T
-        self.full_rows, self.T = rows, T
         self.slice = row_slice
-        self.slots = [(torch.empty(rows, T, dtype=torch.uint8).pin_memory(),
-                       torch.empty(rows, T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
-        if row_slice is not None:
-            br, rank, world = row_slice
-            idx = shard_rows(br, rows // br, rank, world)
-            self.idx = torch.from_numpy(idx)
-            self.out = [(torch.empty(len(idx), T, dtype=torch.uint8).pin_memory(),
-                         torch.empty(len(idx), T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+        self._make_slots(n_slots)
         self.free = [threading.Event() for _ in range(n_slots)]
         self.ready = [threading.Event() for _ in range(n_slots)]
         self.copy_done = [None] * n_slots
@@ -55,6 +45,31 @@ class BatchPipeline:
         self.th = threading.Thread(target=self._run, daemon=True)
         self.th.start()
 
+    # -- CLIP batches: text / image leaves [B(K+1), T] uint8 ------------------------
+    def _make_slots(self, n_slots):
+        rows = self.B * (self.s.K + 1)
+        T = self.s.T
+        self.full_rows, self.T = rows, T
+        self.slots = [(torch.empty(rows, T, dtype=torch.uint8).pin_memory(),
+                       torch.empty(rows, T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+        if self.slice is not None:
+            br, rank, world = self.slice
+            idx = shard_rows(br, rows // br, rank, world)
+            self.idx = torch.from_numpy(idx)
+            self.out = [(torch.empty(len(idx), T, dtype=torch.uint8).pin_memory(),
+                         torch.empty(len(idx), T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+
+    def _fill(self, i):
+        t, im = self.slots[i]
+        self.s.next_into(self.B, t.numpy(), im.numpy())
+        if self.slice is not None:
+            torch.index_select(t, 0, self.idx, out=self.out[i][0])
+            torch.index_select(im, 0, self.idx, out=self.out[i][1])
+
+    def _stage(self, trainer, i):
+        t, im = self.out[i] if self.slice is not None else self.slots[i]
+        trainer.set_tokens(t, im)
+
     def _run(self):
         try:
             while not self.stop:
@@ -66,11 +81,7 @@ class BatchPipeline:
                 if ev is not None:
                     ev.synchronize()  # the previous H2D copy out of this slot is done
                 self.free[i].clear()
-                t, im = self.slots[i]
-                self.s.next_into(self.B, t.numpy(), im.numpy())
-                if self.slice is not None:
-                    torch.index_select(t, 0, self.idx, out=self.out[i][0])
-                    torch.index_select(im, 0, self.idx, out=self.out[i][1])
+                self._fill(i)
                 self.ready[i].set()
                 self.k_prod += 1
         except Exception as e:  # surfaced on the consumer side
@@ -85,8 +96,7 @@ class BatchPipeline:
         if self.err is not None:
             raise self.err
         self.ready[i].clear()
-        t, im = self.out[i] if self.slice is not None else self.slots[i]
-        trainer.set_tokens(t, im)
+        self._stage(trainer, i)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
         self.copy_done[i] = ev
@@ -98,3 +108,40 @@ class BatchPipeline:
         for f in self.free:
             f.set()
         self.th.join(timeout=5)
+
+
+class CdmBatchPipeline(BatchPipeline):
+    """The same producer for ConditionalDenoiseSampler draws (text leaves, image
+    leaves uint8 [B, T], noisy observations z float64 [B, T]).  row_slice:
+    optional (rank, world) — keep a contiguous 1/world of the samples (the CDM
+    loss is a mean over samples, model.py:998)."""
+
+    def __init__(self, native_sampler, batch_size, sigma, n_slots=3, row_slice=None):
+        self.sigma = float(sigma)
+        super().__init__(native_sampler, batch_size, n_slots, row_slice)
+
+    def _make_slots(self, n_slots):
+        B, T = self.B, self.s.T
+        self.T = T
+
+        def slot():
+            return (torch.empty(B, T, dtype=torch.uint8).pin_memory(), torch.empty(B, T, dtype=torch.uint8).pin_memory(),
+                    torch.empty(B, T, dtype=torch.float64).pin_memory())
+        self.slots = [slot() for _ in range(n_slots)]
+        if self.slice is not None:
+            rank, world = self.slice
+            if B % world:
+                raise ValueError("batch size must divide by the world size")
+            per = B // world
+            self.rows = (rank * per, (rank + 1) * per)
+
+    def _fill(self, i):
+        t, im, z = self.slots[i]
+        self.s.next_cdm_into(self.B, self.sigma, t.numpy(), im.numpy(), z.numpy())
+
+    def _stage(self, trainer, i):
+        t, im, z = self.slots[i]
+        if self.slice is not None:
+            a, b = self.rows
+            t, im, z = t[a:b], im[a:b], z[a:b]
+        trainer.set_batch(t, im, z)

@@ -49,10 +49,11 @@ def parse(argv=None):
 
 
 def load_checkpoint(path, device):
-    """checkpoint.pth of train_CLIP (state dicts + numpy histories) with the
-    weights-only unpickler: numpy arrays are allow-listed, nothing else runs."""
-    import numpy.core.multiarray as npm
-    allow = [npm._reconstruct, np.ndarray, np.dtype, type(np.dtype(np.float64)), np.float64]
+    """checkpoint.pth of train_CLIP / train_sequential_DNS (state dicts, numpy
+    histories, numpy scalars) with the weights-only unpickler: numpy arrays and
+    scalars are allow-listed, nothing else runs."""
+    from numpy._core import multiarray as npm
+    allow = [npm._reconstruct, npm.scalar, np.ndarray, np.dtype, type(np.dtype(np.float64)), np.float64]
     with torch.serialization.safe_globals(allow):
         return torch.load(path, map_location=device, weights_only=True)
 

@@ -1,0 +1,155 @@
+"""CPU tests of the sequential CDM path: the oracle against the reference's own
+fixtures (tests/golden/make_golden_cdm.py) and the product's host side (native
+ConditionalDenoiseSampler draws, host BP_DNS, module construction)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import cdm_oracle as CO
+
+P_Y = np.ones(10) / 10
+
+
+def _fix(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def test_oracle_sampler_and_bayes_match_reference():
+    f = _fix("cdm_sampler.npz")
+    CO.seed_everything(224)
+    s = CO.CdmSamplerOracle([4, 4], [3, 3], [0.2, 0.2])
+    np.testing.assert_array_equal(s.t_trans, f["t_transition"])
+    np.testing.assert_array_equal(s.i_trans, f["i_transition"])
+    bayes = s.get_Bayes(10000)
+    np.testing.assert_allclose(bayes, f["bayes"], rtol=1e-12)
+    for k in range(2):
+        tl, root, z, il, post = s.get_batch(int(f["B"]))
+        np.testing.assert_array_equal(tl, f["t_leaves"][k])
+        np.testing.assert_array_equal(root, f["t_root"][k])
+        np.testing.assert_array_equal(z, f["z"][k])
+        np.testing.assert_array_equal(il, f["i_leaves"][k])
+        np.testing.assert_allclose(post, f["post"][k], rtol=0, atol=1e-12)
+
+
+def test_native_sampler_matches_reference():
+    """ConditionalDenoiseSampler (native MT19937 + legacy Gaussians) == the reference's
+    draws bit-for-bit, numpy's global state (incl. the cached Gaussian) left as the
+    reference leaves it; host BP posteriors within 1e-12."""
+    from ghmclip import ConditionalDenoiseSampler, seed_everything
+    f = _fix("cdm_sampler.npz")
+    seed_everything(224)
+    s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1)
+    bayes = s.get_Bayes(n_eval=10000)
+    np.testing.assert_allclose(bayes, f["bayes"], rtol=1e-12)
+    for k in range(2):
+        (t, r, tg, tpp), (z, i, ig, post) = s.get_batch(int(f["B"]))
+        assert tg is None and ig is None
+        np.testing.assert_array_equal(t.numpy(), f["t_leaves"][k])
+        np.testing.assert_array_equal(r.numpy(), f["t_root"][k])
+        np.testing.assert_array_equal(z.numpy(), f["z"][k])
+        np.testing.assert_array_equal(i.numpy(), f["i_leaves"][k])
+        np.testing.assert_allclose(post, f["post"][k], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(tpp, f["t_pp"][k], rtol=0, atol=1e-12)
+    # numpy's global state (MT key, position, cached Gaussian) ends where the
+    # reference's per-node loops + randn leave it
+    mine = np.random.get_state()
+    CO.seed_everything(224)
+    o = CO.CdmSamplerOracle([4, 4], [3, 3], [0.2, 0.2])
+    o.get_Bayes(10000)
+    o.get_batch(int(f["B"]))
+    o.get_batch(int(f["B"]))
+    want = np.random.get_state()
+    np.testing.assert_array_equal(mine[1], want[1])
+    assert mine[2] == want[2] and mine[3] == want[3] and mine[4] == want[4]
+
+
+def test_native_randn_stream():
+    """ghm_sampler_randn == numpy.random.randn, including the cached second deviate."""
+    from ghmclip import ConditionalDenoiseSampler
+    s = ConditionalDenoiseSampler([2, 2], [3, 3], [P_Y, P_Y], [0.2, 0.2])
+    np.random.seed(5)
+    np.random.randn(1)  # leave a cached Gaussian behind
+    nat = s.native
+    nat.pull_numpy_state()
+    out = np.empty(7)
+    from ghmclip import _native
+    assert _native.host_lib().ghm_sampler_randn(nat._h, out.ctypes.data, 7) == 0
+    want = np.random.randn(7)
+    np.testing.assert_array_equal(out, want)
+    np.random.seed(5)
+    np.random.randn(1)
+    nat.pull_numpy_state()
+    nat.push_numpy_state()
+    assert _native.host_lib().ghm_sampler_randn(nat._h, out.ctypes.data, 7) == 0
+    nat.push_numpy_state()  # the native stream hands back to numpy mid-pair
+    np.testing.assert_array_equal(np.random.randn(3), _after(5, 8, 3))
+
+
+def _after(seed, skip, n):
+    np.random.seed(seed)
+    np.random.randn(skip)
+    return np.random.randn(n)
+
+
+def test_oracle_two_steps_match_reference():
+    """Two full training steps at L=1, d=128, B=4 (cdm_tiny.npz): initial weights of
+    both models, predictions, losses, compare and post-step parameters."""
+    g = _fix("cdm_tiny.npz")
+    tr = CO.OracleCdmTrainer(B=4, L=1)
+    assert [n for n, _ in tr.model.named_parameters()] == list(g["param_names"])
+    st = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+    np.testing.assert_array_equal(st, g["init_stats"])
+    cst = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.clip.parameters()])
+    np.testing.assert_array_equal(cst, g["clip_stats"])
+    for k in range(2):
+        ploss, loss, cmp = tr.step()
+        assert ploss == float(g[f"ploss{k}"]) and loss == float(g[f"loss{k}"])
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-6 * cmp
+        np.testing.assert_array_equal(tr.last_pred.numpy(), g[f"pred{k}"])
+        np.testing.assert_array_equal(tr.last_feat[:, 0].numpy(), g[f"feat{k}"])
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.slow
+def test_oracle_curve_head_matches_reference():
+    """First 5 steps of the default CDM config (cdm_curve.npz)."""
+    g = _fix("cdm_curve.npz")
+    tr = CO.OracleCdmTrainer(B=128, L=9)
+    np.testing.assert_allclose(tr.bayes, g["bayes"], rtol=1e-12)
+    for k in range(5):
+        ploss, _, cmp = tr.step()
+        assert abs(ploss - g["ploss"][k]) <= 1e-6 * g["ploss"][k]
+        assert abs(cmp - g["compare"][k]) <= 1e-6 * g["compare"][k]
+
+
+def test_cdm_module_api_matches_reference_construction():
+    """Same parameter names, shapes, registration order and seeded initial values
+    as the reference constructor (via the oracle, itself pinned by cdm_tiny.npz)."""
+    from ghmclip import ConditionalDenoiseEncoderTransformer
+    from ghmclip.models.cdm import cdm_param_names
+    torch.manual_seed(3)
+    m = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 3, [1, 4], 4, 512, sequential=True)
+    torch.manual_seed(3)
+    o = CO.OracleCdm(82, 81, 10, 128, 3, 512)
+    assert list(m.state_dict().keys()) == list(o.state_dict().keys()) == cdm_param_names(3)
+    for (k, a), (_, b) in zip(m.state_dict().items(), o.state_dict().items()):
+        assert torch.equal(a, b), k
+    with pytest.raises(NotImplementedError):
+        ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, sequential=False)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 1, 10), torch.zeros(2, 81))  # CPU tensors: no fallback
+
+
+def test_checkpoint_loader_accepts_numpy_scalars(tmp_path):
+    """The weights-only loader reads the checkpoint dicts the CLIs write (numpy
+    histories, the numpy-scalar Bayes risk, the data-only loss descriptor)."""
+    from ghmclip.training.train_CLIP import load_checkpoint
+    p = tmp_path / "checkpoint.pth"
+    torch.save({"bayes": np.mean(np.ones(3)), "loss_history": np.zeros(4), "iter": 3,
+                "loss": {"type": "ConditionalGuidedLsLoss", "penalty": 0.1, "guide": False}}, p)
+    d = load_checkpoint(str(p), "cpu")
+    assert d["bayes"] == 1.0 and d["iter"] == 3 and d["loss"]["penalty"] == 0.1

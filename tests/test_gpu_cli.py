@@ -1,0 +1,51 @@
+"""The drop-in CLIs end to end on a HIP device: train_CLIP writes a checkpoint
+under logs/CLIP/<tree folder>/TF_L5.../<timestamp>/ (train_CLIP.py:43-60,193-211),
+and train_sequential_DNS discovers it as its frozen text encoder
+(train_sequential_DNS.py:99-111) and trains the CDM, with the flags of
+scripts/experiments/exp_clip_standardTF.sh / exp_cdm_standardTF.sh (shortened)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CLIP_FLAGS = ["--job_name=CLIP", "--n_ttree_layer=4", "--n_itree_layer=4", "--n_ttree_child=3", "--n_itree_child=3",
+              "--p_ttree_flip=0.2", "--p_itree_flip=0.2", "--flip_scale=1", "--K=4", "--batch_size=8",
+              "--variable_type=10", "--clip_tmodel_nlayer=5", "--clip_imodel_nlayer=5", "--clip_tmodel_nhead=4",
+              "--clip_imodel_nhead=4", "--clip_tmodel_deb=128", "--clip_imodel_deb=128", "--clip_layernorm=True",
+              "--clip_attennorm=True", "--clip_guide=False", "--lr_max=3e-4", "--lr_min=3e-7", "--total_iters=4",
+              "--penalty=1e-3", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+CDM_FLAGS = ["--clip_feature=TF", "--job_name=CDM", "--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4",
+             "--n_ttree_child=3", "--n_itree_child=3", "--p_ttree_flip=0.2", "--p_itree_flip=0.2", "--flip_scale=1",
+             "--sigma=1", "--batch_size=8", "--variable_type=10", "--d_eb=128", "--n_model_layer=2", "--n_head=4",
+             "--layernorm=True", "--normalize_attn=True", "--lr_max=1e-3", "--lr_min=1e-6", "--guide=False",
+             "--total_iters=5", "--penalty=0.1", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def test_clip_then_sequential_cdm_cli(tmp_path, monkeypatch):
+    from ghmclip.training import train_CLIP, train_sequential_DNS
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    hist = train_CLIP.main(CLIP_FLAGS)
+    assert len(hist) == 5 and np.isfinite(hist).all()
+    ck_clip = glob.glob("logs/CLIP/K4_L4C3p20_L4C3p20sc10/TF_L5H4D128_L5H4D128/*/checkpoint.pth")
+    assert len(ck_clip) == 1
+    loss, compare = train_sequential_DNS.main(CDM_FLAGS)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/CDM/K4_L4C3p20_L4C3p20sc10/StT_L2H4D128/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert set(d) == {"model_state_dict", "optimizer_state_dict", "loss", "iter", "loss_history", "ploss_history",
+                      "bayes"}
+    assert d["iter"] == 5
+    np.testing.assert_allclose(d["loss_history"], loss)
+    assert os.path.exists(os.path.join(os.path.dirname(ck[0]), "training.log"))
