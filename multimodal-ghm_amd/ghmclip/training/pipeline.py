@@ -23,6 +23,16 @@ def shard_rows(block_rows, n_blocks, rank, world):
                            for k in range(n_blocks)])
 
 
+def shard_samples(batch_size, rank, world):
+    """(start, stop) of the samples rank `rank` of `world` keeps from a CDM batch:
+    a contiguous 1/world of the rows (the CDM loss is a mean over samples,
+    model.py:998, so shard gradients average to the full-batch ones)."""
+    if batch_size % world:
+        raise ValueError("batch size must divide by the world size")
+    per = batch_size // world
+    return rank * per, (rank + 1) * per
+
+
 class BatchPipeline:
     def __init__(self, native_sampler, batch_size, n_slots=3, row_slice=None):
         """native_sampler: data.NativeClipSampler whose MT state is already set.
@@ -129,11 +139,7 @@ class CdmBatchPipeline(BatchPipeline):
                     torch.empty(B, T, dtype=torch.float64).pin_memory())
         self.slots = [slot() for _ in range(n_slots)]
         if self.slice is not None:
-            rank, world = self.slice
-            if B % world:
-                raise ValueError("batch size must divide by the world size")
-            per = B // world
-            self.rows = (rank * per, (rank + 1) * per)
+            self.rows = shard_samples(B, *self.slice)
 
     def _fill(self, i):
         t, im, z = self.slots[i]

@@ -80,3 +80,66 @@ def test_shard_rows_partition():
     # each shard keeps the block structure: block b of the shard = rows b*B + [r*B/4, (r+1)*B/4)
     np.testing.assert_array_equal(parts[1][:4], [4, 5, 6, 7])
     np.testing.assert_array_equal(parts[1][4:8], [20, 21, 22, 23])
+
+
+def _cdm_worker(rank, world, port, B, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-ghm_amd")]
+    from ghmclip.training.pipeline import shard_samples
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    model, batch, cond = _cdm_setup(B)
+    a, b = shard_samples(B, rank, world)
+    loss = _cdm_loss(model, batch, cond, slice(a, b))
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None])
+    dist.all_reduce(g, op=dist.ReduceOp.SUM)
+    g /= world
+    lt = loss.detach().reshape(1).clone()
+    dist.all_reduce(lt, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        out.put((g.numpy(), float(lt.item() / world)))
+    dist.destroy_process_group()
+
+
+def _cdm_setup(B):
+    """Small CDM (27-leaf trees, d=16, L=1) on one global batch, conditioning
+    features standing in for the frozen CLIP embedding."""
+    from oracle import cdm_oracle as CO
+    CO.seed_everything(224)
+    s = CO.CdmSamplerOracle([3, 3], [3, 3], [0.2, 0.2])
+    batch = s.get_batch(B)
+    model = CO.OracleCdm(28, 27, 10, 16, 1, 64)
+    cond = torch.randn(B, 1, 10, generator=torch.Generator().manual_seed(1))
+    return model, batch, cond
+
+
+def _cdm_loss(model, batch, cond, rows):
+    from oracle import cdm_oracle as CO
+    _, _, z, il, _ = batch
+    pred = model(cond[rows], torch.as_tensor(z[rows]))
+    return CO.ls_loss(pred, torch.as_tensor(il[rows], dtype=torch.long))
+
+
+def test_cdm_sharded_grads_equal_full_batch():
+    """Sequential CDM data parallel: each rank's contiguous sample shard
+    (pipeline.shard_samples) + an AVG all-reduce == the full-batch gradient."""
+    B, world = 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_cdm_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    g_dp, loss_dp = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    model, batch, cond = _cdm_setup(B)
+    loss = _cdm_loss(model, batch, cond, slice(0, B))
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None]).numpy()
+    assert abs(loss_dp - loss.item()) <= 1e-6 * loss.item()
+    np.testing.assert_allclose(g_dp, g, rtol=1e-4, atol=1e-6)
