@@ -233,20 +233,25 @@ __global__ __launch_bounds__(256) void k_cdm_readout_fwd(const float* __restrict
 
 // Sum-of-squares loss of the CDM (ConditionalGuidedLsLoss guide=False, LsLoss):
 //   loss = mean_n sum_t (pred - target)^2, compare = the same against the BP
-//   posterior means; dpred = 2 (pred - target) / N.  One 256-thread workgroup,
-//   thread-strided rows and a fixed reduction tree (deterministic).
-//   loss_out[0] <- loss, loss_out[1] <- compare; hist/chist[*step] likewise.
-__global__ __launch_bounds__(256) void k_ls_loss(const float* __restrict__ pred, const uint8_t* __restrict__ target,
-                                                 const float* __restrict__ post, float* __restrict__ dpred,
-                                                 float* __restrict__ loss_out, float* __restrict__ hist,
-                                                 float* __restrict__ chist, const int32_t* __restrict__ step,
-                                                 int N, int Tp) {
-  __shared__ float red[2][4];
+//   posterior means; dpred = 2 (pred - target) / N.  One 1024-thread workgroup:
+//   wave w takes rows w, w+16, ... (lanes over tokens, coalesced), each row sum a
+//   fixed shuffle tree, rows accumulated in order per wave, waves in fixed order
+//   (deterministic).  loss_out[0] <- loss, loss_out[1] <- compare; hist /
+//   chist[*step] likewise.
+constexpr int LS_WAVES = 16;
+__global__ __launch_bounds__(64 * LS_WAVES) void k_ls_loss(const float* __restrict__ pred,
+                                                           const uint8_t* __restrict__ target,
+                                                           const float* __restrict__ post, float* __restrict__ dpred,
+                                                           float* __restrict__ loss_out, float* __restrict__ hist,
+                                                           float* __restrict__ chist,
+                                                           const int32_t* __restrict__ step, int N, int Tp) {
+  __shared__ float red[2][LS_WAVES];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float inv2 = 2.f / static_cast<float>(N);
   float sl = 0.f, sc = 0.f;
-  for (int n = threadIdx.x; n < N; n += 256) {
+  for (int n = w; n < N; n += LS_WAVES) {
     float rl = 0.f, rc = 0.f;
-    for (int t = 0; t < Tp; ++t) {
+    for (int t = lane; t < Tp; t += 64) {
       const int64_t i = static_cast<int64_t>(n) * Tp + t;
       const float p = pred[i];
       const float r = p - static_cast<float>(target[i]);
@@ -257,21 +262,26 @@ __global__ __launch_bounds__(256) void k_ls_loss(const float* __restrict__ pred,
         rc += c * c;
       }
     }
+    rl = sum32(rl);
+    rl += xhalf(rl);
+    rc = sum32(rc);
+    rc += xhalf(rc);
     sl += rl;
     sc += rc;
   }
-  sl = sum32(sl);
-  sl += xhalf(sl);
-  sc = sum32(sc);
-  sc += xhalf(sc);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = sl;
-    red[1][threadIdx.x >> 6] = sc;
+  if (lane == 0) {
+    red[0][w] = sl;
+    red[1][w] = sc;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float l = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) / static_cast<float>(N);
-    const float c = ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) / static_cast<float>(N);
+    float l = 0.f, c = 0.f;
+    for (int k = 0; k < LS_WAVES; ++k) {
+      l += red[0][k];
+      c += red[1][k];
+    }
+    l /= static_cast<float>(N);
+    c /= static_cast<float>(N);
     loss_out[0] = l;
     loss_out[1] = c;
     if (hist && step) hist[*step] = l;
@@ -370,8 +380,8 @@ extern "C" int ghm_ls_loss(const float* pred, const uint8_t* target, const float
                            void* stream) {
   GHM_CHECK(pred && target && loss_out, "null pointer");
   GHM_CHECK(n_seq >= 1 && n_seq <= (1 << 30) && T_img >= 1, "shape");
-  hipLaunchKernelGGL(k_ls_loss, dim3(1), dim3(256), 0, ghm_stream(stream), pred, target, post, dpred, loss_out, hist,
-                     chist, step, static_cast<int>(n_seq), T_img);
+  hipLaunchKernelGGL(k_ls_loss, dim3(1), dim3(64 * LS_WAVES), 0, ghm_stream(stream), pred, target, post, dpred,
+                     loss_out, hist, chist, step, static_cast<int>(n_seq), T_img);
   return ghm_launch_status();
 }
 

@@ -347,19 +347,30 @@ __device__ __forceinline__ int r128_off(int row, int lc) { return row * 32 + 8 *
 // vmcnt), every lane stores to a real row (lanes past M recompute row M-1), so
 // each wave has exactly 4 stores in flight per chunk.
 // ---------------------------------------------------------------------------
+// NW waves fill a plane: wave b issues the instructions of row groups b, b+NW, ...
+template <int NW>
 __device__ __forceinline__ void fill_r32_w8(const __bf16* g, int ldg, int lo_off, __bf16* ih, __bf16* il) {
-  const int b = threadIdx.x >> 6, L = threadIdx.x & 63;
-  const int row = 4 * b + (L >> 4), lc = (L & 15) ^ (row & 15);
-  const __bf16* src = g + row * ldg + 8 * lc;
-  glds16(src, ih + 512 * b);
-  glds16(src + lo_off, il + 512 * b);
+  const int L = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8 / NW; ++k) {
+    const int b = (threadIdx.x >> 6) + NW * k;
+    const int row = 4 * b + (L >> 4), lc = (L & 15) ^ (row & 15);
+    const __bf16* src = g + row * ldg + 8 * lc;
+    glds16(src, ih + 512 * b);
+    glds16(src + lo_off, il + 512 * b);
+  }
 }
+template <int NW>
 __device__ __forceinline__ void fill_r128_w8(const __bf16* g, int ldg, int lo_off, __bf16* ih, __bf16* il) {
-  const int b = threadIdx.x >> 6, L = threadIdx.x & 63;
-  const int row = 16 * b + (L >> 2), lc = (L & 3) ^ ((row >> 2) & 3);
-  const __bf16* src = g + row * ldg + 8 * lc;
-  glds16(src, ih + 512 * b);
-  glds16(src + lo_off, il + 512 * b);
+  const int L = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8 / NW; ++k) {
+    const int b = (threadIdx.x >> 6) + NW * k;
+    const int row = 16 * b + (L >> 2), lc = (L & 3) ^ ((row >> 2) & 3);
+    const __bf16* src = g + row * ldg + 8 * lc;
+    glds16(src, ih + 512 * b);
+    glds16(src + lo_off, il + 512 * b);
+  }
 }
 
 // pick element 4g + r of a wave-uniform 16-float group (scalar registers)
@@ -368,7 +379,10 @@ __device__ __forceinline__ float pick16(const float4* b4, int g, int r) {
   return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
 }
 
-__global__ __launch_bounds__(512, 2) void k_ln_mlp_fwd_x3b(
+// NW = waves per workgroup (8: 128 tokens; 4: 64 tokens, for token counts too
+// small to fill 256 CUs with 128-token workgroups).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
     float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
@@ -381,13 +395,13 @@ __global__ __launch_bounds__(512, 2) void k_ln_mlp_fwd_x3b(
   auto s2l = [&](int buf) { return lds + 4 * PLANE * buf + 3 * PLANE; };
   constexpr int NC = GHM_F / 32;
   const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
-  const int64_t m = (static_cast<int64_t>(blockIdx.x) * 8 + (threadIdx.x >> 6)) * 16 + t;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + (threadIdx.x >> 6)) * 16 + t;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
   const __bf16* W1 = pack + PK_W1_N;
   const __bf16* W2 = pack + PK_W2_P32;
-  fill_r32_w8(W1, GHM_D, PK_W, s1h(0), s1l(0));
-  fill_r128_w8(W2, GHM_F, PK_W, s2h(0), s2l(0));
+  fill_r32_w8<NW>(W1, GHM_D, PK_W, s1h(0), s1l(0));
+  fill_r128_w8<NW>(W2, GHM_F, PK_W, s2h(0), s2l(0));
   // LN2 of the token row, lane holds features 32s + 8g + i
   bf16x8 xh[4], xl[4];
   {
@@ -435,8 +449,8 @@ __global__ __launch_bounds__(512, 2) void k_ln_mlp_fwd_x3b(
     const int cur = c & 1;
     {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
       const int cn = c + 1 < NC ? c + 1 : NC - 1;
-      fill_r32_w8(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
-      fill_r128_w8(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
+      fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
+      fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
     }
     f32x4 u[2];
 #pragma unroll
@@ -1227,8 +1241,14 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
                                   float* stats, int64_t M, int D, int F, float eps, void* stream) {
   GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && G && Dg && stats, "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  hipLaunchKernelGGL(k_ln_mlp_fwd_x3b, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
-                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1, b2,
-                     H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
+  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
+  float2* st = reinterpret_cast<float2*>(stats);
+  if ((M + 127) / 128 >= 256) {  // enough 128-token workgroups to give every CU one
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
+                       ghm_stream(stream), H_mid, ln_w, ln_b, pk, b1, b2, H_out, G, Dg, st, M, eps);
+  } else {
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, dim3(static_cast<unsigned>((M + 63) / 64)), dim3(256), 0,
+                       ghm_stream(stream), H_mid, ln_w, ln_b, pk, b1, b2, H_out, G, Dg, st, M, eps);
+  }
   return ghm_launch_status();
 }
