@@ -49,7 +49,8 @@ int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves
  *   root               : [B] uint8 (may be NULL)
  *   z                  : [B][n_child**n_layer] float64 noisy image observations
  *                        randn * sigma + leaf (the reference's image_tree_noise, transposed)
- * Stream order: choice(V, B), text tree, image tree, randn(T, B) leaf-major. */
+ * Stream order: choice(V, B), text tree, image tree, randn(T, B) leaf-major.
+ * z == NULL draws the two trees only: NextWordPredictSampler.get_batch (:902-907). */
 int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t* t_leaves, uint8_t* i_leaves,
                          uint8_t* root, double* z);
 /* numpy legacy Gaussian cache (RandomState.get_state()[3:5]): import / export. */

@@ -248,16 +248,17 @@ extern "C" int ghm_sampler_randn(ghm_sampler* s, double* out, int64_t n) {
 // stream order: choice(V, B) shared roots (:863), the text tree (:865), the image
 // tree (:866), then np.random.randn(T, B) * sigma + leaves (:869) — drawn
 // leaf-major ([T][B] C order) and written transposed as z[b][t] (the .T at :882).
+// z == NULL: the trees only (NextWordPredictSampler.get_batch, :902-907).
 extern "C" int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t* t_leaves,
                                     uint8_t* i_leaves, uint8_t* root, double* z) {
-  if (!s || B < 1 || !t_leaves || !i_leaves || !z) return -1;
+  if (!s || B < 1 || !t_leaves || !i_leaves) return -1;
   const int V = s->V, T = s->T;
   std::vector<uint8_t> r(B);
   for (int b = 0; b < B; ++b) r[b] = static_cast<uint8_t>(s->mt.bounded(V - 1));
   const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * V * V;
   sample_tree(s, s->cdf.data(), r.data(), B, t_leaves);
   sample_tree(s, s->cdf.data() + per, r.data(), B, i_leaves);
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; z && t < T; ++t) {
     for (int b = 0; b < B; ++b) {
       const double g = legacy_gauss(s);
       z[static_cast<size_t>(b) * T + t] = g * sigma + static_cast<double>(i_leaves[static_cast<size_t>(b) * T + t]);

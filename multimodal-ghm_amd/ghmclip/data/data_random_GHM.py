@@ -18,7 +18,8 @@ import torch
 from .. import _native
 
 __all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior", "guided_targets",
-           "NativeClipSampler", "ConditionalDenoiseSampler", "bp_dns_posterior", "bp_cls_root_message"]
+           "NativeClipSampler", "ConditionalDenoiseSampler", "bp_dns_posterior", "bp_cls_root_message",
+           "NextWordPredictSampler", "bp_nwp_posterior"]
 
 
 def _softmax_row(x):
@@ -107,7 +108,8 @@ class NativeClipSampler:
         """ConditionalDenoiseSampler draw into caller-owned buffers: uint8 [B, T]
         leaves, float64 [B, T] noisy observations z, optional uint8 [B] roots."""
         rc = self._lib.ghm_sampler_next_cdm(self._h, B, float(sigma), _addr(t_leaves), _addr(i_leaves),
-                                            _addr(root) if root is not None else None, _addr(z))
+                                            _addr(root) if root is not None else None,
+                                            _addr(z) if z is not None else None)
         _native_check(rc)
 
     def set_gauss(self, has_gauss, gauss):
@@ -387,3 +389,109 @@ class ConditionalDenoiseSampler(DoubleSampler):
         _, post = self.posterior(tl, z)
         loss = np.sum(np.power(post - il.astype(np.int64), 2), 1)
         return np.mean(loss), np.std(loss) / np.sqrt(n_eval)
+
+
+def bp_nwp_posterior(templ, leaves, ext):
+    """BP_NWP_autoregressive(guide_info=False) (data_random_GHM.py:336-466) on the
+    host, vectorised over the batch: p(leaf p+1 | leaves <= p, image evidence ext)
+    for every position p, [B, n_leaves - 1, V] float32 (the reference's predict_pp
+    tensor dtype).  templ [L][C][V][V]; leaves [B, n_leaves]; ext [V, B].
+    A node's qd message is rewritten whenever it is an ancestor of the current
+    leaf, so completed earlier siblings keep their last (complete) message, as in
+    the reference's mutable tree."""
+    n_layer, C, V, _ = templ.shape
+    lv = np.asarray(leaves).astype(np.int64).T
+    n_leaves, B = lv.shape
+    qd = [None] + [np.zeros((C ** d, V, B)) for d in range(1, n_layer + 1)]
+    hd = [None] + [np.zeros((C ** d, V, B)) for d in range(1, n_layer)]
+    out = np.zeros((B, n_leaves - 1, V), dtype=np.float32)
+    for p in range(n_leaves - 1):
+        q = np.log(templ[-1, p % C][:, lv[p]])  # leaf message :370-371
+        qd[n_layer][p] = q - q.max(0)
+        idn, goal, share = p, [p + 1], [False]
+        for layer in range(n_layer - 1, 0, -1):  # prefix evidence up to the root :381-406
+            par = idn // C
+            h = qd[layer + 1][par * C].copy()
+            for c in range(1, C):
+                if c + par * C <= idn:
+                    h += qd[layer + 1][par * C + c]
+            h -= h.max(0)
+            hd[layer][par] = h
+            qq = np.log(templ[layer - 1, par % C] @ np.exp(h))
+            qd[layer][par] = qq - qq.max(0)
+            goal.append(goal[-1] // C)
+            idn = par
+            share.append(idn == goal[-1])
+        bu = qd[1][0].copy()  # root :410-426
+        for c in range(1, C):
+            if c <= idn:
+                bu += qd[1][c]
+        bu -= bu.max(0)
+        bu = bu + ext
+        bu -= bu.max(0)
+        for layer in range(1, n_layer + 1):  # down the target's path :435-452
+            k = goal[-layer]
+            mat = templ[layer - 1, k % C].T
+            if share[-layer]:
+                b = hd[layer][k] + np.log(mat @ np.exp(bu - qd[layer][k]))
+            else:
+                b = np.log(mat @ np.exp(bu))
+            bu = b - b.max(0)
+        w = np.exp(bu)
+        out[:, p, :] = (w / w.sum(0)).T
+    return out
+
+
+class NextWordPredictSampler(DoubleSampler):
+    """data_random_GHM.py:896-942 with the trees drawn in native code and the BP
+    posteriors (BP_CLS of the image tree, BP_NWP_autoregressive of the text tree)
+    vectorised on the host."""
+
+    def __init__(self, n_layers, n_childs, p_ys, p_flips, flip_scale=1, variable_type=10,
+                 translation_invariance=True, seedtree=42):
+        super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
+                         translation_invariance, seedtree)
+        self.t_templ = _templates(self.t_transition, n_childs[0])
+        self.i_templ = _templates(self.i_transition, n_childs[1])
+        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, 2)
+        self.T = self.native.T
+
+    def draw_numpy(self, batch_size):
+        """One reference-identical draw of the paired trees from numpy's global
+        state: (text leaves uint8 [B, T], image leaves uint8 [B, T], roots [B])."""
+        B, T = batch_size, self.T
+        tl = np.empty((B, T), np.uint8)
+        il = np.empty((B, T), np.uint8)
+        root = np.empty(B, np.uint8)
+        self.native.pull_numpy_state()
+        self.native.next_cdm_into(B, 0.0, tl, il, None, root)
+        self.native.push_numpy_state()
+        return tl, il, root
+
+    def posterior(self, tl, il):
+        """(next-word posteriors [B, T-1, V] float32, image BP_CLS posteriors [B, V])."""
+        p_y = np.ones(self.variable_type) / self.variable_type
+        ext = bp_cls_root_message(self.i_templ, il)
+        return bp_nwp_posterior(self.t_templ, tl, ext), bp_cls_posterior(self.i_templ, il, p_y)
+
+    def get_batch(self, batch_size=128, device="cpu", guide=False):
+        """:902-929.  Returns (text inputs int64 [B, T-1], targets [B, T-1], None,
+        posteriors float32 [B, T-1, V] (torch, on device)), (image leaves int64
+        [B, T], roots [B], None, image posteriors [B, V])."""
+        if guide:
+            raise NotImplementedError("guided VLM (BP_NWP guide_info targets) is not built yet")
+        tl, il, root = self.draw_numpy(batch_size)
+        post, i_pp = self.posterior(tl, il)
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int64)).to(device)  # noqa: E731
+        return ((to(tl[:, :-1]), to(tl[:, 1:]), None, torch.from_numpy(post).to(device)),
+                (to(il), to(root), None, i_pp))
+
+    def get_Bayes(self, n_eval=30000):
+        """:931-942 — mean and standard error of -log p(next leaf) under the exact
+        posterior (float32, as the reference's torch reductions)."""
+        tl, il, _ = self.draw_numpy(n_eval)
+        post, _ = self.posterior(tl, il)
+        pred = torch.from_numpy(post).reshape(-1, self.variable_type)
+        tc = torch.from_numpy(tl[:, 1:].astype(np.int64).reshape(-1))
+        loss = -torch.log(pred[torch.arange(len(tc)), tc])
+        return torch.mean(loss), torch.std(loss) / np.sqrt(n_eval)

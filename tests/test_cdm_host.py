@@ -153,3 +153,61 @@ def test_checkpoint_loader_accepts_numpy_scalars(tmp_path):
                 "loss": {"type": "ConditionalGuidedLsLoss", "penalty": 0.1, "guide": False}}, p)
     d = load_checkpoint(str(p), "cpu")
     assert d["bayes"] == 1.0 and d["iter"] == 3 and d["loss"]["penalty"] == 0.1
+
+
+# ---------------------------------------------------------------------------
+# sequential VLM (BASELINE config 5): oracle and product sampler vs the reference
+# ---------------------------------------------------------------------------
+def test_vlm_oracle_sampler_and_bayes_match_reference():
+    from oracle import vlm_oracle as VO
+    f = _fix("vlm_sampler.npz")
+    s = VO.NwpSamplerOracle([4, 4], [3, 3], [0.2, 0.2])
+    np.testing.assert_array_equal(s.t_trans, f["t_transition"])
+    np.testing.assert_allclose(s.get_Bayes(int(f["n_bayes"])), f["bayes"], rtol=1e-6)
+    np.random.seed(224)
+    for k in range(2):
+        xt, yt, post, il, root = s.get_batch(int(f["B"]))
+        np.testing.assert_array_equal(xt, f["xt"][k])
+        np.testing.assert_array_equal(yt, f["yt"][k])
+        np.testing.assert_array_equal(il, f["i_leaves"][k])
+        np.testing.assert_array_equal(root, f["i_root"][k])
+        np.testing.assert_allclose(post, f["post"][k], rtol=0, atol=1e-7)
+
+
+def test_vlm_native_sampler_matches_reference():
+    """NextWordPredictSampler: native paired trees bit-exact, host BP_NWP_autoregressive
+    posteriors equal to the reference's float32 tensor, Bayes risk."""
+    from ghmclip import NextWordPredictSampler
+    f = _fix("vlm_sampler.npz")
+    s = NextWordPredictSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2])
+    bayes = s.get_Bayes(int(f["n_bayes"]))
+    np.testing.assert_allclose([float(bayes[0]), float(bayes[1])], f["bayes"], rtol=1e-6)
+    np.random.seed(224)
+    for k in range(2):
+        (xt, yt, tg, post), (il, root, ig, ipp) = s.get_batch(int(f["B"]))
+        assert tg is None and ig is None
+        np.testing.assert_array_equal(xt.numpy(), f["xt"][k])
+        np.testing.assert_array_equal(yt.numpy(), f["yt"][k])
+        np.testing.assert_array_equal(il.numpy(), f["i_leaves"][k])
+        np.testing.assert_array_equal(root.numpy(), f["i_root"][k])
+        np.testing.assert_allclose(post.numpy(), f["post"][k], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(ipp, f["i_pp"][k], rtol=0, atol=1e-12)
+
+
+def test_vlm_oracle_two_steps_match_reference():
+    """Two full training steps at d=256, L=1, B=4 (vlm_tiny.npz)."""
+    from oracle import vlm_oracle as VO
+    g = _fix("vlm_tiny.npz")
+    tr = VO.OracleVlmTrainer(B=4, L=1)
+    assert [n for n, _ in tr.model.named_parameters()] == list(g["param_names"])
+    st = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+    np.testing.assert_array_equal(st, g["init_stats"])
+    cst = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.clip.parameters()])
+    np.testing.assert_array_equal(cst, g["clip_stats"])
+    for k in range(2):
+        ploss, loss, cmp = tr.step()
+        assert ploss == float(g[f"ploss{k}"]) and loss == float(g[f"loss{k}"])
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-6 * cmp
+        np.testing.assert_array_equal(tr.last_logits.numpy(), g[f"logits{k}"])
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-12, atol=1e-12)
