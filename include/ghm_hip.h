@@ -254,6 +254,48 @@ int ghm_ls_loss(const float* pred, const uint8_t* target, const float* post, flo
 int ghm_cdm_readout_bwd(const float* H, const float* w_ro, const float* dpred, float* dH, float* part_w,
                         float* part_b, int64_t n_seq, int T, int T_img, int D, void* stream);
 
+/* ---- sequential VLM (next-word prediction, train_sequential_NWP.py) ----------
+ * AutoRegressiveTransformer (models/model.py:132-335, sequential=True,
+ * auto_regressive=True) at width D (256 in exp_vlm_*.sh): its plain projections
+ * (QKV, MLP, readout) are library GEMMs in the host code; these are the operators
+ * between them.  Layouts row-major [rows][D] fp32, M = n_seq * T. */
+/* H0 = token embedding + positions (model.py:274-293, :305): prefix token t < P gets
+ * feat[n, t, 0:V] zero-padded to D, text token t >= P gets tok_w[xt[n, t - P]].
+ * onehot (may be NULL) [M][V] = the text tokens' one-hot rows (0 on prefix rows). */
+int ghm_vlm_embed_fwd(const uint8_t* xt, const float* feat, const float* tok_w, const float* pos_w, float* H0,
+                      float* onehot, int64_t n_seq, int T, int P, int V, int D, void* stream);
+/* Row LayerNorm Y = LN(X) (nn.LayerNorm(D), biased variance), stats [M] (mean, rstd);
+ * D in {128, 256, 512}. */
+int ghm_ln_rows_fwd(const float* X, const float* w, const float* b, float* Y, float* stats, int64_t M, int D,
+                    float eps, void* stream);
+/* dX = dres + LayerNorm backward of dY (dres may alias dX); part [n_blocks][2][D]
+ * per-block (dgamma, dbeta) partials, n_blocks = ghm_ln_rows_blocks(M). */
+int64_t ghm_ln_rows_blocks(int64_t M);
+int ghm_ln_rows_bwd(const float* dY, const float* X, const float* stats, const float* w, const float* dres,
+                    float* dX, float* part, int64_t M, int D, void* stream);
+/* H_mid = H + A V + (A / D) V with A = softmax((Q K^T + mask) / scale_div), the
+ * prefix-causal mask of generate_mask (model.py:24-33) and the reference's double
+ * attention residual (:338-341); P [n_seq][96][96] saved for backward.  q, k, v
+ * [M][D] (T <= 96, D % 64 == 0). */
+int ghm_vlm_attn_fwd(const float* q, const float* k, const float* v, const float* H, float* H_mid, float* P,
+                     int64_t n_seq, int T, int D, int n_prefix, float scale_div, void* stream);
+/* Backward of ghm_vlm_attn_fwd: dq, dk, dv [M][D] from dH_mid (the residual term
+ * dH += dH_mid is the caller's). */
+int ghm_vlm_attn_bwd(const float* q, const float* k, const float* v, const float* P, const float* dH_mid, float* dq,
+                     float* dk, float* dv, int64_t n_seq, int T, int D, float scale_div, void* stream);
+/* G = GELU(U), Dg = GELU'(U) (nn.GELU, approximate='none'); out = a * b; out = a + b. */
+int ghm_gelu_fwd(const float* U, float* G, float* Dg, int64_t n, void* stream);
+int ghm_mul(const float* a, const float* b, float* out, int64_t n, void* stream);
+int ghm_add(const float* a, const float* b, float* out, int64_t n, void* stream);
+/* Next-token cross entropy over the text rows t >= n_prefix of logits [n_seq][T][V]
+ * (ConditionalGuidedCELoss guide=False, model.py:1087-1098) and the batchmean KL of
+ * post [n_seq][T - n_prefix][V] against softmax(logits) (KLdiv, :1067-1078; post may
+ * be NULL); dlogits (may be NULL) = (softmax - onehot) / rows on text rows, 0 on
+ * prefix rows.  loss_out[0..1] <- loss, compare; hist / chist [*step] when non-NULL. */
+int ghm_ce_kl(const float* logits, const uint8_t* targets, const float* post, float* dlogits, float* loss_out,
+              float* hist, float* chist, const int32_t* step, int64_t n_seq, int T, int n_prefix, int V,
+              void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

@@ -61,6 +61,16 @@ HIP_SIGNATURES = {
     "ghm_cdm_readout_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ls_loss": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_cdm_readout_bwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_vlm_embed_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
+    "ghm_ln_rows_fwd": [_p, _p, _p, _p, _p, _i64, _i, _f, _p],
+    "ghm_ln_rows_blocks": [_i64],
+    "ghm_ln_rows_bwd": [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
+    "ghm_vlm_attn_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _p],
+    "ghm_vlm_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_gelu_fwd": [_p, _p, _p, _i64, _p],
+    "ghm_mul": [_p, _p, _p, _i64, _p],
+    "ghm_add": [_p, _p, _p, _i64, _p],
+    "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ln_qkv_fwd_x3": [_p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
@@ -78,7 +88,7 @@ HIP_SIGNATURES = {
     "ghm_add_cols": [_p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64}
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64}
 
 HOST_SIGNATURES = {
     "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],

@@ -1,0 +1,320 @@
+"""Sequential VLM (next-word prediction, BASELINE config 5) on the HIP path.
+
+Reference: models/model.py:132-335 (AutoRegressiveTransformer, sequential=True,
+auto_regressive=True), :24-33 (generate_mask), :1080-1149 (ConditionalGuidedCELoss),
+:1067-1078 (KLdiv); trained by training/train_sequential_NWP.py with a frozen CLIP
+image encoder supplying the one prefix token.
+
+``VlmPlan`` runs one model at one batch shape with no autograd: the plain
+projections (Q/K/V, the MLP's two Linear layers, the readout) are library GEMMs
+(torch.mm / addmm on rocBLAS / hipBLASLt, fp32), every other operator is a
+hand-written kernel of libghm_hip (csrc/ghm_vlm.hip): embedding, row LayerNorm
+forward/backward, the masked double-residual attention forward/backward, GELU,
+elementwise products, the cross-entropy + KL loss.  All buffers are allocated
+once; a step is a fixed launch sequence (graph-capturable).
+
+HBM layout (M = n_seq * T tokens, D = n_embd, F = 4 D, fp32 row-major):
+  H [L+1][M][D], Hmid / X1 (LN1 out) / X2 (LN2 out) / q / k / v [L][M][D],
+  G, Dg (GELU(U), GELU'(U)) [L][M][F], P [L][n_seq][96][96], st1 / st2 [L][M][2];
+  backward scratch dH [2][M][D], dX, dq, dk, dv [M][D], dG [M][F].
+"""
+import ctypes
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _native
+from .hip_encoder import require_hip
+
+__all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names",
+           "VLM_UNTRAINED"]
+
+# never given a gradient by the reference in sequential mode (the image prefix is a
+# frozen CLIP feature, _out is unused): AdamW and clip_grad_norm_ skip them
+VLM_UNTRAINED = ("i_embedding.weight", "_out.weight", "_out.bias")
+
+
+def vlm_param_names(n_layer):
+    """state_dict keys of AutoRegressiveTransformer in registration order
+    (model.py:177-218: the ModuleLists are registered before t_/i_embedding)."""
+    names = ["position_embeddings.weight"]
+    names += [f"_queries.{l}.weight" for l in range(n_layer)]
+    names += [f"_keys.{l}.weight" for l in range(n_layer)]
+    names += [f"_values.{l}.weight" for l in range(n_layer)]
+    for l in range(n_layer):
+        names += [f"_mlps.{l}.0.weight", f"_mlps.{l}.0.bias", f"_mlps.{l}.2.weight", f"_mlps.{l}.2.bias"]
+    for l in range(n_layer):
+        names += [f"_lns_1.{l}.weight", f"_lns_1.{l}.bias"]
+    for l in range(n_layer):
+        names += [f"_lns_2.{l}.weight", f"_lns_2.{l}.bias"]
+    names += ["t_embedding.weight", "i_embedding.weight", "_read_out.weight", "_read_out.bias", "_out.weight",
+              "_out.bias"]
+    return names
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class VlmPlan:
+    def __init__(self, n_layer, n_token, n_seq, n_prefix=1, num_class=10, n_embd=256, eps=1e-5,
+                 normalize_attn=True, device="cuda"):
+        if n_token > 96:
+            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
+        if n_embd not in (128, 256, 512):
+            raise ValueError(f"the HIP VLM kernels take n_embd in (128, 256, 512) (got {n_embd})")
+        self.L, self.T, self.N, self.P, self.V, self.D = n_layer, n_token, n_seq, n_prefix, num_class, n_embd
+        self.F = 4 * n_embd
+        self.M = M = n_seq * n_token
+        self.eps = float(eps)
+        self.scale_div = float(math.sqrt(n_embd)) if normalize_attn else 1.0  # model.py:335-336
+        self.device = torch.device(device)
+        L, D, F, N = n_layer, n_embd, self.F, n_seq
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.H = e(L + 1, M, D)
+        self.Hmid, self.X1, self.X2 = e(L, M, D), e(L, M, D), e(L, M, D)
+        self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
+        self.G, self.Dg = e(L, M, F), e(L, M, F)
+        self.Pm = torch.zeros(L, N, 96, 96, dtype=torch.float32, device=self.device)
+        self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
+        self.U, self.Y = e(M, F), e(M, D)
+        self.logits, self.dlogits = e(M, num_class), e(M, num_class)
+        self.onehot = e(M, num_class)
+        self.dH = e(2, M, D)
+        self.dX, self.dq, self.dk, self.dv = e(M, D), e(M, D), e(M, D), e(M, D)
+        self.dG = e(M, F)
+        self.nblk = int(_native.hip_lib().ghm_ln_rows_blocks(M))
+        self.part_ln = e(self.nblk, 2, D)
+        self.xt = torch.empty(N, n_token - n_prefix, dtype=torch.uint8, device=self.device)
+        self._gen = 0
+
+    # ------------------------------------------------------------------
+    def forward(self, p, xt, feat):
+        """p: name -> fp32 device tensor; xt uint8 [N, T - P] text tokens; feat
+        f32 [N, P, V] prefix features.  Returns self.logits [M, V] (all rows)."""
+        s = _stream()
+        c = _native.call
+        M, D, T, N = self.M, self.D, self.T, self.N
+        c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
+          _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
+        for l in range(self.L):
+            c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+              _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
+            torch.mm(self.X1[l], p[f"_queries.{l}.weight"].t(), out=self.q[l])
+            torch.mm(self.X1[l], p[f"_keys.{l}.weight"].t(), out=self.k[l])
+            torch.mm(self.X1[l], p[f"_values.{l}.weight"].t(), out=self.v[l])
+            c("ghm_vlm_attn_fwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.H[l]),
+              _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, s)
+            c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
+              _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
+            torch.addmm(p[f"_mlps.{l}.0.bias"], self.X2[l], p[f"_mlps.{l}.0.weight"].t(), out=self.U)
+            c("ghm_gelu_fwd", _ptr(self.U), _ptr(self.G[l]), _ptr(self.Dg[l]), M * self.F, s)
+            torch.addmm(p[f"_mlps.{l}.2.bias"], self.G[l], p[f"_mlps.{l}.2.weight"].t(), out=self.Y)
+            c("ghm_add", _ptr(self.Hmid[l]), _ptr(self.Y), _ptr(self.H[l + 1]), M * D, s)  # :344-347
+        torch.addmm(p["_read_out.bias"], self.H[self.L], p["_read_out.weight"].t(), out=self.logits)
+        self._gen += 1
+        return self.logits
+
+    def backward(self, p, g, dlogits=None):
+        """Writes d(loss)/d(param) into g[name] for every trained parameter (not
+        VLM_UNTRAINED) from dlogits [M, V] (defaults to self.dlogits).  Returns
+        dL/dH_0 [M, D] (its prefix rows give the gradient of the features)."""
+        s = _stream()
+        c = _native.call
+        M, D = self.M, self.D
+        dz = self.dlogits if dlogits is None else dlogits
+        cur, nxt = self.dH[0], self.dH[1]
+        torch.mm(dz, p["_read_out.weight"], out=cur)
+        torch.mm(dz.t(), self.H[self.L], out=g["_read_out.weight"])
+        torch.sum(dz, 0, out=g["_read_out.bias"])
+        for l in reversed(range(self.L)):
+            # MLP: H_{l+1} = Hmid + W2 GELU(W1 LN2(Hmid) + b1) + b2
+            torch.mm(cur.t(), self.G[l], out=g[f"_mlps.{l}.2.weight"])
+            torch.sum(cur, 0, out=g[f"_mlps.{l}.2.bias"])
+            torch.mm(cur, p[f"_mlps.{l}.2.weight"], out=self.dG)
+            c("ghm_mul", _ptr(self.dG), _ptr(self.Dg[l]), _ptr(self.dG), M * self.F, s)  # dU
+            torch.mm(self.dG.t(), self.X2[l], out=g[f"_mlps.{l}.0.weight"])
+            torch.sum(self.dG, 0, out=g[f"_mlps.{l}.0.bias"])
+            torch.mm(self.dG, p[f"_mlps.{l}.0.weight"], out=self.dX)
+            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+              _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
+            self._reduce_ln(g, 2, l, s)
+            # attention (nxt = dHmid)
+            c("ghm_vlm_attn_bwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.Pm[l]), _ptr(nxt),
+              _ptr(self.dq), _ptr(self.dk), _ptr(self.dv), self.N, self.T, D, self.scale_div, s)
+            torch.mm(self.dq.t(), self.X1[l], out=g[f"_queries.{l}.weight"])
+            torch.mm(self.dk.t(), self.X1[l], out=g[f"_keys.{l}.weight"])
+            torch.mm(self.dv.t(), self.X1[l], out=g[f"_values.{l}.weight"])
+            torch.mm(self.dq, p[f"_queries.{l}.weight"], out=self.dX)
+            self.dX.addmm_(self.dk, p[f"_keys.{l}.weight"])
+            self.dX.addmm_(self.dv, p[f"_values.{l}.weight"])
+            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+              _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
+            self._reduce_ln(g, 1, l, s)
+        # embedding: positions summed over sequences, token rows through the one-hot
+        torch.sum(cur.view(self.N, self.T, D), 0, out=g["position_embeddings.weight"])
+        torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
+        return cur
+
+    def _reduce_ln(self, g, which, l, s):
+        j = _native.ReduceJob()
+        j.part = self.part_ln.data_ptr()
+        j.n_split = self.nblk
+        j.n_seg = 2
+        j.n = 2 * self.D
+        j.dst[0] = g[f"_lns_{which}.{l}.weight"].data_ptr()
+        j.dst[1] = g[f"_lns_{which}.{l}.bias"].data_ptr()
+        j.off[0], j.off[1], j.off[2] = 0, self.D, 2 * self.D
+        _native.call("ghm_reduce_batch", (_native.ReduceJob * 1)(j), 1, s)
+
+
+class _VlmFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, module, xt, zi, *params):
+        N, T1 = xt.shape
+        plan = module._plan(N, T1 + zi.shape[1], zi.shape[1], xt.device)
+        pd = dict(zip(module._names, params))
+        plan.xt.copy_(xt.to(torch.uint8))
+        feat = zi.contiguous().float()
+        logits = plan.forward(pd, plan.xt, feat)
+        ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
+        ctx.save_for_backward(*params)
+        return logits.view(N, T1 + zi.shape[1], -1)[:, zi.shape[1]:, :].clone()
+
+    @staticmethod
+    def backward(ctx, dlog):
+        plan = ctx.plan
+        if plan._gen != ctx.gen:
+            raise RuntimeError("AutoRegressiveTransformer: another forward of this module overwrote the "
+                               "activations saved for backward")
+        params = ctx.saved_tensors
+        names = ctx.module._names
+        grads = {n: torch.empty_like(p) for n, p in zip(names, params) if n not in VLM_UNTRAINED}
+        dz = torch.zeros(plan.N, plan.T, plan.V, dtype=torch.float32, device=dlog.device)
+        dz[:, plan.P:, :] = dlog
+        dH0 = plan.backward(dict(zip(names, params)), grads, dlogits=dz.view(plan.M, plan.V))
+        d_zi = None
+        if ctx.needs_input_grad[2]:
+            d_zi = dH0.view(plan.N, plan.T, plan.D)[:, :plan.P, :plan.V].clone()
+        return (None, None, d_zi, *[grads.get(n) for n in names])
+
+
+class AutoRegressiveTransformer(nn.Module):
+    """Reference: models/model.py:132-335.  Same constructor, parameter creation order
+    (so torch.manual_seed gives identical weights) and state_dict keys.  The HIP path
+    covers the configuration the VLM experiments train (exp_vlm_{standard,shallow}TF.sh):
+    a frozen-CLIP image feature prefix token, causal text, softmax attention,
+    LayerNorm, MLP, no guide; n_embd in (128, 256, 512)."""
+
+    def __init__(self, n_token=9, n_i_token=4, num_class=10, n_embd=128, n_layer=12, n_guided_layers=(3, 3),
+                 n_head=4, n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True,
+                 auto_regressive=False, sequential=False, layernorm=True, guide=False):
+        super().__init__()
+        self.name = f"EncoderTF_embd={n_embd}_layer={n_layer}_head={n_head}"
+        self.vocab_size = num_class
+        self.context_length = n_token
+        self.n_token = n_token
+        self.n_i_token = n_i_token
+        self.n_embd = n_embd
+        self.n_head = n_head
+        self.n_layer = n_layer
+        self.n_mlp_hidden = n_mlp_hidden
+        self.sequential = sequential
+        self.activation = activation
+        self.mlp = mlp
+        self.normalize_attn = normalize_attn
+        self.layernorm = layernorm
+        self.auto_regressive = auto_regressive
+        self.guide = guide
+        self.n_t_guided_layer = n_guided_layers[0]
+        self.n_i_guided_layer = n_guided_layers[1]
+        self.guided_layer_gap = n_layer // (n_guided_layers[0] * 2 + 1)
+        if activation != "softmax" or not mlp or not layernorm or guide:
+            raise NotImplementedError("HIP VLM: softmax attention, mlp=True, layernorm=True, guide=False")
+        if not (sequential and auto_regressive and n_i_token == 1):
+            raise NotImplementedError("HIP VLM: sequential=True, auto_regressive=True, one prefix token "
+                                      "(train_sequential_NWP.py); the joint model's 161-token sequences "
+                                      "exceed the 96-token attention kernels")
+        if n_mlp_hidden != 4 * n_embd:
+            raise NotImplementedError("HIP VLM: n_mlp_hidden = 4 * n_embd")
+        # construction (RNG) order of the reference, model.py:177-218
+        self.position_embeddings = nn.Embedding(self.context_length, self.n_embd)
+        self._queries = nn.ModuleList()
+        self._keys = nn.ModuleList()
+        self._values = nn.ModuleList()
+        self._mlps = nn.ModuleList()
+        self._lns_1 = nn.ModuleList()
+        self._lns_2 = nn.ModuleList()
+        self.t_guided_layer_flag = [False] * n_layer
+        self.i_guided_layer_flag = [False] * n_layer
+        self.t_embedding = nn.Embedding(self.vocab_size, self.n_embd)
+        self.i_embedding = nn.Embedding(self.vocab_size, self.n_embd)
+        for _ in range(n_layer):
+            self._queries.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._keys.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._values.append(nn.Linear(n_embd, n_embd, bias=False))
+            self._lns_1.append(nn.LayerNorm([self.n_embd]))
+            self._mlps.append(nn.Sequential(nn.Linear(n_embd, n_mlp_hidden), nn.GELU(),
+                                            nn.Linear(n_mlp_hidden, n_embd)))
+            self._lns_2.append(nn.LayerNorm([self.n_embd]))
+        self._read_out = nn.Linear(n_embd, self.vocab_size)
+        self._out = nn.Linear(n_token, 1)
+        self._names = vlm_param_names(n_layer)
+        self._plans = {}
+
+    def _plan(self, n_seq, T, P, device):
+        key = (n_seq, T, P, str(device))
+        if key not in self._plans:
+            self._plans.clear()
+            self._plans[key] = VlmPlan(self.n_layer, T, n_seq, n_prefix=P, num_class=self.vocab_size,
+                                       n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device)
+        return self._plans[key]
+
+    def forward(self, xt, zi):
+        """xt: text tokens [B, T1] (long); zi: the frozen CLIP image feature [B, 1,
+        num_class].  Returns (next-token logits [B, T1, num_class], [[], []])."""
+        require_hip(xt)
+        B, T1 = xt.shape
+        if zi.dim() != 3 or zi.shape[0] != B or zi.shape[1] != self.n_i_token or zi.shape[2] != self.vocab_size:
+            raise ValueError(f"expected zi of shape [{B}, {self.n_i_token}, {self.vocab_size}], got {tuple(zi.shape)}")
+        if T1 + self.n_i_token != self.n_token:
+            raise ValueError(f"expected {self.n_token - self.n_i_token} text tokens, got {T1}")
+        if xt.numel() and (int(xt.min()) < 0 or int(xt.max()) >= self.vocab_size):
+            raise IndexError("token id out of range")
+        sd = dict(self.named_parameters())
+        params = [sd[n] for n in self._names]
+        for prm in params:
+            if prm.dtype != torch.float32 or not prm.is_contiguous():
+                raise RuntimeError("HIP VLM parameters must be contiguous fp32")
+        logits = _VlmFn.apply(self, xt, zi, *params)
+        return logits, [[], []]
+
+
+class ConditionalGuidedCELoss(nn.Module):
+    """models/model.py:1080-1149 (guide=False): returns (loss, 0, 0, 0, 0)."""
+
+    def __init__(self, penalty=1e-4, guide=False):
+        super().__init__()
+        self.penalty = penalty
+        self.guide = guide
+        if guide:
+            raise NotImplementedError("guided VLM penalties are not built yet")
+
+    def forward(self, inputs, targets, verbose=False):
+        logits = inputs[0].reshape(-1, inputs[0].size(-1))
+        loss = nn.functional.cross_entropy(logits, targets[0].reshape(-1), reduction="none")
+        return loss.reshape(-1, targets[0].shape[1]).mean(dim=1).mean(), 0, 0, 0, 0
+
+
+class KLdiv(nn.Module):
+    """models/model.py:1067-1078: batchmean KL of the target distributions against
+    softmax(inputs)."""
+
+    def forward(self, inputs, targets):
+        inputs = nn.functional.log_softmax(inputs.reshape(-1, inputs.size(-1)), dim=1)
+        return nn.functional.kl_div(inputs, targets.reshape(-1, targets.size(-1)), reduction="batchmean")

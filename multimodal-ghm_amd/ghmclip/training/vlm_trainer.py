@@ -1,0 +1,183 @@
+"""Sequential-VLM training step on the HIP path — the hot loop of
+src/ghmclip/training/train_sequential_NWP.py:157-185 (zero_grad, sample, frozen CLIP
+image encoder, next-word model forward, ConditionalGuidedCELoss, KLdiv "Compare",
+backward, clip_grad_norm_, cosine LR, AdamW).
+
+Per step (one captured graph + one optimizer graph): the frozen CLIP image
+EncoderPlan forward -> [B, 10] prefix features, VlmPlan forward, ghm_ce_kl (loss,
+Compare against the host BP posteriors, dlogits, histories), VlmPlan backward;
+then ghm_clip_prepare + ghm_adamw over the flat buffer of the trained parameters
+(i_embedding and _out get no gradient in the reference: skipped, optimizer.py:55-56).
+Data parallel (optional): the loss is a mean over samples; ranks take equal
+sample shards and average gradients with one RCCL all-reduce.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.optimizer import adam_consts, adam_lr_t
+from ..models.vlm import VLM_UNTRAINED, VlmPlan
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class VlmTrainer:
+    def __init__(self, model, clip_model, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
+                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None, precision=None):
+        """model: AutoRegressiveTransformer (sequential); clip_model: the frozen CLIP
+        image EncoderTransformer; lr_schedule: one learning rate per step.
+        precision: matrix-product mode of the frozen CLIP encoder's kernels."""
+        self.device = torch.device(device)
+        self.model, self.clip = model, clip_model
+        self.B = batch_size
+        self.max_norm = float(max_norm)
+        self.pg = process_group
+        sd = dict(model.named_parameters())
+        for p in list(sd.values()) + list(clip_model.parameters()):
+            require_hip(p)
+        trained = [n for n in model._names if n not in VLM_UNTRAINED]
+        n = sum(sd[k].numel() for k in trained)
+        self.n_params = n
+        self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.gflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.pd, self.gd, self.md, self.vd = {}, {}, {}, {}
+        off = 0
+        with torch.no_grad():
+            for k in trained:
+                p = sd[k]
+                c = p.numel()
+                self.pflat[off:off + c].copy_(p.data.reshape(-1))
+                p.data = self.pflat[off:off + c].view(p.shape)
+                p.grad = self.gflat[off:off + c].view(p.shape)
+                self.pd[k], self.gd[k] = p.data, p.grad
+                self.md[k] = self.mflat[off:off + c].view(p.shape)
+                self.vd[k] = self.vflat[off:off + c].view(p.shape)
+                off += c
+            for k in VLM_UNTRAINED:
+                self.pd[k] = sd[k].data
+        self.clip_p = {k: v.data for k, v in clip_model.named_parameters()}
+        self.T, self.P, self.V = model.n_token, model.n_i_token, model.vocab_size
+        self.plan = VlmPlan(model.n_layer, model.n_token, batch_size, n_prefix=model.n_i_token,
+                            num_class=model.vocab_size, n_embd=model.n_embd, normalize_attn=model.normalize_attn,
+                            device=self.device)
+        self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+                                     num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
+                                     n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
+                                     device=self.device, precision=precision)
+        self.precision = self.clip_plan.precision
+        if self.precision == "x3":
+            self.clip_plan.split_weights(self.clip_p)  # frozen: split once
+        Tt = self.T - self.P
+        self.yt = torch.empty(batch_size, Tt, dtype=torch.uint8, device=self.device)
+        self.post = torch.empty(batch_size, Tt, self.V, dtype=torch.float32, device=self.device)
+        self.betas, self.wd = betas, weight_decay
+        self.consts = adam_consts(betas, eps)
+        self.t_offset = t_offset
+        sched = np.zeros((len(lr_schedule), 2), dtype=np.float32)
+        for s, lr in enumerate(lr_schedule):
+            sched[s, 0] = adam_lr_t(lr, s + 1 + t_offset, betas)
+            sched[s, 1] = lr * weight_decay
+        self.sched = torch.from_numpy(sched.reshape(-1)).to(self.device)
+        self.n_sched = len(lr_schedule)
+        self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.hyper = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.work = torch.zeros(1024, dtype=torch.float32, device=self.device)
+        self.loss_out = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
+        self.chist = torch.zeros_like(self.hist)
+        self.graphs = None
+        self.steps_done = 0
+
+    def _fwd_bwd(self):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        emb = self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_NWP.py:163
+        self.plan.forward(self.pd, self.plan.xt, emb)
+        _native.call("ghm_ce_kl", _p(self.plan.logits), _p(self.yt), _p(self.post), _p(self.plan.dlogits),
+                     _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.T, self.P,
+                     self.V, s)
+        self.plan.backward(self.pd, self.gd)
+
+    def _optim(self):
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        b1, omb1, b2, omb2, eps = self.consts
+        _native.call("ghm_clip_prepare", _p(self.gflat), self.n_params, self.max_norm, _p(self.sched),
+                     self.n_sched, _p(self.step_ctr), _p(self.hyper), _p(self.work), s)
+        _native.call("ghm_adamw", _p(self.pflat), _p(self.gflat), _p(self.mflat), _p(self.vflat),
+                     self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
+
+    def _allreduce(self):
+        import torch.distributed as dist
+        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+
+    def set_batch(self, xt, yt, post, i_tokens):
+        """Stage one batch: text inputs / targets uint8 [B, T-1], BP posteriors
+        float32 [B, T-1, V], image leaves uint8 [B, 81] (host-pinned or device)."""
+        self.plan.xt.copy_(xt, non_blocking=True)
+        self.yt.copy_(yt, non_blocking=True)
+        self.post.copy_(post, non_blocking=True)
+        self.clip_plan.tokens.copy_(i_tokens, non_blocking=True)
+
+    def step(self):
+        if self.steps_done >= self.n_sched:
+            raise RuntimeError("schedule exhausted")
+        dp = self.pg is not None or _dist_on()
+        if self.graphs is not None:
+            self.graphs[0].replay()
+            if dp:
+                self._allreduce()
+            self.graphs[1].replay()
+        else:
+            self._fwd_bwd()
+            if dp:
+                self._allreduce()
+            self._optim()
+        self.steps_done += 1
+
+    def capture(self):
+        """Capture the step into HIP graphs (after >= 1 eager step)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g1, stream=s):
+                self._fwd_bwd()
+            with torch.cuda.graph(g2, stream=s):
+                self._optim()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graphs = (g1, g2)
+
+    def loss_history(self, upto=None):
+        n = self.steps_done if upto is None else upto
+        return self.hist[:n].double().cpu().numpy()
+
+    ploss_history = loss_history
+
+    def compare_history(self, upto=None):
+        n = self.steps_done if upto is None else upto
+        return self.chist[:n].double().cpu().numpy()
+
+    def fill_optimizer_state(self, optimizer):
+        t = self.steps_done + self.t_offset
+        for name, p in self.model.named_parameters():
+            if name in self.md:
+                optimizer.state[p] = {"t": t, "m": self.md[name], "v": self.vd[name]}
+
+    def load_optimizer_state(self, optimizer):
+        with torch.no_grad():
+            for name, p in self.model.named_parameters():
+                st = optimizer.state.get(p)
+                if st and name in self.md:
+                    self.md[name].copy_(st["m"])
+                    self.vd[name].copy_(st["v"])
+
+
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
