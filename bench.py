@@ -113,6 +113,38 @@ def make_cdm_ring(sampler, B, R):
     return ring
 
 
+def build_vlm(rank, B, L, p, total_iters, precision=None):
+    """BASELINE config 5 (exp_vlm_standardTF.sh via train_sequential_NWP.py): sequential
+    next-word prediction, AutoRegressiveTransformer(T=81, 1 prefix token, d=256, L=9,
+    MLP 1024), lr 1e-3 -> 1e-6, frozen CLIP image encoder (random init: no checkpoint
+    travels to the box; the step's work does not depend on the weights)."""
+    from ghmclip import (AutoRegressiveTransformer, EncoderTransformer, NextWordPredictSampler,
+                         get_lr_cosine_schedule, seed_everything)
+    from ghmclip.training.vlm_trainer import VlmTrainer
+    p_y = np.ones(10) / 10
+    sampler = NextWordPredictSampler([4, 4], [3, 3], [p_y, p_y], [p, p])
+    torch.manual_seed(7)
+    clip = EncoderTransformer(81, 10, 128, 5).cuda()
+    seed_everything(224 + 1000 * rank)
+    model = AutoRegressiveTransformer(81, 1, 10, 256, L, [4, 1], 4, 1024, auto_regressive=True,
+                                      sequential=True).cuda()
+    sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
+    trainer = VlmTrainer(model, clip, B, sched, device="cuda", precision=precision)
+    return sampler, trainer
+
+
+def make_vlm_ring(sampler, B, R):
+    """R pre-drawn batches (text inputs, targets, host BP posteriors, image leaves)
+    resident in HBM."""
+    ring = []
+    for _ in range(R):
+        tl, il, _ = sampler.draw_numpy(B)
+        post, _ = sampler.posterior(tl, il)
+        ring.append(tuple(torch.from_numpy(np.ascontiguousarray(x)).cuda()
+                          for x in (tl[:, :-1], tl[:, 1:], post.astype(np.float32), il)))
+    return ring
+
+
 def dominant_kernel(trainer):
     """(name, launch) of the step's dominant kernel — the encoder-layer LN2+MLP
     forward (k_ln_mlp_fwd / k_ln_mlp_fwd_x3b) of layer 0 — launched on the
@@ -182,6 +214,18 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
                 "sample": f"{steps} steps (after 1 warm-up) of the sequential CDM config, B={B}, L={L}, fp32 "
                           f"PyTorch-CPU restatement of the reference (oracle/cdm_oracle.py, frozen CLIP "
                           f"forward + BP_DNS posterior included); {dt:.3f} s/step"}
+    if workload == "vlm":
+        from oracle import vlm_oracle as VO
+        tr = VO.OracleVlmTrainer(B=B, L=L)
+        tr.step()
+        t0 = time.time()
+        for _ in range(steps):
+            tr.step()
+        dt = (time.time() - t0) / steps
+        return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+                "sample": f"{steps} steps (after 1 warm-up) of the sequential VLM config, B={B}, L={L}, d=256, fp32 "
+                          f"PyTorch-CPU restatement of the reference (oracle/vlm_oracle.py, frozen CLIP "
+                          f"forward + host BP posteriors included); {dt:.3f} s/step"}
     tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
           else O.OracleTrainer(p=0.2, B=B, L=L))
     tr.step()  # warm-up
@@ -207,8 +251,9 @@ def main():
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
-    ap.add_argument("--workload", default="clip", choices=["clip", "cdm"],
-                    help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4)")
+    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "vlm"],
+                    help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4); "
+                         "vlm: sequential VLM next-word prediction (BASELINE config 5)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
@@ -216,6 +261,8 @@ def main():
     ws, rank, local = setup_dist(a.gpus)
     if a.workload == "cdm":
         return main_cdm(a, ws, rank)
+    if a.workload == "vlm":
+        return main_vlm(a, ws, rank)
     total_iters = max(3000, a.steps + a.warmup + 1)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
     ring = make_ring(sampler, a.batch, a.ring)
@@ -366,6 +413,66 @@ def main_cdm(a, ws, rank):
     }
     if ws == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=8, workload="cdm")
+    print(json.dumps(out), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def main_vlm(a, ws, rank):
+    """Sequential VLM (BASELINE config 5) throughput: samples/s, B rows per rank."""
+    L = 9 if a.layers == 5 else a.layers  # exp_vlm_standardTF.sh: n_model_layer=9
+    total_iters = max(30000, a.steps + a.warmup + 1)
+    sampler, tr = build_vlm(rank, a.batch, L, 0.2, total_iters, a.precision)
+    ring = make_vlm_ring(sampler, a.batch, a.ring)
+
+    def one(k):
+        tr.set_batch(*ring[k % a.ring])
+        tr.step()
+
+    elapsed = timed_steps(a, ws, tr, one)
+    losses = tr.loss_history()
+    # dominant kernel: the MLP up-projection GEMM of one layer ([M,256] x [256,1024] + bias)
+    plan, pd = tr.plan, tr.pd
+    w1, b1 = pd["_mlps.0.0.weight"], pd["_mlps.0.0.bias"]
+    kern_ms = time_kernel(lambda: torch.addmm(b1, plan.X2[0], w1.t(), out=plan.U))
+    if rank != 0:
+        if ws > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    M, D, F = plan.M, plan.D, plan.F
+    gflop = 2.0 * M * D * F / 1e9
+    achieved = gflop / (kern_ms * 1e-3) / 1e3
+    # whole-step algorithmic work (fwd; bwd = 2x): per layer QKV 3*2MD^2, MLP 2*2MDF,
+    # attention 2*2*N*T^2*D (dense, unmasked count), readout 2MDV
+    T = plan.T
+    fwd = L * (6 * M * D * D + 4 * M * D * F + 4 * a.batch * T * T * D) + 2 * M * D * plan.V
+    step_gflop = 3 * fwd / 1e9
+    out = {
+        "metric": "GHM training samples/sec (sequential VLM config)",
+        "value": round(a.batch * ws * a.steps / elapsed, 2),
+        "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic GHM draws (native NextWordPredictSampler, p=0.2, host BP posteriors), ring of {a.ring} "
+                f"batches resident in HBM",
+        "config": {"workload": f"vlm_sequential: AutoRegressiveTransformer(L={L}, d=256, T=81 = 1 prefix + 80 text) "
+                               f"+ frozen CLIP image EncoderTransformer(L=5) forward, CE + KL compare, "
+                               f"fwd+bwd+clip+AdamW",
+                   "batch_rows_per_rank": a.batch, "global_batch_rows": a.batch * ws, "n_layer": L,
+                   "parallelism": f"dp{ws}", "hip_graph": not a.no_graph},
+        "roofline": {"bound": "mfma", "kernel": f"MLP up-projection GEMM (fp32 library, [{M},{D}]x[{D},{F}] + bias)",
+                     "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel_ms": round(kern_ms, 4)},
+        "step_tflops": round(step_gflop * ws * a.steps / elapsed / 1e3, 2),
+        "loss_finite": bool(np.isfinite(losses).all()),
+        "last_loss": float(losses[-1]) if len(losses) else None,
+    }
+    if ws == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=4, workload="vlm")
     print(json.dumps(out), flush=True)
     if ws > 1:
         import torch.distributed as dist

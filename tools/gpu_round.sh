@@ -1,0 +1,23 @@
+# usage: bash tools/gpu_round.sh TAG : all GPU tests, smoke, CLIP / CDM / VLM benches,
+# rocprof kernel stats of the CLIP and VLM benches
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-r1}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+ok() { r=$1; [ $r -eq 0 ] || [ $r -eq 1 ]; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> $OUT/gpu_tests.log
+grep -E "passed|failed" $OUT/gpu_tests.log | tail -2
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 3
+timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
+cat $OUT/bench.json
+timeout -k 10 400 python bench.py --workload vlm > $OUT/bench_vlm.json 2> $OUT/bench_vlm.err || exit 5
+cat $OUT/bench_vlm.json
+timeout -k 10 300 python bench.py --workload cdm --no-cpu-baseline > $OUT/bench_cdm.json 2> $OUT/bench_cdm.err || exit 6
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_vlm -o run -- \
+   python bench.py --workload vlm --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_vlm.json 2> $OUT/prof_vlm.err
+ok $? || exit 7
+echo done
