@@ -296,6 +296,41 @@ int ghm_ce_kl(const float* logits, const uint8_t* targets, const float* post, fl
               float* hist, float* chist, const int32_t* step, int64_t n_seq, int T, int n_prefix, int V,
               void* stream);
 
+/* Split-bf16 MFMA form of ghm_vlm_attn_fwd / _bwd (csrc/ghm_vlm_x3.hip) on the fused
+ * projection layout: q, k, v are columns [0, D), [D, 2D), [2D, 3D) of qkv [M][3D];
+ * the backward writes dq, dk, dv into dqkv [M][3D] the same way, with dS
+ * [n_seq][96][96] scratch.  D in {128, 256}, T <= 96. */
+int ghm_vlm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T, int D,
+                        int n_prefix, float scale_div, void* stream);
+int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
+                        int T, int D, float scale_div, void* stream);
+
+/* ---- split-bf16 (x3) GEMM for the VLM projections (csrc/ghm_gemm.hip) -------
+ * Replaces the nn.Linear products of AutoRegressiveTransformer (models/model.py:
+ * 203-216 _queries/_keys/_values/_mlps, applied at :330-347) and their autograd
+ * backward.  C[m][n] = sum_k A(m,k) B(k,n), fp32 in/out, split-bf16 MFMA inside:
+ *   ta = 0: A(m,k) = A[m*lda + k];  ta = 1: A(m,k) = A[k*lda + m]
+ *   tb = 1: B(k,n) = Bq[n*ldb + k]; tb = 0: B(k,n) = Bq[k*ldb + n]
+ * B may be three tensors B0, B1, B2 stacked along its storage rows (n for tb = 1,
+ * k for tb = 0), b_chunk rows each (0: B0 only).  N % 128 == 0.
+ * epi: 0 C = acc; 1 (u = acc + bias[n]) C = GELU(u), C2 = GELU'(u); 2 C = acc +
+ * bias[n] + R[m][n]; 3 C = acc * R[m][n]; 4 split-k partials C[z][M][N] (nsplit
+ * slabs of ghm_gemm_slab_elems floats in total), summed by ghm_gemm_reduce. */
+int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit);
+int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
+                const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2, const float* bias,
+                const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit, void* stream);
+/* D[m][n] = sum_z slab[z][m][n] (z in order: deterministic); rows stacked into
+ * D0, D1, D2 by chunk (0: D0 only). */
+int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
+                    int64_t chunk, void* stream);
+/* out[n] = sum_m X[m][n] (deterministic two-stage), X [M][N] fp32, N % 4 == 0 and
+ * N/4 dividing 256 or >= 256; part scratch of ghm_colsum_part_elems(M, N) floats.
+ * The bias gradients of the Linear layers and the position-embedding gradient
+ * (autograd's sum over batch rows, model.py:291-293, :330-347). */
+int64_t ghm_colsum_part_elems(int64_t M, int64_t N);
+int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, float* part, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

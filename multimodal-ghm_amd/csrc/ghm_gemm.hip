@@ -1,0 +1,492 @@
+// Split-bf16 (x3) tiled GEMM for the VLM projections (gfx950).
+//
+// C[m][n] = sum_k A(m, k) B(k, n) on v_mfma_f32_32x32x16_bf16 with every f32
+// operand split into (hi, lo) bf16 parts while it is staged into LDS
+// (ghm_split.h: hi·hi + hi·lo + lo·hi, f32 accumulate).  One template covers the
+// three shapes of a Linear layer's training step:
+//   forward   Y  = X W^T    A = X [M][K]        (TA = 0)  B(k,n) = W[n][k] (TB = 1)
+//   data grad dX = dY W     A = dY [M][K]       (TA = 0)  B(k,n) = W[k][n] (TB = 0)
+//   wgrad     dW = dY^T X   A(m,k) = dY[k][m]   (TA = 1)  B(k,n) = X[k][n] (TB = 0),
+//             split over k (tokens) into f32 partial slabs summed in a fixed
+//             order by k_gemm_reduce (deterministic, no atomics).
+// B may be up to three separate tensors stacked along its storage rows (the
+// VLM's separate W_q, W_k, W_v: one launch for the fused QKV product and its
+// data gradient); the reduce writes the wgrad rows back into up to three
+// destinations the same way.
+//
+// Tiling: 256 threads = 4 waves in a 2 x 2 grid, workgroup tile BM x 128
+// (BM = 128 for N >= 768, else 64), K tile 32.  LDS images are [row][k] bf16 with a 40-element
+// pitch (80 B), so each lane reads its 8-element MFMA fragment with one 16-byte
+// load.  Operands whose storage is k-contiguous are staged row by row (8 lanes
+// per 128-B row segment); operands whose storage is [k][outer] are loaded as
+// 4 (or 2) consecutive k rows x 4 columns per thread and transposed in
+// registers before the split store.  The next K tile's global loads are issued
+// before the current tile's MFMAs.
+//
+// The MFMA computes C^T tiles (B image rows as its A operand) so each lane owns
+// one output row and 4 consecutive columns per register quad: the epilogue reads
+// bias / R and writes C with 16-byte accesses (scalar-dword epilogues were
+// store-issue bound: ~1.4 TB/s).  LDS is double-buffered, one barrier per K tile.
+// Epilogues:
+//   EPI_STORE   C = acc
+//   EPI_GELU    u = acc + bias[n]; C = GELU(u), C2 = GELU'(u)   (MLP up, fused)
+//   EPI_RESID   C = acc + bias[n] + R[m][n]                     (MLP down + residual)
+//   EPI_MUL     C = acc * R[m][n]                               (dG * GELU'(U))
+//   EPI_SLAB    slab[z][m][n] = acc                             (split-k wgrad)
+#include "ghm_launch.h"
+#include "ghm_split.h"
+
+namespace {
+
+constexpr int GB_N = 128;   // workgroup tile columns
+constexpr int GB_K = 32;    // K tile
+constexpr int GP = 40;      // LDS pitch (bf16) of a [row][k] image
+
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID = 2, EPI_MUL = 3, EPI_SLAB = 4 };
+
+struct GemmArgs {
+  const float* A;
+  int64_t lda;
+  const float* B[3];
+  int64_t ldb, b_chunk;   // B storage rows per tensor (0: one tensor)
+  float* C;
+  int64_t ldc;
+  float* C2;
+  const float* bias;
+  const float* R;
+  int64_t ldr;
+  int64_t M, N, K, k_per_split;
+};
+
+// k-contiguous tile: rows r0.. r0+ROWS-1 (guard < nrows), k0..k0+31 (guard < K)
+template <int ROWS>
+__device__ __forceinline__ void load_kc(float4* v, const float* __restrict__ base, int64_t ld, int64_t r0,
+                                        int64_t nrows, int64_t k0, int64_t K) {
+  constexpr int N = ROWS * 8 / 256;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int row = idx >> 3, k4 = idx & 7;
+    const int64_t r = r0 + row, k = k0 + 4 * k4;
+    v[i] = (r < nrows && k < K) ? *reinterpret_cast<const float4*>(base + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int ROWS>
+__device__ __forceinline__ void store_kc(const float4* v, __bf16* hi, __bf16* lo) {
+  constexpr int N = ROWS * 8 / 256;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int row = idx >> 3, k4 = idx & 7;
+    bf16x4 a, b;
+    split4(v[i], a, b);
+    stb4(hi + row * GP + 4 * k4, a);
+    stb4(lo + row * GP + 4 * k4, b);
+  }
+}
+
+// [k][outer] tile: k rows k0..k0+31 (guard < kend), outer columns c0..c0+COLS-1;
+// thread = (k group of RPT rows, 4 columns)
+template <int COLS>
+__device__ __forceinline__ void load_oc(float4* v, const float* __restrict__ base, int64_t ld, int64_t k0,
+                                        int64_t kend, int64_t c0) {
+  constexpr int C4 = COLS / 4, RPT = COLS / 32;
+  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int64_t k = k0 + RPT * kg + i;
+    v[i] = k < kend ? *reinterpret_cast<const float4*>(base + k * ld + c0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int COLS>
+__device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo) {
+  constexpr int C4 = COLS / 4, RPT = COLS / 32;
+  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    __bf16 h[RPT], l[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const float x = c == 0 ? v[i].x : (c == 1 ? v[i].y : (c == 2 ? v[i].z : v[i].w));
+      split1(x, h[i], l[i]);
+    }
+    const int off = (4 * c4 + c) * GP + RPT * kg;
+    if constexpr (RPT == 4) {
+      bf16x4 a, b;
+      a[0] = h[0]; a[1] = h[1]; a[2] = h[2]; a[3] = h[3];
+      b[0] = l[0]; b[1] = l[1]; b[2] = l[2]; b[3] = l[3];
+      stb4(hi + off, a);
+      stb4(lo + off, b);
+    } else {
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      bf16x2 a, b;
+      a[0] = h[0]; a[1] = h[1];
+      b[0] = l[0]; b[1] = l[1];
+      *reinterpret_cast<bf16x2*>(hi + off) = a;
+      *reinterpret_cast<bf16x2*>(lo + off) = b;
+    }
+  }
+}
+
+template <bool TA, bool TB, int EPI, int TM>
+__global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
+  constexpr int BM = 64 * TM;
+  constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
+  constexpr int NB = TB ? GB_N * 8 / 256 : GB_N / 32;
+  // double-buffered split images: [buf][row][k]
+  __shared__ __attribute__((aligned(16))) __bf16 ah[2][BM * GP], al[2][BM * GP], bh[2][GB_N * GP], bl[2][GB_N * GP];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * GB_N;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * BM;
+  const int64_t kb = static_cast<int64_t>(blockIdx.z) * g.k_per_split;
+  const int64_t ke = kb + g.k_per_split < g.K ? kb + g.k_per_split : g.K;
+
+  // B tile base: the stacked tensor holding storage row (TB ? n0 : k)
+  auto bbase = [&](int64_t srow, int64_t& local) -> const float* {
+    if (g.b_chunk <= 0) {
+      local = srow;
+      return g.B[0];
+    }
+    const int64_t q = srow / g.b_chunk;
+    local = srow - q * g.b_chunk;
+    return g.B[q];
+  };
+
+  auto load = [&](float4* va, float4* vb, int64_t k0) {
+    if constexpr (TA) load_oc<BM>(va, g.A, g.lda, k0, ke, m0);
+    else load_kc<BM>(va, g.A, g.lda, m0, g.M, k0, ke);
+    if constexpr (TB) {
+      int64_t ln;
+      const float* b = bbase(n0, ln);
+      load_kc<GB_N>(vb, b + ln * g.ldb, g.ldb, 0, GB_N, k0, ke);
+    } else {
+      int64_t lk;
+      const float* b = bbase(k0, lk);
+      load_oc<GB_N>(vb, b + (lk - k0) * g.ldb, g.ldb, k0, ke, n0);
+    }
+  };
+  auto store = [&](const float4* va, const float4* vb, int buf) {
+    if constexpr (TA) store_oc<BM>(va, ah[buf], al[buf]);
+    else store_kc<BM>(va, ah[buf], al[buf]);
+    if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
+    else store_oc<GB_N>(vb, bh[buf], bl[buf]);
+  };
+
+  // acc[i][j] = C^T tile: rows = 32 n (B image rows), lanes = 32 m (A image rows),
+  // so each lane owns one output row m and 4 consecutive n per register quad
+  f32x16 acc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = zero16();
+
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 xh[TM], xl[TM], yh[2], yl[2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int off = (32 * (TM * wm + i) + r) * GP + 16 * s + 8 * h;
+        xh[i] = ldsb8(ah[buf] + off);
+        xl[i] = ldsb8(al[buf] + off);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int off = (32 * (2 * wn + j) + r) * GP + 16 * s + 8 * h;
+        yh[j] = ldsb8(bh[buf] + off);
+        yl[j] = ldsb8(bl[buf] + off);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(yh[j], yl[j], xh[i], xl[i], acc[i][j]);
+    }
+  };
+
+  // two K tiles in flight in registers (sets p, q) ahead of the LDS tile being
+  // multiplied: the global loads of a tile are issued two compute phases before
+  // their split store, which keeps enough bytes in flight per CU to cover HBM
+  // latency (one tile ahead left the streaming GEMMs latency-bound)
+  if constexpr (TM == 2) {
+    // 128 x 128 tiles: one K tile in flight (two would exceed 256 VGPRs)
+    float4 pa[NA], pb[NB];
+    load(pa, pb, kb);
+    store(pa, pb, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += GB_K) {
+      const bool more = k0 + GB_K < ke;
+      if (more) load(pa, pb, k0 + GB_K);
+      issue_fence();
+      compute(buf);
+      if (more) store(pa, pb, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    float4 pa[NA], pb[NB], qa[NA], qb[NB];
+    load(pa, pb, kb);
+    if (kb + GB_K < ke) load(qa, qb, kb + GB_K);
+    issue_fence();
+    store(pa, pb, 0);
+    __syncthreads();
+    if (kb + 2 * GB_K < ke) load(pa, pb, kb + 2 * GB_K);
+    issue_fence();
+    for (int64_t k0 = kb; k0 < ke; k0 += 2 * GB_K) {
+      // LDS[0] = tile k0; q = tile k0 + 32; p = tile k0 + 64 (in flight)
+      compute(0);
+      if (k0 + GB_K < ke) store(qa, qb, 1);
+      __syncthreads();
+      if (k0 + 3 * GB_K < ke) load(qa, qb, k0 + 3 * GB_K);
+      issue_fence();
+      if (k0 + GB_K >= ke) break;
+      compute(1);
+      if (k0 + 2 * GB_K < ke) store(pa, pb, 0);
+      __syncthreads();
+      if (k0 + 4 * GB_K < ke) load(pa, pb, k0 + 4 * GB_K);
+      issue_fence();
+    }
+  }
+
+  // epilogue: lane row m = m0 + 32(TM wm + i) + r; register quad qd of acc[i][j] holds
+  // n = n0 + 32(2 wn + j) + 8 qd + 4 h + 0..3 -> one 16-byte access per quad
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t m = m0 + 32 * (TM * wm + i) + r;
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t nb = n0 + 32 * (2 * wn + j);
+      float4 rv[4], bv[4];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int64_t n = nb + quad_off(qd, h);
+        if constexpr (EPI == EPI_GELU || EPI == EPI_RESID) bv[qd] = *reinterpret_cast<const float4*>(g.bias + n);
+        if constexpr (EPI == EPI_RESID || EPI == EPI_MUL)
+          rv[qd] = *reinterpret_cast<const float4*>(g.R + m * g.ldr + n);
+      }
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const int64_t n = nb + quad_off(qd, h);
+        float x[4] = {acc[i][j][4 * qd], acc[i][j][4 * qd + 1], acc[i][j][4 * qd + 2], acc[i][j][4 * qd + 3]};
+        if constexpr (EPI == EPI_STORE) {
+          st4(g.C + m * g.ldc + n, x[0], x[1], x[2], x[3]);
+        } else if constexpr (EPI == EPI_GELU) {
+          const float bb[4] = {bv[qd].x, bv[qd].y, bv[qd].z, bv[qd].w};
+          float gg[4], dd[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) gelu_fast(x[t] + bb[t], gg[t], dd[t]);
+          st4(g.C + m * g.ldc + n, gg[0], gg[1], gg[2], gg[3]);
+          st4(g.C2 + m * g.ldc + n, dd[0], dd[1], dd[2], dd[3]);
+        } else if constexpr (EPI == EPI_RESID) {
+          st4(g.C + m * g.ldc + n, (x[0] + bv[qd].x) + rv[qd].x, (x[1] + bv[qd].y) + rv[qd].y,
+              (x[2] + bv[qd].z) + rv[qd].z, (x[3] + bv[qd].w) + rv[qd].w);
+        } else if constexpr (EPI == EPI_MUL) {
+          st4(g.C + m * g.ldc + n, x[0] * rv[qd].x, x[1] * rv[qd].y, x[2] * rv[qd].z, x[3] * rv[qd].w);
+        } else {
+          st4(g.C + (static_cast<int64_t>(blockIdx.z) * g.M + m) * g.N + n, x[0], x[1], x[2], x[3]);
+        }
+      }
+    }
+  }
+}
+
+// dst rows (stacked as B is): out = sum_z slab[z] in z order
+__global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ slab, int nsplit, int64_t M, int64_t N,
+                                                      float* d0, float* d1, float* d2, int64_t chunk) {
+  const int64_t i4 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t total = M * N;
+  if (4 * i4 >= total) return;
+  const float4* s = reinterpret_cast<const float4*>(slab) + i4;
+  float4 a = s[0];
+  for (int z = 1; z < nsplit; ++z) {
+    const float4 b = s[static_cast<int64_t>(z) * (total / 4)];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  const int64_t m = (4 * i4) / N, n = (4 * i4) % N;
+  float* d = d0;
+  int64_t lm = m;
+  if (chunk > 0) {
+    const int64_t q = m / chunk;
+    lm = m - q * chunk;
+    d = q == 0 ? d0 : (q == 1 ? d1 : d2);
+  }
+  *reinterpret_cast<float4*>(d + lm * N + n) = a;
+}
+
+// Column sums out[n] = sum_m X[m][n] (bias and position-embedding gradients),
+// deterministic: stage 1 sums a chunk of rows per workgroup (threads split into
+// row groups when N/4 < 256, combined through LDS in group order), stage 2 sums
+// the chunk partials in chunk order.
+__global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ X, int64_t M, int64_t N, int64_t R,
+                                                     float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int64_t N4 = N / 4;
+  const int CB = N4 < 256 ? static_cast<int>(N4) : 256;
+  const int G = 256 / CB;
+  const int t = threadIdx.x, grp = t / CB;
+  const int64_t c4 = static_cast<int64_t>(blockIdx.x) * CB + t % CB;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * R;
+  const int64_t r1 = r0 + R < M ? r0 + R : M;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (grp < G && c4 < N4) {
+    for (int64_t row = r0 + grp; row < r1; row += G) {
+      const float4 v = *reinterpret_cast<const float4*>(X + row * N + 4 * c4);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[t] = a;
+  __syncthreads();
+  if (grp == 0 && c4 < N4) {
+    for (int q = 1; q < G; ++q) {
+      const float4 v = red[t + q * CB];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    reinterpret_cast<float4*>(part + static_cast<int64_t>(blockIdx.y) * N)[c4] = a;
+  }
+}
+
+// chunk partials summed per column: 64 float4 columns per workgroup (fewer when
+// N/4 < 64), the chunks split over 256 / columns thread groups, groups combined in
+// order through LDS
+__global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int nchunk, int64_t N,
+                                                      float* __restrict__ out) {
+  __shared__ float4 red[256];
+  const int64_t N4 = N / 4;
+  const int CB = N4 < 64 ? static_cast<int>(N4) : 64;
+  const int G = 256 / CB;
+  const int t = threadIdx.x, grp = t / CB;
+  const int64_t c4 = static_cast<int64_t>(blockIdx.x) * CB + t % CB;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (grp < G && c4 < N4) {
+    // 8 loads issued together per round (a dependent one-at-a-time chain was
+    // latency-bound: ~18 us for 256 chunks)
+    for (int z0 = grp; z0 < nchunk; z0 += 8 * G) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int z = z0 + u * G;
+        v[u] = z < nchunk ? reinterpret_cast<const float4*>(part + static_cast<int64_t>(z) * N)[c4]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+  }
+  red[t] = a;
+  __syncthreads();
+  if (grp == 0 && c4 < N4) {
+    for (int q = 1; q < G; ++q) {
+      const float4 v = red[t + q * CB];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[c4] = a;
+  }
+}
+
+void colsum_plan(int64_t M, int64_t N, int64_t& colblocks, int64_t& nchunk, int64_t& R) {
+  const int64_t N4 = N / 4;
+  colblocks = N4 < 256 ? 1 : (N4 + 255) / 256;
+  int64_t want = 256 / colblocks;
+  if (want < 1) want = 1;
+  const int64_t cap = (M + 7) / 8;
+  nchunk = want < cap ? want : cap;
+  if (nchunk < 1) nchunk = 1;
+  R = (M + nchunk - 1) / nchunk;
+  nchunk = (M + R - 1) / R;
+}
+
+template <bool TA, bool TB, int EPI>
+void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
+  // measured (VLM shapes, M = 10,368): 128 x 128 tiles with one K tile in flight
+  // are faster for N >= 768; 64 x 128 tiles with two K tiles in flight for N = 256
+  const unsigned gx = static_cast<unsigned>(g.N / GB_N);
+  if (g.N >= 768)
+    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2>), dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit),
+                       dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1>), dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit),
+                       dim3(256), 0, s, g);
+}
+
+}  // namespace
+
+extern "C" int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit) { return M * N * nsplit; }
+
+extern "C" int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
+                           const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2,
+                           const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit,
+                           void* stream) {
+  GHM_CHECK(A && B0 && C, "null pointer");
+  GHM_CHECK(M >= 1 && N >= GB_N && N % GB_N == 0 && K >= 1 && nsplit >= 1 && nsplit <= 256, "shape (N % 128 == 0)");
+  GHM_CHECK(!(ta && tb), "TA and TB together are not a VLM shape");
+  GHM_CHECK(epi >= EPI_STORE && epi <= EPI_SLAB, "epilogue");
+  GHM_CHECK(nsplit == 1 || epi == EPI_SLAB, "split k needs the slab epilogue");
+  GHM_CHECK(epi != EPI_GELU || (bias && C2), "GELU epilogue needs bias and C2");
+  GHM_CHECK(epi != EPI_RESID || (bias && R), "residual epilogue needs bias and R");
+  GHM_CHECK(epi != EPI_MUL || R, "product epilogue needs R");
+  GHM_CHECK(lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && ldr % 4 == 0, "row strides % 4 == 0");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(R) |
+              reinterpret_cast<uintptr_t>(C2) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0,
+            "16-byte aligned operands");
+  // k-contiguous operands are read as float4 along k
+  GHM_CHECK((ta || K % 4 == 0) && (!tb || K % 4 == 0), "K % 4 == 0 for k-contiguous operands");
+  if (b_chunk > 0) {
+    const int64_t rows = tb ? N : K;
+    GHM_CHECK(b_chunk % GB_N == 0 && rows <= 3 * b_chunk && B1 && (rows <= 2 * b_chunk || B2),
+              "stacked B: chunk % 128 == 0, at most 3 tensors");
+  }
+  GemmArgs g;
+  g.A = A; g.lda = lda;
+  g.B[0] = B0; g.B[1] = B1 ? B1 : B0; g.B[2] = B2 ? B2 : B0;
+  g.ldb = ldb; g.b_chunk = b_chunk;
+  g.C = C; g.ldc = ldc; g.C2 = C2; g.bias = bias; g.R = R; g.ldr = ldr;
+  g.M = M; g.N = N; g.K = K;
+  g.k_per_split = ((K + nsplit - 1) / nsplit + GB_K - 1) / GB_K * GB_K;
+  hipStream_t s = ghm_stream(stream);
+#define GHM_GEMM_CASE(TA_, TB_, E_) \
+  if (ta == TA_ && tb == TB_ && epi == E_) { launch_tm<TA_, TB_, E_>(g, nsplit, s); return ghm_launch_status(); }
+  GHM_GEMM_CASE(0, 1, EPI_STORE)
+  GHM_GEMM_CASE(0, 1, EPI_GELU)
+  GHM_GEMM_CASE(0, 1, EPI_RESID)
+  GHM_GEMM_CASE(0, 0, EPI_STORE)
+  GHM_GEMM_CASE(0, 0, EPI_MUL)
+  GHM_GEMM_CASE(1, 0, EPI_SLAB)
+  GHM_GEMM_CASE(1, 0, EPI_STORE)
+#undef GHM_GEMM_CASE
+  GHM_CHECK(false, "unsupported (ta, tb, epilogue) combination");
+}
+
+extern "C" int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
+                               int64_t chunk, void* stream) {
+  GHM_CHECK(slab && D0 && nsplit >= 1 && M >= 1 && N >= 4 && N % 4 == 0, "bad arguments");
+  GHM_CHECK(chunk <= 0 || (M <= 3 * chunk && D1 && (M <= 2 * chunk || D2)), "stacked destination");
+  const int64_t n4 = M * N / 4;
+  hipLaunchKernelGGL(k_gemm_reduce, dim3(static_cast<unsigned>((n4 + 255) / 256)), dim3(256), 0, ghm_stream(stream),
+                     slab, nsplit, M, N, D0, D1, D2, chunk);
+  return ghm_launch_status();
+}
+
+extern "C" int64_t ghm_colsum_part_elems(int64_t M, int64_t N) {
+  int64_t cb, nc, R;
+  colsum_plan(M, N, cb, nc, R);
+  return nc * N;
+}
+
+extern "C" int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, float* part, void* stream) {
+  GHM_CHECK(X && out && part && M >= 1 && N >= 4 && N % 4 == 0, "bad arguments (N % 4 == 0)");
+  GHM_CHECK(N / 4 >= 256 || 256 % (N / 4) == 0, "N / 4 must divide 256 or be >= 256");
+  GHM_CHECK(N / 4 >= 64 || 64 % (N / 4) == 0, "N / 4 must divide 64 or be >= 64");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(part)) &
+             15) == 0, "16-byte aligned operands");
+  int64_t cb, nc, R;
+  colsum_plan(M, N, cb, nc, R);
+  hipStream_t s = ghm_stream(stream);
+  hipLaunchKernelGGL(k_colsum_part, dim3(static_cast<unsigned>(cb), static_cast<unsigned>(nc)), dim3(256), 0, s, X, M,
+                     N, R, part);
+  const int64_t CBf = N / 4 < 64 ? N / 4 : 64;
+  hipLaunchKernelGGL(k_colsum_final, dim3(static_cast<unsigned>((N / 4 + CBf - 1) / CBf)), dim3(256), 0, s, part,
+                     static_cast<int>(nc), N, out);
+  return ghm_launch_status();
+}

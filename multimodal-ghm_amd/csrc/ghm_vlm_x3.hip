@@ -1,0 +1,417 @@
+// Split-bf16 (x3) MFMA attention of the sequential VLM (gfx950).
+//
+// AutoRegressiveTransformer's attention (models/model.py:329-341): single head,
+// S = (Q K^T + mask) / scale_div with generate_mask's prefix-causal mask
+// (:24-33: a prefix query sees the prefix, a text query sees every earlier
+// token), A = softmax(S), and the reference's double residual
+// H_mid = H + A V + (A / D) V, evaluated as (H + o) + o / D.
+//
+// Same compute model as the CLIP attention (ghm_x3.hip): one workgroup per
+// sequence, one wave per 32 queries with the query on the lane; scores S^T come
+// out of v_mfma_f32_32x32x16_bf16 as keys-on-rows accumulators, so the row
+// softmax is a per-lane loop plus one lane-pair exchange, and the probabilities
+// (split in registers) are directly the B operand of O^T = V^T P^T.  K and V are
+// staged through LDS as split (hi, lo) images; V / K / dO / Q column blocks are
+// read with ds_read_b64_tr_b16 transposed reads.  D = 128 or 256 features are
+// processed as 128-feature halves so the query fragments stay at 64 VGPRs.
+// q, k, v live in one [M][3D] buffer (the fused QKV GEMM's output); the
+// backward writes dq, dk, dv into the same layout for the fused data / weight
+// gradient GEMMs.
+#include "ghm_launch.h"
+#include "ghm_split.h"
+
+namespace {
+
+constexpr int VX_PAD = 96;        // padded sequence length of the P / dS layouts
+constexpr int VX_PITCH = 64 + 8;  // [row][h][32] half image row (bf16)
+
+typedef __attribute__((address_space(3))) bf16x4 vx_lds_bf16x4;
+__device__ __forceinline__ bf16x4 vx_ldtr(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((vx_lds_bf16x4*)(p));
+}
+// 8-row transposed fragment of a [row][32] image: lane l of group g = l >> 4
+// receives column 16(g & 1) + (l & 15) of rows r0..r0+3 and r1..r1+3
+__device__ __forceinline__ bf16x8 vx_tr_frag(const __bf16* img, int r0, int r1, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = 16 * (g & 1) + 4 * p;
+  const bf16x4 a = vx_ldtr(img + (r0 + q) * 32 + col);
+  const bf16x4 b = vx_ldtr(img + (r1 + q) * 32 + col);
+  bf16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return v;
+}
+
+// 64 consecutive floats at p -> 8 split k-steps (zeros when inactive)
+__device__ __forceinline__ void vx_load_split64(const float* __restrict__ p, bool active, bf16x8* xh, bf16x8* xl) {
+  float x[64];
+  if (active) {
+    load64(p, x);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x[k] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
+}
+
+// columns col + 64 hh + 0..31 (hh = 0, 1) of rows 0..TP-1 (row stride ld) as a
+// split [row][hh][32] image; rows >= T clamp to T - 1
+template <int NKT>
+__device__ __forceinline__ void vx_stage_half(const float* __restrict__ seq, int64_t ld, int T, int col, __bf16* ih,
+                                              __bf16* il) {
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * ld + col + 64 * hh + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+    bf16x4 a, b;
+    split4(v[k], a, b);
+    stb4(ih + row * VX_PITCH + 32 * hh + 4 * q4, a);
+    stb4(il + row * VX_PITCH + 32 * hh + 4 * q4, b);
+  }
+}
+
+// columns col .. col+31 of rows 0..TP-1 (row stride ld) as a split [row][32]
+// image for transposed reads; rows >= T clamp
+template <int NKT>
+__device__ __forceinline__ void vx_stage_cols(const float* __restrict__ base, int64_t ld, int T, int col, __bf16* ih,
+                                              __bf16* il) {
+  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
+  float4 v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    const int row = idx >> 3, q4 = idx & 7;
+    const int rc = row < T ? row : T - 1;
+    v[k] = *reinterpret_cast<const float4*>(base + static_cast<int64_t>(rc) * ld + col + 4 * q4);
+  }
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = threadIdx.x + NT * k;
+    bf16x4 a, b;
+    split4(v[k], a, b);
+    stb4(ih + idx * 4, a);
+    stb4(il + idx * 4, b);
+  }
+}
+
+// S^T[key][query] += X_rows . Y over the 32-column slab c of a half image
+template <int NKT>
+__device__ __forceinline__ void vx_rows_dot(const __bf16* ih, const __bf16* il, const bf16x8* yh, const bf16x8* yl,
+                                           int c, int j, int h, f32x16* acc) {
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const int off = (32 * kt + j) * VX_PITCH + 32 * h;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+      acc[kt] = mfma_x3(ldsb8(ih + off + 8 * tt), ldsb8(il + off + 8 * tt), yh[4 * c + tt], yl[4 * c + tt], acc[kt]);
+  }
+}
+
+// S^T (keys on rows, this wave's queries on lanes) = X[keys] . Y[query]^T over
+// DD features; X columns xcol.. of the sequence block (row stride ldx), the
+// query-side row at yrow (DD floats)
+template <int NKT, int DD>
+__device__ __forceinline__ void vx_scores(const float* __restrict__ xseq, int64_t ldx, int xcol,
+                                          const float* __restrict__ yrow, int T, int j, int h, __bf16* sh, __bf16* sl,
+                                          f32x16* s) {
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
+#pragma unroll 1
+  for (int e = 0; e < DD / 128; ++e) {
+    bf16x8 yh[8], yl[8];
+    vx_load_split64(yrow + 128 * e + 64 * h, true, yh, yl);  // Y[128e + 64h + 8t + i]
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      vx_stage_half<NKT>(xseq, ldx, T, xcol + 128 * e + 32 * c, sh, sl);
+      __syncthreads();
+      vx_rows_dot<NKT>(sh, sl, yh, yl, c, j, h, s);
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ bool vx_allowed(int q, int key, int npre) { return q < npre ? key < npre : key <= q; }
+
+template <int NKT, int DD>
+__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __restrict__ qkv,
+                                                                 const float* __restrict__ H,
+                                                                 float* __restrict__ Hmid, float* __restrict__ P,
+                                                                 int T, int npre, float scale_div, float dbl) {
+  constexpr int TP = NKT * 32;
+  constexpr int64_t LD = 3 * DD;
+  __shared__ __attribute__((aligned(16))) __bf16 sh[TP * VX_PITCH];
+  __shared__ __attribute__((aligned(16))) __bf16 sl[TP * VX_PITCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * LD;
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  f32x16 s[NKT];
+  vx_scores<NKT, DD>(seq, LD, DD, seq + qc * LD, T, j, h, sh, sl, s);
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = 32 * kt + acc_row(r, h);
+      const float v = (key < T && vx_allowed(qc, key, npre)) ? s[kt][r] / scale_div : -INFINITY;
+      s[kt][r] = v;
+      mx = fmaxf(mx, v);
+    }
+  }
+  mx = fmaxf(mx, xhalf(mx));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kt][r] - mx);
+      s[kt][r] = e;
+      sum += e;
+    }
+  }
+  sum += xhalf(sum);
+  const float inv = qv ? 1.f / sum : 0.f;
+  float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
+  bf16x8 ph[2 * NKT], pl[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kt][r] *= inv;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(prow + 32 * kt + quad_off(qd, h), s[kt][4 * qd], s[kt][4 * qd + 1], s[kt][4 * qd + 2], s[kt][4 * qd + 3]);
+    float pv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pv[r] = s[kt][r];
+    split_acc(pv, 0, ph[2 * kt], pl[2 * kt]);
+    split_acc(pv, 1, ph[2 * kt + 1], pl[2 * kt + 1]);
+  }
+  // O^T[d][q] = sum_key V[key][d] P[q][key], V column blocks of 32 through LDS
+#pragma unroll 1
+  for (int dt = 0; dt < DD / 32; ++dt) {
+    vx_stage_cols<NKT>(seq, LD, T, 2 * DD + 32 * dt, sh, sl);
+    __syncthreads();
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 32 * kt + 16 * ss + 4 * h;
+        acc = mfma_x3(vx_tr_frag(sh, r0, r0 + 8, lane), vx_tr_frag(sl, r0, r0 + 8, lane), ph[2 * kt + ss],
+                      pl[2 * kt + ss], acc);
+      }
+    }
+    __syncthreads();
+    if (qv) {
+      const int64_t row = (base + q) * DD + 32 * dt;
+      float4 hv[4];
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const float o0 = acc[4 * qd], o1 = acc[4 * qd + 1], o2 = acc[4 * qd + 2], o3 = acc[4 * qd + 3];
+        st4(Hmid + row + quad_off(qd, h), (hv[qd].x + o0) + o0 * dbl, (hv[qd].y + o1) + o1 * dbl,
+            (hv[qd].z + o2) + o2 * dbl, (hv[qd].w + o3) + o3 * dbl);
+      }
+    }
+  }
+}
+
+// dA^T = (V dO^T)(1 + 1/D), dS = P (dA - rowsum(P dA)) / scale_div (stored dense),
+// dQ^T = K^T dS^T
+template <int NKT, int DD>
+__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* __restrict__ qkv,
+                                                                   const float* __restrict__ P,
+                                                                   const float* __restrict__ dHmid,
+                                                                   float* __restrict__ dS_out,
+                                                                   float* __restrict__ dqkv, int T, float scale_div,
+                                                                   float dbl) {
+  constexpr int TP = NKT * 32;
+  constexpr int64_t LD = 3 * DD;
+  __shared__ __attribute__((aligned(16))) __bf16 sh[TP * VX_PITCH];
+  __shared__ __attribute__((aligned(16))) __bf16 sl[TP * VX_PITCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * LD;
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  f32x16 dp[NKT];
+  vx_scores<NKT, DD>(seq, LD, 2 * DD, dHmid + (base + qc) * DD, T, j, h, sh, sl, dp);
+  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
+  float delta = 0.f;
+  f32x16 p[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const float4 pv = *reinterpret_cast<const float4*>(prow + 32 * kt + quad_off(qd, h));
+      p[kt][4 * qd + 0] = qv ? pv.x : 0.f;
+      p[kt][4 * qd + 1] = qv ? pv.y : 0.f;
+      p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
+      p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dp[kt][r] = dp[kt][r] + dp[kt][r] * dbl;
+      delta += p[kt][r] * dp[kt][r];
+    }
+  }
+  delta += xhalf(delta);
+  float* srow = dS_out + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
+  bf16x8 dh[2 * NKT], dl[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    float dv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd)
+      st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+    split_acc(dv, 0, dh[2 * kt], dl[2 * kt]);
+    split_acc(dv, 1, dh[2 * kt + 1], dl[2 * kt + 1]);
+  }
+#pragma unroll 1
+  for (int dt = 0; dt < DD / 32; ++dt) {
+    vx_stage_cols<NKT>(seq, LD, T, DD + 32 * dt, sh, sl);  // K
+    __syncthreads();
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 32 * kt + 16 * ss + 4 * h;
+        acc = mfma_x3(vx_tr_frag(sh, r0, r0 + 8, lane), vx_tr_frag(sl, r0, r0 + 8, lane), dh[2 * kt + ss],
+                      dl[2 * kt + ss], acc);
+      }
+    }
+    __syncthreads();
+    if (qv) {
+      float* o = dqkv + (base + q) * LD + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
+    }
+  }
+}
+
+// dV^T = dO^T P (1 + 1/D) and dK^T = Q^T dS, summed over queries; the key on the lane
+template <int NKT, int DD>
+__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* __restrict__ qkv,
+                                                                    const float* __restrict__ P,
+                                                                    const float* __restrict__ dS,
+                                                                    const float* __restrict__ dHmid,
+                                                                    float* __restrict__ dqkv, int T, float dbl) {
+  constexpr int TP = NKT * 32, KS = TP / 16;
+  constexpr int64_t LD = 3 * DD;
+  __shared__ __attribute__((aligned(16))) __bf16 soh[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sol[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sqh[TP * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 sql[TP * 32];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const int key = 32 * w + j;
+  const bool kv = key < T;
+  const float* pc = P + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
+  const float* sc = dS + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
+  bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) {
+    float pv[8], sv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int qq = 16 * st + 8 * h + i;
+      pv[i] = pc[qq * VX_PAD];
+      sv[i] = sc[qq * VX_PAD];
+    }
+    split8(pv, pbh[st], pbl[st]);
+    split8(sv, sbh[st], sbl[st]);
+  }
+#pragma unroll 1
+  for (int dt = 0; dt < DD / 32; ++dt) {
+    vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
+    vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
+    __syncthreads();
+    f32x16 aV = zero16(), aK = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int r0 = 16 * st + 8 * h;
+      aV = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
+      aK = mfma_x3(vx_tr_frag(sqh, r0, r0 + 4, lane), vx_tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
+    }
+    __syncthreads();
+    if (kv) {
+      float* o = dqkv + (base + key) * LD + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        const float v0 = aV[4 * qd], v1 = aV[4 * qd + 1], v2 = aV[4 * qd + 2], v3 = aV[4 * qd + 3];
+        st4(o + 2 * DD + quad_off(qd, h), v0 + v0 * dbl, v1 + v1 * dbl, v2 + v2 * dbl, v3 + v3 * dbl);
+        st4(o + DD + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
+      }
+    }
+  }
+}
+
+template <int DD>
+void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int npre,
+                float sd, float dbl) {
+  if (T <= 32)
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<1, DD>), dim3(g), dim3(64), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if (T <= 64)
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<2, DD>), dim3(g), dim3(128), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<3, DD>), dim3(g), dim3(192), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+}
+
+template <int NKT, int DD>
+void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
+                  float* dqkv, int T, float sd, float dbl) {
+  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD>), dim3(g), dim3(NKT * 64), 0, s, qkv, P, dHm, dS, dqkv, T, sd,
+                     dbl);
+  hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD>), dim3(g), dim3(NKT * 64), 0, s, qkv, P, dS, dHm, dqkv, T, dbl);
+}
+
+template <int DD>
+void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
+                float* dqkv, float sd, float dbl) {
+  if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+  else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+  else launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+}
+
+}  // namespace
+
+extern "C" int ghm_vlm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
+                                   int D, int n_prefix, float scale_div, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= VX_PAD && n_seq >= 1 && n_prefix >= 0 && n_prefix <= T,
+            "shape (T <= 96, D in {128, 256})");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  const float dbl = 1.f / static_cast<float>(D);
+  if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  else launch_fwd<256>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
+                                   int64_t n_seq, int T, int D, float scale_div, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= VX_PAD && n_seq >= 1, "shape (T <= 96, D in {128, 256})");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  const float dbl = 1.f / static_cast<float>(D);
+  if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
+  else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
+  return ghm_launch_status();
+}

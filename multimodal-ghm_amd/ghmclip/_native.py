@@ -68,6 +68,14 @@ HIP_SIGNATURES = {
     "ghm_vlm_attn_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _p],
     "ghm_vlm_attn_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_gelu_fwd": [_p, _p, _p, _i64, _p],
+    "ghm_gemm_slab_elems": [_i64, _i64, _i],
+    "ghm_vlm_attn_fwd_x3": [_p, _p, _p, _p, _i64, _i, _i, _i, _f, _p],
+    "ghm_vlm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_gemm_x3": [_i, _i, _i, _p, _i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64,
+                    _i, _p],
+    "ghm_gemm_reduce": [_p, _i, _i64, _i64, _p, _p, _p, _i64, _p],
+    "ghm_colsum_part_elems": [_i64, _i64],
+    "ghm_colsum": [_p, _i64, _i64, _p, _p, _p],
     "ghm_mul": [_p, _p, _p, _i64, _p],
     "ghm_add": [_p, _p, _p, _i64, _p],
     "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
@@ -88,7 +96,8 @@ HIP_SIGNATURES = {
     "ghm_add_cols": [_p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64}
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64,
+            "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64}
 
 HOST_SIGNATURES = {
     "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],

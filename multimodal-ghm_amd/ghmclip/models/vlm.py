@@ -5,13 +5,19 @@ auto_regressive=True), :24-33 (generate_mask), :1080-1149 (ConditionalGuidedCELo
 :1067-1078 (KLdiv); trained by training/train_sequential_NWP.py with a frozen CLIP
 image encoder supplying the one prefix token.
 
-``VlmPlan`` runs one model at one batch shape with no autograd: the plain
-projections (Q/K/V, the MLP's two Linear layers, the readout) are library GEMMs
-(torch.mm / addmm on rocBLAS / hipBLASLt, fp32), every other operator is a
-hand-written kernel of libghm_hip (csrc/ghm_vlm.hip): embedding, row LayerNorm
-forward/backward, the masked double-residual attention forward/backward, GELU,
-elementwise products, the cross-entropy + KL loss.  All buffers are allocated
-once; a step is a fixed launch sequence (graph-capturable).
+``VlmPlan`` runs one model at one batch shape with no autograd, in one of two
+matrix-product modes:
+  "x3" (default): Q/K/V and the MLP's two Linear layers, forward, data gradient and
+       weight gradient, on the hand-written split-bf16 MFMA GEMM (csrc/ghm_gemm.hip;
+       GELU / GELU', bias + residual and the GELU' product fused into its epilogues,
+       Q/K/V fused into one [M][3D] product), attention on the split-bf16 MFMA
+       kernels of csrc/ghm_vlm_x3.hip;
+  "f32": exact fp32 library GEMMs (torch.mm / addmm on rocBLAS / hipBLASLt) and the
+       fp32 attention kernels of csrc/ghm_vlm.hip.
+Both use the hand-written embedding, row LayerNorm forward/backward and cross-entropy
++ KL kernels (csrc/ghm_vlm.hip); the 10-wide readout and the bias / embedding
+gradient sums stay torch ops.  All buffers are allocated once; a step is a fixed
+launch sequence (graph-capturable).
 
 HBM layout (M = n_seq * T tokens, D = n_embd, F = 4 D, fp32 row-major):
   H [L+1][M][D], Hmid / X1 (LN1 out) / X2 (LN2 out) / q / k / v [L][M][D],
@@ -25,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import require_hip
+from .hip_encoder import PRECISIONS, default_precision, require_hip
 
 __all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names",
            "VLM_UNTRAINED"]
@@ -61,9 +67,21 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _gemm(ta, tb, epi, A, lda, Bs, ldb, b_chunk, C, ldc, M, N, K, C2=None, bias=None, R=None, ldr=0, nsplit=1,
+          s=None):
+    """ghm_gemm_x3 (include/ghm_hip.h): C = A(m,k) B(k,n) with the epilogue epi."""
+    Bs = list(Bs) + [None] * (3 - len(Bs))
+    pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
+    _native.call("ghm_gemm_x3", ta, tb, epi, _ptr(A), lda, pp(Bs[0]), pp(Bs[1]), pp(Bs[2]), ldb, b_chunk, _ptr(C),
+                 ldc, pp(C2), pp(bias), pp(R), ldr, M, N, K, nsplit, _stream() if s is None else s)
+
+
+EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
+
+
 class VlmPlan:
     def __init__(self, n_layer, n_token, n_seq, n_prefix=1, num_class=10, n_embd=256, eps=1e-5,
-                 normalize_attn=True, device="cuda"):
+                 normalize_attn=True, device="cuda", precision=None):
         if n_token > 96:
             raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
         if n_embd not in (128, 256, 512):
@@ -74,20 +92,37 @@ class VlmPlan:
         self.eps = float(eps)
         self.scale_div = float(math.sqrt(n_embd)) if normalize_attn else 1.0  # model.py:335-336
         self.device = torch.device(device)
+        self.precision = default_precision() if precision is None else precision
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}")
+        if self.precision == "x3" and n_embd not in (128, 256):
+            raise ValueError(f"the split-bf16 VLM kernels take n_embd in (128, 256) (got {n_embd})")
         L, D, F, N = n_layer, n_embd, self.F, n_seq
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         self.H = e(L + 1, M, D)
         self.Hmid, self.X1, self.X2 = e(L, M, D), e(L, M, D), e(L, M, D)
-        self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
         self.G, self.Dg = e(L, M, F), e(L, M, F)
         self.Pm = torch.zeros(L, N, 96, 96, dtype=torch.float32, device=self.device)
         self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
-        self.U, self.Y = e(M, F), e(M, D)
         self.logits, self.dlogits = e(M, num_class), e(M, num_class)
         self.onehot = e(M, num_class)
         self.dH = e(2, M, D)
-        self.dX, self.dq, self.dk, self.dv = e(M, D), e(M, D), e(M, D), e(M, D)
+        self.dX = e(M, D)
         self.dG = e(M, F)
+        if self.precision == "x3":
+            # fused projections: q | k | v columns of one [M][3D] buffer; split-k wgrad slabs
+            self.qkv = e(L, M, 3 * D)
+            self.dqkv = e(M, 3 * D)
+            self.dS = torch.zeros(N, 96, 96, dtype=torch.float32, device=self.device)
+            self.nsplit = max(1, min(32, M // 256))
+            self.slab = e(self.nsplit * max(D * F, 3 * D * D))
+            lib = _native.hip_lib()
+            self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
+                                 lib.ghm_colsum_part_elems(N, n_token * D)))
+        else:
+            self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
+            self.U, self.Y = e(M, F), e(M, D)
+            self.dq, self.dk, self.dv = e(M, D), e(M, D), e(M, D)
         self.nblk = int(_native.hip_lib().ghm_ln_rows_blocks(M))
         self.part_ln = e(self.nblk, 2, D)
         self.xt = torch.empty(N, n_token - n_prefix, dtype=torch.uint8, device=self.device)
@@ -97,6 +132,8 @@ class VlmPlan:
     def forward(self, p, xt, feat):
         """p: name -> fp32 device tensor; xt uint8 [N, T - P] text tokens; feat
         f32 [N, P, V] prefix features.  Returns self.logits [M, V] (all rows)."""
+        if self.precision == "x3":
+            return self._forward_x3(p, xt, feat)
         s = _stream()
         c = _native.call
         M, D, T, N = self.M, self.D, self.T, self.N
@@ -124,6 +161,8 @@ class VlmPlan:
         """Writes d(loss)/d(param) into g[name] for every trained parameter (not
         VLM_UNTRAINED) from dlogits [M, V] (defaults to self.dlogits).  Returns
         dL/dH_0 [M, D] (its prefix rows give the gradient of the features)."""
+        if self.precision == "x3":
+            return self._backward_x3(p, g, dlogits)
         s = _stream()
         c = _native.call
         M, D = self.M, self.D
@@ -160,6 +199,76 @@ class VlmPlan:
         torch.sum(cur.view(self.N, self.T, D), 0, out=g["position_embeddings.weight"])
         torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
         return cur
+
+    # ------------------------------------------------------------------
+    # split-bf16 path: every projection on ghm_gemm_x3 (GELU, bias, residual and
+    # GELU' products fused into the GEMM epilogues), attention on ghm_vlm_attn_*_x3
+    def _forward_x3(self, p, xt, feat):
+        s = _stream()
+        c = _native.call
+        M, D, F, T, N = self.M, self.D, self.F, self.T, self.N
+        c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
+          _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
+        for l in range(self.L):
+            c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+              _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
+            wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
+            _gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
+            c("ghm_vlm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T,
+              D, self.P, self.scale_div, s)
+            c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
+              _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
+            _gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
+                  C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
+            _gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
+                  bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
+        torch.addmm(p["_read_out.bias"], self.H[self.L], p["_read_out.weight"].t(), out=self.logits)
+        self._gen += 1
+        return self.logits
+
+    def _wgrad(self, A, lda, m, B, ldb, n, dst, chunk, s):
+        """dst (rows stacked by chunk) = A^T B over the M tokens: split-k slabs + fixed-order reduce."""
+        _gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.M, nsplit=self.nsplit, s=s)
+        d = list(dst) + [None] * (3 - len(dst))
+        pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
+        _native.call("ghm_gemm_reduce", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk, s)
+
+    def _backward_x3(self, p, g, dlogits=None):
+        s = _stream()
+        c = _native.call
+        M, D, F = self.M, self.D, self.F
+        dz = self.dlogits if dlogits is None else dlogits
+        cur, nxt = self.dH[0], self.dH[1]
+        torch.mm(dz, p["_read_out.weight"], out=cur)
+        torch.mm(dz.t(), self.H[self.L], out=g["_read_out.weight"])
+        torch.sum(dz, 0, out=g["_read_out.bias"])
+        for l in reversed(range(self.L)):
+            w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
+            self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s)
+            self._colsum(cur, M, D, g[f"_mlps.{l}.2.bias"], s)
+            _gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
+            self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s)
+            self._colsum(self.dG, M, F, g[f"_mlps.{l}.0.bias"], s)
+            _gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
+            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+              _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
+            self._reduce_ln(g, 2, l, s)
+            # attention (nxt = dHmid) -> dq | dk | dv
+            c("ghm_vlm_attn_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS), _ptr(self.dqkv),
+              self.N, self.T, D, self.scale_div, s)
+            self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D,
+                        (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"]), D, s)
+            wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
+            _gemm(0, 0, EPI_STORE, self.dqkv, 3 * D, wqkv, D, D, self.dX, D, M, D, 3 * D, s=s)
+            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+              _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
+            self._reduce_ln(g, 1, l, s)
+        self._colsum(cur, self.N, self.T * D, g["position_embeddings.weight"], s)  # sum over sequences
+        torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
+        return cur
+
+    def _colsum(self, X, rows, cols, out, s):
+        _native.call("ghm_colsum", _ptr(X), rows, cols, _ptr(out), _ptr(self.colpart), s)
 
     def _reduce_ln(self, g, which, l, s):
         j = _native.ReduceJob()
@@ -266,13 +375,16 @@ class AutoRegressiveTransformer(nn.Module):
         self._out = nn.Linear(n_token, 1)
         self._names = vlm_param_names(n_layer)
         self._plans = {}
+        # matrix-product mode of the HIP plan ("x3" / "f32"; None: $GHM_PRECISION or "x3")
+        self.precision = None
 
     def _plan(self, n_seq, T, P, device):
-        key = (n_seq, T, P, str(device))
+        key = (n_seq, T, P, str(device), self.precision)
         if key not in self._plans:
             self._plans.clear()
             self._plans[key] = VlmPlan(self.n_layer, T, n_seq, n_prefix=P, num_class=self.vocab_size,
-                                       n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device)
+                                       n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
+                                       precision=self.precision)
         return self._plans[key]
 
     def forward(self, xt, zi):

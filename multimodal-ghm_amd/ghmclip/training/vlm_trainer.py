@@ -31,7 +31,8 @@ class VlmTrainer:
                  betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None, precision=None):
         """model: AutoRegressiveTransformer (sequential); clip_model: the frozen CLIP
         image EncoderTransformer; lr_schedule: one learning rate per step.
-        precision: matrix-product mode of the frozen CLIP encoder's kernels."""
+        precision: matrix-product mode ("x3" split-bf16 MFMA or "f32") of the VLM plan
+        and the frozen CLIP encoder's kernels (default $GHM_PRECISION or "x3")."""
         self.device = torch.device(device)
         self.model, self.clip = model, clip_model
         self.B = batch_size
@@ -66,7 +67,7 @@ class VlmTrainer:
         self.T, self.P, self.V = model.n_token, model.n_i_token, model.vocab_size
         self.plan = VlmPlan(model.n_layer, model.n_token, batch_size, n_prefix=model.n_i_token,
                             num_class=model.vocab_size, n_embd=model.n_embd, normalize_attn=model.normalize_attn,
-                            device=self.device)
+                            device=self.device, precision=precision)
         self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
                                      num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
                                      n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,

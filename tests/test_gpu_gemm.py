@@ -1,0 +1,203 @@
+"""Split-bf16 (x3) GEMM (csrc/ghm_gemm.hip) and the VLM's split-bf16 attention
+(csrc/ghm_vlm_x3.hip) against float64 torch references of the same ops.
+
+Tolerance of a split-bf16 product: every bf16 x bf16 partial product is exact in
+f32; the dropped lo*lo term and the bf16 rounding of lo bound the error at about
+2^-16 of sum_k |a||b| per element (tests/test_split_numerics.py pins that bound on
+the CPU), so each element is checked against 4e-5 * (|A| |B|)[m][n]."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
+REL = 4e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ghmclip import _native
+    assert _native.hip_lib().ghm_device_ok() == 1
+
+
+def _gemm(*a, **k):
+    from ghmclip.models.vlm import _gemm as g
+    g(*a, **k)
+
+
+def _gelu64(u):
+    return u * 0.5 * (1 + torch.erf(u / math.sqrt(2)))
+
+
+def _dgelu64(u):
+    return 0.5 * (1 + torch.erf(u / math.sqrt(2))) + u * torch.exp(-0.5 * u * u) / math.sqrt(2 * math.pi)
+
+
+def _check(got, want, bound, what):
+    err = (got.double().cpu() - want).abs()
+    bad = err > bound
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e}, worst ratio {(err / bound).max().item():.2f}"
+
+
+@pytest.mark.parametrize("M", [405, 1280])
+@pytest.mark.parametrize("K,N", [(256, 256), (256, 1024), (128, 512), (1024, 256)])
+def test_forward_shapes(M, K, N):
+    """Y = X W^T (ta=0, tb=1) with the store, GELU and bias+residual epilogues."""
+    g = torch.Generator().manual_seed(M + K + N)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    Xd, Wd, bd, Rd = X.to(DEV), W.to(DEV), b.to(DEV), R.to(DEV)
+    acc = X.double() @ W.double().t()
+    bound = REL * (X.double().abs() @ W.double().abs().t()) + 1e-6
+    C = torch.empty(M, N, device=DEV)
+    _gemm(0, 1, EPI_STORE, Xd, K, (Wd,), K, 0, C, N, M, N, K)
+    torch.cuda.synchronize()
+    _check(C, acc, bound, "store")
+    C2 = torch.empty(M, N, device=DEV)
+    _gemm(0, 1, EPI_GELU, Xd, K, (Wd,), K, 0, C, N, M, N, K, C2=C2, bias=bd)
+    torch.cuda.synchronize()
+    u = acc + b.double()
+    _check(C, _gelu64(u), 1.2 * bound + 1e-6, "gelu")
+    _check(C2, _dgelu64(u), 0.5 * bound + 1e-6, "gelu'")
+    _gemm(0, 1, EPI_RESID, Xd, K, (Wd,), K, 0, C, N, M, N, K, bias=bd, R=Rd, ldr=N)
+    torch.cuda.synchronize()
+    _check(C, acc + b.double() + R.double(), bound + 1e-6, "resid")
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_stacked_qkv_forward_and_data_grad(D):
+    """The fused QKV product over three separate weights, and its data gradient
+    dX = [dq|dk|dv] [Wq; Wk; Wv] (B stacked along k)."""
+    M = 3 * 81
+    g = torch.Generator().manual_seed(D)
+    X = torch.randn(M, D, generator=g)
+    Ws = [torch.randn(D, D, generator=g) / math.sqrt(D) for _ in range(3)]
+    Wd = [w.to(DEV) for w in Ws]
+    Wcat = torch.cat(Ws, 0).double()
+    C = torch.empty(M, 3 * D, device=DEV)
+    _gemm(0, 1, EPI_STORE, X.to(DEV), D, Wd, D, D, C, 3 * D, M, 3 * D, D)
+    torch.cuda.synchronize()
+    _check(C, X.double() @ Wcat.t(), REL * (X.double().abs() @ Wcat.abs().t()) + 1e-6, "qkv")
+    dY = torch.randn(M, 3 * D, generator=g)
+    dX = torch.empty(M, D, device=DEV)
+    _gemm(0, 0, EPI_STORE, dY.to(DEV), 3 * D, Wd, D, D, dX, D, M, D, 3 * D)
+    torch.cuda.synchronize()
+    _check(dX, dY.double() @ Wcat, REL * (dY.double().abs() @ Wcat.abs()) + 1e-6, "dX")
+
+
+def test_data_grad_product_epilogue():
+    """dU = (dY W2) * GELU'(U) (ta=0, tb=0, product epilogue)."""
+    M, D, F = 700, 256, 1024
+    g = torch.Generator().manual_seed(5)
+    dY = torch.randn(M, D, generator=g)
+    W2 = torch.randn(D, F, generator=g) / 16
+    R = torch.rand(M, F, generator=g)
+    C = torch.empty(M, F, device=DEV)
+    _gemm(0, 0, EPI_MUL, dY.to(DEV), D, (W2.to(DEV),), F, 0, C, F, M, F, D, R=R.to(DEV), ldr=F)
+    torch.cuda.synchronize()
+    want = (dY.double() @ W2.double()) * R.double()
+    bound = REL * (dY.double().abs() @ W2.double().abs()) * R.double() + 1e-6
+    _check(C, want, bound, "mul")
+
+
+@pytest.mark.parametrize("M_tok,nsplit", [(405, 1), (2000, 7), (10368, 32)])
+def test_wgrad_split_k(M_tok, nsplit):
+    """dW = dY^T X over tokens (ta=1, tb=0) in split-k slabs and the fixed-order
+    reduce into three stacked destinations; bit-identical when repeated."""
+    D = 256
+    g = torch.Generator().manual_seed(M_tok)
+    dY = torch.randn(M_tok, 3 * D, generator=g)
+    X = torch.randn(M_tok, D, generator=g)
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    slab = torch.empty(nsplit * 3 * D * D, device=DEV)
+    outs = [torch.empty(D, D, device=DEV) for _ in range(3)]
+    want = dY.double().t() @ X.double()
+    bound = REL * (dY.double().abs().t() @ X.double().abs()) + 1e-6
+    res = []
+    for _ in range(2):
+        _gemm(1, 0, EPI_SLAB, dY.to(DEV), 3 * D, (X.to(DEV),), D, 0, slab, D, 3 * D, D, M_tok, nsplit=nsplit)
+        _native.call("ghm_gemm_reduce", _ptr(slab), nsplit, 3 * D, D, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]), D,
+                     ctypes_stream())
+        torch.cuda.synchronize()
+        res.append(torch.cat(outs, 0).cpu())
+    _check(res[0], want, bound, "wgrad")
+    assert torch.equal(res[0], res[1])
+
+
+def ctypes_stream():
+    import ctypes
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _attn_ref(q, k, v, H, npre, D):
+    """float64 restatement of model.py:329-341 on one batch: mask, softmax,
+    double residual."""
+    N, T, _ = q.shape
+    i = torch.arange(T).view(T, 1)
+    j = torch.arange(T).view(1, T)
+    allowed = torch.where(i < npre, j < npre, j <= i)
+    S = (q @ k.transpose(1, 2)).masked_fill(~allowed, float("-inf")) / math.sqrt(D)
+    A = torch.softmax(S, -1)
+    o = A @ v
+    return H + o + o / D, A
+
+
+@pytest.mark.parametrize("D,T", [(256, 81), (128, 81), (256, 40)])
+def test_attention_x3_forward_backward(D, T):
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    N = 6
+    g = torch.Generator().manual_seed(D + T)
+    qkv = torch.randn(N, T, 3 * D, generator=g) * 0.5
+    H = torch.randn(N, T, D, generator=g)
+    dHm = torch.randn(N, T, D, generator=g)
+    q64, k64, v64 = (qkv[..., i * D:(i + 1) * D].double().requires_grad_(True) for i in range(3))
+    want, A = _attn_ref(q64, k64, v64, H.double(), 1, D)
+    (want * dHm.double()).sum().backward()
+    qkv_d, H_d = qkv.to(DEV), H.to(DEV)
+    Hm = torch.empty(N * T, D, device=DEV)
+    P = torch.zeros(N, 96, 96, device=DEV)
+    _native.call("ghm_vlm_attn_fwd_x3", _ptr(qkv_d), _ptr(H_d), _ptr(Hm), _ptr(P), N, T, D, 1, math.sqrt(D),
+                 ctypes_stream())
+    dS = torch.zeros(N, 96, 96, device=DEV)
+    dqkv = torch.empty(N * T, 3 * D, device=DEV)
+    _native.call("ghm_vlm_attn_bwd_x3", _ptr(qkv_d), _ptr(P), _ptr(dHm.to(DEV)), _ptr(dS), _ptr(dqkv), N, T, D,
+                 math.sqrt(D), ctypes_stream())
+    torch.cuda.synchronize()
+    scale = lambda t: t.abs().max().item()  # noqa: E731
+    assert (Hm.cpu().view(N, T, D).double() - want.detach()).abs().max().item() <= 1e-4 * scale(want)
+    assert (P.cpu()[:, :T, :T].double() - A.detach()).abs().max().item() <= 2e-5
+    assert P.cpu()[:, :T, T:].abs().max().item() == 0.0
+    got = dqkv.cpu().view(N, T, 3 * D).double()
+    for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
+        assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 2e-4 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
+
+
+@pytest.mark.parametrize("M,N", [(10368, 1024), (10368, 256), (405, 256), (128, 81 * 256), (7, 16)])
+def test_colsum(M, N):
+    """ghm_colsum (bias / position-embedding gradients): fp32 sums in a fixed order,
+    within fp32 summation error of the float64 sum and bit-identical on repeat."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(M + N)
+    X = torch.randn(M, N, generator=g)
+    Xd = X.to(DEV)
+    part = torch.empty(_native.hip_lib().ghm_colsum_part_elems(M, N), device=DEV)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(N, device=DEV)
+        _native.call("ghm_colsum", _ptr(Xd), M, N, _ptr(out), _ptr(part), ctypes_stream())
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    want = X.double().sum(0)
+    bound = 1e-6 * X.double().abs().sum(0) + 1e-7
+    assert ((outs[0].double() - want).abs() <= bound).all()
+    assert torch.equal(outs[0], outs[1])

@@ -34,7 +34,10 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-def _pair(L=2, d=256, seed=13):
+TOL = {"f32": (2e-5, 1e-4), "x3": (1e-4, 5e-4)}  # (forward / loss, gradients), relative
+
+
+def _pair(L=2, d=256, seed=13, precision="f32"):
     from ghmclip import AutoRegressiveTransformer
     torch.manual_seed(seed)
     prod = AutoRegressiveTransformer(81, 1, 10, d, L, [4, 1], 4, 4 * d, auto_regressive=True, sequential=True)
@@ -48,14 +51,17 @@ def _pair(L=2, d=256, seed=13):
                 dd = 0.1 * torch.randn(vp.shape, generator=g)
                 vp.add_(dd)
                 vr.add_(dd)
+    prod.precision = precision
     return prod.to(DEV), ref
 
 
+@pytest.mark.parametrize("precision", ["f32", "x3"])
 @pytest.mark.parametrize("B,d", [(5, 256), (3, 128)])
-def test_vlm_module_forward_backward(B, d):
+def test_vlm_module_forward_backward(B, d, precision):
     """AutoRegressiveTransformer logits, parameter and prefix-feature gradients vs
     the oracle restatement of model.py:132-335 (mask, double residual)."""
-    prod, ref = _pair(d=d)
+    tf, tg = TOL[precision]
+    prod, ref = _pair(d=d, precision=precision)
     g = torch.Generator().manual_seed(B)
     xt = torch.randint(0, 10, (B, 80), generator=g)
     feat = torch.randn(B, 1, 10, generator=g)
@@ -68,16 +74,16 @@ def test_vlm_module_forward_backward(B, d):
     want = ref(xt, fr)
     (want * R).sum().backward()
     torch.cuda.synchronize()
-    assert _rel(logits, want) < 2e-5
+    assert _rel(logits, want) < tf
     for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
         if pr.grad is None:
             assert pp.grad is None, k
             continue
-        assert _rel(pp.grad, pr.grad) < 1e-4, k
-    assert _rel(fd.grad, fr.grad) < 1e-4
+        assert _rel(pp.grad, pr.grad) < tg, k
+    assert _rel(fd.grad, fr.grad) < tg
 
 
-def _trainer(L, B, total_iters=30000, d=256):
+def _trainer(L, B, total_iters=30000, d=256, precision="f32"):
     """train_sequential_NWP.py order (raw=True): sampler, CLIP image encoder
     (torch.manual_seed(7), as the fixtures), seed_everything(224), the model."""
     from ghmclip import AutoRegressiveTransformer, EncoderTransformer, NextWordPredictSampler, seed_everything
@@ -90,7 +96,7 @@ def _trainer(L, B, total_iters=30000, d=256):
     model = AutoRegressiveTransformer(81, 1, 10, d, L, [4, 1], 4, 4 * d, auto_regressive=True,
                                       sequential=True).to(DEV)
     sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, total_iters) for k in range(total_iters)]
-    tr = VlmTrainer(model, clip, B, sched, device=DEV, precision="f32")
+    tr = VlmTrainer(model, clip, B, sched, device=DEV, precision=precision)
     return s, tr
 
 
@@ -125,10 +131,12 @@ def test_vlm_steps_vs_reference_fixture():
         assert abs(chist[k] - float(f[f"compare{k}"])) <= 2e-5 * float(f[f"compare{k}"]), (k, chist[k])
 
 
-def test_vlm_steps_vs_oracle():
+@pytest.mark.parametrize("precision", ["f32", "x3"])
+def test_vlm_steps_vs_oracle(precision):
     """Fused step == the oracle's step on identical draws: logits, losses and the
     unclipped gradients (clip coefficient hyper[1])."""
-    s, tr = _trainer(2, 6)
+    tf, tg = TOL[precision]
+    s, tr = _trainer(2, 6, precision=precision)
     ref = VO.OracleVlmTrainer(B=6, L=2)
     rparams = dict(ref.model.named_parameters())
     for it in range(2):
@@ -140,33 +148,36 @@ def test_vlm_steps_vs_oracle():
         ploss, _, cmp = ref.step(batch=(tl[:, :-1].astype(np.int64), tl[:, 1:].astype(np.int64), post,
                                         il.astype(np.int64)))
         torch.cuda.synchronize()
-        assert abs(tr.loss_history()[it] - ploss) <= 2e-5 * ploss
-        assert abs(tr.compare_history()[it] - cmp) <= 2e-5 * cmp
+        assert abs(tr.loss_history()[it] - ploss) <= tf * ploss
+        assert abs(tr.compare_history()[it] - cmp) <= tf * cmp
         coef = tr.hyper[1].item()
         for n, p in tr.model.named_parameters():
             if n in tr.gd:
-                assert _rel(p.grad * coef, rparams[n].grad) < 1e-4, n
+                assert _rel(p.grad * coef, rparams[n].grad) < tg, n
 
 
-def test_vlm_graph_replay_matches_eager():
-    s1, t1 = _trainer(1, 4)
+@pytest.mark.parametrize("precision", ["f32", "x3"])
+def test_vlm_graph_replay_matches_eager(precision):
+    s1, t1 = _trainer(1, 4, precision=precision)
     h1 = _run(s1, t1, 4, 5)
-    s2, t2 = _trainer(1, 4)
+    s2, t2 = _trainer(1, 4, precision=precision)
     h2 = _run(s2, t2, 4, 5, graph_after=2)
     np.testing.assert_array_equal(h1[0], h2[0])
     np.testing.assert_array_equal(h1[1], h2[1])
 
 
-def test_vlm_default_config_curve_vs_reference():
+@pytest.mark.parametrize("precision", ["f32", "x3"])
+def test_vlm_default_config_curve_vs_reference(precision):
     """BASELINE config 5 parity: the default VLM config (p=0.2, L=9, d=256, B=128,
     lr 1e-3 -> 1e-6) loss and Compare histories vs the reference PyTorch-CPU run."""
     g = np.load(os.path.join(GOLDEN, "vlm_curve.npz"))
     n = len(g["loss"])
-    s, tr = _trainer(9, 128)
+    s, tr = _trainer(9, 128, precision=precision)
     hist, chist = _run(s, tr, 128, n, graph_after=3)
     dev = np.abs(hist - g["loss"]) / g["loss"]
     cdev = np.abs(chist - g["compare"]) / g["compare"]
-    print(f"VLM curve: {n} steps, max rel dloss {dev.max():.3e} (first 20: {dev[:20].max():.3e}), dcompare "
+    print(f"VLM curve ({precision}): {n} steps, max rel dloss {dev.max():.3e} (first 20: {dev[:20].max():.3e}), dcompare "
           f"{cdev.max():.3e} (first 20: {cdev[:20].max():.3e}), final {hist[-1]:.5f} vs {g['loss'][-1]:.5f}")
-    # measured 2.4e-7 (loss) / 1.0e-6 (compare) over all 40 steps
-    assert dev.max() <= 1e-5 and cdev.max() <= 1e-5
+    # f32: measured 2.4e-7 (loss) / 1.0e-6 (compare) over all 40 steps; x3: budget 1e-4
+    lim = 1e-5 if precision == "f32" else 1e-4
+    assert dev.max() <= lim and cdev.max() <= lim
