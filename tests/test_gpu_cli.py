@@ -25,14 +25,23 @@ CDM_FLAGS = ["--clip_feature=TF", "--job_name=CDM", "--model_type=TF", "--n_ttre
              "--total_iters=5", "--penalty=0.1", "--raw=False", "--log_interval=2", "--eval_interval=2"]
 
 
+VLM_FLAGS = ["--job_name=VLM", "--clip_feature=TF", "--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4",
+             "--n_ttree_child=3", "--n_itree_child=3", "--p_ttree_flip=0.2", "--p_itree_flip=0.2", "--flip_scale=1",
+             "--batch_size=8", "--variable_type=10", "--d_eb=256", "--n_model_layer=2", "--n_head=4",
+             "--layernorm=True", "--normalize_attn=True", "--lr_max=1e-3", "--lr_min=1e-6", "--guide=False",
+             "--total_iters=5", "--penalty=0.001", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+
+
 @pytest.fixture(autouse=True)
 def _need_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
 
 
-def test_clip_then_sequential_cdm_cli(tmp_path, monkeypatch):
-    from ghmclip.training import train_CLIP, train_sequential_DNS
+def test_clip_then_sequential_cdm_and_vlm_cli(tmp_path, monkeypatch):
+    """exp_vlm_standardTF.sh flags (shortened): train_sequential_NWP finds the same
+    CLIP run and loads its image tower (train_sequential_NWP.py:99-117)."""
+    from ghmclip.training import train_CLIP, train_sequential_DNS, train_sequential_NWP
     from ghmclip.training.train_CLIP import load_checkpoint
     monkeypatch.chdir(tmp_path)
     hist = train_CLIP.main(CLIP_FLAGS)
@@ -49,3 +58,13 @@ def test_clip_then_sequential_cdm_cli(tmp_path, monkeypatch):
     assert d["iter"] == 5
     np.testing.assert_allclose(d["loss_history"], loss)
     assert os.path.exists(os.path.join(os.path.dirname(ck[0]), "training.log"))
+    loss, compare = train_sequential_NWP.main(VLM_FLAGS)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/VLM/K4_L4C3p20_L4C3p20sc10/StT_L2H4D256/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert set(d) == {"model_state_dict", "optimizer_state_dict", "loss", "iter", "loss_history", "ploss_history",
+                      "bayes", "compare"}
+    assert d["iter"] == 5
+    np.testing.assert_allclose(d["loss_history"], loss)
+    np.testing.assert_allclose(d["compare"], compare)

@@ -181,3 +181,35 @@ def test_vlm_default_config_curve_vs_reference(precision):
     # f32: measured 2.4e-7 (loss) / 1.0e-6 (compare) over all 40 steps; x3: budget 1e-4
     lim = 1e-5 if precision == "f32" else 1e-4
     assert dev.max() <= lim and cdev.max() <= lim
+
+
+def test_nwp_pipeline_matches_sampler_draws():
+    """NwpBatchPipeline (producer thread, pinned slots) yields the sampler's own
+    reference-order draws and BP posteriors (train_sequential_NWP.py:159)."""
+    from ghmclip import NextWordPredictSampler
+    from ghmclip.training.pipeline import NwpBatchPipeline
+    s = NextWordPredictSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2])
+    np.random.seed(224)
+    want = [_batch(s, 6) for _ in range(3)]
+    np.random.seed(224)
+    s.native.pull_numpy_state()
+
+    class Rec:
+        def __init__(self):
+            self.got = []
+
+        def set_batch(self, xt, yt, post, il):
+            self.got.append([t.clone() for t in (xt, yt, post, il)])
+
+    rec = Rec()
+    pipe = NwpBatchPipeline(s, 6, n_slots=2)
+    try:
+        for _ in range(3):
+            pipe.next_into(rec)
+    finally:
+        pipe.close()
+    for (tl, il, post), (xt, yt, p, i) in zip(want, rec.got):
+        np.testing.assert_array_equal(xt.numpy(), tl[:, :-1])
+        np.testing.assert_array_equal(yt.numpy(), tl[:, 1:])
+        np.testing.assert_array_equal(i.numpy(), il)
+        np.testing.assert_array_equal(p.numpy(), post)
