@@ -58,17 +58,22 @@ struct GemmArgs {
   int64_t M, N, K, k_per_split;
 };
 
-// k-contiguous tile: rows r0.. r0+ROWS-1 (guard < nrows), k0..k0+31 (guard < K)
+// k-contiguous tile: rows r0..r0+ROWS-1 (rows >= nrows read row nrows-1: their
+// outputs are never stored), k0..k0+31 (K % 32 == 0 on this path).  Loads are
+// unconditional and their data is consumed only by the split store: a guard or
+// select on the loaded value forces a vmcnt wait right after the load, which
+// serialises every prefetch.
 template <int ROWS>
 __device__ __forceinline__ void load_kc(float4* v, const float* __restrict__ base, int64_t ld, int64_t r0,
-                                        int64_t nrows, int64_t k0, int64_t K) {
+                                        int64_t nrows, int64_t k0) {
   constexpr int N = ROWS * 8 / 256;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int idx = threadIdx.x + 256 * i;
     const int row = idx >> 3, k4 = idx & 7;
-    const int64_t r = r0 + row, k = k0 + 4 * k4;
-    v[i] = (r < nrows && k < K) ? *reinterpret_cast<const float4*>(base + r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t r = r0 + row;
+    const int64_t rc = r < nrows ? r : nrows - 1;
+    v[i] = *reinterpret_cast<const float4*>(base + rc * ld + k0 + 4 * k4);
   }
 }
 template <int ROWS>
@@ -85,8 +90,9 @@ __device__ __forceinline__ void store_kc(const float4* v, __bf16* hi, __bf16* lo
   }
 }
 
-// [k][outer] tile: k rows k0..k0+31 (guard < kend), outer columns c0..c0+COLS-1;
-// thread = (k group of RPT rows, 4 columns)
+// [k][outer] tile: k rows k0..k0+31, outer columns c0..c0+COLS-1; thread = (k group
+// of RPT rows, 4 columns).  Rows >= kend read a clamped row; with ZERO the store
+// writes zeros for them (the split-k token tail: one operand zeroed suffices).
 template <int COLS>
 __device__ __forceinline__ void load_oc(float4* v, const float* __restrict__ base, int64_t ld, int64_t k0,
                                         int64_t kend, int64_t c0) {
@@ -95,11 +101,12 @@ __device__ __forceinline__ void load_oc(float4* v, const float* __restrict__ bas
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int64_t k = k0 + RPT * kg + i;
-    v[i] = k < kend ? *reinterpret_cast<const float4*>(base + k * ld + c0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t kc = k < kend ? k : kend - 1;  // kend >= 1; an empty split (k0 >= kend) reads row kend - 1
+    v[i] = *reinterpret_cast<const float4*>(base + kc * ld + c0 + 4 * c4);
   }
 }
-template <int COLS>
-__device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo) {
+template <int COLS, bool ZERO>
+__device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo, int64_t k0, int64_t kend) {
   constexpr int C4 = COLS / 4, RPT = COLS / 32;
   const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
 #pragma unroll
@@ -107,7 +114,8 @@ __device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo
     __bf16 h[RPT], l[RPT];
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const float x = c == 0 ? v[i].x : (c == 1 ? v[i].y : (c == 2 ? v[i].z : v[i].w));
+      float x = c == 0 ? v[i].x : (c == 1 ? v[i].y : (c == 2 ? v[i].z : v[i].w));
+      if constexpr (ZERO) x = (k0 + RPT * kg + i < kend) ? x : 0.f;
       split1(x, h[i], l[i]);
     }
     const int off = (4 * c4 + c) * GP + RPT * kg;
@@ -137,10 +145,23 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) __bf16 ah[2][BM * GP], al[2][BM * GP], bh[2][GB_N * GP], bl[2][GB_N * GP];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * GB_N;
-  const int64_t m0 = static_cast<int64_t>(blockIdx.y) * BM;
-  const int64_t kb = static_cast<int64_t>(blockIdx.z) * g.k_per_split;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
+  // linear id w runs on XCD w % 8; remap so each XCD walks a contiguous run of
+  // tiles (n fastest) and the n-tiles sharing an A row block (and, in split-k,
+  // the tiles sharing a token range) hit the same L2
+  int lin = static_cast<int>(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  {
+    const int full = static_cast<int>(gridDim.x * gridDim.y * gridDim.z) / 8 * 8;
+    if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
+  }
+  const int tbx = lin % static_cast<int>(gridDim.x);
+  const int tby = (lin / static_cast<int>(gridDim.x)) % static_cast<int>(gridDim.y);
+  const int tbz = lin / static_cast<int>(gridDim.x * gridDim.y);
+  const int64_t n0 = static_cast<int64_t>(tbx) * GB_N;
+  const int64_t m0 = static_cast<int64_t>(tby) * BM;
+  const int64_t kb = static_cast<int64_t>(tbz) * g.k_per_split;
   const int64_t ke = kb + g.k_per_split < g.K ? kb + g.k_per_split : g.K;
+  const int64_t klast = ke > kb ? kb + (ke - 1 - kb) / GB_K * GB_K : kb;  // start of the last K tile
 
   // B tile base: the stacked tensor holding storage row (TB ? n0 : k)
   auto bbase = [&](int64_t srow, int64_t& local) -> const float* {
@@ -148,29 +169,31 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
       local = srow;
       return g.B[0];
     }
-    const int64_t q = srow / g.b_chunk;
+    // at most three stacked tensors: compares, not a 64-bit division
+    const int q = srow >= 2 * g.b_chunk ? 2 : (srow >= g.b_chunk ? 1 : 0);
     local = srow - q * g.b_chunk;
     return g.B[q];
   };
 
   auto load = [&](float4* va, float4* vb, int64_t k0) {
     if constexpr (TA) load_oc<BM>(va, g.A, g.lda, k0, ke, m0);
-    else load_kc<BM>(va, g.A, g.lda, m0, g.M, k0, ke);
+    else load_kc<BM>(va, g.A, g.lda, m0, g.M, k0);
     if constexpr (TB) {
       int64_t ln;
       const float* b = bbase(n0, ln);
-      load_kc<GB_N>(vb, b + ln * g.ldb, g.ldb, 0, GB_N, k0, ke);
+      load_kc<GB_N>(vb, b + ln * g.ldb, g.ldb, 0, GB_N, k0);
     } else {
       int64_t lk;
       const float* b = bbase(k0, lk);
       load_oc<GB_N>(vb, b + (lk - k0) * g.ldb, g.ldb, k0, ke, n0);
     }
   };
-  auto store = [&](const float4* va, const float4* vb, int buf) {
-    if constexpr (TA) store_oc<BM>(va, ah[buf], al[buf]);
+  // k0: the K tile being stored (zeroes A's token tail in split-k)
+  auto store = [&](const float4* va, const float4* vb, int buf, int64_t k0) {
+    if constexpr (TA) store_oc<BM, true>(va, ah[buf], al[buf], k0, ke);
     else store_kc<BM>(va, ah[buf], al[buf]);
     if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
-    else store_oc<GB_N>(vb, bh[buf], bl[buf]);
+    else store_oc<GB_N, false>(vb, bh[buf], bl[buf], k0, ke);
   };
 
   // acc[i][j] = C^T tile: rows = 32 n (B image rows), lanes = 32 m (A image rows),
@@ -210,39 +233,42 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     // 128 x 128 tiles: one K tile in flight (two would exceed 256 VGPRs)
     float4 pa[NA], pb[NB];
     load(pa, pb, kb);
-    store(pa, pb, 0);
+    store(pa, pb, 0, kb);
     __syncthreads();
     int buf = 0;
     for (int64_t k0 = kb; k0 < ke; k0 += GB_K) {
       const bool more = k0 + GB_K < ke;
-      if (more) load(pa, pb, k0 + GB_K);
+      load(pa, pb, more ? k0 + GB_K : k0);  // unconditional: no branch around the loads
       issue_fence();
       compute(buf);
-      if (more) store(pa, pb, buf ^ 1);
+      if (more) store(pa, pb, buf ^ 1, k0 + GB_K);
       __syncthreads();
       buf ^= 1;
     }
   } else {
     float4 pa[NA], pb[NB], qa[NA], qb[NB];
+    // loads are unconditional (past the last tile they re-read it, unused): a load
+    // under a branch made the wait-count pass drain every load at the next store
+    auto kt = [&](int64_t k) { return k < ke ? k : klast; };
     load(pa, pb, kb);
-    if (kb + GB_K < ke) load(qa, qb, kb + GB_K);
+    load(qa, qb, kt(kb + GB_K));
     issue_fence();
-    store(pa, pb, 0);
+    store(pa, pb, 0, kb);
     __syncthreads();
-    if (kb + 2 * GB_K < ke) load(pa, pb, kb + 2 * GB_K);
+    load(pa, pb, kt(kb + 2 * GB_K));
     issue_fence();
     for (int64_t k0 = kb; k0 < ke; k0 += 2 * GB_K) {
       // LDS[0] = tile k0; q = tile k0 + 32; p = tile k0 + 64 (in flight)
       compute(0);
-      if (k0 + GB_K < ke) store(qa, qb, 1);
+      if (k0 + GB_K < ke) store(qa, qb, 1, k0 + GB_K);
       __syncthreads();
-      if (k0 + 3 * GB_K < ke) load(qa, qb, k0 + 3 * GB_K);
+      load(qa, qb, kt(k0 + 3 * GB_K));
       issue_fence();
       if (k0 + GB_K >= ke) break;
       compute(1);
-      if (k0 + 2 * GB_K < ke) store(pa, pb, 0);
+      if (k0 + 2 * GB_K < ke) store(pa, pb, 0, k0 + 2 * GB_K);
       __syncthreads();
-      if (k0 + 4 * GB_K < ke) load(pa, pb, k0 + 4 * GB_K);
+      load(pa, pb, kt(k0 + 4 * GB_K));
       issue_fence();
     }
   }
@@ -283,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
         } else if constexpr (EPI == EPI_MUL) {
           st4(g.C + m * g.ldc + n, x[0] * rv[qd].x, x[1] * rv[qd].y, x[2] * rv[qd].z, x[3] * rv[qd].w);
         } else {
-          st4(g.C + (static_cast<int64_t>(blockIdx.z) * g.M + m) * g.N + n, x[0], x[1], x[2], x[3]);
+          st4(g.C + (static_cast<int64_t>(tbz) * g.M + m) * g.N + n, x[0], x[1], x[2], x[3]);
         }
       }
     }
@@ -431,7 +457,9 @@ extern "C" int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda,
               reinterpret_cast<uintptr_t>(C2) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0,
             "16-byte aligned operands");
   // k-contiguous operands are read as float4 along k
-  GHM_CHECK((ta || K % 4 == 0) && (!tb || K % 4 == 0), "K % 4 == 0 for k-contiguous operands");
+  // k-contiguous operands (A with ta = 0, B with tb = 1) and the stacked / [k][n]
+  // weights are read in whole 32-deep K tiles; only the split-k wgrad has a tail
+  GHM_CHECK(ta || K % 32 == 0, "K % 32 == 0 unless ta = 1");
   if (b_chunk > 0) {
     const int64_t rows = tb ? N : K;
     GHM_CHECK(b_chunk % GB_N == 0 && rows <= 3 * b_chunk && B1 && (rows <= 2 * b_chunk || B2),

@@ -107,7 +107,7 @@ def test_data_grad_product_epilogue():
     _check(C, want, bound, "mul")
 
 
-@pytest.mark.parametrize("M_tok,nsplit", [(405, 1), (2000, 7), (10368, 32)])
+@pytest.mark.parametrize("M_tok,nsplit", [(405, 1), (2000, 7), (10368, 32), (10368 + 5, 32)])
 def test_wgrad_split_k(M_tok, nsplit):
     """dW = dY^T X over tokens (ta=1, tb=0) in split-k slabs and the fixed-order
     reduce into three stacked destinations; bit-identical when repeated."""
@@ -121,9 +121,15 @@ def test_wgrad_split_k(M_tok, nsplit):
     outs = [torch.empty(D, D, device=DEV) for _ in range(3)]
     want = dY.double().t() @ X.double()
     bound = REL * (dY.double().abs().t() @ X.double().abs()) + 1e-6
+    # NaN guard rows after both operands: any read past the last token (e.g. by an
+    # empty trailing split) would turn the result into NaN
+    dY_big = torch.full((M_tok + 64, 3 * D), float("nan"), device=DEV)
+    X_big = torch.full((M_tok + 64, D), float("nan"), device=DEV)
+    dY_big[:M_tok] = dY.to(DEV)
+    X_big[:M_tok] = X.to(DEV)
     res = []
     for _ in range(2):
-        _gemm(1, 0, EPI_SLAB, dY.to(DEV), 3 * D, (X.to(DEV),), D, 0, slab, D, 3 * D, D, M_tok, nsplit=nsplit)
+        _gemm(1, 0, EPI_SLAB, dY_big, 3 * D, (X_big,), D, 0, slab, D, 3 * D, D, M_tok, nsplit=nsplit)
         _native.call("ghm_gemm_reduce", _ptr(slab), nsplit, 3 * D, D, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]), D,
                      ctypes_stream())
         torch.cuda.synchronize()
