@@ -291,7 +291,10 @@ int ghm_add(const float* a, const float* b, float* out, int64_t n, void* stream)
  * (ConditionalGuidedCELoss guide=False, model.py:1087-1098) and the batchmean KL of
  * post [n_seq][T - n_prefix][V] against softmax(logits) (KLdiv, :1067-1078; post may
  * be NULL); dlogits (may be NULL) = (softmax - onehot) / rows on text rows, 0 on
- * prefix rows.  loss_out[0..1] <- loss, compare; hist / chist [*step] when non-NULL. */
+ * prefix rows.  loss_out[0..1] <- loss, compare; loss_out[2..] holds per-workgroup
+ * partials: the buffer has ghm_ce_kl_out_elems(n_seq, T, n_prefix) floats.
+ * hist / chist [*step] when non-NULL. */
+int64_t ghm_ce_kl_out_elems(int64_t n_seq, int T, int n_prefix);
 int ghm_ce_kl(const float* logits, const uint8_t* targets, const float* post, float* dlogits, float* loss_out,
               float* hist, float* chist, const int32_t* step, int64_t n_seq, int T, int n_prefix, int V,
               void* stream);

@@ -79,6 +79,7 @@ HIP_SIGNATURES = {
     "ghm_mul": [_p, _p, _p, _i64, _p],
     "ghm_add": [_p, _p, _p, _i64, _p],
     "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_ce_kl_out_elems": [_i64, _i, _i],
     "ghm_ln_qkv_fwd_x3": [_p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
@@ -97,7 +98,8 @@ HIP_SIGNATURES = {
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64,
-            "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64}
+            "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
+            "ghm_ce_kl_out_elems": _i64}
 
 HOST_SIGNATURES = {
     "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],

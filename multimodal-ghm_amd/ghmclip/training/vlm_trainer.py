@@ -90,7 +90,9 @@ class VlmTrainer:
         self.step_ctr = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.hyper = torch.zeros(4, dtype=torch.float32, device=self.device)
         self.work = torch.zeros(1024, dtype=torch.float32, device=self.device)
-        self.loss_out = torch.zeros(2, dtype=torch.float32, device=self.device)
+        # [loss, compare, per-workgroup partials] (ghm_ce_kl_out_elems)
+        self.loss_out = torch.zeros(_native.hip_lib().ghm_ce_kl_out_elems(batch_size, self.T, self.P),
+                                    dtype=torch.float32, device=self.device)
         self.hist = torch.zeros(max(1, len(lr_schedule)), dtype=torch.float32, device=self.device)
         self.chist = torch.zeros_like(self.hist)
         self.graphs = None
