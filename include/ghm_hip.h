@@ -308,6 +308,16 @@ int ghm_vlm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P
 int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
                         int T, int D, float scale_div, void* stream);
 
+/* General form of the two above: prefix-causal mask with n_prefix (n_prefix = T: no
+ * mask), H_mid = (H + o) + o * dbl (dbl = 1/D: the VLM's double residual; 0: the
+ * plain residual of the CLIP / CDM encoders, model.py:391-394, 474-478).  D = 128
+ * takes T <= 192 (P, dS [n_seq][192][192] when T > 96, else [n_seq][96][96]);
+ * D = 256 takes T <= 96.  The joint CDM (train_CDNS.py, T = 162) runs on it. */
+int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T, int D,
+                        int n_prefix, float scale_div, float dbl, void* stream);
+int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
+                        int T, int D, float scale_div, float dbl, void* stream);
+
 /* ---- split-bf16 (x3) GEMM for the VLM projections (csrc/ghm_gemm.hip) -------
  * Replaces the nn.Linear products of AutoRegressiveTransformer (models/model.py:
  * 203-216 _queries/_keys/_values/_mlps, applied at :330-347) and their autograd

@@ -22,7 +22,9 @@
 
 namespace {
 
-constexpr int VX_PAD = 96;        // padded sequence length of the P / dS layouts
+// padded sequence length of the P / dS layouts: 96 for T <= 96 (NKT <= 3), 192 above
+template <int NKT>
+__device__ __forceinline__ constexpr int vx_pad() { return NKT <= 3 ? 96 : 192; }
 constexpr int VX_PITCH = 64 + 8;  // [row][h][32] half image row (bf16)
 
 typedef __attribute__((address_space(3))) bf16x4 vx_lds_bf16x4;
@@ -147,6 +149,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __
                                                                  const float* __restrict__ H,
                                                                  float* __restrict__ Hmid, float* __restrict__ P,
                                                                  int T, int npre, float scale_div, float dbl) {
+  constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
   __shared__ __attribute__((aligned(16))) __bf16 sh[TP * VX_PITCH];
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* 
                                                                    float* __restrict__ dS_out,
                                                                    float* __restrict__ dqkv, int T, float scale_div,
                                                                    float dbl) {
+  constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
   __shared__ __attribute__((aligned(16))) __bf16 sh[TP * VX_PITCH];
@@ -314,6 +318,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
                                                                     const float* __restrict__ dS,
                                                                     const float* __restrict__ dHmid,
                                                                     float* __restrict__ dqkv, int T, float dbl) {
+  constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32, KS = TP / 16;
   constexpr int64_t LD = 3 * DD;
   __shared__ __attribute__((aligned(16))) __bf16 soh[TP * 32];
@@ -326,39 +331,78 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
   const bool kv = key < T;
   const float* pc = P + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
   const float* sc = dS + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
-  bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
-#pragma unroll
-  for (int st = 0; st < KS; ++st) {
-    float pv[8], sv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int qq = 16 * st + 8 * h + i;
-      pv[i] = pc[qq * VX_PAD];
-      sv[i] = sc[qq * VX_PAD];
-    }
-    split8(pv, pbh[st], pbl[st]);
-    split8(sv, sbh[st], sbl[st]);
-  }
-#pragma unroll 1
-  for (int dt = 0; dt < DD / 32; ++dt) {
-    vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
-    vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
-    __syncthreads();
-    f32x16 aV = zero16(), aK = zero16();
-#pragma unroll
+  if constexpr (NKT <= 3) {
+    bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
+  #pragma unroll
     for (int st = 0; st < KS; ++st) {
-      const int r0 = 16 * st + 8 * h;
-      aV = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
-      aK = mfma_x3(vx_tr_frag(sqh, r0, r0 + 4, lane), vx_tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
+      float pv[8], sv[8];
+  #pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int qq = 16 * st + 8 * h + i;
+        pv[i] = pc[qq * VX_PAD];
+        sv[i] = sc[qq * VX_PAD];
+      }
+      split8(pv, pbh[st], pbl[st]);
+      split8(sv, sbh[st], sbl[st]);
     }
-    __syncthreads();
-    if (kv) {
-      float* o = dqkv + (base + key) * LD + 32 * dt;
+  #pragma unroll 1
+    for (int dt = 0; dt < DD / 32; ++dt) {
+      vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
+      vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
+      __syncthreads();
+      f32x16 aV = zero16(), aK = zero16();
+  #pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const int r0 = 16 * st + 8 * h;
+        aV = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
+        aK = mfma_x3(vx_tr_frag(sqh, r0, r0 + 4, lane), vx_tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
+      }
+      __syncthreads();
+      if (kv) {
+        float* o = dqkv + (base + key) * LD + 32 * dt;
+  #pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const float v0 = aV[4 * qd], v1 = aV[4 * qd + 1], v2 = aV[4 * qd + 2], v3 = aV[4 * qd + 3];
+          st4(o + 2 * DD + quad_off(qd, h), v0 + v0 * dbl, v1 + v1 * dbl, v2 + v2 * dbl, v3 + v3 * dbl);
+          st4(o + DD + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
+        }
+      }
+    }
+  } else {
+    // T > 96: both products' B fragments (4 x KS x 8 VGPRs) no longer fit beside
+    // the accumulators, so dV^T = dO^T P and dK^T = Q^T dS run as two passes
+#pragma unroll 1
+    for (int which = 0; which < 2; ++which) {
+      const float* src = which == 0 ? pc : sc;
+      bf16x8 bh[KS], bl[KS];
 #pragma unroll
-      for (int qd = 0; qd < 4; ++qd) {
-        const float v0 = aV[4 * qd], v1 = aV[4 * qd + 1], v2 = aV[4 * qd + 2], v3 = aV[4 * qd + 3];
-        st4(o + 2 * DD + quad_off(qd, h), v0 + v0 * dbl, v1 + v1 * dbl, v2 + v2 * dbl, v3 + v3 * dbl);
-        st4(o + DD + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
+      for (int st = 0; st < KS; ++st) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = src[(16 * st + 8 * h + i) * VX_PAD];
+        split8(v, bh[st], bl[st]);
+      }
+#pragma unroll 1
+      for (int dt = 0; dt < DD / 32; ++dt) {
+        if (which == 0) vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
+        else vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, soh, sol);
+        __syncthreads();
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+          const int r0 = 16 * st + 8 * h;
+          acc = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), bh[st], bl[st], acc);
+        }
+        __syncthreads();
+        if (kv) {
+          float* o = dqkv + (base + key) * LD + 32 * dt + (which == 0 ? 2 * DD : DD);
+          const float f = which == 0 ? dbl : 0.f;
+#pragma unroll
+          for (int qd = 0; qd < 4; ++qd) {
+            const float v0 = acc[4 * qd], v1 = acc[4 * qd + 1], v2 = acc[4 * qd + 2], v3 = acc[4 * qd + 3];
+            st4(o + quad_off(qd, h), v0 + v0 * f, v1 + v1 * f, v2 + v2 * f, v3 + v3 * f);
+          }
+        }
       }
     }
   }
@@ -371,8 +415,16 @@ void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<1, DD>), dim3(g), dim3(64), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
   else if (T <= 64)
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<2, DD>), dim3(g), dim3(128), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else
+  else if (T <= 96)
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<3, DD>), dim3(g), dim3(192), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if constexpr (DD == 128) {
+    if (T <= 128)
+      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<4, DD>), dim3(g), dim3(256), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+    else if (T <= 160)
+      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<5, DD>), dim3(g), dim3(320), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+    else
+      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<6, DD>), dim3(g), dim3(384), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  }
 }
 
 template <int NKT, int DD>
@@ -388,7 +440,12 @@ void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
                 float* dqkv, float sd, float dbl) {
   if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
   else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  else launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+  else if (T <= 96) launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+  else if constexpr (DD == 128) {
+    if (T <= 128) launch_bwd_n<4, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+    else if (T <= 160) launch_bwd_n<5, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+    else launch_bwd_n<6, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
+  }
 }
 
 }  // namespace
@@ -396,21 +453,36 @@ void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
 extern "C" int ghm_vlm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                                    int D, int n_prefix, float scale_div, void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= VX_PAD && n_seq >= 1 && n_prefix >= 0 && n_prefix <= T,
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 96 && n_seq >= 1 && n_prefix >= 0 && n_prefix <= T,
             "shape (T <= 96, D in {128, 256})");
-  const unsigned g = static_cast<unsigned>(n_seq);
-  const float dbl = 1.f / static_cast<float>(D);
-  if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
-  else launch_fwd<256>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
-  return ghm_launch_status();
+  return ghm_attn_ext_fwd_x3(qkv, H, H_mid, P, n_seq, T, D, n_prefix, scale_div, 1.f / static_cast<float>(D),
+                             stream);
 }
 
 extern "C" int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                                    int64_t n_seq, int T, int D, float scale_div, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= VX_PAD && n_seq >= 1, "shape (T <= 96, D in {128, 256})");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 96 && n_seq >= 1, "shape (T <= 96, D in {128, 256})");
+  return ghm_attn_ext_bwd_x3(qkv, P, dH_mid, dS, dqkv, n_seq, T, D, scale_div, 1.f / static_cast<float>(D), stream);
+}
+
+extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
+                                   int D, int n_prefix, float scale_div, float dbl, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK((D == 128 && T >= 1 && T <= 192) || (D == 256 && T >= 1 && T <= 96), "shape (D 128: T <= 192; D 256: T <= 96)");
+  GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  const float dbl = 1.f / static_cast<float>(D);
+  if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  else launch_fwd<256>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
+                                   int64_t n_seq, int T, int D, float scale_div, float dbl, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
+  GHM_CHECK((D == 128 && T >= 1 && T <= 192) || (D == 256 && T >= 1 && T <= 96), "shape (D 128: T <= 192; D 256: T <= 96)");
+  GHM_CHECK(n_seq >= 1, "n_seq >= 1");
+  const unsigned g = static_cast<unsigned>(n_seq);
   if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
   else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
   return ghm_launch_status();

@@ -8,7 +8,8 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   H    [L+1, M, 128]   residual stream entering each layer (+ final output)
   Hmid [L,   M, 128]   residual after attention
   qkv  [L,   M, 384]   Q | K | V
-  P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input)
+  P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input);
+       [L, n_seq, 192, 192] for sequences past 96 tokens (x3 only)
   G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (backward inputs)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
   pack [L, 983040] bf16 (precision "x3" only): per-layer pre-split weight planes
@@ -77,13 +78,18 @@ class EncoderPlan:
                  wgrad_min_tokens=None):
         if n_embd != D_MODEL:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
-        if n_token > 96:
-            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
         if num_class != 10 or vocab > 16:
             raise ValueError("the HIP readout is built for num_class == 10 and a vocabulary <= 16")
         self.precision = default_precision() if precision is None else precision
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
+        if n_token > 192 or (n_token > 96 and self.precision != "x3"):
+            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens, <= 192 with the split-bf16 "
+                             f"(x3) kernels (got {n_token}, precision {self.precision})")
+        # sequences past 96 tokens (the joint CDM's 162) run on ghm_attn_ext_*_x3 with
+        # P / dS padded to 192
+        self.long_attn = n_token > 96
+        pad = 192 if self.long_attn else 96
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -96,7 +102,7 @@ class EncoderPlan:
         self.H = e(L + 1, M, D_MODEL)
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
-        self.P = torch.zeros(L, N, 96, 96, dtype=f32, device=dev)
+        self.P = torch.zeros(L, N, pad, pad, dtype=f32, device=dev)
         self.G = e(L, M, D_HIDDEN)
         self.Dg = e(L, M, D_HIDDEN)
         self.st1 = e(L, M, 2)
@@ -107,7 +113,7 @@ class EncoderPlan:
         self.dH = e(2, M, D_MODEL)
         self.dqkv = e(M, 3 * D_MODEL)
         self.dU = e(M, D_HIDDEN)
-        self.dS = torch.zeros(N, 96, 96, dtype=f32, device=dev)
+        self.dS = torch.zeros(N, pad, pad, dtype=f32, device=dev)
         self.nblk = int(_native.hip_lib().ghm_token_blocks(M))
         self.part_ln = e(self.nblk, 2, D_MODEL)
         self.part_ln2 = e(self.nblk, 2, D_MODEL)
@@ -180,8 +186,12 @@ class EncoderPlan:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
                   pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-                c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-                  N, T, D_MODEL, self.scale_div, s)
+                if self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
+                    c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                      _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+                else:
+                    c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                      N, T, D_MODEL, self.scale_div, s)
                 c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
                   _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL,
@@ -302,8 +312,12 @@ class EncoderPlan:
               _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
             jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
-              D_MODEL, self.scale_div, s)
+            if self.long_attn:
+                c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
+                  _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, 0.0, s)
+            else:
+                c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
+                  _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
             c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),

@@ -143,9 +143,9 @@ def ctypes_stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def _attn_ref(q, k, v, H, npre, D):
+def _attn_ref(q, k, v, H, npre, D, dbl=None):
     """float64 restatement of model.py:329-341 on one batch: mask, softmax,
-    double residual."""
+    double residual (dbl = 1/D; 0 for the plain residual of model.py:474-478)."""
     N, T, _ = q.shape
     i = torch.arange(T).view(T, 1)
     j = torch.arange(T).view(1, T)
@@ -153,7 +153,7 @@ def _attn_ref(q, k, v, H, npre, D):
     S = (q @ k.transpose(1, 2)).masked_fill(~allowed, float("-inf")) / math.sqrt(D)
     A = torch.softmax(S, -1)
     o = A @ v
-    return H + o + o / D, A
+    return H + o + o * (1.0 / D if dbl is None else dbl), A
 
 
 @pytest.mark.parametrize("D,T", [(256, 81), (128, 81), (256, 40)])
@@ -207,3 +207,38 @@ def test_colsum(M, N):
     bound = 1e-6 * X.double().abs().sum(0) + 1e-7
     assert ((outs[0].double() - want).abs() <= bound).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("T,npre,dbl", [(162, 162, 0.0), (130, 1, 1 / 128), (81, 81, 0.0), (100, 100, 0.0)])
+def test_attention_ext_long_sequences(T, npre, dbl):
+    """ghm_attn_ext_*_x3 at D = 128: sequences past 96 tokens (the joint CDM's 162,
+    train_CDNS.py) with P / dS padded to 192, unmasked (n_prefix = T) and plain
+    residual (dbl = 0), plus a masked double-residual case."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    N, D = 5, 128
+    pad = 96 if T <= 96 else 192
+    g = torch.Generator().manual_seed(T)
+    qkv = torch.randn(N, T, 3 * D, generator=g) * 0.5
+    H = torch.randn(N, T, D, generator=g)
+    dHm = torch.randn(N, T, D, generator=g)
+    q64, k64, v64 = (qkv[..., i * D:(i + 1) * D].double().requires_grad_(True) for i in range(3))
+    want, A = _attn_ref(q64, k64, v64, H.double(), npre, D, dbl)
+    (want * dHm.double()).sum().backward()
+    qkv_d = qkv.to(DEV)
+    Hm = torch.empty(N * T, D, device=DEV)
+    P = torch.zeros(N, pad, pad, device=DEV)
+    dS = torch.zeros(N, pad, pad, device=DEV)
+    dqkv = torch.empty(N * T, 3 * D, device=DEV)
+    _native.call("ghm_attn_ext_fwd_x3", _ptr(qkv_d), _ptr(H.to(DEV)), _ptr(Hm), _ptr(P), N, T, D, npre, math.sqrt(D),
+                 dbl, ctypes_stream())
+    _native.call("ghm_attn_ext_bwd_x3", _ptr(qkv_d), _ptr(P), _ptr(dHm.to(DEV)), _ptr(dS), _ptr(dqkv), N, T, D,
+                 math.sqrt(D), dbl, ctypes_stream())
+    torch.cuda.synchronize()
+    scale = lambda t: t.abs().max().item()  # noqa: E731
+    assert (Hm.cpu().view(N, T, D).double() - want.detach()).abs().max().item() <= 1e-4 * scale(want)
+    assert (P.cpu()[:, :T, :T].double() - A.detach()).abs().max().item() <= 2e-5
+    assert P.cpu()[:, :T, T:].abs().max().item() == 0.0
+    got = dqkv.cpu().view(N, T, 3 * D).double()
+    for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
+        assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 2e-4 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
