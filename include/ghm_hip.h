@@ -229,6 +229,11 @@ int ghm_add_cols(float* dst, const float* src, int64_t M, int V, void* stream);
  * z: f32 [n_seq][T_img]; cond: f32 [n_seq][T - T_img][cond_ld]; pos_w [T][128]. */
 int ghm_cdm_embed_fwd(const float* z, const float* cond, int cond_ld, const float* pos_w, float* H0,
                       int64_t n_seq, int T, int T_img, int V, int D, void* stream);
+/* Joint CDM (train_CDNS.py: sequential=False, model.py:408-423): text token
+ * t >= T_img gets the row t_emb[tok[n, t - T_img]] ([V][128]); image tokens as
+ * above.  tok uint8 [n_seq][T - T_img]; T <= 192. */
+int ghm_cdm_embed_joint_fwd(const float* z, const uint8_t* tok, const float* t_emb, const float* pos_w, float* H0,
+                            int64_t n_seq, int T, int T_img, int V, int D, void* stream);
 /* Exact BP, f64, one workgroup per sample: the text tree's BP_CLS root message
  * (data_random_GHM.py:185-208) conditions BP_DNS of the image tree (:467-523,
  * external message :875-877).  trans: [L][C][V][V] templates; t_tokens uint8

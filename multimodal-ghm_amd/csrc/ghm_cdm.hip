@@ -51,6 +51,38 @@ __global__ __launch_bounds__(256) void k_cdm_embed_fwd(const float* __restrict__
   st4(H0 + m * GHM_D + 4 * q, e[0] + p.x, e[1] + p.y, e[2] + p.z, e[3] + p.w);
 }
 
+// Joint CDM embedding (ConditionalDenoiseEncoderTransformer, sequential=False,
+// model.py:408-423, :437): image token t < T_img gets -(d - z)^2 / 2 in d < V,
+// text token t >= T_img gets the full row t_emb[tok[n, t - T_img]]; + positions.
+__global__ __launch_bounds__(256) void k_cdm_embed_joint_fwd(const float* __restrict__ z,
+                                                             const uint8_t* __restrict__ tok,
+                                                             const float* __restrict__ t_emb,
+                                                             const float* __restrict__ pos, float* __restrict__ H0,
+                                                             int64_t n_tok, int T, int T_img, int V) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= n_tok * (GHM_D / 4)) return;
+  const int q = static_cast<int>(idx & 31);
+  const int64_t m = idx >> 5;
+  const int64_t n = m / T;
+  const int t = static_cast<int>(m % T);
+  const float4 p = *reinterpret_cast<const float4*>(pos + static_cast<int64_t>(t) * GHM_D + 4 * q);
+  float4 e;
+  if (t < T_img) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int d = 4 * q + k;
+      const float x = static_cast<float>(d) - z[n * T_img + t];
+      v[k] = d < V ? -(x * x) * 0.5f : 0.f;
+    }
+    e = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    const int c = tok[n * (T - T_img) + (t - T_img)];
+    e = *reinterpret_cast<const float4*>(t_emb + static_cast<int64_t>(c) * GHM_D + 4 * q);
+  }
+  st4(H0 + m * GHM_D + 4 * q, e.x + p.x, e.y + p.y, e.z + p.z, e.w + p.w);
+}
+
 // --------------------------------------------------------------------------
 // Exact BP on the device, f64 like the reference's numpy.  One 64-thread
 // workgroup per sample: the text tree's BP_CLS root message (:185-208), then
@@ -339,6 +371,17 @@ extern "C" int ghm_cdm_embed_fwd(const float* z, const float* cond, int cond_ld,
   const int64_t n = n_seq * T * (GHM_D / 4);
   hipLaunchKernelGGL(k_cdm_embed_fwd, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, ghm_stream(stream),
                      z, cond, cond_ld, pos_w, H0, n_seq * T, T, T_img, V);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_cdm_embed_joint_fwd(const float* z, const uint8_t* tok, const float* t_emb, const float* pos_w,
+                                       float* H0, int64_t n_seq, int T, int T_img, int V, int D, void* stream) {
+  GHM_CHECK(z && tok && t_emb && pos_w && H0, "null pointer");
+  GHM_CHECK(D == GHM_D && T > T_img && T_img >= 1 && T <= 192 && V >= 1 && V <= 16 && n_seq >= 1,
+            "shape (D == 128, T_img < T <= 192, V <= 16)");
+  const int64_t n = n_seq * T * (GHM_D / 4);
+  hipLaunchKernelGGL(k_cdm_embed_joint_fwd, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     ghm_stream(stream), z, tok, t_emb, pos_w, H0, n_seq * T, T, T_img, V);
   return ghm_launch_status();
 }
 

@@ -57,6 +57,7 @@ HIP_SIGNATURES = {
     "ghm_clip_prepare": [_p, _i64, _f, _p, _i, _p, _p, _p, _p],
     "ghm_split_weights": [_p, _i, _p],
     "ghm_cdm_embed_fwd": [_p, _p, _i, _p, _p, _i64, _i, _i, _i, _i, _p],
+    "ghm_cdm_embed_joint_fwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
     "ghm_bp_dns": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _i64, _i, _i, _i, _i, _i, _p],
     "ghm_cdm_readout_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ls_loss": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],

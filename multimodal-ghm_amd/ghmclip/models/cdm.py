@@ -16,15 +16,21 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import D_MODEL, EncoderPlan, require_hip
+from .hip_encoder import D_MODEL, EncoderPlan, default_precision, require_hip
+
+
+def self_precision_f32():
+    return default_precision() == "f32"
 
 __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
-           "cdm_param_names", "CDM_UNTRAINED"]
+           "cdm_param_names", "CDM_UNTRAINED", "CDM_JOINT_UNTRAINED"]
 
 # parameters the reference never gives a gradient in sequential mode (the
 # conditioning token bypasses t_embedding, _out is unused by forward): AdamW and
 # clip_grad_norm_ skip them (optimizer.py:55-56)
 CDM_UNTRAINED = ("t_embedding.weight", "_out.weight", "_out.bias")
+# joint model (sequential=False, train_CDNS.py): the text leaves go through t_embedding
+CDM_JOINT_UNTRAINED = ("_out.weight", "_out.bias")
 
 
 def cdm_param_names(n_layer):
@@ -60,12 +66,17 @@ class CdmPlan(EncoderPlan):
     split-K buffers part_w1 / part_b1)."""
 
     def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None):
+                 normalize_attn=True, device="cuda", precision=None, joint=False):
         super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
                          normalize_attn=normalize_attn, device=device, precision=precision)
         if not 1 <= n_i_token <= n_token:
             raise ValueError("n_i_token must be in [1, n_token]")
         self.Ti = n_i_token
+        self.joint = joint
+        if joint:  # text leaves as tokens through t_embedding (sequential=False)
+            self.tok = torch.empty(n_seq, n_token - n_i_token, dtype=torch.uint8, device=self.device)
+            self.onehot = torch.zeros(n_seq * (n_token - n_i_token), num_class, dtype=torch.float32,
+                                      device=self.device)
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         self.pred = e(n_seq, n_i_token)
         self.dpred = e(n_seq, n_i_token)
@@ -78,9 +89,14 @@ class CdmPlan(EncoderPlan):
         s = _stream()
         if self.precision == "x3" and split:
             self.split_weights(p, s)
-        _native.call("ghm_cdm_embed_fwd", _ptr(z), _ptr(cond) if cond is not None else None, cond_ld,
-                     _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), self.N, self.T, self.Ti, self.C,
-                     D_MODEL, s)
+        if self.joint:  # cond unused: self.tok holds the text leaves
+            _native.call("ghm_cdm_embed_joint_fwd", _ptr(z), _ptr(self.tok), _ptr(p["t_embedding.weight"]),
+                         _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), self.N, self.T, self.Ti, self.C,
+                         D_MODEL, s)
+        else:
+            _native.call("ghm_cdm_embed_fwd", _ptr(z), _ptr(cond) if cond is not None else None, cond_ld,
+                         _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), self.N, self.T, self.Ti, self.C,
+                         D_MODEL, s)
         self.layers_fwd(p, s)
         _native.call("ghm_cdm_readout_fwd", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]),
                      _ptr(p["_read_out.bias"]), _ptr(self.pred), self.N, self.T, self.Ti, D_MODEL, s)
@@ -101,6 +117,11 @@ class CdmPlan(EncoderPlan):
         cur = self.layers_bwd(p, g, jobs, s, layer_grad)
         jobs.append(J(cur, self.N, [g["position_embeddings.weight"]]))
         self._flush(jobs, s)
+        if self.joint:  # d t_embedding[v] = sum of the text rows of dH_0 holding token v
+            self.onehot.zero_()
+            self.onehot.scatter_(1, self.tok.view(-1, 1).long(), 1.0)
+            dtext = cur.view(self.N, self.T, D_MODEL)[:, self.Ti:, :].reshape(-1, D_MODEL)
+            torch.mm(self.onehot.t(), dtext, out=g["t_embedding.weight"])
         return cur
 
 
@@ -112,8 +133,12 @@ class _CdmFn(torch.autograd.Function):
         plan = module._plan(N, T1 + T2, T2, zi.device)
         pd = dict(zip(module._names, params))
         z = zi.contiguous().float()
-        cond = xt.contiguous().float()
-        pred = plan.forward(pd, z, cond, cond.shape[2]).clone()
+        if plan.joint:
+            plan.tok.copy_(xt.to(torch.uint8))
+            pred = plan.forward(pd, z, None, 0).clone()
+        else:
+            cond = xt.contiguous().float()
+            pred = plan.forward(pd, z, cond, cond.shape[2]).clone()
         ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
         ctx.T1 = T1
         ctx.save_for_backward(*params)
@@ -127,11 +152,12 @@ class _CdmFn(torch.autograd.Function):
                                "overwrote the activations saved for backward")
         params = ctx.saved_tensors
         names = ctx.module._names
-        trained = [n not in CDM_UNTRAINED for n in names]
+        untrained = CDM_JOINT_UNTRAINED if plan.joint else CDM_UNTRAINED
+        trained = [n not in untrained for n in names]
         grads = {n: torch.empty_like(p) for n, p, t in zip(names, params, trained) if t}
         dH0 = plan.backward(dict(zip(names, params)), grads, dpred=dpred.contiguous().float())
         d_xt = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not plan.joint:
             V = ctx.module.vocab_size
             d_xt = torch.zeros(plan.N, ctx.T1, ctx.module.vocab_size, dtype=torch.float32, device=dH0.device)
             d_xt.copy_(dH0.view(plan.N, plan.T, D_MODEL)[:, plan.Ti:, :V])
@@ -141,9 +167,11 @@ class _CdmFn(torch.autograd.Function):
 class ConditionalDenoiseEncoderTransformer(nn.Module):
     """Reference: models/model.py:337-532.  Same constructor, parameter creation
     order (so torch.manual_seed gives identical weights) and state_dict keys.
-    The HIP path covers the sequential configuration the CDM experiments train
-    (scripts/experiments/exp_cdm_{standard,shallow}TF.sh): a frozen-CLIP feature
-    token, softmax attention, LayerNorm, MLP, no guide, no causal mask, n_embd 128."""
+    The HIP path covers the configurations the CDM experiments train: sequential
+    (exp_cdm_{standard,shallow}TF.sh: a frozen-CLIP feature token, T = 82) and joint
+    (exp_cdm_jointtrain.sh: the 81 text leaves through t_embedding, T = 162, on the
+    split-bf16 attention for sequences past 96 tokens); softmax attention,
+    LayerNorm, MLP, no guide, no causal mask, n_embd 128."""
 
     def __init__(self, n_token, n_i_token, num_class, n_embd=128, n_layer=12, n_guided_layers=(3, 3), n_head=4,
                  n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True, auto_regressive=False,
@@ -173,9 +201,9 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive or guide:
             raise NotImplementedError("HIP CDM: softmax attention, mlp=True, layernorm=True, maxnorm=False, "
                                       "auto_regressive=False, guide=False")
-        if not sequential:
-            raise NotImplementedError("HIP CDM: sequential=True (frozen-CLIP conditioning token); the joint "
-                                      "model's 162-token sequences exceed the 96-token attention kernels")
+        if not sequential and n_token > 96 and self_precision_f32():
+            raise NotImplementedError("HIP CDM: the joint model's sequences past 96 tokens need the split-bf16 "
+                                      "(x3) attention kernels (GHM_PRECISION=f32 is set)")
         if n_mlp_hidden != 4 * n_embd:
             raise NotImplementedError("HIP CDM: n_mlp_hidden = 4 * n_embd")
         # construction (RNG) order of the reference, model.py:382-402
@@ -209,16 +237,22 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
             self._plans.clear()
             self._plans[key] = CdmPlan(self.n_layer, T, T_img, n_seq, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
-                                       precision=self.precision)
+                                       precision=self.precision, joint=not self.sequential)
         return self._plans[key]
 
     def forward(self, xt, zi):
-        """xt: conditioning features [B, T1, num_class] (the frozen CLIP text
-        embedding, unsqueezed); zi: noisy image observations [B, T2] (float).
+        """sequential: xt = conditioning features [B, T1, num_class] (the frozen CLIP
+        text embedding, unsqueezed); joint (sequential=False): xt = text leaves
+        [B, T1] (token ids).  zi: noisy image observations [B, T2] (float).
         Returns (denoised predictions [B, T2], guided layers [[], []])."""
         require_hip(zi)
         B, T2 = zi.shape
-        if xt.dim() != 3 or xt.shape[0] != B or xt.shape[2] != self.vocab_size:
+        if not self.sequential:
+            if xt.dim() != 2 or xt.shape[0] != B:
+                raise ValueError(f"expected text leaves of shape [{B}, T1], got {tuple(xt.shape)}")
+            if xt.numel() and (int(xt.min()) < 0 or int(xt.max()) >= self.vocab_size):
+                raise IndexError("token id out of range")
+        elif xt.dim() != 3 or xt.shape[0] != B or xt.shape[2] != self.vocab_size:
             raise ValueError(f"expected xt of shape [{B}, T1, {self.vocab_size}], got {tuple(xt.shape)}")
         if T2 != self.n_i_token or xt.shape[1] + T2 != self.n_token:
             raise ValueError(f"expected {self.n_i_token} image + {self.n_token - self.n_i_token} conditioning tokens")

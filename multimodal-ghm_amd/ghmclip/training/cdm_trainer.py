@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from ..models.cdm import CDM_UNTRAINED, CdmPlan
+from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
@@ -36,9 +36,14 @@ class CdmTrainer:
     def __init__(self, model, clip_model, batch_size, lr_schedule, t_templ, i_templ, sigma=1.0, max_norm=1.0,
                  weight_decay=0.001, betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
                  precision=None):
-        """model: ConditionalDenoiseEncoderTransformer (sequential); clip_model: the
-        frozen CLIP text EncoderTransformer; lr_schedule: one learning rate per step;
-        t_templ / i_templ: the sampler's transition templates [L][C][V][V]."""
+        """model: ConditionalDenoiseEncoderTransformer; clip_model: the frozen CLIP
+        text EncoderTransformer (sequential model), or None for the joint model
+        (sequential=False, train_CDNS.py: the text leaves go through t_embedding);
+        lr_schedule: one learning rate per step; t_templ / i_templ: the sampler's
+        transition templates [L][C][V][V]."""
+        self.joint = clip_model is None
+        if self.joint == bool(model.sequential):
+            raise ValueError("a sequential model needs its frozen CLIP text encoder; the joint model takes none")
         self.device = torch.device(device)
         self.model, self.clip = model, clip_model
         self.B = batch_size
@@ -47,9 +52,10 @@ class CdmTrainer:
         self.sigma = float(sigma)
         self.names = list(model._names)
         sd = dict(model.named_parameters())
-        for p in list(sd.values()) + list(clip_model.parameters()):
+        untrained = CDM_JOINT_UNTRAINED if self.joint else CDM_UNTRAINED
+        for p in list(sd.values()) + ([] if self.joint else list(clip_model.parameters())):
             require_hip(p)
-        trained = [n for n in self.names if n not in CDM_UNTRAINED]
+        trained = [n for n in self.names if n not in untrained]
         n = sum(sd[k].numel() for k in trained)
         self.n_params = n
         self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
@@ -69,23 +75,31 @@ class CdmTrainer:
                 self.md[k] = self.mflat[off:off + c].view(p.shape)
                 self.vd[k] = self.vflat[off:off + c].view(p.shape)
                 off += c
-            for k in CDM_UNTRAINED:
+            for k in untrained:
                 self.pd[k] = sd[k].data
-        self.clip_p = {k: v.data for k, v in clip_model.named_parameters()}
+        self.clip_p = None if self.joint else {k: v.data for k, v in clip_model.named_parameters()}
         T, Ti = model.n_token, model.n_i_token
         self.T, self.Ti = T, Ti
         self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,
-                            normalize_attn=model.normalize_attn, device=self.device, precision=precision)
+                            normalize_attn=model.normalize_attn, device=self.device, precision=precision,
+                            joint=self.joint)
         self.precision = self.plan.precision
-        self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
-                                     num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
-                                     n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
-                                     device=self.device, precision=self.precision)
-        if self.precision == "x3":
-            self.clip_plan.split_weights(self.clip_p)  # frozen: split once
+        if self.joint:
+            self.clip_plan = None
+            self.t_tok = self.plan.tok  # text leaves [B, T - T_img], read by the embedding and BP
+            n_text = T - Ti
+        else:
+            self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+                                         num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
+                                         n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
+                                         device=self.device, precision=self.precision)
+            if self.precision == "x3":
+                self.clip_plan.split_weights(self.clip_p)  # frozen: split once
+            self.t_tok = self.clip_plan.tokens
+            n_text = clip_model.n_token
         t_templ = np.ascontiguousarray(t_templ, dtype=np.float64)
         i_templ = np.ascontiguousarray(i_templ, dtype=np.float64)
-        if i_templ.shape[1] ** i_templ.shape[0] != Ti or t_templ.shape[1] ** t_templ.shape[0] != clip_model.n_token:
+        if i_templ.shape[1] ** i_templ.shape[0] != Ti or t_templ.shape[1] ** t_templ.shape[0] != n_text:
             raise ValueError("transition templates do not match the token counts")
         self.tree = (t_templ.shape[0], t_templ.shape[1], i_templ.shape[0], i_templ.shape[1], t_templ.shape[2])
         self.t_trans = torch.from_numpy(t_templ).to(self.device)
@@ -122,13 +136,13 @@ class CdmTrainer:
         Lt, Ct, Li, Ci, V = self.tree
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.clip_plan.tokens), _p(self.z64),
+            _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
                          self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V,
                          ctypes.c_void_p(side.cuda_stream))
-        emb = self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_DNS.py:141
+        emb = None if self.joint else self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_DNS.py:141
         main.wait_stream(side)
         s = ctypes.c_void_p(main.cuda_stream)
-        self.plan.forward(self.pd, self.z32, emb, emb.shape[1])
+        self.plan.forward(self.pd, self.z32, emb, 0 if emb is None else emb.shape[1])
         _native.call("ghm_ls_loss", _p(self.plan.pred), _p(self.i_tok), _p(self.post), _p(self.plan.dpred),
                      _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.Ti, s)
         self.plan.backward(self.pd, self.gd)
@@ -148,7 +162,7 @@ class CdmTrainer:
     def set_batch(self, t_tokens, i_tokens, z):
         """Stage one batch: text / image leaves uint8 [B, 81] and the noisy image
         observations z float64 [B, 81] (host-pinned or device), async."""
-        self.clip_plan.tokens.copy_(t_tokens, non_blocking=True)
+        self.t_tok.copy_(t_tokens, non_blocking=True)
         self.i_tok.copy_(i_tokens, non_blocking=True)
         self.z64.copy_(z, non_blocking=True)
 

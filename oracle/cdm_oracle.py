@@ -14,7 +14,8 @@ Reference file:line it follows (relative to src/ghmclip/):
   sampler    data/data_random_GHM.py:641-658 (DoubleSampler), :854-884
              (ConditionalDenoiseSampler.get_batch), :886-894 (get_Bayes)
   BP         data/data_random_GHM.py:185-215 (BP_CLS root message), :467-523 (BP_DNS)
-  model      models/model.py:337-532 (ConditionalDenoiseEncoderTransformer, sequential=True)
+  model      models/model.py:337-532 (ConditionalDenoiseEncoderTransformer, sequential=True;
+             sequential=False for the joint model of train_CDNS.py)
   loss       models/model.py:989-1041 (ConditionalGuidedLsLoss, guide=False), :1152-1160 (LsLoss)
   loop       training/train_sequential_DNS.py:62-168
 """
@@ -103,9 +104,10 @@ class OracleCdm(nn.Module):
     the (then empty) ModuleLists, t_embedding, per layer q, k, v, ln1, mlp, ln2,
     then _read_out Linear(d -> 1) and the unused _out Linear(n_token -> 1)."""
 
-    def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512):
+    def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512, sequential=True):
         super().__init__()
         self.V, self.n_i_token, self.n_embd = num_class, n_i_token, n_embd
+        self.sequential = sequential
         self.position_embeddings = nn.Embedding(n_token, n_embd)
         self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         self._mlps, self._lns_1, self._lns_2 = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -122,13 +124,17 @@ class OracleCdm(nn.Module):
         self._out = nn.Linear(n_token, 1)
 
     def forward(self, xt, zi):
-        """xt: CLIP text features [B, T1, V]; zi: noisy image observations [B, T2]."""
+        """xt: CLIP text features [B, T1, V] (sequential) or text leaves [B, T1] (joint,
+        sequential=False); zi: noisy image observations [B, T2]."""
         B, T2 = zi.shape
         T1 = xt.shape[1]
         emb = torch.zeros(B, T1 + T2, self.n_embd)
         opts = torch.arange(0, self.V).unsqueeze(0).unsqueeze(0).expand(B, T2, self.V)
         emb[:, :T2, :self.V] = -torch.pow(opts - zi.unsqueeze(-1), 2) / 2  # :412-416
-        emb[:, T2:, :] = torch.cat([xt, torch.zeros(B, T1, self.n_embd - self.V)], dim=2)  # :418-423
+        if self.sequential:
+            emb[:, T2:, :] = torch.cat([xt, torch.zeros(B, T1, self.n_embd - self.V)], dim=2)  # :418-421
+        else:
+            emb[:, T2:, :] = self.t_embedding(xt)  # :422-423
         pos = torch.arange(T1 + T2).expand(B, T1 + T2)
         H = emb + self.position_embeddings(pos)  # :437
         for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
@@ -176,6 +182,47 @@ class OracleCdmTrainer:
             feat = self.clip(torch.as_tensor(t_l, dtype=torch.long))[0].unsqueeze(1)
         self.last_feat = feat
         pred = self.model(feat, torch.as_tensor(z, dtype=torch.float32))
+        self.last_pred = pred.detach()
+        target = torch.as_tensor(np.asarray(i_l), dtype=torch.long)
+        loss = ls_loss(pred, target)
+        loss.backward()
+        with torch.no_grad():
+            cmp = ls_loss(pred, torch.tensor(np.asarray(post), dtype=torch.float32))
+        with_grad = [p for p in self.params if p.grad is not None]
+        torch.nn.utils.clip_grad_norm_(with_grad, self.max_norm, norm_type=2)
+        self.opt.set_lr(lr_cosine(self.it, *self.sched))
+        self.opt.step()
+        self.it += 1
+        return float(loss.item()), float(loss.item()), float(cmp.item())
+
+
+class OracleCdmJointTrainer:
+    """train_CDNS.py:60-150 (raw=True, guide=False): the joint model
+    (sequential=False, T = 162: the 81 text leaves through t_embedding), no CLIP.
+    RNG order: sampler (seedtree) -> [get_Bayes, unseeded, skipped] ->
+    seed_everything(seed) -> model -> loop."""
+
+    def __init__(self, p=0.2, B=128, L=9, d=128, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
+                 max_norm=1.0, seed=224, seedtree=42, sigma=1.0, n_layer_tree=4, n_child=3):
+        self.sampler = CdmSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], sigma=sigma, seedtree=seedtree)
+        seed_everything(seed)  # :74
+        T = n_child ** n_layer_tree
+        self.model = OracleCdm(2 * T, T, 10, d, L, 4 * d, sequential=False)
+        self.params = list(self.model.parameters())
+        self.opt = OracleAdamW(self.params)
+        self.B = B
+        self.sched = (lr_max, lr_min, warmup, total_iters)
+        self.max_norm = max_norm
+        self.it = 0
+
+    def step(self, batch=None):
+        """Returns (ploss, loss, compare)."""
+        for p in self.params:
+            p.grad = None
+        if batch is None:
+            batch = self.sampler.get_batch(self.B)
+        t_l, _, z, i_l, post = batch[:5]
+        pred = self.model(torch.as_tensor(np.asarray(t_l), dtype=torch.long), torch.as_tensor(z, dtype=torch.float32))
         self.last_pred = pred.detach()
         target = torch.as_tensor(np.asarray(i_l), dtype=torch.long)
         loss = ls_loss(pred, target)

@@ -114,6 +114,28 @@ def test_oracle_two_steps_match_reference():
         np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-12, atol=1e-12)
 
 
+def test_joint_oracle_two_steps_match_reference():
+    """Joint model (train_CDNS.py, sequential=False, T = 162), two full training steps
+    at L=1, B=4 (cdm_joint_tiny.npz): initial weights, predictions, losses, compare
+    and post-step parameters."""
+    g = _fix("cdm_joint_tiny.npz")
+    tr = CO.OracleCdmJointTrainer(B=4, L=1)
+    assert [n for n, _ in tr.model.named_parameters()] == list(g["param_names"])
+    st = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+    np.testing.assert_array_equal(st, g["init_stats"])
+    for k in range(2):
+        batch = (g[f"t_leaves{k}"], None, g[f"z{k}"], g[f"i_leaves{k}"], g[f"post{k}"])
+        drawn = tr.sampler.get_batch(tr.B)
+        np.testing.assert_array_equal(np.asarray(drawn[0]), g[f"t_leaves{k}"])
+        np.testing.assert_array_equal(np.asarray(drawn[2], dtype=np.float32), g[f"z{k}"])
+        ploss, loss, cmp = tr.step(batch=batch)
+        assert abs(ploss - float(g[f"ploss{k}"])) <= 1e-6 * ploss
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-6 * cmp
+        np.testing.assert_allclose(tr.last_pred.numpy(), g[f"pred{k}"], rtol=1e-5, atol=1e-5)
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-6, atol=1e-9)
+
+
 @pytest.mark.slow
 def test_oracle_curve_head_matches_reference():
     """First 5 steps of the default CDM config (cdm_curve.npz)."""
@@ -138,8 +160,15 @@ def test_cdm_module_api_matches_reference_construction():
     assert list(m.state_dict().keys()) == list(o.state_dict().keys()) == cdm_param_names(3)
     for (k, a), (_, b) in zip(m.state_dict().items(), o.state_dict().items()):
         assert torch.equal(a, b), k
+    # the joint model (sequential=False, train_CDNS.py) is built too, same construction
+    torch.manual_seed(3)
+    mj = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, [4, 4], 4, 512, sequential=False)
+    torch.manual_seed(3)
+    oj = CO.OracleCdm(162, 81, 10, 128, 3, 512, sequential=False)
+    for (k, a), (_, b) in zip(mj.state_dict().items(), oj.state_dict().items()):
+        assert torch.equal(a, b), k
     with pytest.raises(NotImplementedError):
-        ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, sequential=False)
+        ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, sequential=False, guide=True)
     with pytest.raises(RuntimeError):
         m(torch.zeros(2, 1, 10), torch.zeros(2, 81))  # CPU tensors: no fallback
 

@@ -1,0 +1,154 @@
+"""Joint CDM (train_CDNS.py, exp_cdm_jointtrain.sh: sequential=False, the 81 text
+leaves through t_embedding, T = 162) on the HIP path vs the CPU oracle and the
+reference's own fixtures (tests/golden/make_golden_cdm_joint.py).
+
+Sequences past 96 tokens run on the split-bf16 attention only, so every test is
+x3.  Tolerances as tests/test_gpu_cdm.py for x3: forward 1e-4 and gradients 5e-4
+relative to the tensor's max-abs; losses 1e-4 relative."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import cdm_oracle as CO
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+P_Y = np.ones(10) / 10
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = max(b.abs().max().item(), 1e-12)
+    return (a - b).abs().max().item() / scale
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from ghmclip import _native
+    assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
+
+
+@pytest.mark.parametrize("B", [3, 8])
+def test_joint_cdm_module_forward_backward(B):
+    """ConditionalDenoiseEncoderTransformer(sequential=False) forward and every
+    parameter gradient (t_embedding included) vs the oracle restatement."""
+    from ghmclip import ConditionalDenoiseEncoderTransformer
+    torch.manual_seed(11)
+    prod = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 2, [4, 4], 4, 512, sequential=False)
+    torch.manual_seed(11)
+    ref = CO.OracleCdm(162, 81, 10, 128, 2, 512, sequential=False)
+    g = torch.Generator().manual_seed(B)
+    with torch.no_grad():
+        for (kp, vp), (_, vr) in zip(prod.named_parameters(), ref.named_parameters()):
+            assert torch.equal(vp, vr), kp
+            if "_lns_" in kp or kp.endswith("bias"):
+                d = 0.1 * torch.randn(vp.shape, generator=g)
+                vp.add_(d)
+                vr.add_(d)
+    prod.precision = "x3"
+    prod = prod.to(DEV)
+    xt = torch.randint(0, 10, (B, 81), generator=g)
+    z = torch.randint(0, 10, (B, 81), generator=g).float() + torch.randn(B, 81, generator=g)
+    R = torch.randn(B, 81, generator=g)
+    pred, gl = prod(xt.to(DEV), z.to(DEV))
+    assert gl == [[], []]
+    (pred * R.to(DEV)).sum().backward()
+    want = ref(xt, z)
+    (want * R).sum().backward()
+    torch.cuda.synchronize()
+    assert _rel(pred, want) < 1e-4
+    for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
+        if pr.grad is None:
+            assert pp.grad is None, k
+            continue
+        assert _rel(pp.grad, pr.grad) < 5e-4, k
+
+
+def _trainer(L, B, total_iters=30000):
+    """train_CDNS.py order: sampler (seedtree 42), seed_everything(224), the model."""
+    from ghmclip import (ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, get_lr_cosine_schedule,
+                         seed_everything)
+    from ghmclip.training.cdm_trainer import CdmTrainer
+    s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1)
+    seed_everything(224)
+    model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False).to(DEV)
+    sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, total_iters) for k in range(total_iters + 1)]
+    tr = CdmTrainer(model, None, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision="x3")
+    return s, tr
+
+
+def _run(s, tr, B, steps, graph_after=None):
+    for k in range(steps):
+        tl, _, z, il = s.draw_numpy(B)
+        tr.set_batch(torch.from_numpy(tl), torch.from_numpy(il), torch.from_numpy(z))
+        tr.step()
+        if graph_after is not None and k + 1 == graph_after:
+            tr.capture()
+    torch.cuda.synchronize()
+    return tr.loss_history(), tr.compare_history()
+
+
+def test_joint_cdm_steps_vs_reference_fixture():
+    """Two fused steps (L=1, B=4) against the reference's numbers (cdm_joint_tiny.npz):
+    initial weights, loss, compare."""
+    f = np.load(os.path.join(GOLDEN, "cdm_joint_tiny.npz"))
+    s, tr = _trainer(1, 4)
+    for (n, p), want in zip(tr.model.named_parameters(), f["init_stats"]):
+        assert abs((p.double() ** 2).sum().item() - want[1]) <= 1e-12 * want[1] + 1e-12, n
+    hist, chist = _run(s, tr, 4, 2)
+    for k in range(2):
+        assert abs(hist[k] - float(f[f"ploss{k}"])) <= 1e-4 * float(f[f"ploss{k}"]), (k, hist[k])
+        assert abs(chist[k] - float(f[f"compare{k}"])) <= 1e-4 * float(f[f"compare{k}"]), (k, chist[k])
+
+
+def test_joint_cdm_steps_vs_oracle():
+    """Fused joint step == the oracle's step on identical draws: predictions and the
+    unclipped gradients (clip coefficient hyper[1]), t_embedding included."""
+    s, tr = _trainer(2, 6)
+    ref = CO.OracleCdmJointTrainer(B=6, L=2)
+    rparams = dict(ref.model.named_parameters())
+    for it in range(2):
+        tl, root, z, il = s.draw_numpy(6)
+        tr.set_batch(torch.from_numpy(tl), torch.from_numpy(il), torch.from_numpy(z))
+        tr.step()
+        _, post = s.posterior(tl, z)
+        ploss, _, cmp = ref.step(batch=(tl.astype(np.int64), root, z.astype(np.float32), il.astype(np.int64), post))
+        torch.cuda.synchronize()
+        assert abs(tr.loss_history()[it] - ploss) <= 1e-4 * ploss
+        assert abs(tr.compare_history()[it] - cmp) <= 1e-4 * cmp
+        assert _rel(tr.plan.pred, ref.last_pred) < 1e-4
+        coef = tr.hyper[1].item()
+        for n, p in tr.model.named_parameters():
+            if n in tr.gd:
+                assert _rel(p.grad * coef, rparams[n].grad) < 5e-4, n
+        assert "t_embedding.weight" in tr.gd
+
+
+def test_joint_cdm_graph_replay_matches_eager():
+    s1, t1 = _trainer(1, 4)
+    h1 = _run(s1, t1, 4, 5)
+    s2, t2 = _trainer(1, 4)
+    h2 = _run(s2, t2, 4, 5, graph_after=2)
+    np.testing.assert_array_equal(h1[0], h2[0])
+    np.testing.assert_array_equal(h1[1], h2[1])
+
+
+def test_joint_cdm_default_config_curve_vs_reference():
+    """The default joint config (exp_cdm_jointtrain.sh: p=0.2, L=9, d=128, B=128,
+    lr 1e-3 -> 1e-6): loss and compare histories vs the reference PyTorch-CPU run."""
+    g = np.load(os.path.join(GOLDEN, "cdm_joint_curve.npz"))
+    n = len(g["loss"])
+    s, tr = _trainer(9, 128)
+    hist, chist = _run(s, tr, 128, n, graph_after=3)
+    dev = np.abs(hist - g["loss"]) / g["loss"]
+    cdev = np.abs(chist - g["compare"]) / g["compare"]
+    print(f"joint CDM curve (x3): {n} steps, max rel dloss {dev.max():.3e}, dcompare {cdev.max():.3e}, "
+          f"final {hist[-1]:.4f} vs {g['loss'][-1]:.4f}")
+    assert dev.max() <= 1e-3 and cdev.max() <= 1e-3
