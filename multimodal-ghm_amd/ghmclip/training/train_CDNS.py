@@ -1,0 +1,199 @@
+"""Joint conditional-denoising (CDM) training on MI355X — drop-in for
+``python -m ghmclip.training.train_CDNS`` (scripts/experiments/exp_cdm_jointtrain.sh:
+ConditionalDenoiseEncoderTransformer with sequential=False, the 81 text leaves
+through t_embedding next to the 81 noisy image leaves, T = 162).
+
+Same flags, run-folder naming ('JT_' models), RNG order, log line and
+checkpoint.pth keys as the reference (src/ghmclip/training/train_CDNS.py:17-180).
+The hot loop (:108-150) runs as the fused, HIP-graph-replayed CdmTrainer step in
+its joint mode: denoiser forward/backward on the 192-token split-bf16 attention,
+loss, Compare against the exact BP posterior (computed on the device), clip and
+AdamW; the native sampler runs in a producer thread.  Differences, by design:
+  * --device must be a HIP device; guide=True is not built (NotImplementedError);
+  * the split-bf16 (x3) matrix products are required (162-token sequences);
+  * wandb/s3fs are optional (skipped with a warning when not installed);
+  * with torchrun (WORLD_SIZE > 1) each rank takes a contiguous 1/world of the
+    samples of the SAME global batch and gradients are averaged with one RCCL
+    all-reduce (the loss is a mean over samples).
+"""
+import os
+import sys
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..data import ConditionalDenoiseSampler
+from ..models import (AdamW, ConditionalDenoiseEncoderTransformer, ConditionalGuidedLsLoss, get_lr_cosine_schedule,
+                      seed_everything)
+from ..utils import DoubleTreeConfig, GenLogger, ModelConfig, UtilConfig, logging
+from .cdm_trainer import CdmTrainer
+from .pipeline import CdmBatchPipeline
+from .train_CLIP import load_checkpoint
+
+
+@dataclass
+class TrainingConfig(UtilConfig, DoubleTreeConfig, ModelConfig):
+    """CLI configuration for joint conditional denoising (train_CDNS.py:17-22)."""
+    job_name: Optional[str] = field(default='CDNS')
+
+
+def parse(argv=None):
+    from transformers import HfArgumentParser
+    parser = HfArgumentParser(TrainingConfig)
+    if argv is None:
+        return parser.parse_args_into_dataclasses()[0]
+    return parser.parse_args_into_dataclasses(args=argv)[0]
+
+
+def run_names(c):
+    """Folder naming of train_CDNS.py:35-45 (joint models are 'JT_')."""
+    tree_folder = (f'K{c.K}_L{c.n_ttree_layer}C{c.n_ttree_child}p{int(c.p_ttree_flip*100)}'
+                   f'_L{c.n_itree_layer}C{c.n_itree_child}p{int(c.p_itree_flip*100)}sc{int(c.flip_scale*10)}')
+    model_name = f'L{c.n_model_layer}H{c.n_head}D{c.d_eb}'
+    model_name = ('GT_' if c.guide else 'JT_') + model_name
+    return tree_folder, model_name
+
+
+def main(argv=None):
+    c = parse(argv)
+    if c.guide:
+        raise NotImplementedError("guided joint CDM (guide=True) is not built on the HIP path yet")
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        device = torch.device("cuda", local)
+    else:
+        if not torch.cuda.is_available():
+            raise RuntimeError("ghmclip (MI355X build) needs a HIP device")
+        device = torch.device("cuda")
+        print(f"Using GPU: {torch.cuda.get_device_name(0)}")
+    if c.batch_size % ws:
+        raise ValueError(f"batch_size {c.batch_size} must be divisible by the world size {ws}")
+
+    d_tmodel = c.n_ttree_child ** c.n_ttree_layer
+    d_i_model = c.n_itree_child ** c.n_itree_layer
+    d_model = d_i_model + d_tmodel  # :32-34
+    tree_folder, model_name = run_names(c)
+    timestamp = time.strftime('%Y%m%d-%H%M%S', time.localtime())
+    directory = os.path.join("./logs", c.job_name, tree_folder, model_name, timestamp)
+    raw = c.raw or rank != 0
+    logger = GenLogger(directory, c, raw=raw)
+    checkpoint_path = os.path.join(directory, 'checkpoint.pth')
+    wandb = None
+    if not raw:
+        try:
+            import wandb as _wandb
+            wandb = _wandb
+            wandb.init(project=c.wandb_project, name=timestamp + '-' + model_name, tags=[c.job_name, tree_folder],
+                       dir=c.wandb_path)
+            wandb.config.update(asdict(c))
+        except ImportError:
+            logger.warning("wandb not installed: skipping wandb logging")
+
+    p_y = np.ones(c.variable_type) / c.variable_type
+    sampler = ConditionalDenoiseSampler([c.n_ttree_layer, c.n_itree_layer], [c.n_ttree_child, c.n_itree_child],
+                                        [p_y, p_y], [c.p_ttree_flip, c.p_itree_flip], sigma=c.sigma,
+                                        flip_scale=c.flip_scale, variable_type=c.variable_type,
+                                        translation_invariance=True, seedtree=42)  # :60-69
+    Bayes_loss, Bayes_std = sampler.get_Bayes(n_eval=10000)  # :70
+    Bayes_loss, Bayes_std = float(Bayes_loss), float(Bayes_std)
+    logger.info(f'Bayes Loss: {Bayes_loss}, Bayes Std: {Bayes_std}')
+    if wandb:
+        wandb.log({'Bayes_loss': Bayes_loss, 'Bayes_std': Bayes_std})
+
+    seed_everything(c.seed)  # :74, then the model (:75-90)
+    model = ConditionalDenoiseEncoderTransformer(n_token=d_model, n_i_token=d_i_model, num_class=c.variable_type,
+                                                 n_embd=c.d_eb, n_layer=c.n_model_layer,
+                                                 n_guided_layers=[c.n_ttree_layer, c.n_itree_layer],
+                                                 n_head=c.n_head, n_mlp_hidden=4 * c.d_eb, activation=c.activation,
+                                                 mlp=True, normalize_attn=c.normalize_attn, layernorm=c.layernorm,
+                                                 maxnorm=False, sequential=False, guide=c.guide).to(device)
+    loss = ConditionalGuidedLsLoss(penalty=c.penalty, guide=c.guide)
+    optimizer = AdamW(params=model.parameters(), lr=None)
+    ploss_history = np.zeros(c.total_iters)
+    loss_history = np.zeros(c.total_iters)
+    compare_history = np.zeros(c.total_iters)
+    t_offset = 0
+    if c.init_from != 'scratch':  # :132-138 (the reference restarts the loop at iteration 0)
+        ckm = load_checkpoint(c.init_from, device)
+        model.load_state_dict(ckm['model_state_dict'])
+        optimizer.load_state_dict(ckm['optimizer_state_dict'])
+        st = next(iter(optimizer.state.values()), None)
+        t_offset = int(st['t']) if st else 0  # AdamW's step count continues (optimizer.py:58-66)
+
+    sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters)
+             for i in range(c.total_iters)]
+    trainer = CdmTrainer(model, None, c.batch_size // ws, sched, sampler.t_templ, sampler.i_templ,
+                         sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset, precision="x3")
+    if t_offset:
+        trainer.load_optimizer_state(optimizer)
+    sampler.native.pull_numpy_state()  # the producer owns numpy's MT stream from here on
+    pipe = CdmBatchPipeline(sampler.native, c.batch_size, c.sigma, n_slots=3,
+                            row_slice=(rank, ws) if ws > 1 else None)
+
+    def sync_hist(upto):
+        h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
+        if ws > 1:
+            import torch.distributed as dist
+            t = torch.from_numpy(np.stack([h, ch])).to(device)
+            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+            h, ch = t.cpu().numpy()
+        loss_history[:upto] = h
+        ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
+        compare_history[:upto] = ch
+
+    def save(iter_num):
+        trainer.fill_optimizer_state(optimizer)
+        torch.save({'model_state_dict': model.state_dict(), 'optimizer_state_dict': optimizer.state_dict(),
+                    'loss': {'type': type(loss).__name__, 'penalty': loss.penalty, 'guide': loss.guide},
+                    'iter': iter_num, 'loss_history': loss_history, 'ploss_history': ploss_history,
+                    'bayes': Bayes_loss}, checkpoint_path)
+
+    curr_time = time.time()
+    try:
+        for iter_num in range(c.total_iters):
+            pipe.next_into(trainer)
+            trainer.step()
+            if iter_num == 1:
+                trainer.capture()
+            lr = sched[iter_num]
+            if iter_num > 0 and iter_num % c.log_interval == 0:
+                sync_hist(iter_num + 1)
+                finish_time = time.time()
+                h = iter_num // 2
+                logger.info(f'Iter: {iter_num},Penalty train loss: {np.mean(ploss_history[h:iter_num]):.4f}, '
+                            f'Train loss: {np.mean(loss_history[h:iter_num]):.4f}, '
+                            f'Compare: {np.mean(compare_history[h:iter_num]):.4f},  Bayes:{Bayes_loss:.4f}, '
+                            f'LR: {lr:.6f}, Time: {(finish_time - curr_time):.2f}s')  # :128
+                if wandb:
+                    wandb.log({'train_loss': loss_history[iter_num], 'penalty_train_loss': ploss_history[iter_num],
+                               'Compare': compare_history[iter_num], 'lr': lr, 'Bayes_loss': Bayes_loss,
+                               'Bayes_std': Bayes_std, 'iter': iter_num})
+            if iter_num % c.eval_interval == 0 and not raw:
+                sync_hist(iter_num + 1)
+                save(iter_num)
+    finally:
+        pipe.close()
+    sync_hist(c.total_iters)
+    logging.shutdown()
+    if not raw:
+        save(c.total_iters)
+    if c.S3_upload and rank == 0:
+        import s3fs
+        s3fs.S3FileSystem().put(directory, c.S3_bucket_name + f'/GHM/{c.job_name}/{tree_folder}/{model_name}/{timestamp}',
+                                recursive=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return loss_history, compare_history
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
