@@ -269,6 +269,13 @@ int ghm_cdm_readout_bwd(const float* H, const float* w_ro, const float* dpred, f
  * onehot (may be NULL) [M][V] = the text tokens' one-hot rows (0 on prefix rows). */
 int ghm_vlm_embed_fwd(const uint8_t* xt, const float* feat, const float* tok_w, const float* pos_w, float* H0,
                       float* onehot, int64_t n_seq, int T, int P, int V, int D, void* stream);
+/* Joint VLM (train_NWP.py, sequential=False, model.py:221-232): prefix (image) token
+ * t < P gets i_w[it[n, t]] (it uint8 [n_seq][P]), text token t >= P gets
+ * tok_w[xt[n, t - P]]; onehot_t / onehot_i (may be NULL) [M][V] one-hot rows of the
+ * text / image tokens (0 on the other kind). */
+int ghm_vlm_embed_joint_fwd(const uint8_t* xt, const uint8_t* it, const float* i_w, const float* tok_w,
+                            const float* pos_w, float* H0, float* onehot_t, float* onehot_i, int64_t n_seq, int T,
+                            int P, int V, int D, void* stream);
 /* Row LayerNorm Y = LN(X) (nn.LayerNorm(D), biased variance), stats [M] (mean, rstd);
  * D in {128, 256, 512}. */
 int ghm_ln_rows_fwd(const float* X, const float* w, const float* b, float* Y, float* stats, int64_t M, int D,
@@ -315,9 +322,9 @@ int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, f
 
 /* General form of the two above: prefix-causal mask with n_prefix (n_prefix = T: no
  * mask), H_mid = (H + o) + o * dbl (dbl = 1/D: the VLM's double residual; 0: the
- * plain residual of the CLIP / CDM encoders, model.py:391-394, 474-478).  D = 128
- * takes T <= 192 (P, dS [n_seq][192][192] when T > 96, else [n_seq][96][96]);
- * D = 256 takes T <= 96.  The joint CDM (train_CDNS.py, T = 162) runs on it. */
+ * plain residual of the CLIP / CDM encoders, model.py:391-394, 474-478).  D in
+ * {128, 256}, T <= 192 (P, dS [n_seq][192][192] when T > 96, else [n_seq][96][96]).
+ * The joint CDM (train_CDNS.py, T = 162) and joint VLM (train_NWP.py, T = 161) run on it. */
 int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T, int D,
                         int n_prefix, float scale_div, float dbl, void* stream);
 int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,

@@ -55,6 +55,38 @@ __global__ __launch_bounds__(256) void k_vlm_embed_fwd(const uint8_t* __restrict
   }
 }
 
+// Joint VLM embedding (AutoRegressiveTransformer, sequential=False, model.py:221-232):
+// prefix (image) token t < P gets i_w[it[n, t]], text token t >= P gets
+// tok_w[xt[n, t - P]]; + positions.  onehot_t / onehot_i (may be NULL) [M][V]: the
+// text / image tokens' one-hot rows (0 on the other kind), for the two embedding
+// gradients.
+__global__ __launch_bounds__(256) void k_vlm_embed_joint_fwd(const uint8_t* __restrict__ xt,
+                                                             const uint8_t* __restrict__ it,
+                                                             const float* __restrict__ i_w,
+                                                             const float* __restrict__ tok_w,
+                                                             const float* __restrict__ pos, float* __restrict__ H0,
+                                                             float* __restrict__ onehot_t,
+                                                             float* __restrict__ onehot_i, int64_t n_tok, int T,
+                                                             int P, int V, int D) {
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int D4 = D / 4;
+  if (idx >= n_tok * D4) return;
+  const int q = static_cast<int>(idx % D4);
+  const int64_t m = idx / D4;
+  const int64_t n = m / T;
+  const int t = static_cast<int>(m % T);
+  const float4 p = *reinterpret_cast<const float4*>(pos + static_cast<int64_t>(t) * D + 4 * q);
+  const bool pre = t < P;
+  int x = pre ? it[n * P + t] : xt[n * (T - P) + (t - P)];
+  x = x < V ? x : V - 1;
+  const float4 w = *reinterpret_cast<const float4*>((pre ? i_w : tok_w) + static_cast<int64_t>(x) * D + 4 * q);
+  st4(H0 + m * D + 4 * q, w.x + p.x, w.y + p.y, w.z + p.z, w.w + p.w);
+  if (q < V) {
+    if (onehot_t) onehot_t[m * V + q] = (!pre && x == q) ? 1.f : 0.f;
+    if (onehot_i) onehot_i[m * V + q] = (pre && x == q) ? 1.f : 0.f;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Row LayerNorm, one wave per row (D = 64 * R), two-pass statistics like
 // nn.LayerNorm (biased variance, eps inside the sqrt).
@@ -479,6 +511,17 @@ extern "C" int ghm_vlm_embed_fwd(const uint8_t* xt, const float* feat, const flo
   const int64_t n = n_seq * T * (D / 4);
   hipLaunchKernelGGL(k_vlm_embed_fwd, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, ghm_stream(stream),
                      xt, feat, tok_w, pos_w, H0, onehot, n_seq * T, T, P, V, D);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_vlm_embed_joint_fwd(const uint8_t* xt, const uint8_t* it, const float* i_w, const float* tok_w,
+                                       const float* pos_w, float* H0, float* onehot_t, float* onehot_i, int64_t n_seq,
+                                       int T, int P, int V, int D, void* stream) {
+  GHM_CHECK(xt && it && i_w && tok_w && pos_w && H0, "null pointer");
+  GHM_CHECK(n_seq >= 1 && T > P && P >= 1 && V >= 1 && D % 4 == 0 && D >= 4 * V, "shape");
+  const int64_t n = n_seq * T * (D / 4);
+  hipLaunchKernelGGL(k_vlm_embed_joint_fwd, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     ghm_stream(stream), xt, it, i_w, tok_w, pos_w, H0, onehot_t, onehot_i, n_seq * T, T, P, V, D);
   return ghm_launch_status();
 }
 

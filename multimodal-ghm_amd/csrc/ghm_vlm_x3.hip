@@ -417,7 +417,7 @@ void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<2, DD>), dim3(g), dim3(128), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
   else if (T <= 96)
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<3, DD>), dim3(g), dim3(192), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if constexpr (DD == 128) {
+  else {  // T > 96 (D = 256 at NKT = 6 spills 5-12 VGPRs: correct, slower)
     if (T <= 128)
       hipLaunchKernelGGL((k_vlm_attn_fwd_x3<4, DD>), dim3(g), dim3(256), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
     else if (T <= 160)
@@ -441,7 +441,7 @@ void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
   if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
   else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
   else if (T <= 96) launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  else if constexpr (DD == 128) {
+  else {  // T > 96 (D = 256 at NKT = 6 spills 5-12 VGPRs: correct, slower)
     if (T <= 128) launch_bwd_n<4, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
     else if (T <= 160) launch_bwd_n<5, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
     else launch_bwd_n<6, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
@@ -469,7 +469,7 @@ extern "C" int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float
 extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                                    int D, int n_prefix, float scale_div, float dbl, void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
-  GHM_CHECK((D == 128 && T >= 1 && T <= 192) || (D == 256 && T >= 1 && T <= 96), "shape (D 128: T <= 192; D 256: T <= 96)");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
   if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
@@ -480,7 +480,7 @@ extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mi
 extern "C" int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                                    int64_t n_seq, int T, int D, float scale_div, float dbl, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
-  GHM_CHECK((D == 128 && T >= 1 && T <= 192) || (D == 256 && T >= 1 && T <= 96), "shape (D 128: T <= 192; D 256: T <= 96)");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1, "n_seq >= 1");
   const unsigned g = static_cast<unsigned>(n_seq);
   if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);

@@ -63,6 +63,7 @@ HIP_SIGNATURES = {
     "ghm_ls_loss": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_cdm_readout_bwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_vlm_embed_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
+    "ghm_vlm_embed_joint_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
     "ghm_ln_rows_fwd": [_p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_ln_rows_blocks": [_i64],
     "ghm_ln_rows_bwd": [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],

@@ -34,11 +34,13 @@ from .. import _native
 from .hip_encoder import PRECISIONS, default_precision, require_hip
 
 __all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names",
-           "VLM_UNTRAINED"]
+           "VLM_UNTRAINED", "VLM_JOINT_UNTRAINED"]
 
 # never given a gradient by the reference in sequential mode (the image prefix is a
 # frozen CLIP feature, _out is unused): AdamW and clip_grad_norm_ skip them
 VLM_UNTRAINED = ("i_embedding.weight", "_out.weight", "_out.bias")
+# joint model (sequential=False, train_NWP.py): the image leaves go through i_embedding
+VLM_JOINT_UNTRAINED = ("_out.weight", "_out.bias")
 
 
 def vlm_param_names(n_layer):
@@ -81,9 +83,7 @@ EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
 
 class VlmPlan:
     def __init__(self, n_layer, n_token, n_seq, n_prefix=1, num_class=10, n_embd=256, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None):
-        if n_token > 96:
-            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens (got {n_token})")
+                 normalize_attn=True, device="cuda", precision=None, joint=False):
         if n_embd not in (128, 256, 512):
             raise ValueError(f"the HIP VLM kernels take n_embd in (128, 256, 512) (got {n_embd})")
         self.L, self.T, self.N, self.P, self.V, self.D = n_layer, n_token, n_seq, n_prefix, num_class, n_embd
@@ -97,12 +97,20 @@ class VlmPlan:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         if self.precision == "x3" and n_embd not in (128, 256):
             raise ValueError(f"the split-bf16 VLM kernels take n_embd in (128, 256) (got {n_embd})")
+        if n_token > 192 or (n_token > 96 and self.precision != "x3"):
+            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens, <= 192 with the split-bf16 "
+                             f"(x3) kernels (got {n_token}, precision {self.precision})")
+        # joint model (sequential=False): image prefix tokens through i_embedding;
+        # sequences past 96 tokens (161) run on ghm_attn_ext_*_x3 with P / dS padded to 192
+        self.joint = joint
+        self.long_attn = n_token > 96
+        pad = 192 if self.long_attn else 96
         L, D, F, N = n_layer, n_embd, self.F, n_seq
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         self.H = e(L + 1, M, D)
         self.Hmid, self.X1, self.X2 = e(L, M, D), e(L, M, D), e(L, M, D)
         self.G, self.Dg = e(L, M, F), e(L, M, F)
-        self.Pm = torch.zeros(L, N, 96, 96, dtype=torch.float32, device=self.device)
+        self.Pm = torch.zeros(L, N, pad, pad, dtype=torch.float32, device=self.device)
         self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
         self.logits, self.dlogits = e(M, num_class), e(M, num_class)
         self.onehot = e(M, num_class)
@@ -113,7 +121,7 @@ class VlmPlan:
             # fused projections: q | k | v columns of one [M][3D] buffer; split-k wgrad slabs
             self.qkv = e(L, M, 3 * D)
             self.dqkv = e(M, 3 * D)
-            self.dS = torch.zeros(N, 96, 96, dtype=torch.float32, device=self.device)
+            self.dS = torch.zeros(N, pad, pad, dtype=torch.float32, device=self.device)
             self.nsplit = max(1, min(32, M // 256))
             self.slab = e(self.nsplit * max(D * F, 3 * D * D))
             lib = _native.hip_lib()
@@ -126,6 +134,9 @@ class VlmPlan:
         self.nblk = int(_native.hip_lib().ghm_ln_rows_blocks(M))
         self.part_ln = e(self.nblk, 2, D)
         self.xt = torch.empty(N, n_token - n_prefix, dtype=torch.uint8, device=self.device)
+        if joint:
+            self.itok = torch.empty(N, n_prefix, dtype=torch.uint8, device=self.device)
+            self.onehot_i = e(M, num_class)
         self._gen = 0
 
     # ------------------------------------------------------------------
@@ -207,15 +218,20 @@ class VlmPlan:
         s = _stream()
         c = _native.call
         M, D, F, T, N = self.M, self.D, self.F, self.T, self.N
-        c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
-          _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
+        if self.joint:  # feat unused: self.itok holds the image leaves
+            c("ghm_vlm_embed_joint_fwd", _ptr(xt), _ptr(self.itok), _ptr(p["i_embedding.weight"]),
+              _ptr(p["t_embedding.weight"]), _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]),
+              _ptr(self.onehot), _ptr(self.onehot_i), N, T, self.P, self.V, D, s)
+        else:
+            c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
+              _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
         for l in range(self.L):
             c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
             _gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
-            c("ghm_vlm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T,
-              D, self.P, self.scale_div, s)
+            c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T,
+              D, self.P, self.scale_div, 1.0 / D, s)
             c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
             _gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
@@ -254,8 +270,8 @@ class VlmPlan:
               _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 2, l, s)
             # attention (nxt = dHmid) -> dq | dk | dv
-            c("ghm_vlm_attn_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS), _ptr(self.dqkv),
-              self.N, self.T, D, self.scale_div, s)
+            c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS), _ptr(self.dqkv),
+              self.N, self.T, D, self.scale_div, 1.0 / D, s)
             self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D,
                         (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"]), D, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
@@ -265,6 +281,8 @@ class VlmPlan:
             self._reduce_ln(g, 1, l, s)
         self._colsum(cur, self.N, self.T * D, g["position_embeddings.weight"], s)  # sum over sequences
         torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
+        if self.joint:
+            torch.mm(self.onehot_i.t(), cur, out=g["i_embedding.weight"])
         return cur
 
     def _colsum(self, X, rows, cols, out, s):
@@ -289,8 +307,12 @@ class _VlmFn(torch.autograd.Function):
         plan = module._plan(N, T1 + zi.shape[1], zi.shape[1], xt.device)
         pd = dict(zip(module._names, params))
         plan.xt.copy_(xt.to(torch.uint8))
-        feat = zi.contiguous().float()
-        logits = plan.forward(pd, plan.xt, feat)
+        if plan.joint:  # zi: image leaves (token ids)
+            plan.itok.copy_(zi.to(torch.uint8))
+            logits = plan.forward(pd, plan.xt, None)
+        else:
+            feat = zi.contiguous().float()
+            logits = plan.forward(pd, plan.xt, feat)
         ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
         ctx.save_for_backward(*params)
         return logits.view(N, T1 + zi.shape[1], -1)[:, zi.shape[1]:, :].clone()
@@ -303,12 +325,13 @@ class _VlmFn(torch.autograd.Function):
                                "activations saved for backward")
         params = ctx.saved_tensors
         names = ctx.module._names
-        grads = {n: torch.empty_like(p) for n, p in zip(names, params) if n not in VLM_UNTRAINED}
+        untrained = VLM_JOINT_UNTRAINED if plan.joint else VLM_UNTRAINED
+        grads = {n: torch.empty_like(p) for n, p in zip(names, params) if n not in untrained}
         dz = torch.zeros(plan.N, plan.T, plan.V, dtype=torch.float32, device=dlog.device)
         dz[:, plan.P:, :] = dlog
         dH0 = plan.backward(dict(zip(names, params)), grads, dlogits=dz.view(plan.M, plan.V))
         d_zi = None
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[2] and not plan.joint:
             d_zi = dH0.view(plan.N, plan.T, plan.D)[:, :plan.P, :plan.V].clone()
         return (None, None, d_zi, *[grads.get(n) for n in names])
 
@@ -316,9 +339,11 @@ class _VlmFn(torch.autograd.Function):
 class AutoRegressiveTransformer(nn.Module):
     """Reference: models/model.py:132-335.  Same constructor, parameter creation order
     (so torch.manual_seed gives identical weights) and state_dict keys.  The HIP path
-    covers the configuration the VLM experiments train (exp_vlm_{standard,shallow}TF.sh):
-    a frozen-CLIP image feature prefix token, causal text, softmax attention,
-    LayerNorm, MLP, no guide; n_embd in (128, 256, 512)."""
+    covers the configurations the VLM experiments train: sequential
+    (exp_vlm_{standard,shallow}TF.sh: a frozen-CLIP image feature prefix token, T = 81)
+    and joint (exp_vlm_jointtrain.sh: the 81 image leaves through i_embedding as the
+    prefix, T = 161, split-bf16 only); prefix-causal mask, softmax attention,
+    LayerNorm, MLP, no guide; n_embd in (128, 256, 512) (joint: 128, 256)."""
 
     def __init__(self, n_token=9, n_i_token=4, num_class=10, n_embd=128, n_layer=12, n_guided_layers=(3, 3),
                  n_head=4, n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True,
@@ -345,10 +370,10 @@ class AutoRegressiveTransformer(nn.Module):
         self.guided_layer_gap = n_layer // (n_guided_layers[0] * 2 + 1)
         if activation != "softmax" or not mlp or not layernorm or guide:
             raise NotImplementedError("HIP VLM: softmax attention, mlp=True, layernorm=True, guide=False")
-        if not (sequential and auto_regressive and n_i_token == 1):
-            raise NotImplementedError("HIP VLM: sequential=True, auto_regressive=True, one prefix token "
-                                      "(train_sequential_NWP.py); the joint model's 161-token sequences "
-                                      "exceed the 96-token attention kernels")
+        if not auto_regressive or (sequential and n_i_token != 1):
+            raise NotImplementedError("HIP VLM: auto_regressive=True; sequential=True takes one prefix token "
+                                      "(train_sequential_NWP.py), sequential=False the image leaves "
+                                      "(train_NWP.py)")
         if n_mlp_hidden != 4 * n_embd:
             raise NotImplementedError("HIP VLM: n_mlp_hidden = 4 * n_embd")
         # construction (RNG) order of the reference, model.py:177-218
@@ -384,20 +409,26 @@ class AutoRegressiveTransformer(nn.Module):
             self._plans.clear()
             self._plans[key] = VlmPlan(self.n_layer, T, n_seq, n_prefix=P, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
-                                       precision=self.precision)
+                                       precision=self.precision, joint=not self.sequential)
         return self._plans[key]
 
     def forward(self, xt, zi):
         """xt: text tokens [B, T1] (long); zi: the frozen CLIP image feature [B, 1,
-        num_class].  Returns (next-token logits [B, T1, num_class], [[], []])."""
+        num_class] (sequential) or the image leaves [B, n_i_token] (long; joint,
+        sequential=False).  Returns (next-token logits [B, T1, num_class], [[], []])."""
         require_hip(xt)
         B, T1 = xt.shape
-        if zi.dim() != 3 or zi.shape[0] != B or zi.shape[1] != self.n_i_token or zi.shape[2] != self.vocab_size:
-            raise ValueError(f"expected zi of shape [{B}, {self.n_i_token}, {self.vocab_size}], got {tuple(zi.shape)}")
+        if self.sequential:
+            if zi.dim() != 3 or zi.shape[0] != B or zi.shape[1] != self.n_i_token or zi.shape[2] != self.vocab_size:
+                raise ValueError(f"expected zi of shape [{B}, {self.n_i_token}, {self.vocab_size}], "
+                                 f"got {tuple(zi.shape)}")
+        elif zi.dim() != 2 or zi.shape[0] != B or zi.shape[1] != self.n_i_token:
+            raise ValueError(f"expected image leaves of shape [{B}, {self.n_i_token}], got {tuple(zi.shape)}")
         if T1 + self.n_i_token != self.n_token:
             raise ValueError(f"expected {self.n_token - self.n_i_token} text tokens, got {T1}")
-        if xt.numel() and (int(xt.min()) < 0 or int(xt.max()) >= self.vocab_size):
-            raise IndexError("token id out of range")
+        for t in ((xt,) if self.sequential else (xt, zi)):
+            if t.numel() and (int(t.min()) < 0 or int(t.max()) >= self.vocab_size):
+                raise IndexError("token id out of range")
         sd = dict(self.named_parameters())
         params = [sd[n] for n in self._names]
         for prm in params:

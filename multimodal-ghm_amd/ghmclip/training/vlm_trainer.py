@@ -19,7 +19,7 @@ import torch
 from .. import _native
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
-from ..models.vlm import VLM_UNTRAINED, VlmPlan
+from ..models.vlm import VLM_JOINT_UNTRAINED, VLM_UNTRAINED, VlmPlan
 
 
 def _p(t):
@@ -29,19 +29,24 @@ def _p(t):
 class VlmTrainer:
     def __init__(self, model, clip_model, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
                  betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None, precision=None):
-        """model: AutoRegressiveTransformer (sequential); clip_model: the frozen CLIP
-        image EncoderTransformer; lr_schedule: one learning rate per step.
+        """model: AutoRegressiveTransformer; clip_model: the frozen CLIP image
+        EncoderTransformer (sequential model), or None for the joint model
+        (sequential=False, train_NWP.py); lr_schedule: one learning rate per step.
         precision: matrix-product mode ("x3" split-bf16 MFMA or "f32") of the VLM plan
         and the frozen CLIP encoder's kernels (default $GHM_PRECISION or "x3")."""
         self.device = torch.device(device)
         self.model, self.clip = model, clip_model
+        self.joint = clip_model is None  # train_NWP.py: image leaves through i_embedding, no CLIP
+        if self.joint == bool(model.sequential):
+            raise ValueError("a sequential model needs its frozen CLIP image encoder; the joint model takes none")
+        untrained = VLM_JOINT_UNTRAINED if self.joint else VLM_UNTRAINED
         self.B = batch_size
         self.max_norm = float(max_norm)
         self.pg = process_group
         sd = dict(model.named_parameters())
-        for p in list(sd.values()) + list(clip_model.parameters()):
+        for p in list(sd.values()) + ([] if self.joint else list(clip_model.parameters())):
             require_hip(p)
-        trained = [n for n in model._names if n not in VLM_UNTRAINED]
+        trained = [n for n in model._names if n not in untrained]
         n = sum(sd[k].numel() for k in trained)
         self.n_params = n
         self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
@@ -61,20 +66,24 @@ class VlmTrainer:
                 self.md[k] = self.mflat[off:off + c].view(p.shape)
                 self.vd[k] = self.vflat[off:off + c].view(p.shape)
                 off += c
-            for k in VLM_UNTRAINED:
+            for k in untrained:
                 self.pd[k] = sd[k].data
-        self.clip_p = {k: v.data for k, v in clip_model.named_parameters()}
+        self.clip_p = None if self.joint else {k: v.data for k, v in clip_model.named_parameters()}
         self.T, self.P, self.V = model.n_token, model.n_i_token, model.vocab_size
         self.plan = VlmPlan(model.n_layer, model.n_token, batch_size, n_prefix=model.n_i_token,
                             num_class=model.vocab_size, n_embd=model.n_embd, normalize_attn=model.normalize_attn,
-                            device=self.device, precision=precision)
-        self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
-                                     num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
-                                     n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
-                                     device=self.device, precision=precision)
-        self.precision = self.clip_plan.precision
-        if self.precision == "x3":
-            self.clip_plan.split_weights(self.clip_p)  # frozen: split once
+                            device=self.device, precision=precision, joint=self.joint)
+        if self.joint:
+            self.clip_plan = None
+            self.precision = self.plan.precision
+        else:
+            self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+                                         num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
+                                         n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
+                                         device=self.device, precision=precision)
+            self.precision = self.clip_plan.precision
+            if self.precision == "x3":
+                self.clip_plan.split_weights(self.clip_p)  # frozen: split once
         Tt = self.T - self.P
         self.yt = torch.empty(batch_size, Tt, dtype=torch.uint8, device=self.device)
         self.post = torch.empty(batch_size, Tt, self.V, dtype=torch.float32, device=self.device)
@@ -100,7 +109,7 @@ class VlmTrainer:
 
     def _fwd_bwd(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        emb = self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_NWP.py:163
+        emb = None if self.joint else self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_NWP.py:163
         self.plan.forward(self.pd, self.plan.xt, emb)
         _native.call("ghm_ce_kl", _p(self.plan.logits), _p(self.yt), _p(self.post), _p(self.plan.dlogits),
                      _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.T, self.P,
@@ -125,7 +134,7 @@ class VlmTrainer:
         self.plan.xt.copy_(xt, non_blocking=True)
         self.yt.copy_(yt, non_blocking=True)
         self.post.copy_(post, non_blocking=True)
-        self.clip_plan.tokens.copy_(i_tokens, non_blocking=True)
+        (self.plan.itok if self.joint else self.clip_plan.tokens).copy_(i_tokens, non_blocking=True)
 
     def step(self):
         if self.steps_done >= self.n_sched:

@@ -136,9 +136,10 @@ class OracleVlm(nn.Module):
     the (then empty) ModuleLists, t_embedding, i_embedding, per layer q, k, v, ln1,
     mlp, ln2, then _read_out Linear(d -> V) and the unused _out."""
 
-    def __init__(self, n_token, n_i_token=1, num_class=10, n_embd=256, n_layer=9, n_mlp_hidden=1024):
+    def __init__(self, n_token, n_i_token=1, num_class=10, n_embd=256, n_layer=9, n_mlp_hidden=1024, sequential=True):
         super().__init__()
         self.V, self.n_i_token, self.n_embd, self.n_token = num_class, n_i_token, n_embd, n_token
+        self.sequential = sequential
         self.position_embeddings = nn.Embedding(n_token, n_embd)
         self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         self._mlps, self._lns_1, self._lns_2 = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -157,13 +158,17 @@ class OracleVlm(nn.Module):
 
     def forward(self, xt, zi):
         """xt: text tokens [B, T1] (long); zi: the frozen CLIP image feature
-        [B, 1, V].  Returns next-token logits [B, T1, V] (model.py:301-335)."""
+        [B, 1, V] (sequential) or the image leaves [B, n_i_token] (long; joint,
+        sequential=False).  Returns next-token logits [B, T1, V] (model.py:301-335)."""
         B, T1 = xt.shape
         T = T1 + zi.shape[1]
         mask = vlm_mask(self.n_token, self.n_i_token)
         emb = torch.zeros(B, T, self.n_embd)
-        x2 = torch.cat([zi, torch.zeros(B, zi.shape[1], self.n_embd - self.V)], dim=2)  # :281-286
-        emb[:, 0, :] = x2[:, 0, :]
+        if self.sequential:
+            x2 = torch.cat([zi, torch.zeros(B, zi.shape[1], self.n_embd - self.V)], dim=2)  # :281-286
+            emb[:, 0, :] = x2[:, 0, :]
+        else:
+            emb[:, :self.n_i_token, :] = self.i_embedding(zi)  # :287-289
         emb[:, self.n_i_token:, :] = self.t_embedding(xt)  # :292
         H = emb + self.position_embeddings(torch.arange(T).expand(B, T))  # :305
         for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
@@ -226,6 +231,47 @@ class OracleVlmTrainer:
             feat = self.clip(torch.as_tensor(il, dtype=torch.long))[0].unsqueeze(1)
         self.last_feat = feat
         logits = self.model(torch.as_tensor(xt, dtype=torch.long), feat)
+        self.last_logits = logits.detach()
+        loss = ce_loss(logits, torch.as_tensor(yt, dtype=torch.long))
+        loss.backward()
+        with torch.no_grad():
+            cmp = kl_compare(logits, torch.as_tensor(post, dtype=torch.float32))
+        with_grad = [p for p in self.params if p.grad is not None]
+        torch.nn.utils.clip_grad_norm_(with_grad, self.max_norm, norm_type=2)
+        self.opt.set_lr(lr_cosine(self.it, *self.sched))
+        self.opt.step()
+        self.it += 1
+        return float(loss.item()), float(loss.item()), float(cmp.item())
+
+
+class OracleVlmJointTrainer:
+    """train_NWP.py:60-160 (raw=True, guide=False): the joint model (sequential=False,
+    T = 161: 81 image leaves through i_embedding as the prefix, 80 text tokens), no
+    CLIP.  RNG order: sampler (seedtree) -> [get_Bayes, unseeded, skipped] ->
+    seed_everything(seed) -> model -> loop."""
+
+    def __init__(self, p=0.2, B=128, L=9, d=256, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
+                 max_norm=1.0, seed=224, seedtree=42, n_layer_tree=4, n_child=3):
+        self.sampler = NwpSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], seedtree=seedtree)
+        T = n_child ** n_layer_tree
+        torch.manual_seed(seed)  # seed_everything(seed) (:72)
+        np.random.seed(seed)
+        self.model = OracleVlm(2 * T - 1, T, 10, d, L, 4 * d, sequential=False)
+        self.params = list(self.model.parameters())
+        self.opt = OracleAdamW(self.params)
+        self.B = B
+        self.sched = (lr_max, lr_min, warmup, total_iters)
+        self.max_norm = max_norm
+        self.it = 0
+
+    def step(self, batch=None):
+        """Returns (ploss, loss, compare)."""
+        for p in self.params:
+            p.grad = None
+        if batch is None:
+            batch = self.sampler.get_batch(self.B)
+        xt, yt, post, il = batch[:4]
+        logits = self.model(torch.as_tensor(xt, dtype=torch.long), torch.as_tensor(np.asarray(il), dtype=torch.long))
         self.last_logits = logits.detach()
         loss = ce_loss(logits, torch.as_tensor(yt, dtype=torch.long))
         loss.backward()

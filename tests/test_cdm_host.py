@@ -240,3 +240,24 @@ def test_vlm_oracle_two_steps_match_reference():
         np.testing.assert_array_equal(tr.last_logits.numpy(), g[f"logits{k}"])
         ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
         np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-12, atol=1e-12)
+
+
+def test_vlm_joint_oracle_two_steps_match_reference():
+    """Joint VLM (train_NWP.py, sequential=False, T = 161), two full training steps at
+    d=256, L=1, B=4 (vlm_joint_tiny.npz): draws, initial weights, logits, losses."""
+    from oracle import vlm_oracle as VO
+    g = _fix("vlm_joint_tiny.npz")
+    tr = VO.OracleVlmJointTrainer(B=4, L=1)
+    assert [n for n, _ in tr.model.named_parameters()] == list(g["param_names"])
+    st = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+    np.testing.assert_array_equal(st, g["init_stats"])
+    for k in range(2):
+        drawn = tr.sampler.get_batch(tr.B)
+        np.testing.assert_array_equal(np.asarray(drawn[0]), g[f"xt{k}"])
+        np.testing.assert_array_equal(np.asarray(drawn[3]), g[f"i_leaves{k}"])
+        ploss, loss, cmp = tr.step(batch=drawn)
+        assert abs(ploss - float(g[f"ploss{k}"])) <= 1e-6 * ploss
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-5 * cmp
+        np.testing.assert_allclose(tr.last_logits.numpy(), g[f"logits{k}"], rtol=1e-5, atol=1e-5)
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-6, atol=1e-9)
