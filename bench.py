@@ -117,7 +117,7 @@ def make_cdm_ring(sampler, B, R):
     return ring
 
 
-def build_vlm(rank, B, L, p, total_iters, precision=None):
+def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False):
     """BASELINE config 5 (exp_vlm_standardTF.sh via train_sequential_NWP.py): sequential
     next-word prediction, AutoRegressiveTransformer(T=81, 1 prefix token, d=256, L=9,
     MLP 1024), lr 1e-3 -> 1e-6, frozen CLIP image encoder (random init: no checkpoint
@@ -127,6 +127,12 @@ def build_vlm(rank, B, L, p, total_iters, precision=None):
     from ghmclip.training.vlm_trainer import VlmTrainer
     p_y = np.ones(10) / 10
     sampler = NextWordPredictSampler([4, 4], [3, 3], [p_y, p_y], [p, p])
+    if joint:  # train_NWP.py / exp_vlm_jointtrain.sh: 81 image leaves + 80 text tokens, no CLIP
+        seed_everything(224 + 1000 * rank)
+        model = AutoRegressiveTransformer(161, 81, 10, 256, L, [4, 4], 4, 1024, auto_regressive=True,
+                                          sequential=False).cuda()
+        sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
+        return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision="x3")
     torch.manual_seed(7)
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
     seed_everything(224 + 1000 * rank)
@@ -218,18 +224,18 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
                 "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if workload == 'cdm_joint' else 'sequential'} "
                           f"CDM config, B={B}, L={L}, fp32 PyTorch-CPU restatement of the reference "
                           f"(oracle/cdm_oracle.py, BP_DNS posterior included); {dt:.3f} s/step"}
-    if workload == "vlm":
+    if workload in ("vlm", "vlm_joint"):
         from oracle import vlm_oracle as VO
-        tr = VO.OracleVlmTrainer(B=B, L=L)
+        tr = VO.OracleVlmJointTrainer(B=B, L=L) if workload == "vlm_joint" else VO.OracleVlmTrainer(B=B, L=L)
         tr.step()
         t0 = time.time()
         for _ in range(steps):
             tr.step()
         dt = (time.time() - t0) / steps
         return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-                "sample": f"{steps} steps (after 1 warm-up) of the sequential VLM config, B={B}, L={L}, d=256, fp32 "
-                          f"PyTorch-CPU restatement of the reference (oracle/vlm_oracle.py, frozen CLIP "
-                          f"forward + host BP posteriors included); {dt:.3f} s/step"}
+                "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if workload == 'vlm_joint' else 'sequential'} "
+                          f"VLM config, B={B}, L={L}, d=256, fp32 PyTorch-CPU restatement of the reference "
+                          f"(oracle/vlm_oracle.py, host BP posteriors included); {dt:.3f} s/step"}
     tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
           else O.OracleTrainer(p=0.2, B=B, L=L))
     tr.step()  # warm-up
@@ -255,10 +261,10 @@ def main():
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
-    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "cdm_joint", "vlm"],
+    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "cdm_joint", "vlm", "vlm_joint"],
                     help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4); "
                          "cdm_joint: joint CDM (train_CDNS.py, T = 162); vlm: sequential VLM next-word prediction "
-                         "(BASELINE config 5)")
+                         "(BASELINE config 5); vlm_joint: joint VLM (train_NWP.py, T = 161)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
@@ -266,7 +272,7 @@ def main():
     ws, rank, local = setup_dist(a.gpus)
     if a.workload in ("cdm", "cdm_joint"):
         return main_cdm(a, ws, rank)
-    if a.workload == "vlm":
+    if a.workload in ("vlm", "vlm_joint"):
         return main_vlm(a, ws, rank)
     total_iters = max(3000, a.steps + a.warmup + 1)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
@@ -434,7 +440,8 @@ def main_vlm(a, ws, rank):
     """Sequential VLM (BASELINE config 5) throughput: samples/s, B rows per rank."""
     L = 9 if a.layers == 5 else a.layers  # exp_vlm_standardTF.sh: n_model_layer=9
     total_iters = max(30000, a.steps + a.warmup + 1)
-    sampler, tr = build_vlm(rank, a.batch, L, 0.2, total_iters, a.precision)
+    joint = a.workload == "vlm_joint"
+    sampler, tr = build_vlm(rank, a.batch, L, 0.2, total_iters, a.precision, joint=joint)
     ring = make_vlm_ring(sampler, a.batch, a.ring)
 
     def one(k):
@@ -481,7 +488,7 @@ def main_vlm(a, ws, rank):
     fwd = L * (6 * M * D * D + 4 * M * D * F + 4 * a.batch * T * T * D) + 2 * M * D * plan.V
     step_gflop = 3 * fwd / 1e9
     out = {
-        "metric": "GHM training samples/sec (sequential VLM config)",
+        "metric": f"GHM training samples/sec ({'joint' if joint else 'sequential'} VLM config)",
         "value": round(a.batch * ws * a.steps / elapsed, 2),
         "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
@@ -489,9 +496,11 @@ def main_vlm(a, ws, rank):
         "dtype": "f32" if tr.plan.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native NextWordPredictSampler, p=0.2, host BP posteriors), ring of {a.ring} "
                 f"batches resident in HBM",
-        "config": {"workload": f"vlm_sequential: AutoRegressiveTransformer(L={L}, d=256, T=81 = 1 prefix + 80 text) "
-                               f"+ frozen CLIP image EncoderTransformer(L=5) forward, CE + KL compare, "
-                               f"fwd+bwd+clip+AdamW",
+        "config": {"workload": (f"vlm_joint: AutoRegressiveTransformer(L={L}, d=256, T=161 = 81 image leaves + 80 "
+                                f"text, sequential=False), CE + KL compare, fwd+bwd+clip+AdamW" if joint else
+                                f"vlm_sequential: AutoRegressiveTransformer(L={L}, d=256, T=81 = 1 prefix + 80 text) "
+                                f"+ frozen CLIP image EncoderTransformer(L=5) forward, CE + KL compare, "
+                                f"fwd+bwd+clip+AdamW"),
                    "batch_rows_per_rank": a.batch, "global_batch_rows": a.batch * ws, "n_layer": L,
                    "parallelism": f"dp{ws}", "hip_graph": not a.no_graph},
         "roofline": roofline,
@@ -500,7 +509,7 @@ def main_vlm(a, ws, rank):
         "last_loss": float(losses[-1]) if len(losses) else None,
     }
     if ws == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=4, workload="vlm")
+        out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=4, workload=a.workload)
     print(json.dumps(out), flush=True)
     if ws > 1:
         import torch.distributed as dist

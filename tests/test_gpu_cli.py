@@ -92,3 +92,25 @@ def test_joint_cdm_cli(tmp_path, monkeypatch):
     assert d["iter"] == 5
     np.testing.assert_allclose(d["loss_history"], loss)
     assert d["model_state_dict"]["position_embeddings.weight"].shape == (162, 128)
+
+
+NWP_FLAGS = ["--job_name=VLM", "--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4", "--n_ttree_child=3",
+             "--n_itree_child=3", "--p_ttree_flip=0.2", "--p_itree_flip=0.2", "--flip_scale=1", "--batch_size=8",
+             "--variable_type=10", "--d_eb=256", "--n_model_layer=2", "--n_head=4", "--layernorm=True",
+             "--normalize_attn=True", "--lr_max=1e-3", "--lr_min=1e-6", "--guide=False", "--total_iters=5",
+             "--penalty=0.001", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+
+
+def test_joint_vlm_cli(tmp_path, monkeypatch):
+    """exp_vlm_jointtrain.sh flags (shortened): train_NWP writes logs/VLM/<tree>/JT_L2H4D256/."""
+    from ghmclip.training import train_NWP
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    loss, compare = train_NWP.main(NWP_FLAGS)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/VLM/K4_L4C3p20_L4C3p20sc10/JT_L2H4D256/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert set(d) == {"model_state_dict", "optimizer_state_dict", "loss", "iter", "loss_history", "ploss_history",
+                      "bayes", "compare"}
+    assert d["model_state_dict"]["position_embeddings.weight"].shape == (161, 256)
