@@ -1,5 +1,5 @@
-# usage: bash tools/gpu_round.sh TAG : all GPU tests, smoke, CLIP / CDM / VLM benches,
-# rocprof kernel stats of the CLIP and VLM benches
+# usage: bash tools/gpu_round.sh TAG : all GPU tests, smoke, the five workload benches,
+# rocprof kernel stats of the CLIP (headline) and VLM benches
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r1}
@@ -14,9 +14,13 @@ grep -E "passed|failed" $OUT/gpu_tests.log | tail -2
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 3
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
 cat $OUT/bench.json
-timeout -k 10 400 python bench.py --workload vlm > $OUT/bench_vlm.json 2> $OUT/bench_vlm.err || exit 5
-cat $OUT/bench_vlm.json
-timeout -k 10 300 python bench.py --workload cdm --no-cpu-baseline > $OUT/bench_cdm.json 2> $OUT/bench_cdm.err || exit 6
+for w in vlm cdm cdm_joint vlm_joint; do
+  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 5
+  echo "$w $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$w.json)"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_clip -o run -- \
+   python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_clip.json 2> $OUT/prof_clip.err
+ok $? || exit 6
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_vlm -o run -- \
    python bench.py --workload vlm --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_vlm.json 2> $OUT/prof_vlm.err
 ok $? || exit 7
