@@ -328,7 +328,7 @@ int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, f
 int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T, int D,
                         int n_prefix, float scale_div, float dbl, void* stream);
 int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
-                        int T, int D, float scale_div, float dbl, void* stream);
+                        int T, int D, int n_prefix, float scale_div, float dbl, void* stream);
 
 /* ---- split-bf16 (x3) GEMM for the VLM projections (csrc/ghm_gemm.hip) -------
  * Replaces the nn.Linear products of AutoRegressiveTransformer (models/model.py:

@@ -57,61 +57,76 @@ __device__ __forceinline__ void vx_load_split64(const float* __restrict__ p, boo
   for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
 }
 
+// largest chunk <= 8 that divides n (float4 loads in flight per thread while staging)
+__device__ __forceinline__ constexpr int vx_chunk(int n) {
+  return n % 8 == 0 ? 8 : (n % 6 == 0 ? 6 : (n % 4 == 0 ? 4 : (n % 3 == 0 ? 3 : (n % 2 == 0 ? 2 : 1))));
+}
+
 // columns col + 64 hh + 0..31 (hh = 0, 1) of rows 0..TP-1 (row stride ld) as a
-// split [row][hh][32] image; rows >= T clamp to T - 1
-template <int NKT>
+// split [row][hh][32] image; rows >= T clamp to T - 1.  NW waves stage it in
+// chunks of at most 8 float4 per thread.
+template <int NKT, int NW>
 __device__ __forceinline__ void vx_stage_half(const float* __restrict__ seq, int64_t ld, int T, int col, __bf16* ih,
                                               __bf16* il) {
-  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
-  float4 v[NIT];
+  constexpr int NT = NW * 64, NIT = NKT * 32 * 16 / NT, CH = vx_chunk(NIT);
+  static_assert(NKT * 32 * 16 % NT == 0 && NIT % CH == 0, "staging split");
+#pragma unroll 1  // one chunk of loads in flight: unrolled, the compiler hoists every chunk's loads
+  for (int c0 = 0; c0 < NIT; c0 += CH) {
+    float4 v[CH];
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int idx = threadIdx.x + NT * k;
-    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
-    const int rc = row < T ? row : T - 1;
-    v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * ld + col + 64 * hh + 4 * q4);
-  }
+    for (int k = 0; k < CH; ++k) {
+      const int idx = threadIdx.x + NT * (c0 + k);
+      const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+      const int rc = row < T ? row : T - 1;
+      v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * ld + col + 64 * hh + 4 * q4);
+    }
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int idx = threadIdx.x + NT * k;
-    const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
-    bf16x4 a, b;
-    split4(v[k], a, b);
-    stb4(ih + row * VX_PITCH + 32 * hh + 4 * q4, a);
-    stb4(il + row * VX_PITCH + 32 * hh + 4 * q4, b);
+    for (int k = 0; k < CH; ++k) {
+      const int idx = threadIdx.x + NT * (c0 + k);
+      const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
+      bf16x4 a, b;
+      split4(v[k], a, b);
+      stb4(ih + row * VX_PITCH + 32 * hh + 4 * q4, a);
+      stb4(il + row * VX_PITCH + 32 * hh + 4 * q4, b);
+    }
   }
 }
 
 // columns col .. col+31 of rows 0..TP-1 (row stride ld) as a split [row][32]
 // image for transposed reads; rows >= T clamp
-template <int NKT>
+template <int NKT, int NW>
 __device__ __forceinline__ void vx_stage_cols(const float* __restrict__ base, int64_t ld, int T, int col, __bf16* ih,
                                               __bf16* il) {
-  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
-  float4 v[NIT];
+  constexpr int NT = NW * 64, NIT = NKT * 32 * 8 / NT, CH = vx_chunk(NIT);
+  static_assert(NKT * 32 * 8 % NT == 0 && NIT % CH == 0, "staging split");
+#pragma unroll 1  // one chunk of loads in flight: unrolled, the compiler hoists every chunk's loads
+  for (int c0 = 0; c0 < NIT; c0 += CH) {
+    float4 v[CH];
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int idx = threadIdx.x + NT * k;
-    const int row = idx >> 3, q4 = idx & 7;
-    const int rc = row < T ? row : T - 1;
-    v[k] = *reinterpret_cast<const float4*>(base + static_cast<int64_t>(rc) * ld + col + 4 * q4);
-  }
+    for (int k = 0; k < CH; ++k) {
+      const int idx = threadIdx.x + NT * (c0 + k);
+      const int row = idx >> 3, q4 = idx & 7;
+      const int rc = row < T ? row : T - 1;
+      v[k] = *reinterpret_cast<const float4*>(base + static_cast<int64_t>(rc) * ld + col + 4 * q4);
+    }
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
-    const int idx = threadIdx.x + NT * k;
-    bf16x4 a, b;
-    split4(v[k], a, b);
-    stb4(ih + idx * 4, a);
-    stb4(il + idx * 4, b);
+    for (int k = 0; k < CH; ++k) {
+      const int idx = threadIdx.x + NT * (c0 + k);
+      bf16x4 a, b;
+      split4(v[k], a, b);
+      stb4(ih + idx * 4, a);
+      stb4(il + idx * 4, b);
+    }
   }
 }
 
 // S^T[key][query] += X_rows . Y over the 32-column slab c of a half image
 template <int NKT>
 __device__ __forceinline__ void vx_rows_dot(const __bf16* ih, const __bf16* il, const bf16x8* yh, const bf16x8* yl,
-                                           int c, int j, int h, f32x16* acc) {
+                                           int c, int j, int h, int nk, f32x16* acc) {
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
+    if (kt >= nk) break;  // key tiles past the mask bound stay 0 (masked to -inf / P = 0)
     const int off = (32 * kt + j) * VX_PITCH + 32 * h;
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt)
@@ -122,10 +137,10 @@ __device__ __forceinline__ void vx_rows_dot(const __bf16* ih, const __bf16* il, 
 // S^T (keys on rows, this wave's queries on lanes) = X[keys] . Y[query]^T over
 // DD features; X columns xcol.. of the sequence block (row stride ldx), the
 // query-side row at yrow (DD floats)
-template <int NKT, int DD>
+template <int NKT, int DD, int NW>
 __device__ __forceinline__ void vx_scores(const float* __restrict__ xseq, int64_t ldx, int xcol,
-                                          const float* __restrict__ yrow, int T, int j, int h, __bf16* sh, __bf16* sl,
-                                          f32x16* s) {
+                                          const float* __restrict__ yrow, int T, int j, int h, int nk, __bf16* sh,
+                                          __bf16* sl, f32x16* s) {
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
 #pragma unroll 1
@@ -134,9 +149,9 @@ __device__ __forceinline__ void vx_scores(const float* __restrict__ xseq, int64_
     vx_load_split64(yrow + 128 * e + 64 * h, true, yh, yl);  // Y[128e + 64h + 8t + i]
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      vx_stage_half<NKT>(xseq, ldx, T, xcol + 128 * e + 32 * c, sh, sl);
+      vx_stage_half<NKT, NW>(xseq, ldx, T, xcol + 128 * e + 32 * c, sh, sl);
       __syncthreads();
-      vx_rows_dot<NKT>(sh, sl, yh, yl, c, j, h, s);
+      vx_rows_dot<NKT>(sh, sl, yh, yl, c, j, h, nk, s);
       __syncthreads();
     }
   }
@@ -144,8 +159,16 @@ __device__ __forceinline__ void vx_scores(const float* __restrict__ xseq, int64_
 
 __device__ __forceinline__ bool vx_allowed(int q, int key, int npre) { return q < npre ? key < npre : key <= q; }
 
-template <int NKT, int DD>
-__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __restrict__ qkv,
+// key tiles a workgroup of query tiles [32 q0, 32 q1) needs under the prefix-causal
+// mask: keys <= max(npre - 1, last query) (npre = T: all)
+__device__ __forceinline__ int vx_key_tiles(int q1, int T, int npre) {
+  const int qmax = (32 * q1 < T ? 32 * q1 : T) - 1;
+  const int kmax = qmax > npre - 1 ? qmax : npre - 1;
+  return (kmax < T ? kmax : T - 1) / 32 + 1;
+}
+
+template <int NKT, int DD, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __restrict__ qkv,
                                                                  const float* __restrict__ H,
                                                                  float* __restrict__ Hmid, float* __restrict__ P,
                                                                  int T, int npre, float scale_div, float dbl) {
@@ -157,11 +180,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
   const float* seq = qkv + base * LD;
-  const int q = 32 * w + j;
+  // workgroup y takes query tiles NW y .. NW y + NW - 1 (one per wave)
+  const int q = 32 * (NW * static_cast<int>(blockIdx.y) + w) + j;
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
+  const int nk = vx_key_tiles(NW * (static_cast<int>(blockIdx.y) + 1), T, npre);
   f32x16 s[NKT];
-  vx_scores<NKT, DD>(seq, LD, DD, seq + qc * LD, T, j, h, sh, sl, s);
+  vx_scores<NKT, DD, NW>(seq, LD, DD, seq + qc * LD, T, j, h, nk, sh, sl, s);
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -204,11 +229,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __
   // O^T[d][q] = sum_key V[key][d] P[q][key], V column blocks of 32 through LDS
 #pragma unroll 1
   for (int dt = 0; dt < DD / 32; ++dt) {
-    vx_stage_cols<NKT>(seq, LD, T, 2 * DD + 32 * dt, sh, sl);
+    vx_stage_cols<NKT, NW>(seq, LD, T, 2 * DD + 32 * dt, sh, sl);
     __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
+      if (kt >= nk) break;  // P = 0 past the mask bound
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const int r0 = 32 * kt + 16 * ss + 4 * h;
@@ -234,13 +260,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_fwd_x3(const float* __
 
 // dA^T = (V dO^T)(1 + 1/D), dS = P (dA - rowsum(P dA)) / scale_div (stored dense),
 // dQ^T = K^T dS^T
-template <int NKT, int DD>
-__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* __restrict__ qkv,
+template <int NKT, int DD, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* __restrict__ qkv,
                                                                    const float* __restrict__ P,
                                                                    const float* __restrict__ dHmid,
                                                                    float* __restrict__ dS_out,
                                                                    float* __restrict__ dqkv, int T, float scale_div,
-                                                                   float dbl) {
+                                                                   int npre, float dbl) {
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
@@ -249,11 +275,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
   const float* seq = qkv + base * LD;
-  const int q = 32 * w + j;
+  const int q = 32 * (NW * static_cast<int>(blockIdx.y) + w) + j;
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
+  const int nk = vx_key_tiles(NW * (static_cast<int>(blockIdx.y) + 1), T, npre);
   f32x16 dp[NKT];
-  vx_scores<NKT, DD>(seq, LD, 2 * DD, dHmid + (base + qc) * DD, T, j, h, sh, sl, dp);
+  vx_scores<NKT, DD, NW>(seq, LD, 2 * DD, dHmid + (base + qc) * DD, T, j, h, nk, sh, sl, dp);
   const float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
   float delta = 0.f;
   f32x16 p[NKT];
@@ -289,11 +316,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* 
   }
 #pragma unroll 1
   for (int dt = 0; dt < DD / 32; ++dt) {
-    vx_stage_cols<NKT>(seq, LD, T, DD + 32 * dt, sh, sl);  // K
+    vx_stage_cols<NKT, NW>(seq, LD, T, DD + 32 * dt, sh, sl);  // K
     __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
+      if (kt >= nk) break;  // dS = 0 past the mask bound
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const int r0 = 32 * kt + 16 * ss + 4 * h;
@@ -312,12 +340,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_q_x3(const float* 
 }
 
 // dV^T = dO^T P (1 + 1/D) and dK^T = Q^T dS, summed over queries; the key on the lane
-template <int NKT, int DD>
-__global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* __restrict__ qkv,
+template <int NKT, int DD, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* __restrict__ qkv,
                                                                     const float* __restrict__ P,
                                                                     const float* __restrict__ dS,
                                                                     const float* __restrict__ dHmid,
-                                                                    float* __restrict__ dqkv, int T, float dbl) {
+                                                                    float* __restrict__ dqkv, int T, int npre, float dbl) {
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32, KS = TP / 16;
   constexpr int64_t LD = 3 * DD;
@@ -327,14 +355,19 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
   __shared__ __attribute__((aligned(16))) __bf16 sql[TP * 32];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
-  const int key = 32 * w + j;
+  const int key = 32 * (NW * static_cast<int>(blockIdx.y) + w) + j;
   const bool kv = key < T;
+  // queries that see this workgroup's keys: all when a key is in the prefix,
+  // else q >= the first key (P = dS = 0 above the diagonal)
+  const int klo = 32 * NW * static_cast<int>(blockIdx.y);
+  const int st0 = klo >= npre ? klo / 16 : 0;
   const float* pc = P + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
   const float* sc = dS + static_cast<int64_t>(blockIdx.x) * VX_PAD * VX_PAD + key;
   if constexpr (NKT <= 3) {
     bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
   #pragma unroll
     for (int st = 0; st < KS; ++st) {
+      if (st < st0) continue;
       float pv[8], sv[8];
   #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -347,12 +380,14 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
     }
   #pragma unroll 1
     for (int dt = 0; dt < DD / 32; ++dt) {
-      vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
-      vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
+      vx_stage_cols<NKT, NW>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
+      vx_stage_cols<NKT, NW>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
       __syncthreads();
       f32x16 aV = zero16(), aK = zero16();
   #pragma unroll
       for (int st = 0; st < KS; ++st) {
+        if (st < st0) continue;
+      if (st < st0) continue;
         const int r0 = 16 * st + 8 * h;
         aV = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
         aK = mfma_x3(vx_tr_frag(sqh, r0, r0 + 4, lane), vx_tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
@@ -377,6 +412,8 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
       bf16x8 bh[KS], bl[KS];
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
+        if (st < st0) continue;
+      if (st < st0) continue;
         float v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = src[(16 * st + 8 * h + i) * VX_PAD];
@@ -384,12 +421,15 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
       }
 #pragma unroll 1
       for (int dt = 0; dt < DD / 32; ++dt) {
-        if (which == 0) vx_stage_cols<NKT>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
-        else vx_stage_cols<NKT>(qkv + base * LD, LD, T, 32 * dt, soh, sol);
+        if (which == 0) vx_stage_cols<NKT, NW>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
+        else vx_stage_cols<NKT, NW>(qkv + base * LD, LD, T, 32 * dt, soh, sol);
         __syncthreads();
         f32x16 acc = zero16();
 #pragma unroll
         for (int st = 0; st < KS; ++st) {
+          if (st < st0) continue;
+        if (st < st0) continue;
+      if (st < st0) continue;
           const int r0 = 16 * st + 8 * h;
           acc = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), bh[st], bl[st], acc);
         }
@@ -408,44 +448,49 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_vlm_attn_bwd_kv_x3(const float*
   }
 }
 
+// waves (query or key tiles) per workgroup: several workgroups per sequence so a
+// batch of 128 sequences fills the 256 CUs; NW must divide the staging split
+template <int NKT>
+constexpr int vx_nw() { return NKT == 6 ? 3 : (NKT == 4 ? 2 : (NKT == 5 ? 5 : 1)); }
+
+template <int NKT, int DD>
+void launch_fwd_n(unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int T, int npre,
+                  float sd, float dbl) {
+  constexpr int NW = vx_nw<NKT>();
+  hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, H, Hm, P, T, npre,
+                     sd, dbl);
+}
+
 template <int DD>
 void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int npre,
                 float sd, float dbl) {
-  if (T <= 32)
-    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<1, DD>), dim3(g), dim3(64), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 64)
-    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<2, DD>), dim3(g), dim3(128), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 96)
-    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<3, DD>), dim3(g), dim3(192), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else {  // T > 96 (D = 256 at NKT = 6 spills 5-12 VGPRs: correct, slower)
-    if (T <= 128)
-      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<4, DD>), dim3(g), dim3(256), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-    else if (T <= 160)
-      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<5, DD>), dim3(g), dim3(320), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-    else
-      hipLaunchKernelGGL((k_vlm_attn_fwd_x3<6, DD>), dim3(g), dim3(384), 0, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  }
+  if (T <= 32) launch_fwd_n<1, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if (T <= 64) launch_fwd_n<2, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if (T <= 96) launch_fwd_n<3, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if (T <= 128) launch_fwd_n<4, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else if (T <= 160) launch_fwd_n<5, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
+  else launch_fwd_n<6, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);  // D = 256: spills 5-12 VGPRs (correct, slower)
 }
 
 template <int NKT, int DD>
 void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
-                  float* dqkv, int T, float sd, float dbl) {
-  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD>), dim3(g), dim3(NKT * 64), 0, s, qkv, P, dHm, dS, dqkv, T, sd,
-                     dbl);
-  hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD>), dim3(g), dim3(NKT * 64), 0, s, qkv, P, dS, dHm, dqkv, T, dbl);
+                  float* dqkv, int T, int npre, float sd, float dbl) {
+  constexpr int NW = vx_nw<NKT>();
+  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dHm, dS,
+                     dqkv, T, sd, npre, dbl);
+  hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dS, dHm,
+                     dqkv, T, npre, dbl);
 }
 
 template <int DD>
 void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
-                float* dqkv, float sd, float dbl) {
-  if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  else if (T <= 96) launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  else {  // T > 96 (D = 256 at NKT = 6 spills 5-12 VGPRs: correct, slower)
-    if (T <= 128) launch_bwd_n<4, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-    else if (T <= 160) launch_bwd_n<5, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-    else launch_bwd_n<6, DD>(g, s, qkv, P, dHm, dS, dqkv, T, sd, dbl);
-  }
+                float* dqkv, int npre, float sd, float dbl) {
+  if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+  else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+  else if (T <= 96) launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+  else if (T <= 128) launch_bwd_n<4, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+  else if (T <= 160) launch_bwd_n<5, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+  else launch_bwd_n<6, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
 }
 
 }  // namespace
@@ -463,7 +508,8 @@ extern "C" int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float
                                    int64_t n_seq, int T, int D, float scale_div, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 96 && n_seq >= 1, "shape (T <= 96, D in {128, 256})");
-  return ghm_attn_ext_bwd_x3(qkv, P, dH_mid, dS, dqkv, n_seq, T, D, scale_div, 1.f / static_cast<float>(D), stream);
+  // no mask bound known here: n_prefix = T (no key / query tile skipping; P = 0 masks)
+  return ghm_attn_ext_bwd_x3(qkv, P, dH_mid, dS, dqkv, n_seq, T, D, T, scale_div, 1.f / static_cast<float>(D), stream);
 }
 
 extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
@@ -478,12 +524,13 @@ extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mi
 }
 
 extern "C" int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
-                                   int64_t n_seq, int T, int D, float scale_div, float dbl, void* stream) {
+                                   int64_t n_seq, int T, int D, int n_prefix, float scale_div, float dbl,
+                                   void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
-  GHM_CHECK(n_seq >= 1, "n_seq >= 1");
+  GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
-  else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, scale_div, dbl);
+  if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
   return ghm_launch_status();
 }

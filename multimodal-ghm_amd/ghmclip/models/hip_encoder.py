@@ -314,7 +314,7 @@ class EncoderPlan:
             cur, nxt = nxt, cur  # cur = dHmid_l
             if self.long_attn:
                 c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
-                  _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, 0.0, s)
+                  _ptr(self.dqkv), N, T, D_MODEL, T, self.scale_div, 0.0, s)
             else:
                 c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
                   _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)

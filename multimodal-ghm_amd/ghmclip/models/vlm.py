@@ -271,7 +271,7 @@ class VlmPlan:
             self._reduce_ln(g, 2, l, s)
             # attention (nxt = dHmid) -> dq | dk | dv
             c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS), _ptr(self.dqkv),
-              self.N, self.T, D, self.scale_div, 1.0 / D, s)
+              self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
             self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D,
                         (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"]), D, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])

@@ -233,7 +233,7 @@ def test_attention_ext_long_sequences(T, npre, dbl):
     _native.call("ghm_attn_ext_fwd_x3", _ptr(qkv_d), _ptr(H.to(DEV)), _ptr(Hm), _ptr(P), N, T, D, npre, math.sqrt(D),
                  dbl, ctypes_stream())
     _native.call("ghm_attn_ext_bwd_x3", _ptr(qkv_d), _ptr(P), _ptr(dHm.to(DEV)), _ptr(dS), _ptr(dqkv), N, T, D,
-                 math.sqrt(D), dbl, ctypes_stream())
+                 npre, math.sqrt(D), dbl, ctypes_stream())
     torch.cuda.synchronize()
     scale = lambda t: t.abs().max().item()  # noqa: E731
     assert (Hm.cpu().view(N, T, D).double() - want.detach()).abs().max().item() <= 1e-4 * scale(want)
