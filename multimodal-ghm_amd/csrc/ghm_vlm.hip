@@ -141,33 +141,55 @@ __global__ __launch_bounds__(256) void k_ln_rows_bwd(const float* __restrict__ d
   float gacc[R], bacc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) gacc[r] = bacc[r] = 0.f;
-  for (int k = 0; k < LN_ROWS_PER_WAVE; ++k) {
-    const int64_t row = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * LN_ROWS_PER_WAVE + k;
-    if (row >= M) break;
-    const float2 st = stats[row];
-    float xh[R], g[R];
-    float s1 = 0.f, s2 = 0.f;
+  // rows in batches of LN_BATCH whose loads are all issued before the first
+  // row's reductions (one row at a time was load-latency bound: 18 us at M = 10,368)
+  constexpr int LN_BATCH = R <= 4 ? 4 : 2;
+  for (int k0 = 0; k0 < LN_ROWS_PER_WAVE; k0 += LN_BATCH) {
+    const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * LN_ROWS_PER_WAVE + k0;
+    if (row0 >= M) break;
+    float dyv[LN_BATCH][R], xv[LN_BATCH][R], rv[LN_BATCH][R];
+    float2 stv[LN_BATCH];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int c = lane + 64 * r;
-      const float dy = dY[row * D + c];
-      xh[r] = (X[row * D + c] - st.x) * st.y;
-      g[r] = dy * w[c];
-      s1 += g[r];
-      s2 += g[r] * xh[r];
-      gacc[r] += dy * xh[r];
-      bacc[r] += dy;
+    for (int b = 0; b < LN_BATCH; ++b) {
+      const int64_t row = row0 + b < M ? row0 + b : M - 1;  // clamped (unused past M)
+      stv[b] = stats[row];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int c = lane + 64 * r;
+        dyv[b][r] = dY[row * D + c];
+        xv[b][r] = X[row * D + c];
+        rv[b][r] = dres[row * D + c];
+      }
     }
-    s1 = sum32(s1);
-    s1 += xhalf(s1);
-    s2 = sum32(s2);
-    s2 += xhalf(s2);
-    const float m1 = s1 / static_cast<float>(D), m2 = s2 / static_cast<float>(D);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int c = lane + 64 * r;
-      const float d = st.y * (g[r] - m1 - xh[r] * m2);
-      dX[row * D + c] = dres[row * D + c] + d;
+    for (int b = 0; b < LN_BATCH; ++b) {
+      const int64_t row = row0 + b;
+      if (row >= M) break;
+      const float2 st = stv[b];
+      float xh[R], g[R];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int c = lane + 64 * r;
+        const float dy = dyv[b][r];
+        xh[r] = (xv[b][r] - st.x) * st.y;
+        g[r] = dy * w[c];
+        s1 += g[r];
+        s2 += g[r] * xh[r];
+        gacc[r] += dy * xh[r];
+        bacc[r] += dy;
+      }
+      s1 = sum32(s1);
+      s1 += xhalf(s1);
+      s2 = sum32(s2);
+      s2 += xhalf(s2);
+      const float m1 = s1 / static_cast<float>(D), m2 = s2 / static_cast<float>(D);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int c = lane + 64 * r;
+        const float d = st.y * (g[r] - m1 - xh[r] * m2);
+        dX[row * D + c] = rv[b][r] + d;
+      }
     }
   }
 #pragma unroll
