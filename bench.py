@@ -94,8 +94,10 @@ def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False):
     sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
     if joint:  # train_CDNS.py / exp_cdm_jointtrain.sh: 81 text + 81 image tokens, no CLIP
         model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False).cuda()
-        return sampler, CdmTrainer(model, None, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0,
-                                   device="cuda", precision="x3")
+        trainer = CdmTrainer(model, None, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0, device="cuda",
+                             precision="x3")
+        sampler.native.seed(224 + 1000 * rank)
+        return sampler, trainer
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
     model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True).cuda()
     trainer = CdmTrainer(model, clip, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0, device="cuda",
@@ -128,16 +130,18 @@ def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False):
     p_y = np.ones(10) / 10
     sampler = NextWordPredictSampler([4, 4], [3, 3], [p_y, p_y], [p, p])
     if joint:  # train_NWP.py / exp_vlm_jointtrain.sh: 81 image leaves + 80 text tokens, no CLIP
-        seed_everything(224 + 1000 * rank)
+        seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
         model = AutoRegressiveTransformer(161, 81, 10, 256, L, [4, 4], 4, 1024, auto_regressive=True,
                                           sequential=False).cuda()
         sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
+        np.random.seed(224 + 1000 * rank)  # each rank draws its own batches
         return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision="x3")
     torch.manual_seed(7)
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
-    seed_everything(224 + 1000 * rank)
+    seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
     model = AutoRegressiveTransformer(81, 1, 10, 256, L, [4, 1], 4, 1024, auto_regressive=True,
                                       sequential=True).cuda()
+    np.random.seed(224 + 1000 * rank)  # each rank draws its own batches
     sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
     trainer = VlmTrainer(model, clip, B, sched, device="cuda", precision=precision)
     return sampler, trainer
