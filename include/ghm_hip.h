@@ -219,6 +219,17 @@ int ghm_scaled_diff(const float* a, const float* b, const float* scale, float al
                     void* stream);
 int ghm_add_cols(float* dst, const float* src, int64_t M, int V, void* stream);
 
+/* Guided joint CDM (train_CDNS.py --guide=True; model.py:502-527, 1023-1040):
+ * one guided block = V columns [col, col+V) of the tokens [tok0, tok0+ntok) of a
+ * residual stream H [n_seq][T][128], against a BP message that each tree node
+ * repeats over `ext` consecutive tokens (data_random_GHM.py:551-592):
+ *   target(n,t,c) = msgs[n*msg_stride + moff + (t/ext)*V + c]
+ * fwd: part[n] = sum (H - target)^2;  bwd: dH += scale * (H - target). */
+int ghm_guide_blk_fwd(const float* H, int T, int tok0, int ntok, int col, const float* msgs, int64_t msg_stride,
+                      int64_t moff, int ext, int V, float* part, int64_t n_seq, void* stream);
+int ghm_guide_blk_bwd(const float* H, int T, int tok0, int ntok, int col, const float* msgs, int64_t msg_stride,
+                      int64_t moff, int ext, int V, float* dH, float scale, int64_t n_seq, void* stream);
+
 /* ---- sequential conditional denoising (CDM, train_sequential_DNS.py) ---------
  * ConditionalDenoiseEncoderTransformer (models/model.py:337-532, sequential=True)
  * runs the encoder layer kernels above at T = T_img + n_cond tokens; only the
@@ -243,6 +254,14 @@ int ghm_cdm_embed_joint_fwd(const float* z, const uint8_t* tok, const float* t_e
 int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
                double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i, int V,
                void* stream);
+/* As ghm_bp_dns, and also the image tree's messages for the guided CDM
+ * (data_random_GHM.py:551-592): msgs f32 [n_seq][3][n_nodes][V], planes hd, qd,
+ * bu; n_nodes = non-root nodes + 1; depth d (1..L_i) nodes breadth-first from
+ * offset sum_{e<d} C_i^e - 1, the root last (its qd plane is unused; its hd
+ * plane holds bu, as the reference's in-place `+=` aliases them, :501-504). */
+int ghm_bp_dns_msgs(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
+                    double sigma, float* post, float* z32, float* msgs, int64_t n_seq, int L_t, int C_t, int L_i,
+                    int C_i, int V, void* stream);
 /* pred[n, t] = H[n, t, :] . w_ro + b_ro for t < T_img (_read_out Linear(128, 1),
  * model.py:527-531).  H [n_seq][T][128]. */
 int ghm_cdm_readout_fwd(const float* H, const float* w_ro, const float* b_ro, float* pred, int64_t n_seq, int T,

@@ -98,9 +98,21 @@ __device__ __forceinline__ void bp_shift(double* m, int nodes, int V, int tid) {
   }
 }
 
+// Guided-CDM targets (data_random_GHM.py:563-592 reads them off the tree): the
+// image tree's hd / qd / bu messages as f32 planes [n][3][n_nodes][V]; node
+// index = depth-d breadth-first order starting at off[d], root last.  The root
+// has hd and bu only (plane 1 of the root is never read).
+__device__ __forceinline__ void dns_emit(float* msgs, int n, int n_nodes, int plane, int node0, const double* src,
+                                         int cnt, int V, int tid) {
+  if (!msgs) return;
+  float* o = msgs + ((static_cast<int64_t>(n) * 3 + plane) * n_nodes + node0) * V;
+  for (int e = tid; e < cnt * V; e += 64) o[e] = static_cast<float>(src[e]);
+}
+
 __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_trans, const double* __restrict__ i_trans,
                                                const uint8_t* __restrict__ t_tok, const double* __restrict__ z,
                                                double sigma, float* __restrict__ post, float* __restrict__ z32,
+                                               float* __restrict__ msgs, int n_nodes,
                                                int Lt, int Ct, int Tt, int Li, int Ci, int Ti, int V) {
   __shared__ double hd[DNS_MAXNODES * DNS_MAXV];
   __shared__ double qd[DNS_MAXNODES * DNS_MAXV];
@@ -174,6 +186,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
   }
   for (int leaf = tid; leaf < Ti; leaf += 64) z32[static_cast<int64_t>(n) * Ti + leaf] = static_cast<float>(zn[leaf]);
   __syncthreads();
+  dns_emit(msgs, n, n_nodes, 0, off[Li], hd + off[Li] * V, Ti, V, tid);  // leaf hd (not max-shifted, :483)
   // downward pass, leaves -> root (:489-495): qd of depth d from its hd, then
   // hd of depth d-1 = sum of the children's qd (slot order), max-shifted
   for (int d = Li, cnt = Ti; d >= 1; --d, cnt /= Ci) {
@@ -186,6 +199,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
       qd[(off[d] + node) * V + v] = log(a);
     }
     __syncthreads();
+    dns_emit(msgs, n, n_nodes, 1, off[d], qd + off[d] * V, cnt, V, tid);
     if (d == 1) break;
     const int np = cnt / Ci;
     for (int e = tid; e < np * V; e += 64) {
@@ -197,6 +211,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
     __syncthreads();
     bp_shift(hd + off[d - 1] * V, np, V, tid);
     __syncthreads();
+    dns_emit(msgs, n, n_nodes, 0, off[d - 1], hd + off[d - 1] * V, np, V, tid);
   }
   // root: hd = sum of the children's qd, max shift, bu = hd + external (:499-504)
   double* bu = bu_a;
@@ -211,6 +226,16 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
       mx = fmax(mx, s);
     }
     for (int v = 0; v < V; ++v) bu[v] = (r[v] - mx) + ext[v];
+    if (msgs) {
+      float* o = msgs + static_cast<int64_t>(n) * 3 * n_nodes * V;
+      for (int v = 0; v < V; ++v) {
+        // root hd: the reference's `bu_message = hd_message; bu_message += external`
+        // (data_random_GHM.py:501-504) adds in place to the shared numpy array, so
+        // the root's hd guide target is its bu message as well
+        o[(n_nodes - 1) * V + v] = static_cast<float>(bu[v]);
+        o[(2 * n_nodes + n_nodes - 1) * V + v] = static_cast<float>(bu[v]);          // root bu
+      }
+    }
   }
   __syncthreads();
   // upward pass, root -> leaves (:507-512)
@@ -229,6 +254,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
     __syncthreads();
     bp_shift(bn, nodes, V, tid);
     __syncthreads();
+    dns_emit(msgs, n, n_nodes, 2, off[d], bn, nodes, V, tid);
     double* tmp = bu;
     bu = bn;
     bn = tmp;
@@ -391,9 +417,9 @@ static int tree_leaves(int L, int C) {
   return T;
 }
 
-extern "C" int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
-                          double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i,
-                          int V, void* stream) {
+static int bp_dns_launch(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
+                         double sigma, float* post, float* z32, float* msgs, int64_t n_seq, int L_t, int C_t, int L_i,
+                         int C_i, int V, void* stream) {
   GHM_CHECK(t_trans && i_trans && t_tokens && z && post && z32, "null pointer");
   GHM_CHECK(L_t >= 1 && C_t >= 2 && L_i >= 1 && L_i <= 6 && C_i >= 2 && V >= 2 && V <= DNS_MAXV && n_seq >= 1 &&
                 sigma > 0.0,
@@ -404,8 +430,21 @@ extern "C" int ghm_bp_dns(const double* t_trans, const double* i_trans, const ui
   GHM_CHECK(Tt <= DNS_MAXLEAF && Tt / C_t <= DNS_MAXLEAF && Ti <= DNS_MAXLEAF && nonroot <= DNS_MAXNODES,
             "tree too large (leaves <= 96)");
   hipLaunchKernelGGL(k_bp_dns, dim3(static_cast<unsigned>(n_seq)), dim3(64), 0, ghm_stream(stream), t_trans, i_trans,
-                     t_tokens, z, sigma, post, z32, L_t, C_t, Tt, L_i, C_i, Ti, V);
+                     t_tokens, z, sigma, post, z32, msgs, nonroot + 1, L_t, C_t, Tt, L_i, C_i, Ti, V);
   return ghm_launch_status();
+}
+
+extern "C" int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
+                          double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i,
+                          int V, void* stream) {
+  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, nullptr, n_seq, L_t, C_t, L_i, C_i, V, stream);
+}
+
+extern "C" int ghm_bp_dns_msgs(const double* t_trans, const double* i_trans, const uint8_t* t_tokens,
+                               const double* z, double sigma, float* post, float* z32, float* msgs, int64_t n_seq,
+                               int L_t, int C_t, int L_i, int C_i, int V, void* stream) {
+  GHM_CHECK(msgs, "null pointer");
+  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, msgs, n_seq, L_t, C_t, L_i, C_i, V, stream);
 }
 
 extern "C" int ghm_cdm_readout_fwd(const float* H, const float* w_ro, const float* b_ro, float* pred, int64_t n_seq,

@@ -207,6 +207,87 @@ extern "C" int ghm_guide_total(const float* part, int n_parts, int64_t n_seq, fl
 }
 
 // ---------------------------------------------------------------------------
+// Guided joint CDM (train_CDNS.py --guide=True, exp_cdm_guidedTF.sh): each
+// guided output is a V-column block of H_{l+1} over a token range (model.py:
+// 502-527), compared with a BP message that one tree node repeats over `ext`
+// consecutive tokens (data_random_GHM.py:551-592).  One block:
+//   target(n, t, c) = msgs[n * msg_stride + moff + (t / ext) * V + c]
+//   part[n]         = sum_{t < ntok, c < V} (H[n, tok0 + t, col + c] - target)^2
+//   dH[n, tok0 + t, col + c] += scale * (H[...] - target)          (bwd)
+// Blocks that share columns (model.py:513-517 reads q and u from the same
+// slice on the first upward layer) are applied one after another on the stream.
+// ---------------------------------------------------------------------------
+struct GuideBlk {
+  int T, tok0, ntok, col, ext, V;
+  int64_t msg_stride, moff;
+};
+
+__global__ __launch_bounds__(256) void k_guide_blk_fwd(const float* __restrict__ H, const float* __restrict__ msgs,
+                                                       float* __restrict__ part, GuideBlk b) {
+  __shared__ float red[4];
+  const int n = blockIdx.x;
+  const float* h = H + (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+  const float* m = msgs + static_cast<int64_t>(n) * b.msg_stride + b.moff;
+  float s = 0.f;
+  for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
+    const int t = e / b.V, c = e - t * b.V;
+    const float dd = h[static_cast<int64_t>(t) * GHM_D + c] - m[(t / b.ext) * b.V + c];
+    s += dd * dd;
+  }
+  s = sum32(s);
+  s += __shfl_xor(s, 32, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[n] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void k_guide_blk_bwd(const float* __restrict__ H, const float* __restrict__ msgs,
+                                                       float* __restrict__ dH, int64_t total, GuideBlk b,
+                                                       float scale) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t per = static_cast<int64_t>(b.ntok) * b.V;
+  const int64_t n = i / per;
+  const int r = static_cast<int>(i - n * per);
+  const int t = r / b.V, c = r - t * b.V;
+  const int64_t at = (n * b.T + b.tok0 + t) * GHM_D + b.col + c;
+  const float target = msgs[n * b.msg_stride + b.moff + (t / b.ext) * b.V + c];
+  dH[at] += scale * (H[at] - target);
+}
+
+static int guide_blk_check(GuideBlk& b, int T, int tok0, int ntok, int col, int64_t msg_stride, int64_t moff,
+                           int ext, int V, int64_t n_seq) {
+  b = GuideBlk{T, tok0, ntok, col, ext, V, msg_stride, moff};
+  if (!(n_seq >= 1 && T >= 1 && tok0 >= 0 && ntok >= 1 && tok0 + ntok <= T && V >= 1 && col >= 0 &&
+        col + V <= GHM_D && ext >= 1 && moff >= 0 && moff + static_cast<int64_t>((ntok - 1) / ext + 1) * V <= msg_stride))
+    return -1;
+  return 0;
+}
+
+extern "C" int ghm_guide_blk_fwd(const float* H, int T, int tok0, int ntok, int col, const float* msgs,
+                                 int64_t msg_stride, int64_t moff, int ext, int V, float* part, int64_t n_seq,
+                                 void* stream) {
+  GHM_CHECK(H && msgs && part, "null pointer");
+  GuideBlk b;
+  GHM_CHECK(guide_blk_check(b, T, tok0, ntok, col, msg_stride, moff, ext, V, n_seq) == 0, "guide block shape");
+  hipLaunchKernelGGL(k_guide_blk_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream), H, msgs,
+                     part, b);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_blk_bwd(const float* H, int T, int tok0, int ntok, int col, const float* msgs,
+                                 int64_t msg_stride, int64_t moff, int ext, int V, float* dH, float scale,
+                                 int64_t n_seq, void* stream) {
+  GHM_CHECK(H && msgs && dH, "null pointer");
+  GuideBlk b;
+  GHM_CHECK(guide_blk_check(b, T, tok0, ntok, col, msg_stride, moff, ext, V, n_seq) == 0, "guide block shape");
+  const int64_t total = n_seq * ntok * V;
+  hipLaunchKernelGGL(k_guide_blk_bwd, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0,
+                     ghm_stream(stream), H, msgs, dH, total, b, scale);
+  return ghm_launch_status();
+}
+
+// ---------------------------------------------------------------------------
 // Dense-target helpers for the module API (GuidedClipLoss(guide=True) on the
 // guided-layer tensors EncoderTransformer.forward returns)
 // ---------------------------------------------------------------------------

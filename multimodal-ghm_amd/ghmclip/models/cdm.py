@@ -198,9 +198,13 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[1] * 2 + 1)
         self.sigma = sigma
-        if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive or guide:
+        if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive:
             raise NotImplementedError("HIP CDM: softmax attention, mlp=True, layernorm=True, maxnorm=False, "
-                                      "auto_regressive=False, guide=False")
+                                      "auto_regressive=False")
+        if guide and sequential:
+            raise NotImplementedError("HIP CDM: guide=True is built for the joint model (train_CDNS.py) only")
+        if guide and self.guided_layer_gap == 0:
+            raise ValueError("guide=True needs n_layer >= 2 * n_guided_layers[1] + 1 (model.py:372)")
         if not sequential and n_token > 96 and self_precision_f32():
             raise NotImplementedError("HIP CDM: the joint model's sequences past 96 tokens need the split-bf16 "
                                       "(x3) attention kernels (GHM_PRECISION=f32 is set)")
@@ -217,6 +221,14 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         self.t_guided_layer_flag = [False] * n_layer
         self.i_guided_layer_flag = [False] * n_layer
         self.t_embedding = nn.Embedding(self.vocab_size, self.n_embd)
+        counter = 0
+        for i in range(n_layer):  # guided-layer flags of model.py:392-416
+            if guide and counter < 2 * self.n_i_guided_layer + 1 and (i + 1) % self.guided_layer_gap == 0:
+                self.i_guided_layer_flag[i] = True
+                if counter < self.n_t_guided_layer or (counter == self.n_i_guided_layer - 1
+                                                       and self.n_t_guided_layer < self.n_i_guided_layer):
+                    self.t_guided_layer_flag[i] = True
+                counter += 1
         for _ in range(n_layer):
             self._queries.append(nn.Linear(n_embd, n_embd, bias=False))
             self._keys.append(nn.Linear(n_embd, n_embd, bias=False))
@@ -265,6 +277,51 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         return pred, [[], []]
 
 
+def cdm_guide_blocks(model, t_tree, i_tree, V):
+    """The guided outputs of the joint CDM (model.py:458-527) as blocks of the
+    residual stream, each paired with the BP messages that data_random_GHM.py:
+    526-592 (guided_info) lines up against it, in ConditionalGuidedLsLoss order
+    (:1023-1040).  t_tree / i_tree = (L, C).  Returns {layer l: [block, ...]},
+    block = (src, tok0, ntok, col, moff, ext) with src "i" (image messages
+    [n][3][n_nodes][V] of ghm_bp_dns_msgs: planes hd, qd, bu) or "t" (text
+    BP_CLS messages [n][n_total][V] of ghm_bp_cls, depth Lt-1 first)."""
+    Lt, Ct = t_tree
+    Li, Ci = i_tree
+    Ti, Tt = Ci ** Li, Ct ** Lt
+    n_nodes = sum(Ci ** d for d in range(1, Li + 1)) + 1
+
+    def node0(depth):  # first node of a depth in the ghm_bp_dns_msgs order
+        return n_nodes - 1 if depth == 0 else sum(Ci ** e for e in range(1, depth))
+
+    def img(plane, depth, col, ext):
+        return ("i", 0, Ti, col, (plane * n_nodes + node0(depth)) * V, ext)
+
+    nt = model.n_t_guided_layer
+    blocks = {}
+    ig = [l for l, f in enumerate(model.i_guided_layer_flag) if f]
+    tg = [l for l, f in enumerate(model.t_guided_layer_flag) if f]
+    if len(ig) != 2 * Li + 1 or len(tg) > Lt:
+        raise ValueError("guided layers do not match the trees (n_guided_layers vs tree depths)")
+    for k, l in enumerate(ig):
+        if k <= Li:  # downward h / q (root: hd / bu), :505-511
+            depth, ext = Li - k, Ci ** k
+            b = [img(0, depth, k * V, ext), img(1 if depth else 2, depth, (nt + k) * V, ext)]
+        else:  # upward h / q / u, :512-518
+            j = k - Li - 1
+            depth = j + 1
+            ext = Ci ** (Li - depth)
+            b = [img(0, depth, (2 * Li + 1 - k) * V, ext), img(1, depth, (nt + 2 * Li + 1 - k) * V, ext),
+                 img(2, depth, (2 * nt + j) * V, ext)]
+        blocks.setdefault(l, []).extend(b)
+    off = 0
+    nodes = Tt // Ct
+    for k, l in enumerate(tg):  # text id blocks, :522-527 against BP_CLS depth Lt-1-k
+        blocks.setdefault(l, []).append(("t", Ti, Tt, k * V, off * V, Ct ** (k + 1)))
+        off += nodes
+        nodes //= Ct
+    return blocks
+
+
 class LsLoss(nn.Module):
     """models/model.py:1152-1160: mean over samples of the summed squared error."""
 
@@ -273,15 +330,17 @@ class LsLoss(nn.Module):
 
 
 class ConditionalGuidedLsLoss(nn.Module):
-    """models/model.py:989-1041 (guide=False): returns (loss, 0, 0, 0, 0)."""
+    """models/model.py:989-1041: returns (loss, 0, 0, 0, 0); the guide=True branch is
+    computed by CdmTrainer (fused, on the device)."""
 
     def __init__(self, penalty=1e-4, guide=False):
         super().__init__()
         self.penalty = penalty
         self.guide = guide
-        if guide:
-            raise NotImplementedError("guided CDM penalties are not built yet")
 
     def forward(self, inputs, targets, verbose=False):
+        if self.guide:
+            raise NotImplementedError("guided CDM penalties run inside the fused CdmTrainer step "
+                                      "(training/cdm_trainer.py, train_CDNS.py --guide=True), not on module outputs")
         loss = torch.sum(torch.pow(inputs[0] - targets[0], 2), dim=1)
         return loss.mean(), 0, 0, 0, 0

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan
+from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan, cdm_guide_blocks
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
@@ -35,7 +35,7 @@ def _p(t):
 class CdmTrainer:
     def __init__(self, model, clip_model, batch_size, lr_schedule, t_templ, i_templ, sigma=1.0, max_norm=1.0,
                  weight_decay=0.001, betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
-                 precision=None):
+                 precision=None, penalty=0.1):
         """model: ConditionalDenoiseEncoderTransformer; clip_model: the frozen CLIP
         text EncoderTransformer (sequential model), or None for the joint model
         (sequential=False, train_CDNS.py: the text leaves go through t_embedding);
@@ -128,6 +128,56 @@ class CdmTrainer:
         self.graphs = None
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
+        self._setup_guide(penalty)
+
+    def _setup_guide(self, penalty):
+        """Guided joint CDM (train_CDNS.py --guide=True): BP message buffers (image
+        hd/qd/bu planes, text BP_CLS levels), one penalty partial row per guided
+        block, and the penalised loss history (ploss_history)."""
+        self.guide = bool(getattr(self.model, "guide", False))
+        self.phist = None
+        if not self.guide:
+            return
+        if not self.joint:
+            raise NotImplementedError("guided CDM is built for the joint model only")
+        Lt, Ct, Li, Ci, V = self.tree
+        self.penalty = float(penalty)
+        self.gblocks = cdm_guide_blocks(self.model, (Lt, Ct), (Li, Ci), V)
+        self.n_inodes = sum(Ci ** d for d in range(1, Li + 1)) + 1
+        n_tnodes = sum(Ct ** d for d in range(Lt))
+        self.imsgs = torch.zeros(self.B, 3, self.n_inodes, V, dtype=torch.float32, device=self.device)
+        self.tmsgs = torch.zeros(self.B, n_tnodes, V, dtype=torch.float32, device=self.device)
+        self.n_gparts = sum(len(b) for b in self.gblocks.values())
+        self.gpart = torch.zeros(self.n_gparts, self.B, dtype=torch.float32, device=self.device)
+        self.gloss = torch.zeros(3, dtype=torch.float32, device=self.device)
+        self.phist = torch.zeros_like(self.hist)
+
+    def _blk_args(self, blk):
+        src, tok0, ntok, col, moff, ext = blk
+        msgs = self.imsgs if src == "i" else self.tmsgs
+        return tok0, ntok, col, _p(msgs), msgs[0].numel(), moff, ext, self.tree[4]
+
+    def _guide_fwd(self, s):
+        k = 0
+        for l, blks in sorted(self.gblocks.items()):
+            for blk in blks:
+                _native.call("ghm_guide_blk_fwd", _p(self.plan.H[l + 1]), self.T, *self._blk_args(blk),
+                             _p(self.gpart[k]), self.B, s)
+                k += 1
+
+    def _guide_hooks(self):
+        """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / B."""
+        if not self.guide:
+            return None
+        scale = 2.0 * self.penalty / self.B
+        hooks = {}
+        for l, blks in self.gblocks.items():
+            def fn(dH, s, l=l, blks=blks):
+                for blk in blks:
+                    _native.call("ghm_guide_blk_bwd", _p(self.plan.H[l + 1]), self.T, *self._blk_args(blk),
+                                 _p(dH), scale, self.B, s)
+            hooks[l] = fn
+        return hooks
 
     # -- the launch sequence -----------------------------------------------------
     def _fwd_bwd(self):
@@ -136,16 +186,26 @@ class CdmTrainer:
         Lt, Ct, Li, Ci, V = self.tree
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
-                         self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V,
-                         ctypes.c_void_p(side.cuda_stream))
+            ss = ctypes.c_void_p(side.cuda_stream)
+            if self.guide:
+                _native.call("ghm_bp_dns_msgs", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
+                             self.sigma, _p(self.post), _p(self.z32), _p(self.imsgs), self.B, Lt, Ct, Li, Ci, V, ss)
+                _native.call("ghm_bp_cls", _p(self.t_trans), _p(self.t_tok), _p(self.tmsgs), self.B, Lt, Ct, V, ss)
+            else:
+                _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
+                             self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V, ss)
         emb = None if self.joint else self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_DNS.py:141
         main.wait_stream(side)
         s = ctypes.c_void_p(main.cuda_stream)
         self.plan.forward(self.pd, self.z32, emb, 0 if emb is None else emb.shape[1])
         _native.call("ghm_ls_loss", _p(self.plan.pred), _p(self.i_tok), _p(self.post), _p(self.plan.dpred),
                      _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.Ti, s)
-        self.plan.backward(self.pd, self.gd)
+        if self.guide:  # ConditionalGuidedLsLoss guide branch (model.py:1023-1040)
+            self._guide_fwd(s)
+            self.gloss[0:1].copy_(self.loss_out[0:1])
+            _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.B, self.penalty, _p(self.gloss),
+                         _p(self.phist), _p(self.step_ctr), s)
+        self.plan.backward(self.pd, self.gd, layer_grad=self._guide_hooks())
 
     def _optim(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -203,7 +263,13 @@ class CdmTrainer:
         n = self.steps_done if upto is None else upto
         return self.hist[:n].double().cpu().numpy()
 
-    ploss_history = loss_history
+    def ploss_history(self, upto=None):
+        """Penalised loss per step (train_CDNS.py ploss_history): the loss plus the
+        guided penalties when the model is guided, else the loss itself."""
+        if not self.guide:
+            return self.loss_history(upto)
+        n = self.steps_done if upto is None else upto
+        return self.phist[:n].double().cpu().numpy()
 
     def compare_history(self, upto=None):
         """Squared error against the BP posterior means per step (compare_history)."""

@@ -9,7 +9,10 @@ The hot loop (:108-150) runs as the fused, HIP-graph-replayed CdmTrainer step in
 its joint mode: denoiser forward/backward on the 192-token split-bf16 attention,
 loss, Compare against the exact BP posterior (computed on the device), clip and
 AdamW; the native sampler runs in a producer thread.  Differences, by design:
-  * --device must be a HIP device; guide=True is not built (NotImplementedError);
+  * --device must be a HIP device;
+  * --guide=True (exp_cdm_guidedTF.sh) computes the BP guide targets on the device
+    (image hd/qd/bu and text BP_CLS messages) and adds the guided penalties and
+    their gradients inside the same fused step;
   * the split-bf16 (x3) matrix products are required (162-token sequences);
   * wandb/s3fs are optional (skipped with a warning when not installed);
   * with torchrun (WORLD_SIZE > 1) each rank takes a contiguous 1/world of the
@@ -59,8 +62,6 @@ def run_names(c):
 
 def main(argv=None):
     c = parse(argv)
-    if c.guide:
-        raise NotImplementedError("guided joint CDM (guide=True) is not built on the HIP path yet")
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if ws > 1:
@@ -131,7 +132,8 @@ def main(argv=None):
     sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters)
              for i in range(c.total_iters)]
     trainer = CdmTrainer(model, None, c.batch_size // ws, sched, sampler.t_templ, sampler.i_templ,
-                         sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset, precision="x3")
+                         sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset, precision="x3",
+                         penalty=c.penalty)
     if t_offset:
         trainer.load_optimizer_state(optimizer)
     sampler.native.pull_numpy_state()  # the producer owns numpy's MT stream from here on
@@ -139,14 +141,14 @@ def main(argv=None):
                             row_slice=(rank, ws) if ws > 1 else None)
 
     def sync_hist(upto):
-        h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
+        h, ph, ch = trainer.loss_history(upto), trainer.ploss_history(upto), trainer.compare_history(upto)
         if ws > 1:
             import torch.distributed as dist
-            t = torch.from_numpy(np.stack([h, ch])).to(device)
+            t = torch.from_numpy(np.stack([h, ph, ch])).to(device)
             dist.all_reduce(t, op=dist.ReduceOp.AVG)
-            h, ch = t.cpu().numpy()
+            h, ph, ch = t.cpu().numpy()
         loss_history[:upto] = h
-        ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
+        ploss_history[:upto] = ph  # equals the loss without guidance
         compare_history[:upto] = ch
 
     def save(iter_num):

@@ -18,6 +18,10 @@ cdm_joint_tiny.npz   L=1, d=128, B=4, 2 steps: the batch (text leaves, z, image
                      grad / param checksums (sum, sum of squares, first 64 values).
 cdm_joint_curve.npz  default joint config (p=0.2, L=9, d=128, B=128, lr 1e-3 ->
                      1e-6 over 30000 iters): ploss / loss / compare of the first N steps.
+cdm_guided_tiny.npz  guided joint model (exp_cdm_guidedTF.sh: guide=True, penalty
+                     0.1, lr 1e-2 -> 1e-5), L=9, B=4, 2 steps: batches, the
+                     sampler's guided targets, predictions, losses, grad checksums.
+cdm_guided_curve.npz the guided default config (B=128): first N ploss / loss / compare.
 """
 import argparse
 import os
@@ -46,7 +50,8 @@ P_Y = np.ones(10) / 10
 class Loop:
     """train_CDNS.py:60-150 (raw=True, guide=False)."""
 
-    def __init__(self, p, L, B, seed=224, total_iters=30000, lr_max=1e-3, lr_min=1e-6, penalty=0.1, max_norm=1.0):
+    def __init__(self, p, L, B, seed=224, total_iters=30000, lr_max=1e-3, lr_min=1e-6, penalty=0.1, max_norm=1.0,
+                 guide=False):
         self.s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [p, p], sigma=1, flip_scale=1,
                                            variable_type=10, translation_invariance=True, seedtree=42)
         seed_everything(seed)  # :74
@@ -54,8 +59,9 @@ class Loop:
                                                           n_layer=L, n_guided_layers=[4, 4], n_head=4,
                                                           n_mlp_hidden=512, activation="softmax", mlp=True,
                                                           normalize_attn=True, layernorm=True, maxnorm=False,
-                                                          sequential=False, guide=False)  # :75-89
-        self.loss = ConditionalGuidedLsLoss(penalty=penalty, guide=False)
+                                                          sequential=False, guide=guide)  # :75-89
+        self.loss = ConditionalGuidedLsLoss(penalty=penalty, guide=guide)
+        self.guide = guide
         self.loss_nop = LsLoss()
         self.opt = AdamW(params=self.model.parameters(), lr=None)
         self.B, self.it = B, 0
@@ -64,7 +70,7 @@ class Loop:
 
     def step(self):
         self.opt.zero_grad()
-        rt, ri = self.s.get_batch(device="cpu", batch_size=self.B, guide=False)
+        rt, ri = self.s.get_batch(device="cpu", batch_size=self.B, guide=self.guide)
         guided = [rt[2], ri[2]]
         post = torch.tensor(ri[3], dtype=torch.float32)
         out = self.model(rt[0], ri[0])
@@ -106,6 +112,42 @@ def tiny_fixture(L=1, B=4, nsteps=2, p=0.2):
     print("wrote cdm_joint_tiny.npz", [rec[f"ploss{k}"] for k in range(nsteps)])
 
 
+def guided_fixture(L=9, B=4, nsteps=2, p=0.2, curve_steps=30):
+    """exp_cdm_guidedTF.sh (--guide=True, penalty 0.1, lr 1e-2 -> 1e-5): the tiny
+    case's batches, guided targets, predictions, losses and gradient checksums, and
+    the default config's first curve_steps losses."""
+    lp = Loop(p, L, B, lr_max=1e-2, lr_min=1e-5, guide=True)
+    init = checksums(lp.model.named_parameters())
+    rec = {}
+    for k in range(nsteps):
+        r = lp.step()
+        for key in ("ploss", "loss", "compare"):
+            rec[f"{key}{k}"] = r[key]
+        rec[f"pred{k}"] = r["pred"].numpy()
+        rt, ri = r["batch"]
+        rec[f"t_leaves{k}"] = rt[0].numpy().astype(np.uint8)
+        rec[f"z{k}"] = ri[0].numpy()
+        rec[f"i_leaves{k}"] = ri[1].numpy().astype(np.uint8)
+        for j, g in enumerate(rt[2]):
+            rec[f"t_guide{k}_{j}"] = g.numpy()
+        for j, g in enumerate(ri[2]):
+            rec[f"i_guide{k}_{j}"] = g.numpy()
+        gn, gs, gh = checksums(r["grads"])
+        rec[f"grad_names{k}"], rec[f"grad_stats{k}"], rec[f"grad_heads{k}"] = gn, gs, gh
+    np.savez_compressed(os.path.join(HERE, "cdm_guided_tiny.npz"), L=L, B=B, p=p, nsteps=nsteps,
+                        param_names=init[0], init_stats=init[1], init_heads=init[2], **rec)
+    print("wrote cdm_guided_tiny.npz", [rec[f"ploss{k}"] for k in range(nsteps)])
+    lp = Loop(p, 9, 128, lr_max=1e-2, lr_min=1e-5, guide=True)
+    hist = np.zeros((3, curve_steps))
+    for k in range(curve_steps):
+        r = lp.step()
+        hist[:, k] = (r["ploss"], r["loss"], r["compare"])
+    np.savez_compressed(os.path.join(HERE, "cdm_guided_curve.npz"), p=p, L=9, B=128, total_iters=30000, lr_max=1e-2,
+                        lr_min=1e-5, penalty=0.1, ploss=hist[0], loss=hist[1], compare=hist[2],
+                        threads=torch.get_num_threads())
+    print("wrote cdm_guided_curve.npz", hist[0, :3])
+
+
 def curve_fixture(steps, p=0.2, L=9, B=128):
     lp = Loop(p, L, B)
     hist = np.zeros((3, steps))
@@ -130,3 +172,5 @@ if __name__ == "__main__":
         tiny_fixture()
     if not only or "curve" in only:
         curve_fixture(a.curve_steps)
+    if not only or "guided" in only:
+        guided_fixture(curve_steps=a.curve_steps)

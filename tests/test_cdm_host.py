@@ -167,8 +167,26 @@ def test_cdm_module_api_matches_reference_construction():
     oj = CO.OracleCdm(162, 81, 10, 128, 3, 512, sequential=False)
     for (k, a), (_, b) in zip(mj.state_dict().items(), oj.state_dict().items()):
         assert torch.equal(a, b), k
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):  # guided-layer gap 3 // 7 == 0 (the reference divides by it)
         ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, sequential=False, guide=True)
+    with pytest.raises(NotImplementedError):  # guidance is built for the joint model
+        ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 9, [4, 4], sequential=True, guide=True)
+    # guided joint model (exp_cdm_guidedTF.sh): flags and guide blocks as model.py:392-416, 458-527
+    from ghmclip.models.cdm import cdm_guide_blocks
+    torch.manual_seed(3)
+    mg = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 9, [4, 4], 4, 512, sequential=False, guide=True)
+    torch.manual_seed(3)
+    og = CO.OracleCdm(162, 81, 10, 128, 9, 512, sequential=False)
+    for (k, a), (_, b) in zip(mg.state_dict().items(), og.state_dict().items()):
+        assert torch.equal(a, b), k  # the flags draw no random numbers
+    assert mg.i_guided_layer_flag == [True] * 9 and mg.t_guided_layer_flag == [True] * 4 + [False] * 5
+    blocks = cdm_guide_blocks(mg, (4, 3), (4, 3), 10)
+    cols = {l: [(b[0], b[3]) for b in blocks[l]] for l in blocks}
+    assert cols[0] == [("i", 0), ("i", 40), ("t", 0)]      # leaves h / q, text depth 3
+    assert cols[4] == [("i", 40), ("i", 80)]                # root hd / bu
+    assert cols[5] == [("i", 40), ("i", 80), ("i", 80)]     # first upward layer: q and u share a slice
+    assert cols[8] == [("i", 10), ("i", 50), ("i", 110)]
+    assert [b[5] for b in blocks[0]] == [1, 1, 3] and blocks[4][0][5] == 81 and blocks[8][0][5] == 1
     with pytest.raises(RuntimeError):
         m(torch.zeros(2, 1, 10), torch.zeros(2, 81))  # CPU tensors: no fallback
 

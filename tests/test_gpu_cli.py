@@ -94,6 +94,25 @@ def test_joint_cdm_cli(tmp_path, monkeypatch):
     assert d["model_state_dict"]["position_embeddings.weight"].shape == (162, 128)
 
 
+def test_guided_cdm_cli(tmp_path, monkeypatch):
+    """exp_cdm_guidedTF.sh flags (shortened, L=9 for the 9 guided layers): train_CDNS
+    --guide=True writes logs/CDM/<tree>/GT_L9H4D128/ with the penalised loss in
+    ploss_history (above the plain loss)."""
+    from ghmclip.training import train_CDNS
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    flags = [f for f in CDNS_FLAGS if not f.startswith(("--guide", "--n_model_layer", "--lr_max", "--lr_min"))]
+    flags += ["--guide=True", "--n_model_layer=9", "--lr_max=1e-2", "--lr_min=1e-5"]
+    loss, compare = train_CDNS.main(flags)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/CDM/K4_L4C3p20_L4C3p20sc10/GT_L9H4D128/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert d["loss"]["guide"] is True and d["iter"] == 5
+    np.testing.assert_allclose(d["loss_history"], loss)
+    assert (d["ploss_history"] > d["loss_history"]).all()
+
+
 NWP_FLAGS = ["--job_name=VLM", "--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4", "--n_ttree_child=3",
              "--n_itree_child=3", "--p_ttree_flip=0.2", "--p_itree_flip=0.2", "--flip_scale=1", "--batch_size=8",
              "--variable_type=10", "--d_eb=256", "--n_model_layer=2", "--n_head=4", "--layernorm=True",
