@@ -13,7 +13,8 @@ first 100 steps of the default config (cdm_curve.npz).
 Reference file:line it follows (relative to src/ghmclip/):
   sampler    data/data_random_GHM.py:641-658 (DoubleSampler), :854-884
              (ConditionalDenoiseSampler.get_batch), :886-894 (get_Bayes)
-  BP         data/data_random_GHM.py:185-215 (BP_CLS root message), :467-523 (BP_DNS)
+  BP         data/data_random_GHM.py:185-215 (BP_CLS root message), :467-523 (BP_DNS),
+             :526-592 (guided_info: the guided CDM targets, pinned by cdm_guided_tiny.npz)
   model      models/model.py:337-532 (ConditionalDenoiseEncoderTransformer, sequential=True;
              sequential=False for the joint model of train_CDNS.py)
   loss       models/model.py:989-1041 (ConditionalGuidedLsLoss, guide=False), :1152-1160 (LsLoss)
@@ -24,15 +25,19 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .ghm_oracle import (OracleAdamW, OracleEncoder, bp_cls_messages, gen_leaves, gen_transition, lr_cosine,
-                         seed_everything)
+from .ghm_oracle import (OracleAdamW, OracleEncoder, bp_cls_messages, expand_messages, gen_leaves, gen_transition,
+                         lr_cosine, seed_everything)
 
 
-def bp_dns_posterior(trans, z, sigma, ext):
+def bp_dns_messages(trans, z, sigma, ext):
     """BP_DNS (data_random_GHM.py:467-523), vectorised over the nodes of a layer
     (translation invariance: node n of a layer uses its child-slot matrix n % C).
     z: noisy leaf observations [n_leaves, B]; ext: the text tree's BP_CLS root
-    message [V, B] (:875-877).  Returns the posterior means [n_leaves, B]."""
+    message [V, B] (:875-877).  Returns (hd, qd, bu, root_hd, root_bu, post):
+    per-depth dicts (1..L) of [n_nodes, V, B] messages, the root's hd / bu [V, B]
+    and the posterior means [n_leaves, B].  root_hd is the root's bu: the
+    reference's `bu_message = hd_message; bu_message += external` (:501-504) adds
+    in place to the one numpy array both names hold."""
     n_layer, C, V, _ = trans.shape
     vt = np.linspace(0, V - 1, V).reshape(1, V, 1)
 
@@ -57,7 +62,9 @@ def bp_dns_posterior(trans, z, sigma, ext):
         qd[layer] = up(h, trans[layer - 1])
     root = children_sum(qd[1])  # :499-504
     root = root - root.max(axis=1, keepdims=True)
-    bu = root + ext[None]
+    root_bu = root + ext[None]
+    bu_all = {}
+    bu = root_bu
     for layer in range(1, n_layer + 1):  # upward pass :507-512
         parent = np.repeat(bu, C, axis=0)
         diff = parent - qd[layer]
@@ -66,8 +73,38 @@ def bp_dns_posterior(trans, z, sigma, ext):
             out[c::C] = np.log(np.einsum("ji,njb->nib", trans[layer - 1, c], np.exp(diff[c::C])))
         b = hd[layer] + out
         bu = b - b.max(axis=1, keepdims=True)
+        bu_all[layer] = bu
     w = np.exp(bu)  # :514-518
-    return (vt * w).sum(axis=1) / w.sum(axis=1)
+    post = (vt * w).sum(axis=1) / w.sum(axis=1)
+    return hd, qd, bu_all, root_bu[0], root_bu[0], post
+
+
+def bp_dns_posterior(trans, z, sigma, ext):
+    """BP_DNS posterior means [n_leaves, B] (data_random_GHM.py:514-518)."""
+    return bp_dns_messages(trans, z, sigma, ext)[-1]
+
+
+def cdm_guided_targets(t_trans, i_trans, t_leaves, z, sigma):
+    """The guided targets ConditionalDenoiseSampler.get_batch(guide=True) returns
+    (data_random_GHM.py:871-877 -> guided_info :551-592 for the image tree, :531-549
+    for the text tree): (text [B, T, V] x L_t, depth L_t-1 first; image [B, T, 2V]
+    x (L_i + 1) downward leaves -> root, then [B, T, 3V] x L_i upward depth 1 ->
+    leaves), float32 torch tensors.  t_leaves [B, T] ints, z [B, T] float64."""
+    tm = bp_cls_messages(t_trans, t_leaves)
+    ext = tm[-1][:, 0, :].T
+    hd, qd, bu, r_hd, r_bu, _ = bp_dns_messages(i_trans, np.asarray(z, dtype=np.float64).T, sigma, ext)
+    L = i_trans.shape[0]
+    T = z.shape[1]
+
+    def rep(*ms):  # [n_nodes, V, B] each -> [B, T, k V]
+        cat = np.concatenate(ms, axis=1)
+        cat = np.repeat(cat, T // cat.shape[0], axis=0)
+        return torch.from_numpy(cat.transpose(2, 0, 1).astype(np.float32))
+
+    img = [rep(hd[d], qd[d]) for d in range(L, 0, -1)]
+    img.append(rep(r_hd[None], r_bu[None]))
+    img += [rep(hd[d], qd[d], bu[d]) for d in range(1, L + 1)]
+    return expand_messages(tm, T), img
 
 
 class CdmSamplerOracle:

@@ -279,3 +279,24 @@ def test_vlm_joint_oracle_two_steps_match_reference():
         np.testing.assert_allclose(tr.last_logits.numpy(), g[f"logits{k}"], rtol=1e-5, atol=1e-5)
         ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
         np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-6, atol=1e-9)
+
+
+def test_oracle_guided_targets_match_reference():
+    """The oracle's BP_DNS / BP_CLS message restatement, assembled as guided_info
+    (data_random_GHM.py:526-592), equals the reference sampler's guided targets of
+    cdm_guided_tiny.npz (z stored as float32 there; the reference ran BP on the f64
+    draw, hence 1e-5 relative).  Includes the root's aliased hd (= bu) target."""
+    f = np.load(os.path.join(GOLDEN, "cdm_guided_tiny.npz"))
+    s = CO.CdmSamplerOracle([4, 4], [3, 3], [0.2, 0.2])
+    for k in range(int(f["nsteps"])):
+        tt, it = CO.cdm_guided_targets(s.t_trans, s.i_trans, f[f"t_leaves{k}"].astype(np.int64),
+                                       f[f"z{k}"].astype(np.float64), 1.0)
+        assert len(tt) == 4 and len(it) == 9
+        for j, g in enumerate(tt):
+            want = f[f"t_guide{k}_{j}"]
+            assert g.shape == want.shape
+            assert np.abs(g.numpy() - want).max() <= 1e-5 * np.abs(want).max(), ("text", k, j)
+        for j, g in enumerate(it):
+            want = f[f"i_guide{k}_{j}"]
+            assert g.shape == want.shape, (j, g.shape, want.shape)
+            assert np.abs(g.numpy() - want).max() <= 1e-5 * np.abs(want).max() + 1e-6, ("image", k, j)
