@@ -81,7 +81,7 @@ def make_ring(sampler, B, R):
     return ring.cuda()
 
 
-def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False):
+def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False, guide=False):
     """BASELINE config 4 (exp_cdm_standardTF.sh): sequential CDM, L=9, d=128,
     lr 1e-3 -> 1e-6, sigma 1, frozen CLIP text encoder (random init: no checkpoint
     travels to the box; the step's work does not depend on the weights)."""
@@ -91,11 +91,13 @@ def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False):
     p_y = np.ones(10) / 10
     seed_everything(224)
     sampler = ConditionalDenoiseSampler([4, 4], [3, 3], [p_y, p_y], [p, p], sigma=1)
-    sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
-    if joint:  # train_CDNS.py / exp_cdm_jointtrain.sh: 81 text + 81 image tokens, no CLIP
-        model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False).cuda()
+    lr = (1e-2, 1e-5) if guide else (1e-3, 1e-6)  # exp_cdm_guidedTF.sh / the other CDM scripts
+    sched = [get_lr_cosine_schedule(s, lr[0], lr[1], 0, total_iters) for s in range(total_iters)]
+    if joint:  # train_CDNS.py / exp_cdm_{jointtrain,guidedTF}.sh: 81 text + 81 image tokens, no CLIP
+        model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False,
+                                                     guide=guide).cuda()
         trainer = CdmTrainer(model, None, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0, device="cuda",
-                             precision="x3")
+                             precision="x3", penalty=0.1)
         sampler.native.seed(224 + 1000 * rank)
         return sampler, trainer
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
@@ -216,17 +218,21 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     from oracle import ghm_oracle as O
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
-    if workload in ("cdm", "cdm_joint"):
+    if workload in ("cdm", "cdm_joint", "cdm_guided"):
         from oracle import cdm_oracle as CO
-        tr = CO.OracleCdmJointTrainer(B=B, L=L) if workload == "cdm_joint" else CO.OracleCdmTrainer(B=B, L=L, n_bayes=0)
+        joint = workload != "cdm"
+        tr = CO.OracleCdmJointTrainer(B=B, L=L) if joint else CO.OracleCdmTrainer(B=B, L=L, n_bayes=0)
         tr.step()
         t0 = time.time()
         for _ in range(steps):
             tr.step()
         dt = (time.time() - t0) / steps
+        note = (" (unguided: the oracle has no guided step; guidance adds BP messages and 26 small penalty "
+                "blocks)" if workload == "cdm_guided" else "")
         return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-                "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if workload == 'cdm_joint' else 'sequential'} "
-                          f"CDM config, B={B}, L={L}, fp32 PyTorch-CPU restatement of the reference "
+                "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if joint else 'sequential'} "
+                          f"CDM config{note}, "
+                          f"B={B}, L={L}, fp32 PyTorch-CPU restatement of the reference "
                           f"(oracle/cdm_oracle.py, BP_DNS posterior included); {dt:.3f} s/step"}
     if workload in ("vlm", "vlm_joint"):
         from oracle import vlm_oracle as VO
@@ -265,16 +271,17 @@ def main():
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
-    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "cdm_joint", "vlm", "vlm_joint"],
+    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "cdm_joint", "cdm_guided", "vlm", "vlm_joint"],
                     help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4); "
-                         "cdm_joint: joint CDM (train_CDNS.py, T = 162); vlm: sequential VLM next-word prediction "
+                         "cdm_joint: joint CDM (train_CDNS.py, T = 162); cdm_guided: the same with --guide=True "
+                         "(exp_cdm_guidedTF.sh); vlm: sequential VLM next-word prediction "
                          "(BASELINE config 5); vlm_joint: joint VLM (train_NWP.py, T = 161)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
-    if a.workload in ("cdm", "cdm_joint"):
+    if a.workload in ("cdm", "cdm_joint", "cdm_guided"):
         return main_cdm(a, ws, rank)
     if a.workload in ("vlm", "vlm_joint"):
         return main_vlm(a, ws, rank)
@@ -386,9 +393,10 @@ def main_cdm(a, ws, rank):
     """Sequential CDM (BASELINE config 4) throughput: samples/s, B rows per rank."""
     L = 9 if a.layers == 5 else a.layers  # exp_cdm_standardTF.sh: n_model_layer=9
     total_iters = max(30000, a.steps + a.warmup + 1)
-    joint = a.workload == "cdm_joint"
+    joint = a.workload in ("cdm_joint", "cdm_guided")
+    guide = a.workload == "cdm_guided"
     T = 162 if joint else 82
-    sampler, tr = build_cdm(rank, a.batch, L, 0.2, total_iters, a.precision, joint=joint)
+    sampler, tr = build_cdm(rank, a.batch, L, 0.2, total_iters, a.precision, joint=joint, guide=guide)
     ring = make_cdm_ring(sampler, a.batch, a.ring)
 
     def one(k):
@@ -409,7 +417,8 @@ def main_cdm(a, ws, rank):
     mlp_bytes = 4 * M * (128 + 128 + 512 + 512)
     achieved = mlp_bytes / (kern_ms * 1e-3) / 1e9
     out = {
-        "metric": f"GHM training samples/sec ({'joint' if joint else 'sequential'} CDM config)",
+        "metric": f"GHM training samples/sec ({'guided joint' if guide else 'joint' if joint else 'sequential'} "
+                  f"CDM config)",
         "value": round(a.batch * ws * a.steps / elapsed, 2),
         "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
@@ -418,7 +427,8 @@ def main_cdm(a, ws, rank):
         "data": f"synthetic GHM draws (native ConditionalDenoiseSampler, p=0.2, sigma=1), ring of {a.ring} "
                 f"batches resident in HBM",
         "config": {"workload": (f"cdm_joint: ConditionalDenoiseEncoderTransformer(L={L}, d=128, T=162 = 81 text "
-                                f"tokens + 81 noisy image leaves, sequential=False) + on-device BP_DNS compare, "
+                                f"tokens + 81 noisy image leaves, sequential=False{', guide=True' if guide else ''}) + on-device "
+                                f"BP_DNS compare{' and BP guide targets + 26 guided-block penalties' if guide else ''}, "
                                 f"fwd+bwd+clip+AdamW" if joint else
                                 f"cdm_sequential: ConditionalDenoiseEncoderTransformer(L={L}, d=128, T=82) + frozen "
                                 f"CLIP text EncoderTransformer(L=5) forward + on-device BP_DNS compare, "

@@ -14,7 +14,7 @@ grep -E "passed|failed" $OUT/gpu_tests.log | tail -2
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 3
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
 cat $OUT/bench.json
-for w in vlm cdm cdm_joint vlm_joint; do
+for w in vlm cdm cdm_joint cdm_guided vlm_joint; do
   timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 5
   echo "$w $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$w.json)"
 done
