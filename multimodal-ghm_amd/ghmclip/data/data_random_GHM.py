@@ -376,7 +376,8 @@ class ConditionalDenoiseSampler(DoubleSampler):
         t_pp [V, B]), (z float32 [B, T], image_leaves int64 [B, T], None,
         posterior means float64 [B, T])."""
         if guide:
-            raise NotImplementedError("guided CDM (guided_info targets) is not built yet")
+            raise NotImplementedError("guided CDM targets (guided_info) are computed on the device inside the "
+                                      "fused CdmTrainer step (ghm_bp_dns_msgs / ghm_bp_cls), not by the sampler")
         tl, root, z, il = self.draw_numpy(batch_size)
         t_pp, post = self.posterior(tl, z)
         to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
