@@ -229,6 +229,14 @@ int ghm_guide_blk_fwd(const float* H, int T, int tok0, int ntok, int col, const 
                       int64_t moff, int ext, int V, float* part, int64_t n_seq, void* stream);
 int ghm_guide_blk_bwd(const float* H, int T, int tok0, int ntok, int col, const float* msgs, int64_t msg_stride,
                       int64_t moff, int ext, int V, float* dH, float scale, int64_t n_seq, void* stream);
+/* The same for a list of nb <= 32 blocks in one launch (block k: residual stream
+ * H[k], messages msgs[k], desc[6k..6k+5] = {T, tok0, ntok, col, ext, V},
+ * desc64[2k..2k+1] = {msg_stride, moff}); blocks apply in list order.
+ * fwd: part[k*n_seq + n];  bwd: every block adds into the one dH. */
+int ghm_guide_blks_fwd(const float* const* H, const float* const* msgs, const int32_t* desc, const int64_t* desc64,
+                       int nb, float* part, int64_t n_seq, void* stream);
+int ghm_guide_blks_bwd(const float* const* H, const float* const* msgs, const int32_t* desc, const int64_t* desc64,
+                       int nb, float* dH, float scale, int64_t n_seq, void* stream);
 
 /* ---- sequential conditional denoising (CDM, train_sequential_DNS.py) ---------
  * ConditionalDenoiseEncoderTransformer (models/model.py:337-532, sequential=True)

@@ -287,6 +287,93 @@ extern "C" int ghm_guide_blk_bwd(const float* H, int T, int tok0, int ntok, int 
   return ghm_launch_status();
 }
 
+// One launch for a list of guided blocks (the 26 blocks of the guided joint CDM
+// cost one launch each otherwise).  One workgroup per sequence walks the blocks
+// in list order with a barrier between them, so blocks that share columns of dH
+// are applied one after another exactly as the per-block launches do.
+// fwd: part[k * n_seq + n] for block k;  bwd: dH (shared by every block) +=.
+constexpr int GUIDE_MAXBLK = 32;
+struct GuideBlkSet {
+  const float* H[GUIDE_MAXBLK];
+  const float* msgs[GUIDE_MAXBLK];
+  GuideBlk b[GUIDE_MAXBLK];
+  int nb;
+};
+
+__global__ __launch_bounds__(256) void k_guide_blks_fwd(GuideBlkSet set, float* __restrict__ part, int n_seq) {
+  __shared__ float red[4];
+  const int n = blockIdx.x;
+  for (int k = 0; k < set.nb; ++k) {
+    const GuideBlk& b = set.b[k];
+    const float* h = set.H[k] + (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+    const float* m = set.msgs[k] + static_cast<int64_t>(n) * b.msg_stride + b.moff;
+    float s = 0.f;
+    for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
+      const int t = e / b.V, c = e - t * b.V;
+      const float dd = h[static_cast<int64_t>(t) * GHM_D + c] - m[(t / b.ext) * b.V + c];
+      s += dd * dd;
+    }
+    s = sum32(s);
+    s += __shfl_xor(s, 32, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[static_cast<int64_t>(k) * n_seq + n] = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_guide_blks_bwd(GuideBlkSet set, float* __restrict__ dH, float scale) {
+  const int n = blockIdx.x;
+  for (int k = 0; k < set.nb; ++k) {
+    const GuideBlk& b = set.b[k];
+    const float* m = set.msgs[k] + static_cast<int64_t>(n) * b.msg_stride + b.moff;
+    const int64_t base = (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+    for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
+      const int t = e / b.V, c = e - t * b.V;
+      const int64_t at = base + static_cast<int64_t>(t) * GHM_D + c;
+      dH[at] += scale * (set.H[k][at] - m[(t / b.ext) * b.V + c]);
+    }
+    __syncthreads();
+  }
+}
+
+// desc[k*6 ..] = {T, tok0, ntok, col, ext, V}, desc64[k*2 ..] = {msg_stride, moff}
+static int guide_blks_set(GuideBlkSet& set, const float* const* H, const float* const* msgs, const int32_t* desc,
+                          const int64_t* desc64, int nb, int64_t n_seq) {
+  if (!(H && msgs && desc && desc64 && nb >= 1 && nb <= GUIDE_MAXBLK)) return -1;
+  set.nb = nb;
+  for (int k = 0; k < nb; ++k) {
+    const int32_t* d = desc + 6 * k;
+    if (!H[k] || !msgs[k]) return -1;
+    if (guide_blk_check(set.b[k], d[0], d[1], d[2], d[3], desc64[2 * k], desc64[2 * k + 1], d[4], d[5], n_seq))
+      return -1;
+    set.H[k] = H[k];
+    set.msgs[k] = msgs[k];
+  }
+  return 0;
+}
+
+extern "C" int ghm_guide_blks_fwd(const float* const* H, const float* const* msgs, const int32_t* desc,
+                                  const int64_t* desc64, int nb, float* part, int64_t n_seq, void* stream) {
+  GHM_CHECK(part, "null pointer");
+  GuideBlkSet set;
+  GHM_CHECK(guide_blks_set(set, H, msgs, desc, desc64, nb, n_seq) == 0, "guide block list");
+  hipLaunchKernelGGL(k_guide_blks_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream), set,
+                     part, static_cast<int>(n_seq));
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_blks_bwd(const float* const* H, const float* const* msgs, const int32_t* desc,
+                                  const int64_t* desc64, int nb, float* dH, float scale, int64_t n_seq,
+                                  void* stream) {
+  GHM_CHECK(dH, "null pointer");
+  GuideBlkSet set;
+  GHM_CHECK(guide_blks_set(set, H, msgs, desc, desc64, nb, n_seq) == 0, "guide block list");
+  hipLaunchKernelGGL(k_guide_blks_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream), set,
+                     dH, scale);
+  return ghm_launch_status();
+}
+
 // ---------------------------------------------------------------------------
 // Dense-target helpers for the module API (GuidedClipLoss(guide=True) on the
 // guided-layer tensors EncoderTransformer.forward returns)

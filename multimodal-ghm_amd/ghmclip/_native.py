@@ -62,6 +62,8 @@ HIP_SIGNATURES = {
     "ghm_bp_dns_msgs": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _p],
     "ghm_guide_blk_fwd": [_p, _i, _i, _i, _i, _p, _i64, _i64, _i, _i, _p, _i64, _p],
     "ghm_guide_blk_bwd": [_p, _i, _i, _i, _i, _p, _i64, _i64, _i, _i, _p, _f, _i64, _p],
+    "ghm_guide_blks_fwd": [_p, _p, _p, _p, _i, _p, _i64, _p],
+    "ghm_guide_blks_bwd": [_p, _p, _p, _p, _i, _p, _f, _i64, _p],
     "ghm_cdm_readout_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ls_loss": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_cdm_readout_bwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],

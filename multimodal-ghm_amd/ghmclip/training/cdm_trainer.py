@@ -151,31 +151,50 @@ class CdmTrainer:
         self.gpart = torch.zeros(self.n_gparts, self.B, dtype=torch.float32, device=self.device)
         self.gloss = torch.zeros(3, dtype=torch.float32, device=self.device)
         self.phist = torch.zeros_like(self.hist)
+        self._blk_lists, self._gfwd, self._gbwd = [], None, {}
 
     def _blk_args(self, blk):
         src, tok0, ntok, col, moff, ext = blk
         msgs = self.imsgs if src == "i" else self.tmsgs
         return tok0, ntok, col, _p(msgs), msgs[0].numel(), moff, ext, self.tree[4]
 
+    def _blk_list(self, items):
+        """Host arrays for ghm_guide_blks_{fwd,bwd}: items = [(layer, block), ...]
+        in launch order; kept alive on self (the HIP graph replays the launch)."""
+        n = len(items)
+        H = (ctypes.c_void_p * n)(*[self.plan.H[l + 1].data_ptr() for l, _ in items])
+        M = (ctypes.c_void_p * n)()
+        desc = (ctypes.c_int32 * (6 * n))()
+        desc64 = (ctypes.c_int64 * (2 * n))()
+        for k, (l, blk) in enumerate(items):
+            tok0, ntok, col, msgs, stride, moff, ext, V = self._blk_args(blk)
+            M[k] = msgs
+            desc[6 * k:6 * k + 6] = [self.T, tok0, ntok, col, ext, V]
+            desc64[2 * k:2 * k + 2] = [stride, moff]
+        lst = (H, M, desc, desc64, n)
+        self._blk_lists.append(lst)
+        return lst
+
     def _guide_fwd(self, s):
-        k = 0
-        for l, blks in sorted(self.gblocks.items()):
-            for blk in blks:
-                _native.call("ghm_guide_blk_fwd", _p(self.plan.H[l + 1]), self.T, *self._blk_args(blk),
-                             _p(self.gpart[k]), self.B, s)
-                k += 1
+        """All guided blocks in one launch; part row k = the k-th block in layer order."""
+        if self._gfwd is None:
+            self._gfwd = self._blk_list([(l, b) for l, blks in sorted(self.gblocks.items()) for b in blks])
+        H, M, desc, desc64, n = self._gfwd
+        _native.call("ghm_guide_blks_fwd", H, M, desc, desc64, n, _p(self.gpart), self.B, s)
 
     def _guide_hooks(self):
-        """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / B."""
+        """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / B,
+        one launch per guided layer."""
         if not self.guide:
             return None
         scale = 2.0 * self.penalty / self.B
         hooks = {}
         for l, blks in self.gblocks.items():
             def fn(dH, s, l=l, blks=blks):
-                for blk in blks:
-                    _native.call("ghm_guide_blk_bwd", _p(self.plan.H[l + 1]), self.T, *self._blk_args(blk),
-                                 _p(dH), scale, self.B, s)
+                if l not in self._gbwd:
+                    self._gbwd[l] = self._blk_list([(l, b) for b in blks])
+                H, M, desc, desc64, n = self._gbwd[l]
+                _native.call("ghm_guide_blks_bwd", H, M, desc, desc64, n, _p(dH), scale, self.B, s)
             hooks[l] = fn
         return hooks
 
