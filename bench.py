@@ -26,11 +26,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-ghm_amd"))
 
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 STEP_GFLOP = 625.87            # algorithmic work per step at B=128
 MLP_FWD_GFLOP_PER_LAUNCH = 4 * 51840 * 128 * 512 / 1e9  # one encoder-layer MLP: 2 GEMMs
 # algorithmic HBM bytes of one LN2+MLP forward launch (fp32): Hmid in + H out
 # ([M,128] each) + G and GELU'(U) out ([M,512] each), M = 51,840 tokens
 MLP_FWD_BYTES_PER_LAUNCH = 4 * 51840 * (128 + 128 + 512 + 512)
+# ... of which only Hmid in and H out must move
+MLP_FWD_MUST_BYTES = 4 * 51840 * (128 + 128)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
@@ -39,16 +42,11 @@ def log(*a):
 
 
 def setup_dist(n_gpus):
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return ws, rank, local
+    """One process per GPU (torchrun env); RCCL, or $GHM_DIST_BACKEND."""
+    from ghmclip.training import distributed
+    ws, rank, device = distributed.setup()
+    torch.cuda.set_device(device)
+    return ws, rank, device.index or 0
 
 
 def build(rank, B, L, p, total_iters, precision=None, guide=False):
@@ -188,6 +186,11 @@ def dominant_kernel(trainer):
     return "k_ln_mlp_fwd", launch
 
 
+def teardown():
+    from ghmclip.training import distributed
+    distributed.teardown()
+
+
 def time_kernel(launch, reps=20):
     """Average duration (ms) of `launch` on the current stream, bracketed by HIP
     events recorded on that same stream."""
@@ -200,6 +203,37 @@ def time_kernel(launch, reps=20):
     e1.record(s)
     e1.synchronize()
     return e0.elapsed_time(e1) / reps
+
+
+def time_kernel_in_step(trainer, kernel, steps=3):
+    """Average duration (ms) of `kernel` INSIDE eager training steps (both towers'
+    streams live, so it shares the GPU exactly as in the step): every launch of
+    that entry point is bracketed by HIP events recorded on the stream it is
+    launched on (its last argument).  Eager steps run the same launch sequence as
+    the captured graph.  Leaves the trainer's step count advanced by `steps`."""
+    from ghmclip import _native
+    real = _native.call
+    pairs = []
+
+    def call(name, *args):
+        if name != kernel:
+            return real(name, *args)
+        st = torch.cuda.ExternalStream(args[-1].value or 0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        real(name, *args)
+        e1.record(st)
+        pairs.append((e0, e1))
+    graphs, trainer.graphs = trainer.graphs, None
+    _native.call = call
+    try:
+        for _ in range(steps):
+            trainer.step()
+    finally:
+        _native.call = real
+        trainer.graphs = graphs
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in pairs) / max(1, len(pairs))
 
 
 def pmc_traffic(kernel):
@@ -259,6 +293,46 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
                       f"{dt:.3f} s/step"}
 
 
+def final_risk(a, ws):
+    """The BASELINE metric's second half: the reference's own default (or guided)
+    CLIP run, exp_clip_{standard,guided}TF.sh at p = 0.2, total_iters = 3000, through
+    the drop-in CLI code path (train_CLIP.run: RNG order sampler(42) -> get_Bayes ->
+    seed(224) -> encoders; live native sampler in its producer thread + pinned
+    H2D, HIP-graph steps), global batch 128 split over the ranks (strong scaling,
+    the same objective as one GPU).  final_risk = mean(loss_history[-100:])
+    (figures/eval-clip-risk.py:29), against the published value
+    (figures/data/ghm-data/clip-risk.json).  The run's loop time is the
+    live-sampler throughput (sampler, staging and every step included)."""
+    import contextlib
+    from ghmclip.training.clip_runs import run_clip
+    arch = "Guided TF" if a.guide else "Standard TF"
+    with contextlib.redirect_stdout(sys.stderr):
+        r = run_clip(arch, 0.2, total_iters=a.risk_iters, teardown=False)
+    loop = r["loop_seconds"]
+    if ws > 1:
+        import torch.distributed as dist
+        t = torch.tensor([loop], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        loop = float(t.item())
+    pub = None
+    path = os.path.join(ROOT, "tests", "golden", "clip_risk_published.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            d = json.load(f)
+        pub = d[arch][d["p_flip"].index(20)]
+    hist = r["loss_history"]
+    return {"value": round(r["final_risk"], 6), "published": pub, "arch": arch, "p_flip": 0.2,
+            "bayes": round(float(r["bayes"]), 6), "total_iters": a.risk_iters,
+            "definition": "mean(loss_history[-100:]) (figures/eval-clip-risk.py:29)",
+            "global_batch_rows": 128, "parallelism": f"dp{ws} (strong: 128 rows split over the ranks)",
+            "first_losses": [round(float(x), 6) for x in hist[:3]],
+            "live_sampler": {"steps": r["steps"], "seconds": round(loop, 3),
+                             "ms_per_step": round(1000 * loop / r["steps"], 4),
+                             "samples_per_s": round(128 * r["steps"] / loop, 1),
+                             "note": "train_CLIP loop: native sampler producer thread + pinned H2D + graph step + "
+                                     "the reference's log-line history sync every 20 steps"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +342,10 @@ def main():
     ap.add_argument("--layers", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-final-risk", action="store_true",
+                    help="skip the reference run (total_iters=3000 through train_CLIP with the live sampler) that "
+                         "gives final_risk and the live-sampler throughput")
+    ap.add_argument("--risk-iters", type=int, default=3000, help="total_iters of the final-risk run (reference: 3000)")
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
@@ -298,35 +376,43 @@ def main():
     finite = bool(np.isfinite(losses).all())
     kname, klaunch = dominant_kernel(tr)
     kern_ms = time_kernel(klaunch)
+    kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
+    risk = None if a.no_final_risk else final_risk(a, ws)
+    del ring, tr
     if rank != 0:
-        if ws > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
+        teardown()
         return
 
     ms = 1000.0 * elapsed / a.steps
     steps_per_s = a.steps / elapsed
     samples = a.batch * ws * a.steps
     step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
-    if tr.precision == "x3":
-        # split-bf16 products run at 5.3x the exact-f32 rate: the kernel's roof is
-        # HBM (algorithmic bytes: Hmid in, H out, G and GELU' out, fp32)
-        traffic = pmc_traffic(kname)
-        achieved = MLP_FWD_BYTES_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
-                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": None if traffic is None else round(traffic * (a.batch / 128)),
-                    "algorithmic_bytes": round(MLP_FWD_BYTES_PER_LAUNCH * (a.batch / 128)),
-                    "kernel_ms": round(kern_ms, 4)}
-    else:
-        traffic = pmc_traffic(kname)
-        achieved = MLP_FWD_GFLOP_PER_LAUNCH * (a.batch / 128) / (kern_ms * 1e-3) / 1e3
-        roofline = {"bound": "mfma", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
-                    "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                    "traffic": None if traffic is None else round(traffic * (a.batch / 128)),
-                    "kernel_ms": round(kern_ms, 4)}
+    scale = a.batch / 128
+    traffic = pmc_traffic(kname)
+    x3 = kname.endswith("x3b")
+    # The kernel's work is 13.59 GFLOP (f32 products) per launch; the bytes that
+    # MUST move are Hmid in and H out (the hidden activation never needs to leave
+    # the chip): AI = 13.59e9 / 53.1e6 = 256 FLOP/B, so the roof is the matrix
+    # cores.  x3 evaluates each f32 product as 3 bf16 MFMA products: its
+    # achieved rate is counted in those (3 x 13.59 GF) against the dense bf16
+    # peak; the f32 mode against the f32 MFMA peak.
+    mult, peak = (3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (1.0, F32_MFMA_PEAK_TFLOPS)
+    kflop = mult * MLP_FWD_GFLOP_PER_LAUNCH * scale
+    achieved = kflop / (kern_ms * 1e-3) / 1e3
+    achieved_step = kflop / (kern_ms_step * 1e-3) / 1e3
+    roofline = {"bound": "mfma", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
+                "basis": ("bf16 MFMA products issued (3 per f32 product, split-bf16)" if x3
+                          else "f32 MFMA products"),
+                "traffic": None if traffic is None else round(traffic * scale),
+                "algorithmic_bytes": round(MLP_FWD_MUST_BYTES * scale),
+                "design_bytes": round(MLP_FWD_BYTES_PER_LAUNCH * scale),
+                "kernel_ms": round(kern_ms, 4),
+                "kernel_ms_in_step": round(kern_ms_step, 4),
+                "achieved_in_step": round(achieved_step, 2),
+                "frac_in_step": round(achieved_step / peak, 4),
+                "hbm_gbs_design": round(MLP_FWD_BYTES_PER_LAUNCH * scale / (kern_ms * 1e-3) / 1e9, 1)}
     out = {
         "metric": "GHM training samples/sec (CLIP default config)",
         "value": round(samples / elapsed, 2),
@@ -338,7 +424,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
+        "dtype": "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
         "config": {"workload": ("clip_guided: " if a.guide else "clip_default: ")
                    + "2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW"
@@ -350,16 +436,17 @@ def main():
         "steps_per_s": round(steps_per_s, 3),
         "sequences_per_s": round(samples * 10 / elapsed, 1),
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
-        "step_mfma_frac": round(step_gflop * steps_per_s / 1e3 / F32_MFMA_PEAK_TFLOPS, 4),
+        "step_mfma_frac": round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
+        "step_mfma_basis": f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s",
         "loss_finite": finite,
         "last_loss": float(losses[-1]) if len(losses) else None,
     }
+    if risk is not None:
+        out["final_risk"] = risk
     if ws == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.batch, a.layers, guide=a.guide)
     print(json.dumps(out), flush=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    teardown()
 
 
 def timed_steps(a, ws, tr, one):
@@ -409,9 +496,7 @@ def main_cdm(a, ws, rank):
     kname, klaunch = dominant_kernel(tr)
     kern_ms = time_kernel(klaunch)
     if rank != 0:
-        if ws > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
+        teardown()
         return
     M = a.batch * T
     mlp_bytes = 4 * M * (128 + 128 + 512 + 512)
@@ -445,9 +530,7 @@ def main_cdm(a, ws, rank):
     if ws == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=8 if not joint else 4, workload=a.workload)
     print(json.dumps(out), flush=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    teardown()
 
 
 def main_vlm(a, ws, rank):
@@ -476,9 +559,7 @@ def main_vlm(a, ws, rank):
     else:
         kern_ms = time_kernel(lambda: torch.addmm(b1, plan.X2[0], w1.t(), out=plan.U))
     if rank != 0:
-        if ws > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
+        teardown()
         return
     gflop = 2.0 * M * D * F / 1e9
     if plan.precision == "x3":
@@ -525,9 +606,7 @@ def main_vlm(a, ws, rank):
     if ws == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.batch, L, steps=4, workload=a.workload)
     print(json.dumps(out), flush=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    teardown()
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import distributed
 from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan, cdm_guide_blocks
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
@@ -235,8 +236,7 @@ class CdmTrainer:
                      self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
 
     def _allreduce(self):
-        import torch.distributed as dist
-        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+        distributed.allreduce_mean_(self.gflat, group=self.pg)
 
     def set_batch(self, t_tokens, i_tokens, z):
         """Stage one batch: text / image leaves uint8 [B, 81] and the noisy image
@@ -249,7 +249,7 @@ class CdmTrainer:
         """One training step on the staged batch (async; no host sync)."""
         if self.steps_done >= self.n_sched:
             raise RuntimeError("schedule exhausted")
-        dp = self.pg is not None or _dist_on()
+        dp = self.pg is not None or distributed.is_on()
         if self.graphs is not None:
             self.graphs[0].replay()
             if dp:
@@ -310,8 +310,3 @@ class CdmTrainer:
                 if st and name in self.md:
                     self.md[name].copy_(st["m"])
                     self.vd[name].copy_(st["v"])
-
-
-def _dist_on():
-    import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import distributed
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
@@ -201,8 +202,7 @@ class ClipTrainer:
                      self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
 
     def _allreduce(self):
-        import torch.distributed as dist
-        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+        distributed.allreduce_mean_(self.gflat, group=self.pg)
 
     def set_tokens(self, t_tokens, i_tokens):
         """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
@@ -217,12 +217,12 @@ class ClipTrainer:
             raise RuntimeError("schedule exhausted")
         if self.graphs is not None:
             self.graphs[0].replay()
-            if self.pg is not None or _dist_on():
+            if self.pg is not None or distributed.is_on():
                 self._allreduce()
             self.graphs[1].replay()
         else:
             self._fwd_bwd()
-            if self.pg is not None or _dist_on():
+            if self.pg is not None or distributed.is_on():
                 self._allreduce()
             self._optim()
         self.steps_done += 1
@@ -271,8 +271,3 @@ class ClipTrainer:
                     if st:
                         md[name].copy_(st["m"])
                         vd[name].copy_(st["v"])
-
-
-def _dist_on():
-    import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1

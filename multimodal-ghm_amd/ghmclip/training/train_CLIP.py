@@ -30,6 +30,7 @@ import torch
 from ..data import ClipSampler
 from ..models import AdamW, EncoderTransformer, GuidedClipLoss, get_lr_cosine_schedule, seed_everything  # noqa: F401
 from ..utils import ClipModelConfig, DoubleTreeConfig, GenLogger, UtilConfig, logging
+from . import distributed
 from .clip_trainer import ClipTrainer
 from .pipeline import BatchPipeline
 
@@ -69,20 +70,18 @@ def run_names(c):
 
 
 def main(argv=None):
-    c = parse(argv)
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if ws > 1:
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        device = torch.device("cuda", local)
-    else:
-        if not torch.cuda.is_available():
-            raise RuntimeError("ghmclip (MI355X build) needs a HIP device")
-        device = torch.device("cuda")
-        print(f"Using GPU: {torch.cuda.get_device_name(0)}")
+    """The CLI entry point: returns loss_history (length total_iters + 1)."""
+    return run(parse(argv))["loss_history"]
+
+
+def run(c, teardown=True):
+    """Train with configuration c; returns the histories, the Bayes loss, the
+    final CLIP risk (figures/eval-clip-risk.py:29: mean of the last 100
+    loss_history entries) and the wall time of the training loop (sampler,
+    H2D staging and every step included)."""
+    ws, rank, device = distributed.setup()
+    if ws == 1:
+        print(f"Using GPU: {torch.cuda.get_device_name(0)}", file=sys.stderr if c.raw else sys.stdout)
     if c.batch_size % ws:
         raise ValueError(f"batch_size {c.batch_size} must be divisible by the world size {ws}")
 
@@ -164,11 +163,7 @@ def main(argv=None):
     def sync_hist(upto):
         h = trainer.loss_history(upto - start)
         ph = trainer.ploss_history(upto - start)  # == h without guidance
-        if ws > 1:
-            import torch.distributed as dist
-            t = torch.from_numpy(np.stack([h, ph])).to(device)
-            dist.all_reduce(t, op=dist.ReduceOp.AVG)
-            h, ph = t.cpu().numpy()
+        h, ph = distributed.mean_histories([h, ph], device)  # every rank
         loss_history[start:upto] = h
         ploss_history[start:upto] = ph
 
@@ -178,6 +173,7 @@ def main(argv=None):
 
     curr_time = time.time()
     lr = sched[0]
+    loop_t0 = time.perf_counter()
     try:
         for iter_num in range(start, total):
             pipe.next_into(trainer)
@@ -198,11 +194,15 @@ def main(argv=None):
                 if wandb:
                     wandb.log({'train_loss': loss_history[iter_num], 'penalty_train_loss': ploss_history[iter_num],
                                'lr': lr, 'Bayes_loss': Bayes_loss, 'Bayes_std': Bayes_std, 'iter': iter_num})
-            if iter_num % c.eval_interval == 0 and not raw:
-                sync_hist(iter_num + 1)
-                save(iter_num)
+            if iter_num % c.eval_interval == 0:
+                sync_hist(iter_num + 1)  # a collective: every rank, not only the saving one
+                if not raw:
+                    save(iter_num)
     finally:
         pipe.close()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    loop_s = time.perf_counter() - loop_t0
     sync_hist(total)
     if not raw:
         save(total)
@@ -211,10 +211,11 @@ def main(argv=None):
         import s3fs
         s3fs.S3FileSystem().put(directory, c.S3_bucket_name + f'/GHM/{c.job_name}/{tree_folder}/{model_name}/{timestamp}',
                                 recursive=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
-    return loss_history
+    if teardown:
+        distributed.teardown()
+    return {"loss_history": loss_history, "ploss_history": ploss_history, "bayes": Bayes_loss,
+            "final_risk": float(np.mean(loss_history[-100:])), "loop_seconds": loop_s, "steps": total - start,
+            "world_size": ws, "batch_size": c.batch_size}
 
 
 if __name__ == "__main__":

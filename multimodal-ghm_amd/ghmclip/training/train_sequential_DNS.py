@@ -28,6 +28,7 @@ from ..data import ConditionalDenoiseSampler
 from ..models import (AdamW, ConditionalDenoiseEncoderTransformer, ConditionalGuidedLsLoss, EncoderTransformer,
                       get_lr_cosine_schedule, seed_everything)
 from ..utils import DoubleTreeConfig, GenLogger, ModelConfig, UtilConfig, logging
+from . import distributed
 from .cdm_trainer import CdmTrainer
 from .pipeline import CdmBatchPipeline
 from .train_CLIP import load_checkpoint
@@ -82,18 +83,8 @@ def main(argv=None):
     c = parse(argv)
     if c.guide:
         raise NotImplementedError("guided CDM (guide=True) is not built on the HIP path yet")
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if ws > 1:
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        device = torch.device("cuda", local)
-    else:
-        if not torch.cuda.is_available():
-            raise RuntimeError("ghmclip (MI355X build) needs a HIP device")
-        device = torch.device("cuda")
+    ws, rank, device = distributed.setup()
+    if ws == 1:
         print(f"Using GPU: {torch.cuda.get_device_name(0)}")
     if c.batch_size % ws:
         raise ValueError(f"batch_size {c.batch_size} must be divisible by the world size {ws}")
@@ -167,11 +158,7 @@ def main(argv=None):
 
     def sync_hist(upto):
         h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
-        if ws > 1:
-            import torch.distributed as dist
-            t = torch.from_numpy(np.stack([h, ch])).to(device)
-            dist.all_reduce(t, op=dist.ReduceOp.AVG)
-            h, ch = t.cpu().numpy()
+        h, ch = distributed.mean_histories([h, ch], device)  # every rank
         loss_history[:upto] = h
         ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
         compare_history[:upto] = ch
@@ -204,9 +191,10 @@ def main(argv=None):
                     wandb.log({'train_loss': loss_history[iter_num], 'penalty_train_loss': ploss_history[iter_num],
                                'Compare': compare_history[iter_num], 'lr': lr, 'Bayes_loss': Bayes_loss,
                                'Bayes_std': Bayes_std, 'iter': iter_num})
-            if iter_num % c.eval_interval == 0 and not raw:
-                sync_hist(iter_num + 1)
-                save(iter_num)
+            if iter_num % c.eval_interval == 0:
+                sync_hist(iter_num + 1)  # a collective: every rank, not only the saving one
+                if not raw:
+                    save(iter_num)
     finally:
         pipe.close()
     sync_hist(c.total_iters)
@@ -217,9 +205,7 @@ def main(argv=None):
         import s3fs
         s3fs.S3FileSystem().put(directory, c.S3_bucket_name + f'/GHM/{c.job_name}/{tree_folder}/{model_name}/{timestamp}',
                                 recursive=True)
-    if ws > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    distributed.teardown()
     return loss_history, compare_history
 
 

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import distributed
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 from ..models.vlm import VLM_JOINT_UNTRAINED, VLM_UNTRAINED, VlmPlan
@@ -125,8 +126,7 @@ class VlmTrainer:
                      self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
 
     def _allreduce(self):
-        import torch.distributed as dist
-        dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.pg)
+        distributed.allreduce_mean_(self.gflat, group=self.pg)
 
     def set_batch(self, xt, yt, post, i_tokens):
         """Stage one batch: text inputs / targets uint8 [B, T-1], BP posteriors
@@ -139,7 +139,7 @@ class VlmTrainer:
     def step(self):
         if self.steps_done >= self.n_sched:
             raise RuntimeError("schedule exhausted")
-        dp = self.pg is not None or _dist_on()
+        dp = self.pg is not None or distributed.is_on()
         if self.graphs is not None:
             self.graphs[0].replay()
             if dp:
@@ -188,8 +188,3 @@ class VlmTrainer:
                 if st and name in self.md:
                     self.md[name].copy_(st["m"])
                     self.vd[name].copy_(st["v"])
-
-
-def _dist_on():
-    import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1

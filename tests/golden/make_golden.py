@@ -141,8 +141,10 @@ def step_fixture(name, L, d, B, nsteps, p=0.2, total_iters=3000, checksum_only=F
     print("wrote", name)
 
 
-def curve_fixture(steps, p=0.2, B=128, total_iters=3000):
-    """Default CLIP config (scripts/experiments/exp_clip_standardTF.sh:15-40)."""
+def curve_fixture(steps, p=0.2, B=128, total_iters=3000, out="clip_default_curve.npz"):
+    """Default CLIP config (scripts/experiments/exp_clip_standardTF.sh:15-40).
+    With steps = total_iters + 1 this is the whole reference run (F5): its final
+    risk is mean(loss_history[-100:]) (figures/eval-clip-risk.py:29)."""
     s = make_sampler(p)
     seed_everything(224)
     tm, im = build_models(81, 5, 128)
@@ -167,10 +169,13 @@ def curve_fixture(steps, p=0.2, B=128, total_iters=3000):
         opt.step()
         if it % 20 == 0:
             print(f"curve step {it} loss {hist[it]:.6f} ({time.time()-t0:.0f}s)", flush=True)
-    np.savez_compressed(os.path.join(HERE, "clip_default_curve.npz"), loss_history=hist,
+        if it % 200 == 0 and steps > 1000:  # checkpoint the long run
+            np.savez_compressed(os.path.join(HERE, out), loss_history=hist[:it + 1], grad_norm=norms[:it + 1],
+                                p=p, B=B, total_iters=total_iters, threads=torch.get_num_threads())
+    np.savez_compressed(os.path.join(HERE, out), loss_history=hist,
                         grad_norm=norms, p=p, B=B, total_iters=total_iters,
                         threads=torch.get_num_threads())
-    print("wrote clip_default_curve.npz")
+    print("wrote", out)
 
 
 def build_guided(T, L, d):
@@ -294,9 +299,13 @@ def bayes_fixture():
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--curve-steps", type=int, default=200)
+    ap.add_argument("--curve-out", default="clip_default_curve.npz")
+    ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--only", default="")
     ap.add_argument("--guide-steps", type=int, default=100)
     a = ap.parse_args()
+    if a.threads:
+        torch.set_num_threads(a.threads)
     jobs = a.only.split(",") if a.only else ["sampler", "tiny", "d128", "bayes", "curve"]
     if "sampler" in jobs:
         sampler_fixture(0.2, 128, 3, "sampler_p20.npz")
@@ -308,7 +317,7 @@ if __name__ == "__main__":
     if "bayes" in jobs:
         bayes_fixture()
     if "curve" in jobs:
-        curve_fixture(a.curve_steps)
+        curve_fixture(a.curve_steps, out=a.curve_out)
     if "guide_bp" in jobs:
         guide_bp_fixture()
     if "guide_tiny" in jobs:

@@ -133,3 +133,58 @@ def test_joint_vlm_cli(tmp_path, monkeypatch):
     assert set(d) == {"model_state_dict", "optimizer_state_dict", "loss", "iter", "loss_history", "ploss_history",
                       "bayes", "compare"}
     assert d["model_state_dict"]["position_embeddings.weight"].shape == (161, 256)
+
+
+CLIP_CKPT_KEYS = {"tmodel_state_dict", "imodel_state_dict", "optimizer_state_dict", "iter", "loss_history",
+                  "ploss_history", "bayes"}  # /root/reference/src/ghmclip/training/train_CLIP.py:193-211
+
+
+def test_clip_checkpoint_contract_and_resume(tmp_path, monkeypatch):
+    """The CLIP checkpoint dict (train_CLIP.py:193-211): exactly the reference's keys,
+    state dicts with the reference's key names, loss_history of length
+    total_iters + 1 (what figures/eval-clip-risk.py:29 averages the last 100 of),
+    iter = total_iters + 1 after the final save.  Resume (--init_from) from the
+    eval-interval save at iter 4 reproduces the uninterrupted run bit for bit
+    (weights, AdamW moments and step count, the sampler stream and both histories)."""
+    import shutil
+
+    from ghmclip import EncoderTransformer
+    from ghmclip.training import train_CLIP
+    from ghmclip.training.train_CLIP import load_checkpoint
+    flags = [f for f in CLIP_FLAGS if not f.startswith(("--total_iters", "--eval_interval"))]
+    flags += ["--total_iters=8", "--eval_interval=4"]
+    real_save = torch.save
+    snap = str(tmp_path / "ck_iter4.pth")
+
+    def save(obj, path, *a, **k):
+        real_save(obj, path, *a, **k)
+        if isinstance(obj, dict) and obj.get("iter") == 4:
+            shutil.copy(path, snap)
+    monkeypatch.setattr(torch, "save", save)
+    (tmp_path / "a").mkdir()
+    monkeypatch.chdir(tmp_path / "a")
+    full = train_CLIP.main(flags)
+    ck = glob.glob("logs/CLIP/*/*/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert set(d) == CLIP_CKPT_KEYS
+    assert d["iter"] == 9 and len(d["loss_history"]) == 9 and len(d["ploss_history"]) == 9
+    np.testing.assert_array_equal(d["loss_history"], full)
+    ref_keys = set(EncoderTransformer(81, 10, 128, 5).state_dict())
+    assert set(d["tmodel_state_dict"]) == ref_keys and set(d["imodel_state_dict"]) == ref_keys
+    assert len(d["optimizer_state_dict"]["state"]) == 2 * len(ref_keys)
+    assert float(d["loss_history"][-100:].mean()) == float(np.mean(full))  # eval-clip-risk.py:29
+
+    d4 = load_checkpoint(snap, "cpu")
+    assert d4["iter"] == 4
+    (tmp_path / "b").mkdir()
+    monkeypatch.chdir(tmp_path / "b")
+    resumed = train_CLIP.main(flags + [f"--init_from={snap}"])
+    np.testing.assert_array_equal(resumed, full)
+    d2 = load_checkpoint(glob.glob("logs/CLIP/*/*/*/checkpoint.pth")[0], "cpu")
+    for k in ("tmodel_state_dict", "imodel_state_dict"):
+        for n, v in d[k].items():
+            assert torch.equal(v, d2[k][n]), n
+    for pid, st in d["optimizer_state_dict"]["state"].items():
+        st2 = d2["optimizer_state_dict"]["state"][pid]
+        assert st["t"] == st2["t"] and torch.equal(st["m"], st2["m"]) and torch.equal(st["v"], st2["v"])
