@@ -17,7 +17,7 @@ $(LIBDIR)/libghm_hip.so: $(HIP_SRCS) $(HIP_HDRS)
 
 $(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h
 	@mkdir -p $(LIBDIR)
-	$(CXX) -O3 -std=c++17 -fPIC -shared -o $@ $(SRC)/ghm_sampler.cpp
+	$(CXX) -O3 -std=c++17 -fPIC -shared -pthread -o $@ $(SRC)/ghm_sampler.cpp
 
 resource-usage: $(HIP_SRCS) $(HIP_HDRS)
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_fwd.hip -o /tmp/ghm_fwd.o

@@ -79,6 +79,22 @@ def make_ring(sampler, B, R):
     return ring.cuda()
 
 
+def time_sampler(sampler, B, reps=40):
+    """Host cost of one ClipSampler.get_batch(B) draw on the native sampler
+    (serial MT19937 stream + threaded inverse-CDF expansion), ms per batch."""
+    rows = B * 5
+    t = np.empty((rows, 81), np.uint8)
+    i = np.empty((rows, 81), np.uint8)
+    for _ in range(5):
+        sampler.native.next_into(B, t, i)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sampler.native.next_into(B, t, i)
+    ms = 1000 * (time.perf_counter() - t0) / reps
+    return {"ms_per_batch": round(ms, 3), "batch_rows": B, "threads": int(os.environ.get("GHM_SAMPLER_THREADS", "4")),
+            "what": "ClipSampler.get_batch(B) equivalent (both trees, 2 x B(K+1) sequences), native"}
+
+
 def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False, guide=False):
     """BASELINE config 4 (exp_cdm_standardTF.sh): sequential CDM, L=9, d=128,
     lr 1e-3 -> 1e-6, sigma 1, frozen CLIP text encoder (random init: no checkpoint
@@ -366,6 +382,7 @@ def main():
     total_iters = max(3000, a.steps + a.warmup + 1)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
     ring = make_ring(sampler, a.batch, a.ring)
+    host_sampler = time_sampler(sampler, a.batch)
 
     def one(k):
         tr.set_tokens(ring[k % a.ring, 0], ring[k % a.ring, 1])
@@ -441,6 +458,7 @@ def main():
         "loss_finite": finite,
         "last_loss": float(losses[-1]) if len(losses) else None,
     }
+    out["host_sampler"] = host_sampler
     if risk is not None:
         out["final_risk"] = risk
     if ws == 1 and not a.no_cpu_baseline:

@@ -9,7 +9,8 @@
  *
  * Ownership: the handle owns only host memory; output buffers are caller-owned.
  * Errors: int return, 0 = success, negative GHM_E* on bad arguments.
- * Threading: one handle per thread; no global state.
+ * Threading: one handle per calling thread (each handle owns a small worker pool
+ * for the tree expansion); no global state.
  */
 #ifndef GHM_SAMPLER_H
 #define GHM_SAMPLER_H
@@ -42,6 +43,15 @@ int ghm_sampler_get_state(const ghm_sampler* s, uint32_t* key, int* pos);
  * (image rows [0,2B) reuse the text roots), text tree, image tree. */
 int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves,
                      uint8_t* t_root, uint8_t* i_root);
+
+/* The same draw (the stream advances by the WHOLE batch, as get_batch(B) does),
+ * returning only the data-parallel shard: rows [k*B + lo, k*B + lo + n) of every
+ * block k = 0..K, i.e. outputs are [(K+1)*n][T] (and [(K+1)*n] roots).  The
+ * serial part is the MT19937 stream; the inverse-CDF expansion runs only for the
+ * shard's rows, on $GHM_SAMPLER_THREADS (default 4) threads.  Replaces
+ * get_batch + the per-rank row slice of the data-parallel CLI. */
+int ghm_sampler_next_shard(ghm_sampler* s, int B, int lo, int n, uint8_t* t_leaves, uint8_t* i_leaves,
+                           uint8_t* t_root, uint8_t* i_root);
 
 /* One ConditionalDenoiseSampler.get_batch(batch_size=B) draw
  * (data_random_GHM.py:854-869; replaces the per-node Python loop and np.random.randn):

@@ -9,7 +9,13 @@
 #include "../../include/ghm_sampler.h"
 
 #include <cmath>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -29,20 +35,31 @@ struct MT19937 {
     pos = kN;
   }
 
+  // One MT19937 twist, written so that the compiler vectorises it: within a
+  // group of 4 words, key[kk + 1 .. kk + 4] are read before group kk writes
+  // them (the only in-place overlap), which the explicit temporaries make plain.
   void generate() {
-    static const uint32_t mag01[2] = {0u, 0x9908b0dfu};
+    constexpr uint32_t UP = 0x80000000u, LO = 0x7fffffffu, MAG = 0x9908b0dfu;
     int kk = 0;
-    uint32_t y;
+    for (; kk + 4 <= kN - kM; kk += 4) {
+      uint32_t y[4], r[4];
+      for (int i = 0; i < 4; ++i) y[i] = (key[kk + i] & UP) | (key[kk + i + 1] & LO);
+      for (int i = 0; i < 4; ++i) r[i] = key[kk + i + kM] ^ (y[i] >> 1) ^ ((0u - (y[i] & 1u)) & MAG);
+      for (int i = 0; i < 4; ++i) key[kk + i] = r[i];
+    }
     for (; kk < kN - kM; ++kk) {
-      y = (key[kk] & 0x80000000u) | (key[kk + 1] & 0x7fffffffu);
-      key[kk] = key[kk + kM] ^ (y >> 1) ^ mag01[y & 1u];
+      const uint32_t y = (key[kk] & UP) | (key[kk + 1] & LO);
+      key[kk] = key[kk + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & MAG);
     }
-    for (; kk < kN - 1; ++kk) {
-      y = (key[kk] & 0x80000000u) | (key[kk + 1] & 0x7fffffffu);
-      key[kk] = key[kk + (kM - kN)] ^ (y >> 1) ^ mag01[y & 1u];
+    for (; kk + 4 <= kN - 1; kk += 4) {
+      uint32_t y[4], r[4];
+      for (int i = 0; i < 4; ++i) y[i] = (key[kk + i] & UP) | (key[kk + i + 1] & LO);
+      for (int i = 0; i < 4; ++i) r[i] = key[kk + i + (kM - kN)] ^ (y[i] >> 1) ^ ((0u - (y[i] & 1u)) & MAG);
+      for (int i = 0; i < 4; ++i) key[kk + i] = r[i];
     }
-    y = (key[kN - 1] & 0x80000000u) | (key[0] & 0x7fffffffu);
-    key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ mag01[y & 1u];
+    static_assert((kN - 1 - (kN - kM)) % 4 == 0, "second twist range is whole groups of 4");
+    const uint32_t y = (key[kN - 1] & UP) | (key[0] & LO);
+    key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & MAG);
     pos = 0;
   }
 
@@ -54,6 +71,28 @@ struct MT19937 {
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     return y;
+  }
+
+  static inline uint32_t temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+
+  // n consecutive next32() outputs: whole 624-word blocks are regenerated and
+  // tempered in straight loops (vectorised), the partial ends word by word
+  void fill(uint32_t* out, size_t n) {
+    size_t i = 0;
+    while (i < n && pos < kN) out[i++] = temper(key[pos++]);
+    while (n - i >= static_cast<size_t>(kN)) {
+      generate();
+      for (int k = 0; k < kN; ++k) out[i + k] = temper(key[k]);
+      i += kN;
+      pos = kN;
+    }
+    while (i < n) out[i++] = next32();
   }
 
   inline double next_double() {  // numpy legacy random_sample
@@ -76,14 +115,85 @@ struct MT19937 {
 
 }  // namespace
 
+// Fixed worker pool for the tree expansion (the MT stream itself is serial).
+// Workers park on a condition variable between batches; run(f) calls f(w) for
+// w = 0..n-1, w = 0 on the calling thread, and returns when all are done.
+class Pool {
+ public:
+  explicit Pool(int n) : n_(n < 1 ? 1 : n) {
+    for (int w = 1; w < n_; ++w) th_.emplace_back([this, w] { loop(w); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int)>& f) {
+    if (n_ == 1) {
+      f(0);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &f;
+      left_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [this] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int w) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(w);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--left_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+  bool stop_ = false;
+};
+
+static int pool_threads() {
+  const char* e = std::getenv("GHM_SAMPLER_THREADS");
+  int n = e ? std::atoi(e) : 4;
+  const int hw = static_cast<int>(std::thread::hardware_concurrency());
+  if (hw > 0 && n > hw) n = hw;
+  return n < 1 ? 1 : (n > 64 ? 64 : n);
+}
+
 struct ghm_sampler {
-  int n_layer, n_child, V, K, T;
+  int n_layer, n_child, V, K, T, n_runs;  // n_runs = tree nodes below the root
   // cdf[tree][layer][child][row][col], cumulative sums in the reference's order
   std::vector<double> cdf;
   MT19937 mt;
   int has_gauss = 0;  // numpy legacy Gaussian cache (RandomState state[3], state[4])
   double gauss = 0.0;
-  std::vector<uint8_t> plane_a, plane_b;  // [n_nodes][rows] value planes
+  std::vector<uint32_t> stream;  // raw u32 draws of the current batch's trees
+  std::unique_ptr<Pool> pool;
 };
 
 // numpy legacy_gauss: polar Box-Muller on random_sample pairs, the second
@@ -128,6 +238,9 @@ extern "C" ghm_sampler* ghm_sampler_create(const double* t_trans, const double* 
   if (T > (1 << 20)) return nullptr;
   ghm_sampler* s = new ghm_sampler();
   s->n_layer = n_layer; s->n_child = n_child; s->V = V; s->K = K; s->T = static_cast<int>(T);
+  s->n_runs = static_cast<int>((T * n_child - 1) / (n_child - 1 > 0 ? n_child - 1 : 1)) - 1;
+  if (n_child == 1) s->n_runs = n_layer;
+  s->pool.reset(new Pool(pool_threads()));
   const size_t per = static_cast<size_t>(n_layer) * n_child * V * V;
   s->cdf.resize(2 * per);
   build_cdf(t_trans, n_layer, n_child, V, s->cdf.data());
@@ -170,58 +283,113 @@ extern "C" int ghm_sampler_choice(ghm_sampler* s, int V, int64_t n, int64_t* out
   return 0;
 }
 
-// One tree: roots [rows] -> leaves [rows][T] (uint8, row-major).
-static void sample_tree(ghm_sampler* s, const double* cdf, const uint8_t* root, int rows,
-                        uint8_t* leaves) {
-  const int V = s->V, C = s->n_child;
-  std::vector<uint8_t>& cur = s->plane_a;
-  std::vector<uint8_t>& nxt = s->plane_b;
-  cur.assign(root, root + rows);
-  int n_par = 1;
-  for (int layer = 0; layer < s->n_layer; ++layer) {
-    nxt.resize(static_cast<size_t>(n_par) * C * rows);
-    for (int p = 0; p < n_par; ++p) {
-      const uint8_t* pv = cur.data() + static_cast<size_t>(p) * rows;
-      for (int c = 0; c < C; ++c) {
-        const double* m = cdf + static_cast<size_t>(layer * C + c) * V * V;
-        uint8_t* out = nxt.data() + (static_cast<size_t>(p) * C + c) * rows;
-        for (int b = 0; b < rows; ++b) {
-          const double u = s->mt.next_double();
-          const double* row = m + static_cast<size_t>(pv[b]) * V;
-          int v = 0;  // (u < cdf).argmax(): first True, 0 when none is True
-          for (int k = 0; k < V; ++k) {
-            if (u < row[k]) { v = k; break; }
+// The reference draws a tree level by level: for each parent node (BFS) and
+// child slot, ONE np.random.rand(rows) vector, i.e. a run of `rows` consecutive
+// doubles (2 u32 each) per child node, in the child's BFS order
+// (data_random_GHM.py:153-165).  The whole run of a tree is therefore a fixed
+// slice of the stream once the roots are drawn: it is pulled serially here
+// (0.6 M u32 for the default batch), and the inverse-CDF expansion of any set
+// of rows runs in parallel (expand_rows), reading each row's draws at fixed
+// offsets.  The result is bit-identical to the reference's draw.
+static void pull_stream(ghm_sampler* s, size_t n_u32, uint32_t* out) { s->mt.fill(out, n_u32); }
+
+static inline double to_double(uint32_t a, uint32_t b) {  // numpy legacy random_sample
+  return (static_cast<int32_t>(a >> 5) * 67108864.0 + static_cast<int32_t>(b >> 6)) / 9007199254740992.0;
+}
+
+// Expand rows [r0, r1) of the rows listed in `sel` (indices into the batch of
+// `rows` trees whose draws start at `draws`): values of every node in a
+// [n_nodes][RB] scratch plane, leaves written row-major to out[i][T].
+static void expand_rows(const ghm_sampler* s, const double* cdf, const uint32_t* draws, int rows,
+                        const uint8_t* root, const int* sel, int r0, int r1, uint8_t* out) {
+  constexpr int RB = 32;
+  const int V = s->V, C = s->n_child, T = s->T;
+  const int n_nodes = s->n_runs + 1;
+  std::vector<uint8_t> val(static_cast<size_t>(n_nodes) * RB);
+  for (int i0 = r0; i0 < r1; i0 += RB) {
+    const int nb = (r1 - i0) < RB ? (r1 - i0) : RB;
+    for (int i = 0; i < nb; ++i) val[i] = root[sel[i0 + i]];
+    int first = 0, n_par = 1;  // BFS index of the level's first node, its width
+    for (int layer = 0; layer < s->n_layer; ++layer) {
+      const int child0 = first + n_par;
+      for (int p = 0; p < n_par; ++p) {
+        const uint8_t* pv = val.data() + static_cast<size_t>(first + p) * RB;
+        for (int c = 0; c < C; ++c) {
+          const int node = child0 + p * C + c;
+          const double* m = cdf + static_cast<size_t>(layer * C + c) * V * V;
+          const uint32_t* run = draws + static_cast<size_t>(node - 1) * rows * 2;
+          uint8_t* o = val.data() + static_cast<size_t>(node) * RB;
+          for (int i = 0; i < nb; ++i) {
+            const int b = sel[i0 + i];
+            const double u = to_double(run[2 * b], run[2 * b + 1]);
+            const double* row = m + static_cast<size_t>(pv[i]) * V;
+            // (u < cdf).argmax(): the cdf is non-decreasing, so the first True is
+            // the number of entries <= u; none True (count == V) gives 0
+            int v = 0;
+            for (int k = 0; k < V; ++k) v += row[k] <= u;
+            o[i] = static_cast<uint8_t>(v == V ? 0 : v);
           }
-          out[b] = static_cast<uint8_t>(v);
         }
       }
+      first = child0;
+      n_par *= C;
     }
-    std::swap(cur, nxt);
-    n_par *= C;
-  }
-  // cur: [T][rows] -> leaves [rows][T]
-  const int T = s->T;
-  for (int t = 0; t < T; ++t) {
-    const uint8_t* src = cur.data() + static_cast<size_t>(t) * rows;
-    for (int b = 0; b < rows; ++b) leaves[static_cast<size_t>(b) * T + t] = src[b];
+    for (int i = 0; i < nb; ++i) {
+      uint8_t* dst = out + static_cast<size_t>(i0 + i) * T;
+      for (int t = 0; t < T; ++t) dst[t] = val[static_cast<size_t>(first + t) * RB + i];
+    }
   }
 }
 
-extern "C" int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves,
-                                uint8_t* t_root, uint8_t* i_root) {
-  if (!s || B < 1 || !t_leaves || !i_leaves) return -1;
+// Draw the text and image trees of `rows` sequences (roots given) and expand
+// the selected rows of both in parallel.
+static void draw_trees(ghm_sampler* s, int rows, const uint8_t* troot, const uint8_t* iroot, const int* sel,
+                       int nsel, uint8_t* t_out, uint8_t* i_out) {
+  const size_t per_tree = static_cast<size_t>(s->n_runs) * rows * 2;
+  s->stream.resize(2 * per_tree);
+  pull_stream(s, 2 * per_tree, s->stream.data());
+  const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * s->V * s->V;
+  const uint32_t* ts = s->stream.data();
+  const uint32_t* is = ts + per_tree;
+  const int nw = s->pool->size();
+  // 2 trees x row chunks of 32, dealt round-robin over the workers
+  const int nch = (nsel + 31) / 32;
+  s->pool->run([&](int w) {
+    for (int k = w; k < 2 * nch; k += nw) {
+      const int tree = k / nch, ch = k % nch;
+      const int r0 = 32 * ch, r1 = (r0 + 32 < nsel) ? r0 + 32 : nsel;
+      if (tree == 0)
+        expand_rows(s, s->cdf.data(), ts, rows, troot, sel, r0, r1, t_out);
+      else
+        expand_rows(s, s->cdf.data() + per, is, rows, iroot, sel, r0, r1, i_out);
+    }
+  });
+}
+
+extern "C" int ghm_sampler_next_shard(ghm_sampler* s, int B, int lo, int n, uint8_t* t_leaves,
+                                      uint8_t* i_leaves, uint8_t* t_root, uint8_t* i_root) {
+  if (!s || B < 1 || lo < 0 || n < 1 || lo + n > B || !t_leaves || !i_leaves) return -1;
   const int K = s->K, V = s->V;
   const int rows = B * (K + 1);
   std::vector<uint8_t> tr(rows), ir(rows);
   for (int r = 0; r < rows; ++r) tr[r] = static_cast<uint8_t>(s->mt.bounded(V - 1));
   for (int r = 0; r < 2 * B; ++r) ir[r] = tr[r];
   for (int r = 2 * B; r < rows; ++r) ir[r] = static_cast<uint8_t>(s->mt.bounded(V - 1));
-  const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * V * V;
-  sample_tree(s, s->cdf.data(), tr.data(), rows, t_leaves);
-  sample_tree(s, s->cdf.data() + per, ir.data(), rows, i_leaves);
-  if (t_root) std::memcpy(t_root, tr.data(), rows);
-  if (i_root) std::memcpy(i_root, ir.data(), rows);
+  std::vector<int> sel;
+  sel.reserve(static_cast<size_t>(K + 1) * n);
+  for (int k = 0; k <= K; ++k)
+    for (int i = 0; i < n; ++i) sel.push_back(k * B + lo + i);
+  draw_trees(s, rows, tr.data(), ir.data(), sel.data(), static_cast<int>(sel.size()), t_leaves, i_leaves);
+  for (size_t i = 0; i < sel.size(); ++i) {
+    if (t_root) t_root[i] = tr[sel[i]];
+    if (i_root) i_root[i] = ir[sel[i]];
+  }
   return 0;
+}
+
+extern "C" int ghm_sampler_next(ghm_sampler* s, int B, uint8_t* t_leaves, uint8_t* i_leaves,
+                                uint8_t* t_root, uint8_t* i_root) {
+  return ghm_sampler_next_shard(s, B, 0, B, t_leaves, i_leaves, t_root, i_root);
 }
 
 extern "C" int ghm_sampler_set_gauss(ghm_sampler* s, int has_gauss, double gauss) {
@@ -255,9 +423,9 @@ extern "C" int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t
   const int V = s->V, T = s->T;
   std::vector<uint8_t> r(B);
   for (int b = 0; b < B; ++b) r[b] = static_cast<uint8_t>(s->mt.bounded(V - 1));
-  const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * V * V;
-  sample_tree(s, s->cdf.data(), r.data(), B, t_leaves);
-  sample_tree(s, s->cdf.data() + per, r.data(), B, i_leaves);
+  std::vector<int> sel(B);
+  for (int b = 0; b < B; ++b) sel[b] = b;
+  draw_trees(s, B, r.data(), r.data(), sel.data(), B, t_leaves, i_leaves);
   for (int t = 0; z && t < T; ++t) {
     for (int b = 0; b < B; ++b) {
       const double g = legacy_gauss(s);

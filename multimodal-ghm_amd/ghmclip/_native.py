@@ -117,6 +117,7 @@ HOST_SIGNATURES = {
     "ghm_sampler_set_state": [_p, _p, _i],
     "ghm_sampler_get_state": [_p, _p, _p],
     "ghm_sampler_next": [_p, _i, _p, _p, _p, _p],
+    "ghm_sampler_next_shard": [_p, _i, _i, _i, _p, _p, _p, _p],
     "ghm_sampler_random_sample": [_p, _p, _i64],
     "ghm_sampler_choice": [_p, _i, _i64, _p],
     "ghm_sampler_next_cdm": [_p, _i, ctypes.c_double, _p, _p, _p, _p],

@@ -103,6 +103,14 @@ class NativeClipSampler:
                                         _addr(i_root) if i_root is not None else None)
         _native_check(rc)
 
+    def next_shard_into(self, B, lo, n, t_leaves, i_leaves, t_root=None, i_root=None):
+        """The same draw, keeping only rows [k*B + lo, k*B + lo + n) of every block
+        k (the data-parallel shard): buffers [(K+1)*n, T]."""
+        rc = self._lib.ghm_sampler_next_shard(self._h, B, lo, n, _addr(t_leaves), _addr(i_leaves),
+                                              _addr(t_root) if t_root is not None else None,
+                                              _addr(i_root) if i_root is not None else None)
+        _native_check(rc)
+
     # numpy global-state bridge -------------------------------------------------
     def next_cdm_into(self, B, sigma, t_leaves, i_leaves, z, root=None):
         """ConditionalDenoiseSampler draw into caller-owned buffers: uint8 [B, T]

@@ -60,24 +60,27 @@ class BatchPipeline:
         rows = self.B * (self.s.K + 1)
         T = self.s.T
         self.full_rows, self.T = rows, T
+        if self.slice is not None:  # this rank's shard only: (K+1) * B/world rows
+            br, rank, world = self.slice
+            if br != self.B or br % world:
+                raise ValueError("row_slice must be (batch_size, rank, world) with world | batch_size")
+            self.lo, self.n = rank * (br // world), br // world
+            rows = (self.s.K + 1) * self.n
         self.slots = [(torch.empty(rows, T, dtype=torch.uint8).pin_memory(),
                        torch.empty(rows, T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
-        if self.slice is not None:
-            br, rank, world = self.slice
-            idx = shard_rows(br, rows // br, rank, world)
-            self.idx = torch.from_numpy(idx)
-            self.out = [(torch.empty(len(idx), T, dtype=torch.uint8).pin_memory(),
-                         torch.empty(len(idx), T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
 
     def _fill(self, i):
+        """One draw of the global batch (the MT stream advances by all of it; only
+        this rank's rows are expanded: ghm_sampler_next_shard == shard_rows of the
+        full draw)."""
         t, im = self.slots[i]
-        self.s.next_into(self.B, t.numpy(), im.numpy())
         if self.slice is not None:
-            torch.index_select(t, 0, self.idx, out=self.out[i][0])
-            torch.index_select(im, 0, self.idx, out=self.out[i][1])
+            self.s.next_shard_into(self.B, self.lo, self.n, t.numpy(), im.numpy())
+        else:
+            self.s.next_into(self.B, t.numpy(), im.numpy())
 
     def _stage(self, trainer, i):
-        t, im = self.out[i] if self.slice is not None else self.slots[i]
+        t, im = self.slots[i]
         trainer.set_tokens(t, im)
 
     def _run(self):

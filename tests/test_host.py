@@ -147,3 +147,37 @@ def test_guided_targets_host_match_reference():
             np.testing.assert_allclose(t.numpy(), np.repeat(want, ext, axis=1), rtol=1e-6, atol=1e-6)
         pp = bp_cls_posterior(g[f"{pref}_transition"], leaves, np.ones(10) / 10)
         np.testing.assert_allclose(pp, g[f"{pref}_pp"], rtol=1e-10, atol=1e-12)
+
+
+def test_sampler_shard_equals_row_slice():
+    """ghm_sampler_next_shard (the data-parallel producer) returns exactly
+    shard_rows of the full draw and leaves the stream where the full draw does."""
+    from ghmclip import ClipSampler
+    from ghmclip.training.pipeline import shard_rows
+    p_y = np.ones(10) / 10
+    full = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    part = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    full.native.seed(11)
+    part.native.seed(11)
+    B, world = 16, 4
+    t = np.empty((5 * B, 81), np.uint8)
+    i = np.empty((5 * B, 81), np.uint8)
+    tr = np.empty(5 * B, np.uint8)
+    ir = np.empty(5 * B, np.uint8)
+    for step in range(3):
+        rank = step % world
+        n = B // world
+        ts = np.empty((5 * n, 81), np.uint8)
+        is_ = np.empty((5 * n, 81), np.uint8)
+        trs = np.empty(5 * n, np.uint8)
+        irs = np.empty(5 * n, np.uint8)
+        full.native.next_into(B, t, i, tr, ir)
+        part.native.next_shard_into(B, rank * n, n, ts, is_, trs, irs)
+        idx = shard_rows(B, 5, rank, world)
+        np.testing.assert_array_equal(ts, t[idx])
+        np.testing.assert_array_equal(is_, i[idx])
+        np.testing.assert_array_equal(trs, tr[idx])
+        np.testing.assert_array_equal(irs, ir[idx])
+    k1, p1 = full.native.get_state()
+    k2, p2 = part.native.get_state()
+    assert p1 == p2 and (k1 == k2).all()
