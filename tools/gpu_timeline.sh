@@ -1,0 +1,15 @@
+# usage: bash tools/gpu_timeline.sh TAG [bench args...] -> gpurun_out/tl_TAG/ (kernel trace + stats + timeline)
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-x}
+shift
+mkdir -p gpurun_out/tl_$TAG
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tl_$TAG -o run -- \
+   python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-final-risk "$@" > gpurun_out/tl_$TAG/bench.json 2> gpurun_out/tl_$TAG/bench.err
+rc=$?
+echo "prof rc=$rc" >> gpurun_out/tl_$TAG/bench.err
+[ $rc -eq 0 ] || exit $rc
+f=$(find gpurun_out/tl_$TAG -name '*kernel_trace.csv' | head -1)
+python tools/timeline.py "$f" k_adamw -8 -v > gpurun_out/tl_$TAG/timeline.txt
+s=$(find gpurun_out/tl_$TAG -name '*kernel_stats.csv' | head -1)
+python tools/kstats.py "$s" 26 30 > gpurun_out/tl_$TAG/kstats.txt
