@@ -191,7 +191,8 @@ def dominant_kernel(trainer):
         def launch():
             _native.call("ghm_ln_mlp_fwd_x3b", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                          ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]),
-                         ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
+                         None if plan.mlp_rc else ptr(plan.G[0]), None if plan.mlp_rc else ptr(plan.Dg[0]),
+                         ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
         return "k_ln_mlp_fwd_x3b", launch
 
     def launch():
@@ -395,6 +396,7 @@ def main():
     kern_ms = time_kernel(klaunch)
     kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
     risk = None if a.no_final_risk else final_risk(a, ws)
+    rc = tr.precision == "x3" and tr.plans[0].mlp_rc
     del ring, tr
     if rank != 0:
         teardown()
@@ -424,12 +426,13 @@ def main():
                           else "f32 MFMA products"),
                 "traffic": None if traffic is None else round(traffic * scale),
                 "algorithmic_bytes": round(MLP_FWD_MUST_BYTES * scale),
-                "design_bytes": round(MLP_FWD_BYTES_PER_LAUNCH * scale),
+                "design_bytes": round((MLP_FWD_MUST_BYTES if rc else MLP_FWD_BYTES_PER_LAUNCH) * scale),
                 "kernel_ms": round(kern_ms, 4),
                 "kernel_ms_in_step": round(kern_ms_step, 4),
                 "achieved_in_step": round(achieved_step, 2),
                 "frac_in_step": round(achieved_step / peak, 4),
-                "hbm_gbs_design": round(MLP_FWD_BYTES_PER_LAUNCH * scale / (kern_ms * 1e-3) / 1e9, 1)}
+                "hbm_gbs_design": round((MLP_FWD_MUST_BYTES if rc else MLP_FWD_BYTES_PER_LAUNCH) * scale
+                                        / (kern_ms * 1e-3) / 1e9, 1)}
     out = {
         "metric": "GHM training samples/sec (CLIP default config)",
         "value": round(samples / elapsed, 2),

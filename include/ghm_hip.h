@@ -169,7 +169,9 @@ int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, 
                       const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
                       int64_t M, int D, int F, float eps, void* stream);
 /* Same contract and results as ghm_ln_mlp_fwd_x3 (model.py:741-747,784-788), 16 tokens per
-   wave on v_mfma_f32_16x16x32_bf16 (the variant the trainer launches). */
+   wave on v_mfma_f32_16x16x32_bf16 (the variant the trainer launches).  G == Dg == NULL:
+   nothing but H_out and the LN2 stats leaves the chip (the backward is then
+   ghm_mlp_bwd_rc_x3, which recomputes U). */
 int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                        const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
                        int64_t M, int D, int F, float eps, void* stream);
@@ -177,6 +179,14 @@ int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b,
 int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                    const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln, int64_t M,
                    int D, int F, void* stream);
+/* MLP + LN2 backward with the up-projection recomputed from H_mid and the LN2
+ * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
+ * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),
+ * dH_mid = dH_out + dLN2 (must not alias dH_out) and part_ln as ghm_mlp_bwd
+ * (n_blocks = ghm_token_blocks(M))  —  backward of model.py:741-747,784-788. */
+int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
+                      const float* ln_b, const void* pack, const float* b1, float* G, float* dU, float* dH_mid,
+                      float* part_ln, int64_t M, int D, int F, void* stream);
 /* As ghm_qkv_bwd (backward of model.py:772-775). */
 int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
                    const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, void* stream);

@@ -13,6 +13,13 @@
 #include "ghm_split.h"
 #include "ghm_launch.h"
 
+// Timing ablations of k_ln_mlp_fwd_x3b<., false> (experiment builds only; results
+// are wrong when set): 1 no weight refill, 2 no GELU, 3 no up-projection MFMAs,
+// 4 no down-projection MFMAs, 5 no refill and no per-chunk barrier.
+#ifndef GHM_ABL
+#define GHM_ABL 0
+#endif
+
 // ---------------------------------------------------------------------------
 // Weight pack (bf16 elements per layer; each region = hi plane then lo plane)
 // ---------------------------------------------------------------------------
@@ -325,7 +332,9 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd_x3(
 // chunks; the swizzle goes on each lane's SOURCE address and again on the read
 // (conflict-free ds_read_b128):
 //   R32  [32 rows][128] (256-B rows):  chunk c of row r at c ^ (r & 15)
-//   R128 [128 rows][32] (64-B rows):   chunk c of row r at c ^ ((r >> 2) & 3)
+//   R128 [128 rows][32] (64-B rows):   chunk c of row r at c ^ s((r >> 2) & 3), s = {0, 2, 3, 1}
+//                                      (with s = identity the 16x16x32 operand reads were
+//                                      2-way bank conflicted in every ds_read_b128 lane group)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void glds16(const __bf16* src, __bf16* lds_base) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src),
@@ -333,7 +342,8 @@ __device__ __forceinline__ void glds16(const __bf16* src, __bf16* lds_base) {
 }
 constexpr int PLANE = 32 * GHM_D;  // bf16 elements of one tile plane (8 KB)
 __device__ __forceinline__ int r32_off(int row, int lc) { return row * 128 + 8 * (lc ^ (row & 15)); }
-__device__ __forceinline__ int r128_off(int row, int lc) { return row * 32 + 8 * (lc ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int r128_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+__device__ __forceinline__ int r128_off(int row, int lc) { return row * 32 + 8 * (lc ^ r128_swz(row)); }
 
 // ---------------------------------------------------------------------------
 // 16-token-per-wave variant of LN2 + MLP (v_mfma_f32_16x16x32_bf16).
@@ -369,7 +379,7 @@ __device__ __forceinline__ void fill_r128_w8(const __bf16* g, int ldg, int lo_of
   for (int k = 0; k < (8 + NW - 1) / NW; ++k) {
     const int b = (threadIdx.x >> 6) + NW * k;
     if (8 % NW == 0 || b < 8) {
-      const int row = 16 * b + (L >> 2), lc = (L & 3) ^ ((row >> 2) & 3);
+      const int row = 16 * b + (L >> 2), lc = (L & 3) ^ r128_swz(row);
       const __bf16* src = g + row * ldg + 8 * lc;
       glds16(src, ih + 512 * b);
       glds16(src + lo_off, il + 512 * b);
@@ -386,15 +396,22 @@ __device__ __forceinline__ float pick16(const float4* b4, int g, int r) {
 // NW = waves per workgroup (8: 128 tokens; 4: 64 tokens, for token counts too
 // small to fill 256 CUs with 128-token workgroups).  Measured: a 7-wave /
 // 112-token variant (463 workgroups instead of 405) runs 96.6 us vs 79.1 us at
-// the CLIP's 51,840 tokens.
-template <int NW>
+// the CLIP's 51,840 tokens.  SAVE = false: only H_out leaves the chip (the
+// backward recomputes U, k_mlp_bwd_rc_x3): 2 x [M,128] of HBM traffic instead of
+// 2 x [M,128] + 2 x [M,512].
+template <int NW, bool SAVE>
 __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
     float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
     int64_t M, float eps) {
-  // ONE __shared__ object: [W1 hi|lo][W2 hi|lo] x 2 buffers
-  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE];
+  // ONE __shared__ object: [W1 hi|lo][W2 hi|lo] x 2 buffers, then b1 (f32).  The
+  // chunk's b1 values are read at the top of the iteration, before its LDS-DMA
+  // fills: any LDS read issued after them gets an s_waitcnt vmcnt(0) on the new
+  // fills (the compiler cannot prove it disjoint from the DMA target; a separate
+  // __shared__ object for b1 made it wait before EVERY ring read instead).
+  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE + 2 * GHM_F];
+  float* sb1 = reinterpret_cast<float*>(lds + 8 * PLANE);
   auto s1h = [&](int buf) { return lds + 4 * PLANE * buf; };
   auto s1l = [&](int buf) { return lds + 4 * PLANE * buf + PLANE; };
   auto s2h = [&](int buf) { return lds + 4 * PLANE * buf + 2 * PLANE; };
@@ -408,6 +425,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
   const __bf16* W2 = pack + PK_W2_P32;
   fill_r32_w8<NW>(W1, GHM_D, PK_W, s1h(0), s1l(0));
   fill_r128_w8<NW>(W2, GHM_F, PK_W, s2h(0), s2l(0));
+  if (threadIdx.x < GHM_F / 4)  // b1 -> LDS: each lane reads its 4 hidden units as one float4
+    reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
   // LN2 of the token row, lane holds features 32s + 8g + i
   bf16x8 xh[4], xl[4];
   {
@@ -453,35 +472,38 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
     const int cur = c & 1;
+    float4 bb[2];  // b1 of hidden units 32c + 16jt + 4g + r
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
+    issue_fence();
+#if GHM_ABL != 1 && GHM_ABL != 5
     {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
       const int cn = c + 1 < NC ? c + 1 : NC - 1;
       fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
       fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
     }
+#endif
     f32x4 u[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       u[jt] = zero4();
 #pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
+      for (int s2 = 0; s2 < 4 * (GHM_ABL != 3); ++s2) {
         const int o = r32_off(16 * jt + t, 4 * s2 + g);
         u[jt] = mfma16_x3(ldsb8(s1h(cur) + o), ldsb8(s1l(cur) + o), xh[s2], xl[s2], u[jt]);
       }
     }
     float gv[8], dg[8];
-    {  // + b1 (wave-uniform scalar loads: no ordinary load beside the LDS-DMA)
-      const float4* bc = reinterpret_cast<const float4*>(b1 + 32 * c);
-      float4 bv[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) bv[k] = bc[k];
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gv[4 * jt + r] = u[jt][r] + pick16(bv + 4 * jt, g, r);
+    for (int jt = 0; jt < 2; ++jt) {  // + b1
+      gv[4 * jt + 0] = u[jt][0] + bb[jt].x;
+      gv[4 * jt + 1] = u[jt][1] + bb[jt].y;
+      gv[4 * jt + 2] = u[jt][2] + bb[jt].z;
+      gv[4 * jt + 3] = u[jt][3] + bb[jt].w;
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) gelu_fast(gv[r], gv[r], dg[r]);
-    {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward: 4 stores per wave
+    for (int r = 0; r < 8 * (GHM_ABL != 2); ++r) gelu_fast(gv[r], gv[r], dg[r]);
+    if (SAVE) {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward: 4 stores per wave
       float* grow = G + mc * GHM_F + 32 * c + 4 * g;
       float* drow = Dg + mc * GHM_F + 32 * c + 4 * g;
       st4(grow, gv[0], gv[1], gv[2], gv[3]);
@@ -492,12 +514,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     bf16x8 gh, gl;
     split8(gv, gh, gl);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8 * (GHM_ABL != 4); ++j) {
       const int o = r128_off(16 * j + t, g);
       y[j] = mfma16_x3(ldsb8(s2h(cur) + o), ldsb8(s2l(cur) + o), gh, gl, y[j]);
     }
     // retire this iteration's 4 LDS-DMA fills (issued before the 4 stores)
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (SAVE)
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (GHM_ABL != 5)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if (valid) {
     const float* hr = Hmid + m * GHM_D;
@@ -510,6 +535,225 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       st4(orow + f, hv.x + (y[j][0] + bv.x), hv.y + (y[j][1] + bv.y), hv.z + (y[j][2] + bv.z),
           hv.w + (y[j][3] + bv.w));
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MLP + LN2 backward with the up-projection recomputed       (model.py:784-788)
+// 16 tokens per wave, 8 waves (128 tokens) per workgroup, weight tiles by
+// LDS-DMA as in k_ln_mlp_fwd_x3b.  The forward saved only Hmid and the LN2
+// statistics; per 32-unit hidden chunk c:
+//   U^T   = W1[c] LN2(Hmid)^T + b1       (recomputed, 2 tiles x 4 k-steps)
+//   dG^T  = W2^T[c] dY^T                 (2 tiles x 4 k-steps over the 128 outputs)
+//   G = GELU(U), dU = dG * GELU'(U)      -> HBM (inputs of dW2 and dW1)
+//   dX2^T += W1^T[:, c] dU^T             (8 tiles, one k-step of 32 hidden units)
+// then LN2 backward + residual: dHmid = dY + LN2'(dX2), and the workgroup's
+// (sum dX2 * xhat, sum dX2) partials of the LN2 weight / bias gradients.
+// Every lane runs a real row (lanes past M recompute row M-1 and store the same
+// bytes), so each wave has exactly 4 stores in flight per chunk.
+// ---------------------------------------------------------------------------
+// Butterfly reduce-scatter of 32 values over the 16 lanes t = lane & 15 of a
+// lane group: lane t returns the 16-lane sums of values 2t (.x) and 2t + 1 (.y).
+__device__ __forceinline__ float2 reduce_scatter32_t16(float* v, int t) {
+#pragma unroll
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    const int m = 8 >> lvl;         // lane-bit of this level
+    const int half = 16 >> lvl;     // live values 32 >> lvl
+    const bool upper = (t & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float lo = v[i], hi = v[i + half];
+      const float send = upper ? lo : hi;
+      const float keep = upper ? hi : lo;
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  return make_float2(v[0], v[1]);
+}
+
+__global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
+    const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
+    float* __restrict__ Gout, float* __restrict__ dU, float* __restrict__ dHmid, float* __restrict__ part_ln,
+    int64_t M) {
+  constexpr int NW = 8, NC = GHM_F / 32;
+  // [W1 hi|lo][W2^T hi|lo][W1^T hi|lo] x 2 buffers (96 KB); the LN partial
+  // buffer aliases it after the loop
+  __shared__ __attribute__((aligned(16))) __bf16 lds[12 * PLANE + 2 * GHM_F];
+  float* sb1 = reinterpret_cast<float*>(lds + 12 * PLANE);  // read before the fills: see k_ln_mlp_fwd_x3b
+  auto sw1h = [&](int b) { return lds + 6 * PLANE * b; };
+  auto sw1l = [&](int b) { return lds + 6 * PLANE * b + PLANE; };
+  auto sw2h = [&](int b) { return lds + 6 * PLANE * b + 2 * PLANE; };
+  auto sw2l = [&](int b) { return lds + 6 * PLANE * b + 3 * PLANE; };
+  auto sw3h = [&](int b) { return lds + 6 * PLANE * b + 4 * PLANE; };
+  auto sw3l = [&](int b) { return lds + 6 * PLANE * b + 5 * PLANE; };
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + wave) * 16 + t;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W1 = pack + PK_W1_N;    // [512 f][128 d]
+  const __bf16* W2T = pack + PK_W2_T;   // [512 f][128 o]
+  const __bf16* W1T = pack + PK_W1_T32; // [128 d][512 q], q perm32
+  fill_r32_w8<NW>(W1, GHM_D, PK_W, sw1h(0), sw1l(0));
+  fill_r32_w8<NW>(W2T, GHM_D, PK_W, sw2h(0), sw2l(0));
+  fill_r128_w8<NW>(W1T, GHM_F, PK_W, sw3h(0), sw3l(0));
+  if (threadIdx.x < GHM_F / 4)
+    reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
+  // B operands: LN2(Hmid) and dY of the token, lane holds features 32 s2 + 8 g + i
+  bf16x8 xh[4], xl[4], yh[4], yl[4];
+  const float2 st = stats[mc];
+  {
+    const float* row = Hmid + mc * GHM_D;
+    const float* dyr = dHout + mc * GHM_D;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int f0 = 32 * s2 + 8 * g;
+      const float4 a = *reinterpret_cast<const float4*>(row + f0);
+      const float4 b = *reinterpret_cast<const float4*>(row + f0 + 4);
+      const float4 ga = *reinterpret_cast<const float4*>(lnw + f0);
+      const float4 gb = *reinterpret_cast<const float4*>(lnw + f0 + 4);
+      const float4 ba = *reinterpret_cast<const float4*>(lnb + f0);
+      const float4 bb = *reinterpret_cast<const float4*>(lnb + f0 + 4);
+      float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const float gw[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+      const float bw[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = (x[i] - st.x) * st.y * gw[i] + bw[i];
+      split8(x, xh[s2], xl[s2]);
+      const float4 c = *reinterpret_cast<const float4*>(dyr + f0);
+      const float4 d = *reinterpret_cast<const float4*>(dyr + f0 + 4);
+      const float y[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+      split8(y, yh[s2], yl[s2]);
+    }
+  }
+  f32x4 dx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dx[j] = zero4();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const int cur = c & 1;
+    float4 bb[2];  // b1 of hidden units 32c + 16jt + 4g + r
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
+    issue_fence();
+    {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
+      const int cn = c + 1 < NC ? c + 1 : NC - 1;
+      fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, sw1h(cur ^ 1), sw1l(cur ^ 1));
+      fill_r32_w8<NW>(W2T + cn * 32 * GHM_D, GHM_D, PK_W, sw2h(cur ^ 1), sw2l(cur ^ 1));
+      fill_r128_w8<NW>(W1T + cn * 32, GHM_F, PK_W, sw3h(cur ^ 1), sw3l(cur ^ 1));
+    }
+    f32x4 u[2], dg[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      u[jt] = zero4();
+      dg[jt] = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int o = r32_off(16 * jt + t, 4 * s2 + g);
+        u[jt] = mfma16_x3(ldsb8(sw1h(cur) + o), ldsb8(sw1l(cur) + o), xh[s2], xl[s2], u[jt]);
+        dg[jt] = mfma16_x3(ldsb8(sw2h(cur) + o), ldsb8(sw2l(cur) + o), yh[s2], yl[s2], dg[jt]);
+      }
+    }
+    float gv[8], du[8];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {  // + b1, GELU, GELU'
+      const float bs[4] = {bb[jt].x, bb[jt].y, bb[jt].z, bb[jt].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float gd;
+        gelu_fast(u[jt][r] + bs[r], gv[4 * jt + r], gd);
+        du[4 * jt + r] = dg[jt][r] * gd;
+      }
+    }
+    {  // G (for dW2) and dU (for dW1): 4 stores per wave
+      float* grow = Gout + mc * GHM_F + 32 * c + 4 * g;
+      float* drow = dU + mc * GHM_F + 32 * c + 4 * g;
+      st4(grow, gv[0], gv[1], gv[2], gv[3]);
+      st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
+      st4(drow, du[0], du[1], du[2], du[3]);
+      st4(drow + 16, du[4], du[5], du[6], du[7]);
+    }
+    bf16x8 dh, dl;
+    split8(du, dh, dl);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = r128_off(16 * j + t, g);
+      dx[j] = mfma16_x3(ldsb8(sw3h(cur) + o), ldsb8(sw3l(cur) + o), dh, dl, dx[j]);
+    }
+    // retire this iteration's 6 LDS-DMA fills (issued before the 4 stores)
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // LN2 backward: lane holds dX2 of features d = 16 j + 4 g + r
+  const float mean = st.x, rstd = st.y;
+  float xhat[32], dyg[32];
+  float s1 = 0.f, s2 = 0.f;
+  {
+    const float* row = Hmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 xv = *reinterpret_cast<const float4*>(row + f);
+      const float4 gv = *reinterpret_cast<const float4*>(lnw + f);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float xh_ = (xs[r] - mean) * rstd;
+        xhat[4 * j + r] = xh_;
+        const float v = dx[j][r] * gs[r];
+        dyg[4 * j + r] = v;
+        s1 += v;
+        s2 += v * xh_;
+      }
+    }
+  }
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float m1 = s1 * (1.f / GHM_D), m2 = s2 * (1.f / GHM_D);
+  {
+    const float* dres = dHout + mc * GHM_D;
+    float* orow = dHmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 rv = *reinterpret_cast<const float4*>(dres + f);
+      const float rs[4] = {rv.x, rv.y, rv.z, rv.w};
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = rs[r] + rstd * (dyg[4 * j + r] - m1 - xhat[4 * j + r] * m2);
+      st4(orow + f, o[0], o[1], o[2], o[3]);
+    }
+  }
+  // LN2 weight / bias partials of the workgroup: per wave a reduce-scatter over
+  // its 16 tokens (lane t ends with features of value slots 2t, 2t + 1), then
+  // the 8 waves in a fixed order
+  float vg[32], vb[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const float d = valid ? dx[k >> 2][k & 3] : 0.f;
+    vb[k] = d;
+    vg[k] = d * xhat[k];
+  }
+  const float2 rg = reduce_scatter32_t16(vg, t);
+  const float2 rb = reduce_scatter32_t16(vb, t);
+  float* red = reinterpret_cast<float*>(lds);  // [2][NW][128]; the ring is idle after the last barrier
+  {
+    const int k0 = 2 * t;  // value slot k = 4 j + r -> feature 16 j + 4 g + r
+    const int f0 = 16 * (k0 >> 2) + 4 * g + (k0 & 3);
+    red[wave * GHM_D + f0] = rg.x;
+    red[wave * GHM_D + f0 + 1] = rg.y;
+    red[NW * GHM_D + wave * GHM_D + f0] = rb.x;
+    red[NW * GHM_D + wave * GHM_D + f0 + 1] = rb.y;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * GHM_D) {
+    const int q = threadIdx.x >> 7, f = threadIdx.x & 127;
+    const float* rr = red + q * NW * GHM_D + f;
+    const float sum = ((rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D])) +
+                      ((rr[4 * GHM_D] + rr[5 * GHM_D]) + (rr[6 * GHM_D] + rr[7 * GHM_D]));
+    part_ln[static_cast<int64_t>(blockIdx.x) * 2 * GHM_D + q * GHM_D + f] = sum;
   }
 }
 
@@ -1174,6 +1418,18 @@ extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const flo
   return ghm_launch_status();
 }
 
+extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
+                                 const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
+                                 float* dH_mid, float* part_ln, int64_t M, int D, int F, void* stream) {
+  GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
+  hipLaunchKernelGGL(k_mlp_bwd_rc_x3, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
+                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w, ln_b,
+                     reinterpret_cast<const __bf16*>(pack), b1, G, dU, dH_mid, part_ln, M);
+  return ghm_launch_status();
+}
+
 extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w,
                               const void* pack, const float* dH_mid, float* dH, float* part_ln, int64_t M,
                               int D, void* stream) {
@@ -1245,16 +1501,28 @@ extern "C" int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH
 extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                                   const float* b1, const float* b2, float* H_out, float* G, float* Dg,
                                   float* stats, int64_t M, int D, int F, float eps, void* stream) {
-  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && G && Dg && stats, "null pointer");
+  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && stats, "null pointer");
+  GHM_CHECK((G == nullptr) == (Dg == nullptr), "G and Dg: both or neither");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
   float2* st = reinterpret_cast<float2*>(stats);
-  if ((M + 127) / 128 >= 256) {  // enough 128-token workgroups to give every CU one
-    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
-                       ghm_stream(stream), H_mid, ln_w, ln_b, pk, b1, b2, H_out, G, Dg, st, M, eps);
+  hipStream_t s = ghm_stream(stream);
+  const bool big = (M + 127) / 128 >= 256;  // enough 128-token workgroups to give every CU one
+  const dim3 g8(static_cast<unsigned>((M + 127) / 128)), g4(static_cast<unsigned>((M + 63) / 64));
+  if (G) {
+    if (big)
+      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<8, true>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, G,
+                         Dg, st, M, eps);
+    else
+      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<4, true>), g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, G,
+                         Dg, st, M, eps);
   } else {
-    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, dim3(static_cast<unsigned>((M + 63) / 64)), dim3(256), 0,
-                       ghm_stream(stream), H_mid, ln_w, ln_b, pk, b1, b2, H_out, G, Dg, st, M, eps);
+    if (big)
+      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<8, false>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out,
+                         G, Dg, st, M, eps);
+    else
+      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<4, false>), g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out,
+                         G, Dg, st, M, eps);
   }
   return ghm_launch_status();
 }

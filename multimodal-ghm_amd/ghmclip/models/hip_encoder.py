@@ -10,7 +10,9 @@ HBM layout (one encoder, M = n_seq * T tokens, fp32):
   qkv  [L,   M, 384]   Q | K | V
   P    [L, n_seq, 96, 96] attention probabilities, dense and padded (backward input);
        [L, n_seq, 192, 192] for sequences past 96 tokens (x3 only)
-  G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (backward inputs)
+  G/Dg [L,   M, 512]   GELU(U) and GELU'(U) of the MLP pre-activation U (f32 mode only:
+       the x3 forward saves nothing of the MLP; its backward recomputes U and writes
+       G [M, 512] as per-layer scratch for dW2)
   st1/st2 [L, M, 2]    LayerNorm (mean, rstd)
   pack [L, 983040] bf16 (precision "x3" only): per-layer pre-split weight planes
 Backward scratch (reused across layers): dH ping-pong [2, M, 128], dqkv
@@ -103,8 +105,13 @@ class EncoderPlan:
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
         self.P = torch.zeros(L, N, pad, pad, dtype=f32, device=dev)
-        self.G = e(L, M, D_HIDDEN)
-        self.Dg = e(L, M, D_HIDDEN)
+        # x3: the MLP forward saves nothing and its backward recomputes U
+        # (GHM_MLP_RECOMPUTE=1, default) or the forward saves G and GELU'(U) (=0)
+        self.mlp_rc = self.precision == "x3" and os.environ.get("GHM_MLP_RECOMPUTE", "1") != "0"
+        if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2)
+            self.G, self.Dg = e(M, D_HIDDEN), None
+        else:
+            self.G, self.Dg = e(L, M, D_HIDDEN), e(L, M, D_HIDDEN)
         self.st1 = e(L, M, 2)
         self.st2 = e(L, M, 2)
         self.emb = e(N, num_class)
@@ -194,8 +201,8 @@ class EncoderPlan:
                       N, T, D_MODEL, self.scale_div, s)
                 c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
-                  _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL,
-                  D_HIDDEN, self.eps, s)
+                  _ptr(self.H[l + 1]), None if self.mlp_rc else _ptr(self.G[l]),
+                  None if self.mlp_rc else _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
                 continue
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
@@ -293,17 +300,22 @@ class EncoderPlan:
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
-            if x3:
+            if x3 and not self.mlp_rc:
                 c("ghm_mlp_bwd_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL,
                   D_HIDDEN, s)
+            elif x3:  # recomputes U; writes G (scratch) and dU
+                c("ghm_mlp_bwd_rc_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]),
+                  _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]),
+                  _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(self.part_ln2), M,
+                  D_MODEL, D_HIDDEN, s)
             else:
                 c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
                   _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
             jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
-            c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G[l]), D_HIDDEN, D_HIDDEN, 0,
+            c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G if self.mlp_rc else self.G[l]), D_HIDDEN, D_HIDDEN, 0,
               None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)
             jobs += [J(self.part_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(self.part_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU

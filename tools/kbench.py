@@ -4,8 +4,8 @@
 
 Builds the default-config trainer, runs two real steps to populate every
 activation, then re-launches each kernel of encoder 0 / layer 0 `reps` times
-on the current stream between two events.  Prints us/launch and the f32 MFMA
-fraction for the GEMM-shaped kernels.
+on the current stream between two events.  Prints us/launch and the MFMA
+fraction for the GEMM-shaped kernels (f32 peak; x3 kernels: bf16 peak / 3).
 """
 import argparse
 import ctypes
@@ -20,7 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-ghm_amd"))
 sys.path.insert(0, ROOT)
 
-PEAK = 157.3e12
+PEAK = 157.3e12       # f32 MFMA, dense
+BF16_PEAK = 2.5e15    # bf16 MFMA, dense (x3 issues 3 bf16 products per f32 product)
 
 
 def main():
@@ -51,67 +52,55 @@ def main():
     tps_w1, ns_w1 = plan.wg["w1"]
     tps_q, ns_q = plan.wg["qkv"]
     gf = lambda flop: flop / 1e9  # noqa: E731
-    kernels = {
-        "ln_qkv_fwd": (lambda: c("ghm_ln_qkv_fwd", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
-                                 P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
-                                 P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
-        "attn_fwd": (lambda: c("ghm_attn_fwd", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]), N, T,
-                               128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
-        "ln_mlp_fwd": (lambda: c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
-                                 P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.weight"]),
-                                 P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
-                                 plan.eps, sp), gf(4 * M * 128 * 512)),
-        "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]),
-                              P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]), P(plan.Dg[l]), P(plan.dU),
-                              P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
-        "wgrad_w2": (lambda: c("ghm_wgrad", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None, None, None,
-                               P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp), gf(2 * M * 128 * 512)),
-        "wgrad_w1": (lambda: c("ghm_wgrad", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2, P(plan.st2[l]),
-                               P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), P(plan.part_w1), P(plan.part_b1), M,
-                               tps_w1, sp), gf(2 * M * 128 * 512)),
-        "attn_bwd": (lambda: c("ghm_attn_bwd", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS), P(plan.dqkv),
-                               N, T, 128, plan.scale_div, sp), gf(8 * N * T * T * 128)),
-        "wgrad_qkv": (lambda: c("ghm_wgrad", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2, P(plan.st1[l]),
-                                P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]), P(plan.part_wq), None, M, tps_q, sp),
-                      gf(2 * M * 128 * 384)),
-        "qkv_bwd": (lambda: c("ghm_qkv_bwd", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]),
-                              P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
-                              P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, sp), gf(2 * M * 128 * 384)),
-        "reduce_w2": (lambda: plan._reduce(plan.part_w2, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
-        "reduce_ln": (lambda: plan._reduce(plan.part_ln, plan.nblk, 256, [g["_lns_1.0.weight"], g["_lns_1.0.bias"]], sp),
-                      None),
-        "readout_bwd": (lambda: c("ghm_readout_bwd", P(plan.H[5]), P(p["_read_out.weight"]), P(p["_read_out.bias"]),
-                                  P(p["_out.weight"]), P(plan.d_emb), P(plan.dH[0]), P(plan.part_ro), P(plan.part_bro),
-                                  P(plan.part_wout), P(plan.part_bout), N, T, 128, 10, sp), None),
-        "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
-                      None),
-    }
-    xo = {"H": torch.empty_like(plan.H[l + 1]), "G": torch.empty_like(plan.G[l]), "Dg": torch.empty_like(plan.Dg[l]),
-          "st": torch.empty_like(plan.st2[l])}
-    if plan.pack is not None:
-        pk = P(plan.pack[l])
+    kernels = {}
+    if plan.pack is None:  # exact-f32 kernels
         kernels.update({
-            "ln_qkv_fwd_x3": (lambda: c("ghm_ln_qkv_fwd_x3", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
-                                        pk, P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
-            "ln_mlp_fwd_x3": (lambda: c("ghm_ln_mlp_fwd_x3", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
-                                        P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
-                                        P(plan.H[l + 1]), P(plan.G[l]), P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512,
-                                        plan.eps, sp), gf(4 * M * 128 * 512)),
+            "ln_qkv_fwd": (lambda: c("ghm_ln_qkv_fwd", P(plan.H[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
+                                     P(p["_queries.0.weight"]), P(p["_keys.0.weight"]), P(p["_values.0.weight"]),
+                                     P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
+            "attn_fwd": (lambda: c("ghm_attn_fwd", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]), N, T,
+                                   128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
+            "ln_mlp_fwd": (lambda: c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                     P(p["_lns_2.0.bias"]), P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]),
+                                     P(p["_mlps.0.2.weight"]), P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]),
+                                     P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
+            "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
+                                  P(p["_lns_2.0.weight"]), P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]),
+                                  P(plan.Dg[l]), P(plan.dU), P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp),
+                        gf(4 * M * 128 * 512)),
+        })
+    else:  # the split-bf16 kernels the x3 step launches (+ the superseded MLP pair)
+        pk = P(plan.pack[l])
+        xo = {"H": torch.empty_like(plan.H[l + 1]), "st": torch.empty_like(plan.st2[l]),
+              "G": torch.empty(M, 512, device=plan.H.device), "Dg": torch.empty(M, 512, device=plan.H.device),
+              "dHm": torch.empty_like(plan.H[l + 1])}
+        kernels.update({
+            "ln_qkv_fwd_x3": (lambda: c("ghm_ln_qkv_fwd_x3", P(plan.H[l]), P(p["_lns_1.0.weight"]),
+                                        P(p["_lns_1.0.bias"]), pk, P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps,
+                                        sp), gf(2 * M * 128 * 384)),
+            "attn_fwd_x3": (lambda: c("ghm_attn_fwd_x3", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]),
+                                      N, T, 128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
             "ln_mlp_fwd_x3b": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                          P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
-                                         P(xo["H"]), P(xo["G"]), P(xo["Dg"]), P(xo["st"]), M, 128, 512,
-                                         plan.eps, sp), gf(4 * M * 128 * 512)),
+                                         P(xo["H"]), None, None, P(xo["st"]), M, 128, 512, plan.eps, sp),
+                               gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3b_save": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                              P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
+                                              P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["G"]), P(xo["Dg"]),
+                                              P(xo["st"]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
+            "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
+                                        P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
+                                        P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln), M, 128, 512, sp),
+                              gf(6 * M * 128 * 512)),
             "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
-                                     P(p["_lns_2.0.weight"]), pk, P(plan.Dg[l]), P(plan.dU), P(plan.dH[1]),
+                                     P(p["_lns_2.0.weight"]), pk, P(xo["Dg"]), P(plan.dU), P(xo["dHm"]),
                                      P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
             "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]),
                                      P(p["_lns_1.0.weight"]), pk, P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M,
                                      128, sp), gf(2 * M * 128 * 384)),
-            "attn_fwd_x3": (lambda: c("ghm_attn_fwd_x3", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]),
-                                      N, T, 128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
             "attn_bwd_x3": (lambda: c("ghm_attn_bwd_x3", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS),
                                       P(plan.dqkv), N, T, 128, plan.scale_div, sp), gf(8 * N * T * T * 128)),
-            "wgrad_w2_x3": (lambda: c("ghm_wgrad_x3", P(plan.H[l + 1]), 128, 128, P(plan.G[l]), 512, 512, 0, None,
+            "wgrad_w2_x3": (lambda: c("ghm_wgrad_x3", P(plan.H[l + 1]), 128, 128, P(plan.G), 512, 512, 0, None,
                                       None, None, P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp),
                             gf(2 * M * 128 * 512)),
             "wgrad_w1_x3": (lambda: c("ghm_wgrad_x3", P(plan.dU), 512, 512, P(plan.Hmid[l]), 128, 128, 2,
@@ -121,6 +110,16 @@ def main():
                                        P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                        P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
         })
+    kernels.update({
+        "reduce_w2": (lambda: plan._reduce(plan.part_w2, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
+        "reduce_ln": (lambda: plan._reduce(plan.part_ln, plan.nblk, 256, [g["_lns_1.0.weight"], g["_lns_1.0.bias"]],
+                                           sp), None),
+        "readout_bwd": (lambda: c("ghm_readout_bwd", P(plan.H[5]), P(p["_read_out.weight"]), P(p["_read_out.bias"]),
+                                  P(p["_out.weight"]), P(plan.d_emb), P(plan.dH[0]), P(plan.part_ro),
+                                  P(plan.part_bro), P(plan.part_wout), P(plan.part_bout), N, T, 128, 10, sp), None),
+        "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
+                      None),
+    })
     only = set(a.only.split(",")) if a.only else None
     res = {}
     for name, (fn, gflop) in kernels.items():
@@ -135,18 +134,11 @@ def main():
         e1.record(s)
         e1.synchronize()
         us = e0.elapsed_time(e1) / a.reps * 1e3
-        frac = (gflop * 1e9 / (us * 1e-6)) / PEAK if gflop else None
+        peak = PEAK if plan.pack is None else BF16_PEAK / 3  # x3: 3 bf16 products per f32 product
+        frac = (gflop * 1e9 / (us * 1e-6)) / peak if gflop else None
         res[name] = {"us": round(us, 2), "gflop": gflop, "mfma_frac": round(frac, 4) if frac else None}
-        print(f"{name:14s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of f32 MFMA peak" if gflop else ""),
+        print(f"{name:20s} {us:9.2f} us" + (f"   {gflop:7.3f} GF  {frac*100:5.1f}% of MFMA peak" if gflop else ""),
               flush=True)
-    if "ln_mlp_fwd_x3b" in res:  # variant vs the production kernel on the same inputs
-        kernels["ln_mlp_fwd_x3b"][0]()  # both on the current Hmid (later kernels rewrote it)
-        kernels["ln_mlp_fwd_x3"][0]()
-        torch.cuda.synchronize()
-        for k, ref in (("H", plan.H[l + 1]), ("G", plan.G[l]), ("Dg", plan.Dg[l]), ("st", plan.st2[l])):
-            d = (xo[k] - ref).abs().max().item() / ref.abs().max().item()
-            print(f"x3b vs x3 {k}: max rel-to-maxabs diff {d:.3e}", flush=True)
-            res["ln_mlp_fwd_x3b"]["diff_" + k] = d
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)
