@@ -135,7 +135,7 @@ def make_cdm_ring(sampler, B, R):
     return ring
 
 
-def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False):
+def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False, guide=False):
     """BASELINE config 5 (exp_vlm_standardTF.sh via train_sequential_NWP.py): sequential
     next-word prediction, AutoRegressiveTransformer(T=81, 1 prefix token, d=256, L=9,
     MLP 1024), lr 1e-3 -> 1e-6, frozen CLIP image encoder (random init: no checkpoint
@@ -145,13 +145,13 @@ def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False):
     from ghmclip.training.vlm_trainer import VlmTrainer
     p_y = np.ones(10) / 10
     sampler = NextWordPredictSampler([4, 4], [3, 3], [p_y, p_y], [p, p])
-    if joint:  # train_NWP.py / exp_vlm_jointtrain.sh: 81 image leaves + 80 text tokens, no CLIP
+    if joint:  # train_NWP.py / exp_vlm_{jointtrain,guidedTF}.sh: 81 image leaves + 80 text tokens, no CLIP
         seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
         model = AutoRegressiveTransformer(161, 81, 10, 256, L, [4, 4], 4, 1024, auto_regressive=True,
-                                          sequential=False).cuda()
+                                          sequential=False, guide=guide).cuda()
         sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
         np.random.seed(224 + 1000 * rank)  # each rank draws its own batches
-        return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision="x3")
+        return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision="x3", penalty=0.001)
     torch.manual_seed(7)
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
     seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)
@@ -163,15 +163,21 @@ def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False):
     return sampler, trainer
 
 
-def make_vlm_ring(sampler, B, R):
-    """R pre-drawn batches (text inputs, targets, host BP posteriors, image leaves)
-    resident in HBM."""
+def make_vlm_ring(sampler, B, R, guide=False):
+    """R pre-drawn batches (text inputs, targets, host BP posteriors, image leaves;
+    guided: + the packed BP guide targets) resident in HBM."""
+    from ghmclip.data.data_random_GHM import vlm_guide_planes
     ring = []
     for _ in range(R):
         tl, il, _ = sampler.draw_numpy(B)
-        post, _ = sampler.posterior(tl, il)
+        if guide:
+            post, _, tg, ig = sampler.posterior(tl, il, guide=True)
+            extra = (vlm_guide_planes(tg, ig, 10),)
+        else:
+            post, _ = sampler.posterior(tl, il)
+            extra = ()
         ring.append(tuple(torch.from_numpy(np.ascontiguousarray(x)).cuda()
-                          for x in (tl[:, :-1], tl[:, 1:], post.astype(np.float32), il)))
+                          for x in (tl[:, :-1], tl[:, 1:], post.astype(np.float32), il) + extra))
     return ring
 
 
@@ -285,16 +291,18 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
                           f"CDM config{note}, "
                           f"B={B}, L={L}, fp32 PyTorch-CPU restatement of the reference "
                           f"(oracle/cdm_oracle.py, BP_DNS posterior included); {dt:.3f} s/step"}
-    if workload in ("vlm", "vlm_joint"):
+    if workload in ("vlm", "vlm_joint", "vlm_guided"):
         from oracle import vlm_oracle as VO
-        tr = VO.OracleVlmJointTrainer(B=B, L=L) if workload == "vlm_joint" else VO.OracleVlmTrainer(B=B, L=L)
+        jt = workload != "vlm"
+        tr = VO.OracleVlmJointTrainer(B=B, L=L) if jt else VO.OracleVlmTrainer(B=B, L=L)
         tr.step()
         t0 = time.time()
         for _ in range(steps):
             tr.step()
         dt = (time.time() - t0) / steps
         return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
-                "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if workload == 'vlm_joint' else 'sequential'} "
+                "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if jt else 'sequential'} "
+                          f"{'(unguided: the oracle has no guided VLM step) ' if workload == 'vlm_guided' else ''}"
                           f"VLM config, B={B}, L={L}, d=256, fp32 PyTorch-CPU restatement of the reference "
                           f"(oracle/vlm_oracle.py, host BP posteriors included); {dt:.3f} s/step"}
     tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
@@ -366,11 +374,13 @@ def main():
     ap.add_argument("--ring", type=int, default=16)
     ap.add_argument("--guide", action="store_true",
                     help="guided CLIP (clip_guide=True, exp_clip_guidedTF.sh) instead of the default config")
-    ap.add_argument("--workload", default="clip", choices=["clip", "cdm", "cdm_joint", "cdm_guided", "vlm", "vlm_joint"],
+    ap.add_argument("--workload", default="clip",
+                    choices=["clip", "cdm", "cdm_joint", "cdm_guided", "vlm", "vlm_joint", "vlm_guided"],
                     help="clip: the default CLIP config (BASELINE metric); cdm: sequential CDM (BASELINE config 4); "
                          "cdm_joint: joint CDM (train_CDNS.py, T = 162); cdm_guided: the same with --guide=True "
                          "(exp_cdm_guidedTF.sh); vlm: sequential VLM next-word prediction "
-                         "(BASELINE config 5); vlm_joint: joint VLM (train_NWP.py, T = 161)")
+                         "(BASELINE config 5); vlm_joint: joint VLM (train_NWP.py, T = 161); vlm_guided: the same "
+                         "with --guide=True (exp_vlm_guidedTF.sh)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
@@ -378,7 +388,7 @@ def main():
     ws, rank, local = setup_dist(a.gpus)
     if a.workload in ("cdm", "cdm_joint", "cdm_guided"):
         return main_cdm(a, ws, rank)
-    if a.workload in ("vlm", "vlm_joint"):
+    if a.workload in ("vlm", "vlm_joint", "vlm_guided"):
         return main_vlm(a, ws, rank)
     total_iters = max(3000, a.steps + a.warmup + 1)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
@@ -558,12 +568,13 @@ def main_vlm(a, ws, rank):
     """Sequential VLM (BASELINE config 5) throughput: samples/s, B rows per rank."""
     L = 9 if a.layers == 5 else a.layers  # exp_vlm_standardTF.sh: n_model_layer=9
     total_iters = max(30000, a.steps + a.warmup + 1)
-    joint = a.workload == "vlm_joint"
-    sampler, tr = build_vlm(rank, a.batch, L, 0.2, total_iters, a.precision, joint=joint)
-    ring = make_vlm_ring(sampler, a.batch, a.ring)
+    guide = a.workload == "vlm_guided"
+    joint = a.workload in ("vlm_joint", "vlm_guided")
+    sampler, tr = build_vlm(rank, a.batch, L, 0.2, total_iters, a.precision, joint=joint, guide=guide)
+    ring = make_vlm_ring(sampler, a.batch, min(a.ring, 4) if guide else a.ring, guide=guide)
 
     def one(k):
-        tr.set_batch(*ring[k % a.ring])
+        tr.set_batch(*ring[k % len(ring)])
         tr.step()
 
     elapsed = timed_steps(a, ws, tr, one)
@@ -604,7 +615,8 @@ def main_vlm(a, ws, rank):
     fwd = L * (6 * M * D * D + 4 * M * D * F + 4 * a.batch * T * T * D) + 2 * M * D * plan.V
     step_gflop = 3 * fwd / 1e9
     out = {
-        "metric": f"GHM training samples/sec ({'joint' if joint else 'sequential'} VLM config)",
+        "metric": f"GHM training samples/sec ({'guided joint' if guide else 'joint' if joint else 'sequential'} "
+                  f"VLM config)",
         "value": round(a.batch * ws * a.steps / elapsed, 2),
         "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
@@ -612,8 +624,10 @@ def main_vlm(a, ws, rank):
         "dtype": "f32" if tr.plan.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native NextWordPredictSampler, p=0.2, host BP posteriors), ring of {a.ring} "
                 f"batches resident in HBM",
-        "config": {"workload": (f"vlm_joint: AutoRegressiveTransformer(L={L}, d=256, T=161 = 81 image leaves + 80 "
-                                f"text, sequential=False), CE + KL compare, fwd+bwd+clip+AdamW" if joint else
+        "config": {"workload": (f"vlm_{'guided' if guide else 'joint'}: AutoRegressiveTransformer(L={L}, d=256, "
+                                f"T=161 = 81 image leaves + 80 text, sequential=False{', guide=True' if guide else ''})"
+                                f", CE + KL compare{' + 17 guided-block BP penalties (host targets)' if guide else ''}"
+                                f", fwd+bwd+clip+AdamW" if joint else
                                 f"vlm_sequential: AutoRegressiveTransformer(L={L}, d=256, T=81 = 1 prefix + 80 text) "
                                 f"+ frozen CLIP image EncoderTransformer(L=5) forward, CE + KL compare, "
                                 f"fwd+bwd+clip+AdamW"),

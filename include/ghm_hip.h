@@ -247,6 +247,15 @@ int ghm_guide_blks_fwd(const float* const* H, const float* const* msgs, const in
                        int nb, float* part, int64_t n_seq, void* stream);
 int ghm_guide_blks_bwd(const float* const* H, const float* const* msgs, const int32_t* desc, const int64_t* desc64,
                        int nb, float* dH, float scale, int64_t n_seq, void* stream);
+/* The same for a residual stream of row pitch D (block columns col + V <= D): the
+ * guided joint VLM (train_NWP.py --guide=True, model.py:303-331, loss :1122-1149,
+ * D = 256, dense per-position targets: ext = 1). */
+int ghm_guide_blks_fwd_d(const float* const* H, const float* const* msgs, const int32_t* desc,
+                         const int64_t* desc64, int nb, int D, float* part, int64_t n_seq, void* stream);
+int ghm_guide_blks_bwd_d(const float* const* H, const float* const* msgs, const int32_t* desc,
+                         const int64_t* desc64, int nb, int D, float* dH, float scale, int64_t n_seq, void* stream);
+/* Largest nb the block-list launches take (32). */
+int ghm_guide_max_blocks(void);
 
 /* ---- sequential conditional denoising (CDM, train_sequential_DNS.py) ---------
  * ConditionalDenoiseEncoderTransformer (models/model.py:337-532, sequential=True)

@@ -220,18 +220,19 @@ extern "C" int ghm_guide_total(const float* part, int n_parts, int64_t n_seq, fl
 struct GuideBlk {
   int T, tok0, ntok, col, ext, V;
   int64_t msg_stride, moff;
+  int ld;  // row pitch of H (the model width: 128 for the encoder / CDM, 256 for the VLM)
 };
 
 __global__ __launch_bounds__(256) void k_guide_blk_fwd(const float* __restrict__ H, const float* __restrict__ msgs,
                                                        float* __restrict__ part, GuideBlk b) {
   __shared__ float red[4];
   const int n = blockIdx.x;
-  const float* h = H + (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+  const float* h = H + (static_cast<int64_t>(n) * b.T + b.tok0) * b.ld + b.col;
   const float* m = msgs + static_cast<int64_t>(n) * b.msg_stride + b.moff;
   float s = 0.f;
   for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
     const int t = e / b.V, c = e - t * b.V;
-    const float dd = h[static_cast<int64_t>(t) * GHM_D + c] - m[(t / b.ext) * b.V + c];
+    const float dd = h[static_cast<int64_t>(t) * b.ld + c] - m[(t / b.ext) * b.V + c];
     s += dd * dd;
   }
   s = sum32(s);
@@ -250,16 +251,16 @@ __global__ __launch_bounds__(256) void k_guide_blk_bwd(const float* __restrict__
   const int64_t n = i / per;
   const int r = static_cast<int>(i - n * per);
   const int t = r / b.V, c = r - t * b.V;
-  const int64_t at = (n * b.T + b.tok0 + t) * GHM_D + b.col + c;
+  const int64_t at = (n * b.T + b.tok0 + t) * b.ld + b.col + c;
   const float target = msgs[n * b.msg_stride + b.moff + (t / b.ext) * b.V + c];
   dH[at] += scale * (H[at] - target);
 }
 
 static int guide_blk_check(GuideBlk& b, int T, int tok0, int ntok, int col, int64_t msg_stride, int64_t moff,
-                           int ext, int V, int64_t n_seq) {
-  b = GuideBlk{T, tok0, ntok, col, ext, V, msg_stride, moff};
-  if (!(n_seq >= 1 && T >= 1 && tok0 >= 0 && ntok >= 1 && tok0 + ntok <= T && V >= 1 && col >= 0 &&
-        col + V <= GHM_D && ext >= 1 && moff >= 0 && moff + static_cast<int64_t>((ntok - 1) / ext + 1) * V <= msg_stride))
+                           int ext, int V, int64_t n_seq, int ld = GHM_D) {
+  b = GuideBlk{T, tok0, ntok, col, ext, V, msg_stride, moff, ld};
+  if (!(n_seq >= 1 && T >= 1 && tok0 >= 0 && ntok >= 1 && tok0 + ntok <= T && V >= 1 && col >= 0 && ld >= 1 &&
+        col + V <= ld && ext >= 1 && moff >= 0 && moff + static_cast<int64_t>((ntok - 1) / ext + 1) * V <= msg_stride))
     return -1;
   return 0;
 }
@@ -305,12 +306,12 @@ __global__ __launch_bounds__(256) void k_guide_blks_fwd(GuideBlkSet set, float* 
   const int n = blockIdx.x;
   for (int k = 0; k < set.nb; ++k) {
     const GuideBlk& b = set.b[k];
-    const float* h = set.H[k] + (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+    const float* h = set.H[k] + (static_cast<int64_t>(n) * b.T + b.tok0) * b.ld + b.col;
     const float* m = set.msgs[k] + static_cast<int64_t>(n) * b.msg_stride + b.moff;
     float s = 0.f;
     for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
       const int t = e / b.V, c = e - t * b.V;
-      const float dd = h[static_cast<int64_t>(t) * GHM_D + c] - m[(t / b.ext) * b.V + c];
+      const float dd = h[static_cast<int64_t>(t) * b.ld + c] - m[(t / b.ext) * b.V + c];
       s += dd * dd;
     }
     s = sum32(s);
@@ -327,10 +328,10 @@ __global__ __launch_bounds__(256) void k_guide_blks_bwd(GuideBlkSet set, float* 
   for (int k = 0; k < set.nb; ++k) {
     const GuideBlk& b = set.b[k];
     const float* m = set.msgs[k] + static_cast<int64_t>(n) * b.msg_stride + b.moff;
-    const int64_t base = (static_cast<int64_t>(n) * b.T + b.tok0) * GHM_D + b.col;
+    const int64_t base = (static_cast<int64_t>(n) * b.T + b.tok0) * b.ld + b.col;
     for (int e = threadIdx.x; e < b.ntok * b.V; e += 256) {
       const int t = e / b.V, c = e - t * b.V;
-      const int64_t at = base + static_cast<int64_t>(t) * GHM_D + c;
+      const int64_t at = base + static_cast<int64_t>(t) * b.ld + c;
       dH[at] += scale * (set.H[k][at] - m[(t / b.ext) * b.V + c]);
     }
     __syncthreads();
@@ -339,13 +340,13 @@ __global__ __launch_bounds__(256) void k_guide_blks_bwd(GuideBlkSet set, float* 
 
 // desc[k*6 ..] = {T, tok0, ntok, col, ext, V}, desc64[k*2 ..] = {msg_stride, moff}
 static int guide_blks_set(GuideBlkSet& set, const float* const* H, const float* const* msgs, const int32_t* desc,
-                          const int64_t* desc64, int nb, int64_t n_seq) {
+                          const int64_t* desc64, int nb, int64_t n_seq, int ld = GHM_D) {
   if (!(H && msgs && desc && desc64 && nb >= 1 && nb <= GUIDE_MAXBLK)) return -1;
   set.nb = nb;
   for (int k = 0; k < nb; ++k) {
     const int32_t* d = desc + 6 * k;
     if (!H[k] || !msgs[k]) return -1;
-    if (guide_blk_check(set.b[k], d[0], d[1], d[2], d[3], desc64[2 * k], desc64[2 * k + 1], d[4], d[5], n_seq))
+    if (guide_blk_check(set.b[k], d[0], d[1], d[2], d[3], desc64[2 * k], desc64[2 * k + 1], d[4], d[5], n_seq, ld))
       return -1;
     set.H[k] = H[k];
     set.msgs[k] = msgs[k];
@@ -373,6 +374,31 @@ extern "C" int ghm_guide_blks_bwd(const float* const* H, const float* const* msg
                      dH, scale);
   return ghm_launch_status();
 }
+
+// The same block lists for a residual stream of row pitch D (the guided joint VLM,
+// D = 256: train_NWP.py --guide=True, model.py:303-331, 1122-1149)
+extern "C" int ghm_guide_blks_fwd_d(const float* const* H, const float* const* msgs, const int32_t* desc,
+                                    const int64_t* desc64, int nb, int D, float* part, int64_t n_seq, void* stream) {
+  GHM_CHECK(part, "null pointer");
+  GuideBlkSet set;
+  GHM_CHECK(guide_blks_set(set, H, msgs, desc, desc64, nb, n_seq, D) == 0, "guide block list");
+  hipLaunchKernelGGL(k_guide_blks_fwd, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream), set,
+                     part, static_cast<int>(n_seq));
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_blks_bwd_d(const float* const* H, const float* const* msgs, const int32_t* desc,
+                                    const int64_t* desc64, int nb, int D, float* dH, float scale, int64_t n_seq,
+                                    void* stream) {
+  GHM_CHECK(dH, "null pointer");
+  GuideBlkSet set;
+  GHM_CHECK(guide_blks_set(set, H, msgs, desc, desc64, nb, n_seq, D) == 0, "guide block list");
+  hipLaunchKernelGGL(k_guide_blks_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream), set,
+                     dH, scale);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_guide_max_blocks(void) { return GUIDE_MAXBLK; }
 
 // ---------------------------------------------------------------------------
 // Dense-target helpers for the module API (GuidedClipLoss(guide=True) on the

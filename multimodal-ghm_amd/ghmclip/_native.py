@@ -64,6 +64,9 @@ HIP_SIGNATURES = {
     "ghm_guide_blk_bwd": [_p, _i, _i, _i, _i, _p, _i64, _i64, _i, _i, _p, _f, _i64, _p],
     "ghm_guide_blks_fwd": [_p, _p, _p, _p, _i, _p, _i64, _p],
     "ghm_guide_blks_bwd": [_p, _p, _p, _p, _i, _p, _f, _i64, _p],
+    "ghm_guide_blks_fwd_d": [_p, _p, _p, _p, _i, _i, _p, _i64, _p],
+    "ghm_guide_blks_bwd_d": [_p, _p, _p, _p, _i, _i, _p, _f, _i64, _p],
+    "ghm_guide_max_blocks": [],
     "ghm_cdm_readout_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ls_loss": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_cdm_readout_bwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
@@ -107,7 +110,7 @@ HIP_SIGNATURES = {
     "ghm_add_cols": [_p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64,
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64,
             "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
             "ghm_ce_kl_out_elems": _i64}
 

@@ -18,6 +18,7 @@ import torch
 from .. import _native
 
 __all__ = ["GenTransition", "PPCLIPLoss", "DoubleSampler", "ClipSampler", "bp_cls_posterior", "guided_targets",
+           "vlm_guide_planes",
            "NativeClipSampler", "ConditionalDenoiseSampler", "bp_dns_posterior", "bp_cls_root_message",
            "NextWordPredictSampler", "bp_nwp_posterior"]
 
@@ -400,23 +401,35 @@ class ConditionalDenoiseSampler(DoubleSampler):
         return np.mean(loss), np.std(loss) / np.sqrt(n_eval)
 
 
-def bp_nwp_posterior(templ, leaves, ext):
-    """BP_NWP_autoregressive(guide_info=False) (data_random_GHM.py:336-466) on the
-    host, vectorised over the batch: p(leaf p+1 | leaves <= p, image evidence ext)
-    for every position p, [B, n_leaves - 1, V] float32 (the reference's predict_pp
-    tensor dtype).  templ [L][C][V][V]; leaves [B, n_leaves]; ext [V, B].
+def bp_nwp_posterior(templ, leaves, ext, guide=False):
+    """BP_NWP_autoregressive (data_random_GHM.py:336-466) on the host, vectorised
+    over the batch: p(leaf p+1 | leaves <= p, image evidence ext) for every
+    position p, [B, n_leaves - 1, V] float32 (the reference's predict_pp tensor
+    dtype).  templ [L][C][V][V]; leaves [B, n_leaves]; ext [V, B].
     A node's qd message is rewritten whenever it is an ancestor of the current
     leaf, so completed earlier siblings keep their last (complete) message, as in
-    the reference's mutable tree."""
+    the reference's mutable tree.
+    guide=True (guide_info=True) also returns the 2L + 1 guide targets of every
+    position, float32: [0] the leaf's qd [B, n-1, V] (:372-373); [1..L-1] the
+    (hd, qd) of its ancestors at depth L-1 .. 1 [B, n-1, 2V] (:392-394); [L] the
+    root's (hd, bu) — one array in the reference (bu_message = hd_message, then
+    += in place, :414-421), so both halves hold the final bu; [L+1 .. 2L] the bu
+    of the target leaf's path from depth 1 down to the leaf [B, n-1, V] (:449-451)."""
     n_layer, C, V, _ = templ.shape
     lv = np.asarray(leaves).astype(np.int64).T
     n_leaves, B = lv.shape
     qd = [None] + [np.zeros((C ** d, V, B)) for d in range(1, n_layer + 1)]
     hd = [None] + [np.zeros((C ** d, V, B)) for d in range(1, n_layer)]
     out = np.zeros((B, n_leaves - 1, V), dtype=np.float32)
+    if guide:
+        gl = ([np.zeros((B, n_leaves - 1, V), np.float32)] +
+              [np.zeros((B, n_leaves - 1, 2 * V), np.float32) for _ in range(n_layer)] +
+              [np.zeros((B, n_leaves - 1, V), np.float32) for _ in range(n_layer)])
     for p in range(n_leaves - 1):
         q = np.log(templ[-1, p % C][:, lv[p]])  # leaf message :370-371
         qd[n_layer][p] = q - q.max(0)
+        if guide:
+            gl[0][:, p, :] = qd[n_layer][p].T
         idn, goal, share = p, [p + 1], [False]
         for layer in range(n_layer - 1, 0, -1):  # prefix evidence up to the root :381-406
             par = idn // C
@@ -428,6 +441,9 @@ def bp_nwp_posterior(templ, leaves, ext):
             hd[layer][par] = h
             qq = np.log(templ[layer - 1, par % C] @ np.exp(h))
             qd[layer][par] = qq - qq.max(0)
+            if guide:
+                gl[n_layer - layer][:, p, :V] = h.T
+                gl[n_layer - layer][:, p, V:] = qd[layer][par].T
             goal.append(goal[-1] // C)
             idn = par
             share.append(idn == goal[-1])
@@ -438,6 +454,9 @@ def bp_nwp_posterior(templ, leaves, ext):
         bu -= bu.max(0)
         bu = bu + ext
         bu -= bu.max(0)
+        if guide:
+            gl[n_layer][:, p, :V] = bu.T
+            gl[n_layer][:, p, V:] = bu.T
         for layer in range(1, n_layer + 1):  # down the target's path :435-452
             k = goal[-layer]
             mat = templ[layer - 1, k % C].T
@@ -446,8 +465,34 @@ def bp_nwp_posterior(templ, leaves, ext):
             else:
                 b = np.log(mat @ np.exp(bu))
             bu = b - b.max(0)
+            if guide:
+                gl[n_layer + layer][:, p, :] = bu.T
         w = np.exp(bu)
         out[:, p, :] = (w / w.sum(0)).T
+    return (out, gl) if guide else out
+
+
+def vlm_guide_planes(text_targets, image_targets, V, out=None):
+    """Pack the guided-VLM targets into the per-sample block planes the fused
+    trainer's penalty kernels read (VLM_GUIDE_BLOCKS order): the 13 text blocks
+    [n_text][V] (leaf q; (hd, qd) of depths L-1 .. 1 and of the root, split in
+    two; the path bu), then the L image blocks [n_image][V].  Returns float32
+    [B, 13 * n_text * V + L * n_image * V]."""
+    planes = []
+    for t in text_targets:
+        if t.shape[2] == V:
+            planes.append(t)
+        else:
+            planes += [t[:, :, :V], t[:, :, V:]]
+    planes += [np.asarray(x) for x in image_targets]
+    B = planes[0].shape[0]
+    flat = [np.ascontiguousarray(p, dtype=np.float32).reshape(B, -1) for p in planes]
+    if out is None:
+        return np.concatenate(flat, axis=1)
+    off = 0
+    for p in flat:
+        out[:, off:off + p.shape[1]] = p
+        off += p.shape[1]
     return out
 
 
@@ -477,23 +522,37 @@ class NextWordPredictSampler(DoubleSampler):
         self.native.push_numpy_state()
         return tl, il, root
 
-    def posterior(self, tl, il):
-        """(next-word posteriors [B, T-1, V] float32, image BP_CLS posteriors [B, V])."""
+    def posterior(self, tl, il, guide=False):
+        """(next-word posteriors [B, T-1, V] float32, image BP_CLS posteriors [B, V]);
+        guide=True: (posteriors, image posteriors, text guide targets (the 2L + 1
+        arrays of bp_nwp_posterior), image guide targets (GHMTree.guided_info of the
+        image tree: L float32 [B, T, V]))."""
         p_y = np.ones(self.variable_type) / self.variable_type
         ext = bp_cls_root_message(self.i_templ, il)
-        return bp_nwp_posterior(self.t_templ, tl, ext), bp_cls_posterior(self.i_templ, il, p_y)
+        i_pp = bp_cls_posterior(self.i_templ, il, p_y)
+        if not guide:
+            return bp_nwp_posterior(self.t_templ, tl, ext), i_pp
+        post, tg = bp_nwp_posterior(self.t_templ, tl, ext, guide=True)
+        ig = [m.numpy() for m in guided_targets(self.i_templ, il)]
+        return post, i_pp, tg, ig
 
     def get_batch(self, batch_size=128, device="cpu", guide=False):
-        """:902-929.  Returns (text inputs int64 [B, T-1], targets [B, T-1], None,
-        posteriors float32 [B, T-1, V] (torch, on device)), (image leaves int64
-        [B, T], roots [B], None, image posteriors [B, V])."""
-        if guide:
-            raise NotImplementedError("guided VLM (BP_NWP guide_info targets) is not built yet")
+        """:902-929.  Returns (text inputs int64 [B, T-1], targets [B, T-1], text
+        guide targets, posteriors float32 [B, T-1, V] (torch, on device)), (image
+        leaves int64 [B, T], roots [B], image guide targets, image posteriors
+        [B, V]); the guide targets (guide=True, else None) are lists of float32
+        torch tensors in the reference's order (BP_NWP_autoregressive guide_info,
+        GHMTree.guided_info)."""
         tl, il, root = self.draw_numpy(batch_size)
-        post, i_pp = self.posterior(tl, il)
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a).astype(np.int64)).to(device)  # noqa: E731
-        return ((to(tl[:, :-1]), to(tl[:, 1:]), None, torch.from_numpy(post).to(device)),
-                (to(il), to(root), None, i_pp))
+        if guide:
+            post, i_pp, tg, ig = self.posterior(tl, il, guide=True)
+            tg = [torch.from_numpy(x).to(device) for x in tg]
+            ig = [torch.from_numpy(x).to(device) for x in ig]
+        else:
+            (post, i_pp), tg, ig = self.posterior(tl, il), None, None
+        return ((to(tl[:, :-1]), to(tl[:, 1:]), tg, torch.from_numpy(post).to(device)),
+                (to(il), to(root), ig, i_pp))
 
     def get_Bayes(self, n_eval=30000):
         """:931-942 — mean and standard error of -log p(next leaf) under the exact

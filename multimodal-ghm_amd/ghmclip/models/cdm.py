@@ -16,11 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import D_MODEL, EncoderPlan, default_precision, require_hip
-
-
-def self_precision_f32():
-    return default_precision() == "f32"
+from .hip_encoder import D_MODEL, EncoderPlan, require_hip
 
 __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
            "cdm_param_names", "CDM_UNTRAINED", "CDM_JOINT_UNTRAINED"]
@@ -205,9 +201,6 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
             raise NotImplementedError("HIP CDM: guide=True is built for the joint model (train_CDNS.py) only")
         if guide and self.guided_layer_gap == 0:
             raise ValueError("guide=True needs n_layer >= 2 * n_guided_layers[1] + 1 (model.py:372)")
-        if not sequential and n_token > 96 and self_precision_f32():
-            raise NotImplementedError("HIP CDM: the joint model's sequences past 96 tokens need the split-bf16 "
-                                      "(x3) attention kernels (GHM_PRECISION=f32 is set)")
         if n_mlp_hidden != 4 * n_embd:
             raise NotImplementedError("HIP CDM: n_mlp_hidden = 4 * n_embd")
         # construction (RNG) order of the reference, model.py:382-402

@@ -85,11 +85,12 @@ class EncoderPlan:
         self.precision = default_precision() if precision is None else precision
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
-        if n_token > 192 or (n_token > 96 and self.precision != "x3"):
-            raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens, <= 192 with the split-bf16 "
-                             f"(x3) kernels (got {n_token}, precision {self.precision})")
+        if n_token > 192:
+            raise ValueError(f"the HIP attention kernels take sequences of <= 192 tokens (got {n_token})")
         # sequences past 96 tokens (the joint CDM's 162) run on ghm_attn_ext_*_x3 with
-        # P / dS padded to 192
+        # P / dS padded to 192; precision "f32" there takes the exact-f32 attention of
+        # _attn_fwd_f32 / _attn_bwd_f32 (fp32 library products: a validation mode that
+        # separates the split-bf16 rounding from the curve's chaos)
         self.long_attn = n_token > 96
         pad = 192 if self.long_attn else 96
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
@@ -207,12 +208,41 @@ class EncoderPlan:
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-            c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-              N, T, D_MODEL, self.scale_div, s)
+            if self.long_attn:
+                self._attn_fwd_f32(l)
+            else:
+                c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                  N, T, D_MODEL, self.scale_div, s)
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
               _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
               _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+
+    def _attn_fwd_f32(self, l):
+        """Exact-f32 single-head attention past 96 tokens (model.py:489-497 of the
+        joint CDM: softmax(QK^T / sqrt(d)) V, plain residual), on the current stream:
+        Hmid = H + P V, P saved (dense, padded) for the backward."""
+        N, T = self.N, self.T
+        q = self.qkv[l].view(N, T, 3 * D_MODEL)
+        Q, K, V = q[..., :D_MODEL], q[..., D_MODEL:2 * D_MODEL], q[..., 2 * D_MODEL:]
+        A = torch.softmax(torch.bmm(Q, K.transpose(1, 2)) / self.scale_div, dim=-1)
+        self.P[l, :, :T, :T] = A
+        torch.baddbmm(self.H[l].view(N, T, D_MODEL), A, V, out=self.Hmid[l].view(N, T, D_MODEL))
+
+    def _attn_bwd_f32(self, l, dHmid):
+        """Backward of _attn_fwd_f32 into dqkv = [dQ | dK | dV] (the residual's
+        gradient stays in dHmid, as ghm_attn_bwd)."""
+        N, T = self.N, self.T
+        q = self.qkv[l].view(N, T, 3 * D_MODEL)
+        Q, K, V = q[..., :D_MODEL], q[..., D_MODEL:2 * D_MODEL], q[..., 2 * D_MODEL:]
+        A = self.P[l, :, :T, :T]
+        dO = dHmid.view(N, T, D_MODEL)
+        dq = self.dqkv.view(N, T, 3 * D_MODEL)
+        dA = torch.bmm(dO, V.transpose(1, 2))
+        dS = A * (dA - (dA * A).sum(-1, keepdim=True)) / self.scale_div
+        dq[..., :D_MODEL] = torch.bmm(dS, K)
+        dq[..., D_MODEL:2 * D_MODEL] = torch.bmm(dS.transpose(1, 2), Q)
+        dq[..., 2 * D_MODEL:] = torch.bmm(A.transpose(1, 2), dO)
 
     def split_weights(self, p, s=None):
         """Write every layer's pre-split bf16 weight pack (precision "x3")."""
@@ -324,7 +354,9 @@ class EncoderPlan:
               _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
             jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            if self.long_attn:
+            if self.long_attn and not x3:
+                self._attn_bwd_f32(l, cur)
+            elif self.long_attn:
                 c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
                   _ptr(self.dqkv), N, T, D_MODEL, T, self.scale_div, 0.0, s)
             else:

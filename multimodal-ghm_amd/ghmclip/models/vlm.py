@@ -34,6 +34,7 @@ from .. import _native
 from .hip_encoder import PRECISIONS, default_precision, require_hip
 
 __all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names",
+           "vlm_guide_blocks", "vlm_guide_plane_elems",
            "VLM_UNTRAINED", "VLM_JOINT_UNTRAINED"]
 
 # never given a gradient by the reference in sequential mode (the image prefix is a
@@ -168,12 +169,17 @@ class VlmPlan:
         self._gen += 1
         return self.logits
 
-    def backward(self, p, g, dlogits=None):
+    def backward(self, p, g, dlogits=None, layer_grad=None):
         """Writes d(loss)/d(param) into g[name] for every trained parameter (not
         VLM_UNTRAINED) from dlogits [M, V] (defaults to self.dlogits).  Returns
-        dL/dH_0 [M, D] (its prefix rows give the gradient of the features)."""
+        dL/dH_0 [M, D] (its prefix rows give the gradient of the features).
+        layer_grad: optional {layer l: fn(dH, stream)} adding a loss term's gradient
+        w.r.t. H[l+1] (the guided layers, model.py:303-331) before layer l's
+        backward (split-bf16 path)."""
         if self.precision == "x3":
-            return self._backward_x3(p, g, dlogits)
+            return self._backward_x3(p, g, dlogits, layer_grad)
+        if layer_grad:
+            raise NotImplementedError("guided VLM layers run on the split-bf16 (x3) path")
         s = _stream()
         c = _native.call
         M, D = self.M, self.D
@@ -249,7 +255,7 @@ class VlmPlan:
         pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
         _native.call("ghm_gemm_reduce", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk, s)
 
-    def _backward_x3(self, p, g, dlogits=None):
+    def _backward_x3(self, p, g, dlogits=None, layer_grad=None):
         s = _stream()
         c = _native.call
         M, D, F = self.M, self.D, self.F
@@ -259,6 +265,8 @@ class VlmPlan:
         torch.mm(dz.t(), self.H[self.L], out=g["_read_out.weight"])
         torch.sum(dz, 0, out=g["_read_out.bias"])
         for l in reversed(range(self.L)):
+            if layer_grad and l in layer_grad:
+                layer_grad[l](cur, s)
             w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
             self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s)
             self._colsum(cur, M, D, g[f"_mlps.{l}.2.bias"], s)
@@ -300,6 +308,68 @@ class VlmPlan:
         _native.call("ghm_reduce_batch", (_native.ReduceJob * 1)(j), 1, s)
 
 
+def vlm_guide_blocks(model, n_text, V):
+    """The guided outputs of AutoRegressiveTransformer.forward (model.py:303-331) as
+    column blocks of H[l+1] and their targets in vlm_guide_planes' per-sample
+    layout: {layer: [(tok0, ntok, col, plane_offset, group)]} in the reference's
+    loss-term order, group in ("loss2", "loss4", "loss5", "loss3") = the
+    ConditionalGuidedCELoss penalty terms (model.py:1122-1144: text downward incl.
+    the leaf, text root, text upward, image).  Text block k (k-th text-guided
+    layer): k = 0 the leaf q at columns index_q; 0 < k <= n_t the (h, q) pair at
+    (index_h, index_q); k > n_t the u at index_u; image blocks at index_i."""
+    n_t, n_i, P = model.n_t_guided_layer, model.n_i_guided_layer, model.n_i_token
+    n_tplanes = 3 * n_t + 1
+    tplane = lambda k: n_text * V * k  # noqa: E731
+    iplane = lambda j: n_text * V * n_tplanes + P * V * j  # noqa: E731
+    index_q, index_h, index_u, index_i = 0, (n_t + 1) * V, (2 * n_t + 1) * V, 0
+    counter, img = 0, 0
+    blocks = {}
+    for l in range(model.n_layer):
+        blks = []
+        if model.t_guided_layer_flag[l]:
+            if counter == 0:
+                blks.append((P, n_text, index_q, tplane(0), "loss2"))
+                index_q += V
+            elif counter < n_t + 1:
+                grp = "loss2" if counter < n_t else "loss4"
+                blks.append((P, n_text, index_h, tplane(2 * counter - 1), grp))
+                blks.append((P, n_text, index_q, tplane(2 * counter), grp))
+                index_h += V
+                index_q += V
+            else:
+                blks.append((P, n_text, index_u, tplane(2 * n_t + counter - n_t), "loss5"))
+                index_u += V
+            counter += 1
+        if model.i_guided_layer_flag[l]:
+            blks.append((0, P, index_i, iplane(img), "loss3"))
+            index_i += V
+            img += 1
+        if blks:
+            blocks[l] = blks
+    return blocks
+
+
+def _guided_slices(model, n_text):
+    """The reference's guided outputs in return order: text outputs (one per
+    text-guided layer; the (h, q) pair concatenated) then image outputs, each as
+    (layer, [(tok0, ntok, col)], kind)."""
+    blocks = vlm_guide_blocks(model, n_text, model.vocab_size)
+    text, image = [], []
+    for l in sorted(blocks):
+        tb = [(t0, nt, c) for (t0, nt, c, _, g) in blocks[l] if g != "loss3"]
+        ib = [(t0, nt, c) for (t0, nt, c, _, g) in blocks[l] if g == "loss3"]
+        if tb:
+            text.append((l, tb, "t"))
+        if ib:
+            image.append((l, ib, "i"))
+    return text + image
+
+
+def vlm_guide_plane_elems(model, n_text, V):
+    """Floats per sample of the guide target planes (vlm_guide_planes)."""
+    return n_text * V * (3 * model.n_t_guided_layer + 1) + model.n_i_token * V * model.n_i_guided_layer
+
+
 class _VlmFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, module, xt, zi, *params):
@@ -315,11 +385,33 @@ class _VlmFn(torch.autograd.Function):
             logits = plan.forward(pd, plan.xt, feat)
         ctx.module, ctx.plan, ctx.gen = module, plan, plan._gen
         ctx.save_for_backward(*params)
-        return logits.view(N, T1 + zi.shape[1], -1)[:, zi.shape[1]:, :].clone()
+        out = logits.view(N, T1 + zi.shape[1], -1)[:, zi.shape[1]:, :].clone()
+        if not module.guide:
+            return out
+        # guided outputs (model.py:303-331): copies of the column blocks of H[l+1]
+        ctx.gslices = _guided_slices(module, T1)
+        Hv = plan.H.view(plan.L + 1, N, plan.T, plan.D)
+        guided = [torch.cat([Hv[l + 1, :, t0:t0 + nt, c:c + module.vocab_size] for (t0, nt, c) in blks], dim=2)
+                  for (l, blks, _) in ctx.gslices]
+        return (out, *guided)
 
     @staticmethod
-    def backward(ctx, dlog):
+    def backward(ctx, dlog, *dguided):
         plan = ctx.plan
+        layer_grad = None
+        if ctx.module.guide:  # add each guided output's gradient into dH[l+1] before layer l's backward
+            V = ctx.module.vocab_size
+            hooks = {}
+            for (l, blks, _), gd in zip(ctx.gslices, dguided):
+                if gd is None:
+                    continue
+
+                def fn(dH, s, blks=blks, gd=gd):
+                    dv = dH.view(plan.N, plan.T, plan.D)
+                    for j, (t0, nt, c) in enumerate(blks):
+                        dv[:, t0:t0 + nt, c:c + V] += gd[:, :, j * V:(j + 1) * V]
+                hooks.setdefault(l, []).append(fn)
+            layer_grad = {l: (lambda dH, s, fs=fs: [f(dH, s) for f in fs]) for l, fs in hooks.items()}
         if plan._gen != ctx.gen:
             raise RuntimeError("AutoRegressiveTransformer: another forward of this module overwrote the "
                                "activations saved for backward")
@@ -329,7 +421,7 @@ class _VlmFn(torch.autograd.Function):
         grads = {n: torch.empty_like(p) for n, p in zip(names, params) if n not in untrained}
         dz = torch.zeros(plan.N, plan.T, plan.V, dtype=torch.float32, device=dlog.device)
         dz[:, plan.P:, :] = dlog
-        dH0 = plan.backward(dict(zip(names, params)), grads, dlogits=dz.view(plan.M, plan.V))
+        dH0 = plan.backward(dict(zip(names, params)), grads, dlogits=dz.view(plan.M, plan.V), layer_grad=layer_grad)
         d_zi = None
         if ctx.needs_input_grad[2] and not plan.joint:
             d_zi = dH0.view(plan.N, plan.T, plan.D)[:, :plan.P, :plan.V].clone()
@@ -368,8 +460,11 @@ class AutoRegressiveTransformer(nn.Module):
         self.n_t_guided_layer = n_guided_layers[0]
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[0] * 2 + 1)
-        if activation != "softmax" or not mlp or not layernorm or guide:
-            raise NotImplementedError("HIP VLM: softmax attention, mlp=True, layernorm=True, guide=False")
+        if activation != "softmax" or not mlp or not layernorm:
+            raise NotImplementedError("HIP VLM: softmax attention, mlp=True, layernorm=True")
+        if guide and sequential:
+            raise NotImplementedError("HIP VLM: guide=True is built for the joint model (train_NWP.py, "
+                                      "exp_vlm_guidedTF.sh)")
         if not auto_regressive or (sequential and n_i_token != 1):
             raise NotImplementedError("HIP VLM: auto_regressive=True; sequential=True takes one prefix token "
                                       "(train_sequential_NWP.py), sequential=False the image leaves "
@@ -388,7 +483,8 @@ class AutoRegressiveTransformer(nn.Module):
         self.i_guided_layer_flag = [False] * n_layer
         self.t_embedding = nn.Embedding(self.vocab_size, self.n_embd)
         self.i_embedding = nn.Embedding(self.vocab_size, self.n_embd)
-        for _ in range(n_layer):
+        counter = 0
+        for i in range(n_layer):
             self._queries.append(nn.Linear(n_embd, n_embd, bias=False))
             self._keys.append(nn.Linear(n_embd, n_embd, bias=False))
             self._values.append(nn.Linear(n_embd, n_embd, bias=False))
@@ -396,6 +492,15 @@ class AutoRegressiveTransformer(nn.Module):
             self._mlps.append(nn.Sequential(nn.Linear(n_embd, n_mlp_hidden), nn.GELU(),
                                             nn.Linear(n_mlp_hidden, n_embd)))
             self._lns_2.append(nn.LayerNorm([self.n_embd]))
+            # guided-layer flags (model.py:207-216); n_layer < 2 n_t + 1 divides by
+            # zero in the reference too
+            if guide and counter < self.n_t_guided_layer * 2 + 1 and (i + 1) % self.guided_layer_gap == 0:
+                self.t_guided_layer_flag[i] = True
+                if counter < self.n_i_guided_layer:
+                    self.i_guided_layer_flag[i] = True
+                if counter == self.n_t_guided_layer - 1 and self.n_i_guided_layer < self.n_t_guided_layer:
+                    self.i_guided_layer_flag[i] = True
+                counter += 1
         self._read_out = nn.Linear(n_embd, self.vocab_size)
         self._out = nn.Linear(n_token, 1)
         self._names = vlm_param_names(n_layer)
@@ -434,24 +539,41 @@ class AutoRegressiveTransformer(nn.Module):
         for prm in params:
             if prm.dtype != torch.float32 or not prm.is_contiguous():
                 raise RuntimeError("HIP VLM parameters must be contiguous fp32")
-        logits = _VlmFn.apply(self, xt, zi, *params)
-        return logits, [[], []]
+        res = _VlmFn.apply(self, xt, zi, *params)
+        if not self.guide:
+            return res, [[], []]
+        n_t = sum(self.t_guided_layer_flag)
+        return res[0], [list(res[1:1 + n_t]), list(res[1 + n_t:])]
 
 
 class ConditionalGuidedCELoss(nn.Module):
-    """models/model.py:1080-1149 (guide=False): returns (loss, 0, 0, 0, 0)."""
+    """models/model.py:1080-1149: per-sample mean cross entropy; with guide the
+    penalty * squared Frobenius norms of the guided outputs against their BP
+    targets, grouped as the reference logs them (text downward incl. the leaf,
+    text root, text upward, image).  Returns (loss, loss2, loss4, loss5, loss3).
+    The fused VlmTrainer evaluates the same terms on the device."""
 
     def __init__(self, penalty=1e-4, guide=False):
         super().__init__()
         self.penalty = penalty
         self.guide = guide
-        if guide:
-            raise NotImplementedError("guided VLM penalties are not built yet")
 
     def forward(self, inputs, targets, verbose=False):
         logits = inputs[0].reshape(-1, inputs[0].size(-1))
         loss = nn.functional.cross_entropy(logits, targets[0].reshape(-1), reduction="none")
-        return loss.reshape(-1, targets[0].shape[1]).mean(dim=1).mean(), 0, 0, 0, 0
+        loss = loss.reshape(-1, targets[0].shape[1]).mean(dim=1)
+        if not self.guide:
+            return loss.mean(), 0, 0, 0, 0
+        sq = lambda a, b: self.penalty * ((a - b) ** 2).sum(dim=(1, 2))  # noqa: E731
+        gin, gtg = inputs[1][0], targets[1][0]
+        half = len(gin) // 2
+        loss2 = sum(sq(gin[i], gtg[i]) for i in range(half))
+        loss5 = sum(sq(gin[i + half + 1], gtg[i + half + 1]) for i in range(half))
+        loss4 = sq(gin[half], gtg[half])
+        loss3 = sum(sq(a, b) for a, b in zip(inputs[1][1], targets[1][1]))
+        total = loss + loss2 + loss3 + loss4 + loss5
+        return (total.mean(), loss2.mean().item(), loss4.mean().item(), loss5.mean().item(),
+                loss3.mean().item())
 
 
 class KLdiv(nn.Module):

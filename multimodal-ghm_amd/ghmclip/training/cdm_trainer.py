@@ -177,11 +177,15 @@ class CdmTrainer:
         return lst
 
     def _guide_fwd(self, s):
-        """All guided blocks in one launch; part row k = the k-th block in layer order."""
+        """All guided blocks, in launches of at most ghm_guide_max_blocks() blocks
+        (one launch for the default 26); part row k = the k-th block in layer order."""
         if self._gfwd is None:
-            self._gfwd = self._blk_list([(l, b) for l, blks in sorted(self.gblocks.items()) for b in blks])
-        H, M, desc, desc64, n = self._gfwd
-        _native.call("ghm_guide_blks_fwd", H, M, desc, desc64, n, _p(self.gpart), self.B, s)
+            items = [(l, b) for l, blks in sorted(self.gblocks.items()) for b in blks]
+            mx = int(_native.hip_lib().ghm_guide_max_blocks())
+            self._gfwd = [(a, self._blk_list(items[a:a + mx])) for a in range(0, len(items), mx)]
+        for a, (H, M, desc, desc64, n) in self._gfwd:
+            _native.call("ghm_guide_blks_fwd", H, M, desc, desc64, n, ctypes.c_void_p(self.gpart[a].data_ptr()),
+                         self.B, s)
 
     def _guide_hooks(self):
         """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / B,
@@ -193,9 +197,11 @@ class CdmTrainer:
         for l, blks in self.gblocks.items():
             def fn(dH, s, l=l, blks=blks):
                 if l not in self._gbwd:
-                    self._gbwd[l] = self._blk_list([(l, b) for b in blks])
-                H, M, desc, desc64, n = self._gbwd[l]
-                _native.call("ghm_guide_blks_bwd", H, M, desc, desc64, n, _p(dH), scale, self.B, s)
+                    mx = int(_native.hip_lib().ghm_guide_max_blocks())
+                    self._gbwd[l] = [self._blk_list([(l, b) for b in blks[a:a + mx]])
+                                     for a in range(0, len(blks), mx)]
+                for H, M, desc, desc64, n in self._gbwd[l]:  # in list order: shared columns accumulate
+                    _native.call("ghm_guide_blks_bwd", H, M, desc, desc64, n, _p(dH), scale, self.B, s)
             hooks[l] = fn
         return hooks
 

@@ -159,24 +159,29 @@ class CdmBatchPipeline(BatchPipeline):
 class NwpBatchPipeline(BatchPipeline):
     """The same producer for NextWordPredictSampler draws: text inputs / targets
     uint8 [B, T-1], the exact next-word posteriors float32 [B, T-1, V] (host BP,
-    bp_nwp_posterior) and image leaves uint8 [B, T].  sampler: the
-    NextWordPredictSampler (its native MT state already pulled from numpy).
-    row_slice: optional (rank, world) — a contiguous 1/world of the samples (the
-    VLM loss is a mean over samples, model.py:1087-1098)."""
+    bp_nwp_posterior) and image leaves uint8 [B, T]; guide=True also the packed
+    BP guide targets float32 [B, n] (vlm_guide_planes: train_NWP.py --guide=True).
+    sampler: the NextWordPredictSampler (its native MT state already pulled from
+    numpy).  row_slice: optional (rank, world) — a contiguous 1/world of the
+    samples (the VLM loss is a mean over samples, model.py:1087-1098)."""
 
-    def __init__(self, sampler, batch_size, n_slots=3, row_slice=None):
+    def __init__(self, sampler, batch_size, n_slots=3, row_slice=None, guide=False):
         self.sampler = sampler
+        self.guide = guide
         super().__init__(sampler.native, batch_size, n_slots, row_slice)
 
     def _make_slots(self, n_slots):
         B, T, V = self.B, self.s.T, self.sampler.variable_type
         self.T = T
+        L = self.sampler.n_layers
+        ng = (T - 1) * V * (3 * L[0] + 1) + T * V * L[1] if self.guide else 0
 
         def slot():
             return (torch.empty(B, T - 1, dtype=torch.uint8).pin_memory(),
                     torch.empty(B, T - 1, dtype=torch.uint8).pin_memory(),
                     torch.empty(B, T - 1, V, dtype=torch.float32).pin_memory(),
-                    torch.empty(B, T, dtype=torch.uint8).pin_memory())
+                    torch.empty(B, T, dtype=torch.uint8).pin_memory(),
+                    torch.empty(B, ng, dtype=torch.float32).pin_memory() if ng else None)
         self.slots = [slot() for _ in range(n_slots)]
         self.tl = np.empty((B, T), np.uint8)
         self.root = np.empty(B, np.uint8)
@@ -184,16 +189,23 @@ class NwpBatchPipeline(BatchPipeline):
             self.rows = shard_samples(B, *self.slice)
 
     def _fill(self, i):
-        xt, yt, post, il = self.slots[i]
+        from ..data.data_random_GHM import vlm_guide_planes
+        xt, yt, post, il, gt = self.slots[i]
         tl = self.tl
         self.s.next_cdm_into(self.B, 0.0, tl, il.numpy(), None, self.root)
         xt.numpy()[:] = tl[:, :-1]
         yt.numpy()[:] = tl[:, 1:]
-        post.numpy()[:] = self.sampler.posterior(tl, il.numpy())[0]
+        if self.guide:
+            p, _, tg, ig = self.sampler.posterior(tl, il.numpy(), guide=True)
+            post.numpy()[:] = p
+            vlm_guide_planes(tg, ig, self.sampler.variable_type, out=gt.numpy())
+        else:
+            post.numpy()[:] = self.sampler.posterior(tl, il.numpy())[0]
 
     def _stage(self, trainer, i):
-        xt, yt, post, il = self.slots[i]
+        xt, yt, post, il, gt = self.slots[i]
         if self.slice is not None:
             a, b = self.rows
             xt, yt, post, il = xt[a:b], yt[a:b], post[a:b], il[a:b]
-        trainer.set_batch(xt, yt, post, il)
+            gt = None if gt is None else gt[a:b]
+        trainer.set_batch(xt, yt, post, il, gt)

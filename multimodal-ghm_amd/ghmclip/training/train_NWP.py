@@ -9,7 +9,11 @@ The hot loop (:109-158) runs as the fused, HIP-graph-replayed VlmTrainer step in
 its joint mode (split-bf16 products and attention past 96 tokens); the native
 sampler and the host BP posteriors run in a producer thread.
 Differences, by design:
-  * --device must be a HIP device; guide=True is not built (NotImplementedError);
+  * --device must be a HIP device;
+  * --guide=True (exp_vlm_guidedTF.sh): the producer thread computes the BP guide
+    targets on the host next to the posteriors (bp_nwp_posterior(guide=True), the
+    image guided_info) and stages them with the batch; the penalties and their
+    gradients run inside the fused step (VlmTrainer guide branch);
   * checkpoints are read with the weights-only unpickler, and the saved 'loss'
     entry is a plain dict (type, penalty, guide) instead of the pickled module;
   * wandb/s3fs are optional (skipped with a warning when not installed);
@@ -53,8 +57,6 @@ def parse(argv=None):
 
 def main(argv=None):
     c = parse(argv)
-    if c.guide:
-        raise NotImplementedError("guided joint VLM (guide=True) is not built on the HIP path yet")
     ws, rank, device = distributed.setup()
     if ws == 1:
         print(f"Using GPU: {torch.cuda.get_device_name(0)}")
@@ -114,17 +116,18 @@ def main(argv=None):
     sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters)
              for i in range(c.total_iters)]
     trainer = VlmTrainer(model, None, c.batch_size // ws, sched, max_norm=c.max_norm, device=device,
-                         t_offset=t_offset, precision="x3")
+                         t_offset=t_offset, precision="x3", penalty=c.penalty)
     if t_offset:
         trainer.load_optimizer_state(optimizer)
     sampler.native.pull_numpy_state()  # the producer owns numpy's MT stream from here on
-    pipe = NwpBatchPipeline(sampler, c.batch_size, n_slots=3, row_slice=(rank, ws) if ws > 1 else None)
+    pipe = NwpBatchPipeline(sampler, c.batch_size, n_slots=3, row_slice=(rank, ws) if ws > 1 else None,
+                            guide=c.guide)
 
     def sync_hist(upto):
-        h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
-        h, ch = distributed.mean_histories([h, ch], device)  # every rank
+        h, ph, ch = trainer.loss_history(upto), trainer.ploss_history(upto), trainer.compare_history(upto)
+        h, ph, ch = distributed.mean_histories([h, ph, ch], device)  # every rank
         loss_history[:upto] = h
-        ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
+        ploss_history[:upto] = ph  # equals the loss without guidance
         compare_history[:upto] = ch
 
     def save(iter_num):
@@ -146,10 +149,11 @@ def main(argv=None):
                 sync_hist(iter_num + 1)
                 finish_time = time.time()
                 h = iter_num // 2
+                pen = trainer.guide_penalties()  # this rank's last step: output[1:5] of the reference
                 logger.info(f'Iter: {iter_num},Penalty train loss: {np.mean(ploss_history[h:iter_num]):.4f}, '
                             f'Train loss: {np.mean(loss_history[h:iter_num]):.4f}, '
                             f'Compare: {np.mean(compare_history[h:iter_num]):.4f}, '
-                            f'Penalty: [{0:.4f}, {0:.4f},{0:.4f},{0:.4f}],  Bayes:{Bayes_loss:.4f}, '
+                            f'Penalty: [{pen[0]:.4f}, {pen[1]:.4f},{pen[2]:.4f},{pen[3]:.4f}],  Bayes:{Bayes_loss:.4f}, '
                             f'LR: {lr:.6f}, Time: {(finish_time - curr_time):.2f}s')  # :135
                 if wandb:
                     wandb.log({'train_loss': loss_history[iter_num], 'penalty_train_loss': ploss_history[iter_num],

@@ -20,7 +20,7 @@ from .. import _native
 from . import distributed
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
-from ..models.vlm import VLM_JOINT_UNTRAINED, VLM_UNTRAINED, VlmPlan
+from ..models.vlm import VLM_JOINT_UNTRAINED, VLM_UNTRAINED, VlmPlan, vlm_guide_blocks, vlm_guide_plane_elems
 
 
 def _p(t):
@@ -29,7 +29,8 @@ def _p(t):
 
 class VlmTrainer:
     def __init__(self, model, clip_model, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
-                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None, precision=None):
+                 betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None, precision=None,
+                 penalty=0.001):
         """model: AutoRegressiveTransformer; clip_model: the frozen CLIP image
         EncoderTransformer (sequential model), or None for the joint model
         (sequential=False, train_NWP.py); lr_schedule: one learning rate per step.
@@ -107,6 +108,61 @@ class VlmTrainer:
         self.chist = torch.zeros_like(self.hist)
         self.graphs = None
         self.steps_done = 0
+        self._setup_guide(penalty)
+
+    def _setup_guide(self, penalty):
+        """Guided joint VLM (train_NWP.py --guide=True, exp_vlm_guidedTF.sh): the
+        host stages per-position BP targets (bp_nwp_posterior(guide=True) and the
+        image guided_info, packed by vlm_guide_planes); the penalty partials of
+        every guided block (model.py:303-331, 1122-1144) are one launch after the
+        forward, their gradients one launch per guided layer in the backward."""
+        self.guide = bool(getattr(self.model, "guide", False))
+        self.phist = None
+        if not self.guide:
+            return
+        if not self.joint or self.precision != "x3":
+            raise NotImplementedError("guided VLM runs on the joint model's split-bf16 path")
+        Tt = self.T - self.P
+        self.penalty = float(penalty)
+        self.gblocks = vlm_guide_blocks(self.model, Tt, self.V)
+        self.n_gelems = vlm_guide_plane_elems(self.model, Tt, self.V)
+        self.gtgt = torch.zeros(self.B, self.n_gelems, dtype=torch.float32, device=self.device)
+        self.gitems = [(l, b) for l in sorted(self.gblocks) for b in self.gblocks[l]]
+        self.gpart = torch.zeros(len(self.gitems), self.B, dtype=torch.float32, device=self.device)
+        self.gbuf = torch.zeros(3, dtype=torch.float32, device=self.device)
+        self.phist = torch.zeros_like(self.hist)
+        self._glists = []
+        mx = int(_native.hip_lib().ghm_guide_max_blocks())
+        self._gfwd = [(a, self._blk_list(self.gitems[a:a + mx])) for a in range(0, len(self.gitems), mx)]
+        self._gbwd = {l: [self._blk_list([(l, b) for b in blks[a:a + mx]]) for a in range(0, len(blks), mx)]
+                      for l, blks in self.gblocks.items()}
+
+    def _blk_list(self, items):
+        """Host arrays of ghm_guide_blks_{fwd,bwd}_d (kept alive: graphs replay them)."""
+        n = len(items)
+        H = (ctypes.c_void_p * n)(*[self.plan.H[l + 1].data_ptr() for l, _ in items])
+        M = (ctypes.c_void_p * n)(*[self.gtgt.data_ptr()] * n)
+        desc = (ctypes.c_int32 * (6 * n))()
+        desc64 = (ctypes.c_int64 * (2 * n))()
+        for k, (_, (tok0, ntok, col, off, _)) in enumerate(items):
+            desc[6 * k:6 * k + 6] = [self.T, tok0, ntok, col, 1, self.V]
+            desc64[2 * k:2 * k + 2] = [self.n_gelems, off]
+        lst = (H, M, desc, desc64, n)
+        self._glists.append(lst)
+        return lst
+
+    def _guide_hooks(self):
+        if not self.guide:
+            return None
+        scale = 2.0 * self.penalty / self.B
+        hooks = {}
+        for l in self.gblocks:
+            def fn(dH, s, l=l):
+                for H, M, desc, desc64, n in self._gbwd[l]:
+                    _native.call("ghm_guide_blks_bwd_d", H, M, desc, desc64, n, self.plan.D, _p(dH), scale, self.B,
+                                 s)
+            hooks[l] = fn
+        return hooks
 
     def _fwd_bwd(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -115,7 +171,14 @@ class VlmTrainer:
         _native.call("ghm_ce_kl", _p(self.plan.logits), _p(self.yt), _p(self.post), _p(self.plan.dlogits),
                      _p(self.loss_out), _p(self.hist), _p(self.chist), _p(self.step_ctr), self.B, self.T, self.P,
                      self.V, s)
-        self.plan.backward(self.pd, self.gd)
+        if self.guide:  # ConditionalGuidedCELoss guide branch: ploss = CE + penalty * mean_b sum ||H - target||^2
+            for a, (H, M, desc, desc64, n) in self._gfwd:
+                _native.call("ghm_guide_blks_fwd_d", H, M, desc, desc64, n, self.plan.D,
+                             ctypes.c_void_p(self.gpart[a].data_ptr()), self.B, s)
+            self.gbuf[0:1].copy_(self.loss_out[0:1])
+            _native.call("ghm_guide_total", _p(self.gpart), len(self.gitems), self.B, self.penalty, _p(self.gbuf),
+                         _p(self.phist), _p(self.step_ctr), s)
+        self.plan.backward(self.pd, self.gd, layer_grad=self._guide_hooks())
 
     def _optim(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -128,13 +191,18 @@ class VlmTrainer:
     def _allreduce(self):
         distributed.allreduce_mean_(self.gflat, group=self.pg)
 
-    def set_batch(self, xt, yt, post, i_tokens):
+    def set_batch(self, xt, yt, post, i_tokens, guide_targets=None):
         """Stage one batch: text inputs / targets uint8 [B, T-1], BP posteriors
-        float32 [B, T-1, V], image leaves uint8 [B, 81] (host-pinned or device)."""
+        float32 [B, T-1, V], image leaves uint8 [B, 81] (host-pinned or device);
+        guided: the packed guide targets float32 [B, n_gelems] (vlm_guide_planes)."""
         self.plan.xt.copy_(xt, non_blocking=True)
         self.yt.copy_(yt, non_blocking=True)
         self.post.copy_(post, non_blocking=True)
         (self.plan.itok if self.joint else self.clip_plan.tokens).copy_(i_tokens, non_blocking=True)
+        if self.guide:
+            if guide_targets is None:
+                raise ValueError("the guided VLM needs its guide targets every step")
+            self.gtgt.copy_(guide_targets, non_blocking=True)
 
     def step(self):
         if self.steps_done >= self.n_sched:
@@ -169,7 +237,24 @@ class VlmTrainer:
         n = self.steps_done if upto is None else upto
         return self.hist[:n].double().cpu().numpy()
 
-    ploss_history = loss_history
+    def ploss_history(self, upto=None):
+        """Loss including the guide penalties (train_NWP.py ploss_history); equals
+        loss_history without guidance."""
+        if self.phist is None:
+            return self.loss_history(upto)
+        n = self.steps_done if upto is None else upto
+        return self.phist[:n].double().cpu().numpy()
+
+    def guide_penalties(self):
+        """The last step's penalty terms as ConditionalGuidedCELoss returns them
+        (model.py:1144-1149): [loss2, loss4, loss5, loss3] (host sync)."""
+        if not self.guide:
+            return [0.0, 0.0, 0.0, 0.0]
+        part = self.gpart.double().cpu().numpy()
+        out = {"loss2": 0.0, "loss4": 0.0, "loss5": 0.0, "loss3": 0.0}
+        for k, (_, blk) in enumerate(self.gitems):
+            out[blk[4]] += self.penalty * float(part[k].mean())
+        return [out["loss2"], out["loss4"], out["loss5"], out["loss3"]]
 
     def compare_history(self, upto=None):
         n = self.steps_done if upto is None else upto

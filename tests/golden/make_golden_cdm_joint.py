@@ -22,6 +22,9 @@ cdm_guided_tiny.npz  guided joint model (exp_cdm_guidedTF.sh: guide=True, penalt
                      0.1, lr 1e-2 -> 1e-5), L=9, B=4, 2 steps: batches, the
                      sampler's guided targets, predictions, losses, grad checksums.
 cdm_guided_curve.npz the guided default config (B=128): first N ploss / loss / compare.
+cdm_joint_curve_t2.npz, cdm_guided_curve_t2.npz  (--spread) the same two curves with
+                     2 CPU threads instead of 8: the reference's own reduction-order
+                     spread, which bounds the curve tolerance where it exceeds 1e-4.
 """
 import argparse
 import os
@@ -148,7 +151,19 @@ def guided_fixture(L=9, B=4, nsteps=2, p=0.2, curve_steps=30):
     print("wrote cdm_guided_curve.npz", hist[0, :3])
 
 
-def curve_fixture(steps, p=0.2, L=9, B=128):
+def guided_curve(steps, p=0.2, out="cdm_guided_curve.npz"):
+    lp = Loop(p, 9, 128, lr_max=1e-2, lr_min=1e-5, guide=True)
+    hist = np.zeros((3, steps))
+    for k in range(steps):
+        r = lp.step()
+        hist[:, k] = (r["ploss"], r["loss"], r["compare"])
+    np.savez_compressed(os.path.join(HERE, out), p=p, L=9, B=128, total_iters=30000, lr_max=1e-2,
+                        lr_min=1e-5, penalty=0.1, ploss=hist[0], loss=hist[1], compare=hist[2],
+                        threads=torch.get_num_threads())
+    print("wrote", out, hist[0, :3])
+
+
+def curve_fixture(steps, p=0.2, L=9, B=128, out="cdm_joint_curve.npz"):
     lp = Loop(p, L, B)
     hist = np.zeros((3, steps))
     t0 = time.time()
@@ -157,17 +172,24 @@ def curve_fixture(steps, p=0.2, L=9, B=128):
         hist[:, k] = (r["ploss"], r["loss"], r["compare"])
         if k % 10 == 0:
             print(f"step {k} ploss {r['ploss']:.6f} compare {r['compare']:.6f} ({time.time() - t0:.1f}s)", flush=True)
-    np.savez_compressed(os.path.join(HERE, "cdm_joint_curve.npz"), p=p, L=L, B=B, total_iters=30000, lr_max=1e-3,
+    np.savez_compressed(os.path.join(HERE, out), p=p, L=L, B=B, total_iters=30000, lr_max=1e-3,
                         lr_min=1e-6, ploss=hist[0], loss=hist[1], compare=hist[2], threads=torch.get_num_threads())
-    print("wrote cdm_joint_curve.npz")
+    print("wrote", out)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--curve-steps", type=int, default=30)
     ap.add_argument("--only", default="")
+    ap.add_argument("--spread", action="store_true",
+                    help="write the 2-thread curves (*_t2.npz) next to the 8-thread fixtures")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
+    if a.spread:
+        torch.set_num_threads(2)
+        curve_fixture(a.curve_steps, out="cdm_joint_curve_t2.npz")
+        guided_curve(a.curve_steps, out="cdm_guided_curve_t2.npz")
+        sys.exit(0)
     if not only or "tiny" in only:
         tiny_fixture()
     if not only or "curve" in only:
