@@ -111,7 +111,7 @@ def build_cdm(rank, B, L, p, total_iters, precision=None, joint=False, guide=Fal
         model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False,
                                                      guide=guide).cuda()
         trainer = CdmTrainer(model, None, B, sched, sampler.t_templ, sampler.i_templ, sigma=1.0, device="cuda",
-                             precision="x3", penalty=0.1)
+                             precision=precision, penalty=0.1)
         sampler.native.seed(224 + 1000 * rank)
         return sampler, trainer
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
@@ -151,7 +151,7 @@ def build_vlm(rank, B, L, p, total_iters, precision=None, joint=False, guide=Fal
                                           sequential=False, guide=guide).cuda()
         sched = [get_lr_cosine_schedule(s, 1e-3, 1e-6, 0, total_iters) for s in range(total_iters)]
         np.random.seed(224 + 1000 * rank)  # each rank draws its own batches
-        return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision="x3", penalty=0.001)
+        return sampler, VlmTrainer(model, None, B, sched, device="cuda", precision=precision, penalty=0.001)
     torch.manual_seed(7)
     clip = EncoderTransformer(81, 10, 128, 5).cuda()
     seed_everything(224)  # identical initial weights on every rank (as DDP would broadcast)

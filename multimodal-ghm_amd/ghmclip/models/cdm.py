@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import D_MODEL, EncoderPlan, require_hip
+from .hip_encoder import D_MODEL, EncoderPlan, default_precision, require_hip
 
 __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
            "cdm_param_names", "CDM_UNTRAINED", "CDM_JOINT_UNTRAINED"]
@@ -63,6 +63,8 @@ class CdmPlan(EncoderPlan):
 
     def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", precision=None, joint=False):
+        if precision is None:  # the joint model (T = 162) defaults to exact f32
+            precision = default_precision("f32" if joint else "x3")
         super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
                          normalize_attn=normalize_attn, device=device, precision=precision)
         if not 1 <= n_i_token <= n_token:

@@ -58,11 +58,13 @@ def _stream():
 PRECISIONS = ("f32", "x3")
 
 
-def default_precision():
-    """GHM_PRECISION env var: "x3" (default: split-bf16 MFMA, fp32-accurate to
-    ~1e-5 relative per product, the reference's 200-step loss curve within
-    3e-6) or "f32" (exact-f32 MFMA, the curve within 5e-7)."""
-    p = os.environ.get("GHM_PRECISION", "x3")
+def default_precision(fallback="x3"):
+    """GHM_PRECISION env var: "x3" (split-bf16 MFMA, fp32-accurate to ~1e-5
+    relative per product; the CLIP and VLM default: the reference's CLIP curve
+    within 6e-6 over 1400 steps) or "f32" (exact-f32 MFMA; the joint CDM default,
+    whose lr-1e-2 guided run amplifies x3 rounding past the reference's own
+    thread-count spread)."""
+    p = os.environ.get("GHM_PRECISION", fallback)
     if p not in PRECISIONS:
         raise ValueError(f"GHM_PRECISION must be one of {PRECISIONS} (got {p!r})")
     return p
@@ -109,6 +111,7 @@ class EncoderPlan:
         # x3: the MLP forward saves nothing and its backward recomputes U
         # (GHM_MLP_RECOMPUTE=1, default) or the forward saves G and GELU'(U) (=0)
         self.mlp_rc = self.precision == "x3" and os.environ.get("GHM_MLP_RECOMPUTE", "1") != "0"
+        self.attn_f32 = self.long_attn and self.precision == "f32"
         if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2)
             self.G, self.Dg = e(M, D_HIDDEN), None
         else:
@@ -194,7 +197,9 @@ class EncoderPlan:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
                   pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-                if self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
+                if self.attn_f32:
+                    self._attn_fwd_f32(l)
+                elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
                     c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
                       _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
                 else:
@@ -354,7 +359,7 @@ class EncoderPlan:
               _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
             jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            if self.long_attn and not x3:
+            if self.attn_f32:
                 self._attn_bwd_f32(l, cur)
             elif self.long_attn:
                 c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),

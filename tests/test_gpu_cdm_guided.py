@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, curve_bound
 
 pytestmark = pytest.mark.gpu
 
@@ -34,7 +34,7 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-def _trainer(L, B, total_iters=30000):
+def _trainer(L, B, total_iters=30000, precision="x3"):
     """train_CDNS.py order: sampler (seedtree 42), seed_everything(224), the model."""
     from ghmclip import (ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, get_lr_cosine_schedule,
                          seed_everything)
@@ -44,7 +44,7 @@ def _trainer(L, B, total_iters=30000):
     model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False,
                                                  guide=True).to(DEV)
     sched = [get_lr_cosine_schedule(k, 1e-2, 1e-5, 0, total_iters) for k in range(total_iters + 1)]
-    tr = CdmTrainer(model, None, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision="x3",
+    tr = CdmTrainer(model, None, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision=precision,
                     penalty=0.1)
     return s, tr
 
@@ -129,10 +129,15 @@ def test_guided_graph_replay_matches_eager():
     np.testing.assert_array_equal(hs[0][1], hs[1][1])
 
 
-def test_guided_default_config_curve_vs_reference():
+@pytest.mark.parametrize("precision", ["x3", "f32"])
+def test_guided_default_config_curve_vs_reference(precision):
+    """exp_cdm_guidedTF.sh (lr 1e-2, penalty 0.1, B=128): ploss / loss / compare vs
+    the reference's 8-thread CPU run.  f32: within 1e-4 or twice the reference's
+    own 2-vs-8-thread spread up to that step (conftest.curve_bound); x3: 2e-3."""
     g = np.load(os.path.join(GOLDEN, "cdm_guided_curve.npz"))
+    g2 = np.load(os.path.join(GOLDEN, "cdm_guided_curve_t2.npz"))
     n = len(g["ploss"])
-    s, tr = _trainer(9, 128)
+    s, tr = _trainer(9, 128, precision=precision)
     for k in range(n):
         _draw(s, tr, 128)
         tr.step()
@@ -140,11 +145,14 @@ def test_guided_default_config_curve_vs_reference():
             tr.capture()
     torch.cuda.synchronize()
     ph, h, ch = tr.ploss_history(), tr.loss_history(), tr.compare_history()
-    dp = np.abs(ph - g["ploss"]) / g["ploss"]
-    dl = np.abs(h - g["loss"]) / g["loss"]
-    dc = np.abs(ch - g["compare"]) / g["compare"]
-    print(f"guided CDM curve (x3): {n} steps, max rel dploss {dp.max():.3e}, dloss {dl.max():.3e}, "
-          f"dcompare {dc.max():.3e}, final ploss {ph[-1]:.4f} vs {g['ploss'][-1]:.4f}")
-    # lr 1e-2 (10x the unguided runs) amplifies the split-bf16 rounding along the
-    # trajectory; the penalised loss stays within 1e-3, loss / compare within 2e-3
-    assert dp.max() <= 1e-3 and dl.max() <= 2e-3 and dc.max() <= 2e-3
+    msg = []
+    ok = True
+    for key, got in (("ploss", ph), ("loss", h), ("compare", ch)):
+        d = np.abs(got - g[key]) / np.abs(g[key])
+        b, w, sp = curve_bound(g[key], g2[key])
+        msg.append(f"{key} {d.max():.3e} (spread {sp[-1]:.3e}, window {w}, in-window {d[:w].max() if w else 0:.3e})")
+        # f32 (the joint default) is the parity claim; x3 is opt-in: lr 1e-2 grows
+        # its rounding to ~1e-3 over 30 steps (measured 1.3e-4 / 6.6e-4 / 9.3e-4)
+        ok = ok and bool((d <= b).all() if precision == "f32" else d.max() <= 2e-3)
+    print(f"guided CDM curve ({precision}), {n} steps: " + "; ".join(msg))
+    assert ok

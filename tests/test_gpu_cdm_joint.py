@@ -2,16 +2,18 @@
 leaves through t_embedding, T = 162) on the HIP path vs the CPU oracle and the
 reference's own fixtures (tests/golden/make_golden_cdm_joint.py).
 
-Sequences past 96 tokens run on the split-bf16 attention only, so every test is
-x3.  Tolerances as tests/test_gpu_cdm.py for x3: forward 1e-4 and gradients 5e-4
-relative to the tensor's max-abs; losses 1e-4 relative."""
+Sequences past 96 tokens run on the split-bf16 attention kernels; the exact-f32
+mode ("f32") takes the validation attention of EncoderPlan._attn_fwd_f32.
+Tolerances as tests/test_gpu_cdm.py for x3: forward 1e-4 and gradients 5e-4
+relative to the tensor's max-abs; losses 1e-4 relative; curves 1e-4 or twice the
+reference's own 2-vs-8-thread spread (conftest.curve_bound)."""
 import os
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, curve_bound
 from oracle import cdm_oracle as CO
 
 pytestmark = pytest.mark.gpu
@@ -71,7 +73,7 @@ def test_joint_cdm_module_forward_backward(B):
         assert _rel(pp.grad, pr.grad) < 5e-4, k
 
 
-def _trainer(L, B, total_iters=30000):
+def _trainer(L, B, total_iters=30000, precision="x3"):
     """train_CDNS.py order: sampler (seedtree 42), seed_everything(224), the model."""
     from ghmclip import (ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, get_lr_cosine_schedule,
                          seed_everything)
@@ -80,7 +82,7 @@ def _trainer(L, B, total_iters=30000):
     seed_everything(224)
     model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, L, [4, 4], 4, 512, sequential=False).to(DEV)
     sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, total_iters) for k in range(total_iters + 1)]
-    tr = CdmTrainer(model, None, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision="x3")
+    tr = CdmTrainer(model, None, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision=precision)
     return s, tr
 
 
@@ -140,15 +142,27 @@ def test_joint_cdm_graph_replay_matches_eager():
     np.testing.assert_array_equal(h1[1], h2[1])
 
 
-def test_joint_cdm_default_config_curve_vs_reference():
+@pytest.mark.parametrize("precision", ["x3", "f32"])
+def test_joint_cdm_default_config_curve_vs_reference(precision):
     """The default joint config (exp_cdm_jointtrain.sh: p=0.2, L=9, d=128, B=128,
-    lr 1e-3 -> 1e-6): loss and compare histories vs the reference PyTorch-CPU run."""
+    lr 1e-3 -> 1e-6): loss and compare histories vs the reference PyTorch-CPU run
+    (8 threads).  f32 (the joint default): within 1e-4 relative where the
+    reference agrees with its own 2-thread run to 1e-4, and within twice that
+    spread past it.  x3 rounding (~1e-5 per product) grows past that spread
+    along the trajectory; it is held to the 1e-3 envelope of an opt-in mode."""
     g = np.load(os.path.join(GOLDEN, "cdm_joint_curve.npz"))
+    g2 = np.load(os.path.join(GOLDEN, "cdm_joint_curve_t2.npz"))
     n = len(g["loss"])
-    s, tr = _trainer(9, 128)
+    s, tr = _trainer(9, 128, precision=precision)
     hist, chist = _run(s, tr, 128, n, graph_after=3)
     dev = np.abs(hist - g["loss"]) / g["loss"]
     cdev = np.abs(chist - g["compare"]) / g["compare"]
-    print(f"joint CDM curve (x3): {n} steps, max rel dloss {dev.max():.3e}, dcompare {cdev.max():.3e}, "
-          f"final {hist[-1]:.4f} vs {g['loss'][-1]:.4f}")
-    assert dev.max() <= 1e-3 and cdev.max() <= 1e-3
+    bl, wl, sl = curve_bound(g["loss"], g2["loss"])
+    bc, wc, sc = curve_bound(g["compare"], g2["compare"])
+    print(f"joint CDM curve ({precision}): {n} steps, max rel dloss {dev.max():.3e} (reference spread "
+          f"{sl[-1]:.3e}, self-consistent window {wl} steps), dcompare {cdev.max():.3e} (spread {sc[-1]:.3e}, "
+          f"window {wc}); in-window max {dev[:wl].max() if wl else 0:.3e} / {cdev[:wc].max() if wc else 0:.3e}")
+    if precision == "f32":  # the joint CDM default: the parity claim
+        assert (dev <= bl).all() and (cdev <= bc).all()
+    else:  # opt-in speed mode (GHM_PRECISION=x3): measured 8.3e-5 / 1.6e-4, envelope 1e-3
+        assert dev.max() <= 1e-3 and cdev.max() <= 1e-3

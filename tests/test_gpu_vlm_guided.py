@@ -38,12 +38,16 @@ def _trainer(B, total_iters=30000):
     return s, tr
 
 
-def _stage(s, tr, B):
+def _stage(s, trs, B):
+    """Draw one batch (the sampler uses numpy's global stream, as the reference)
+    and stage it on every trainer in `trs`."""
     from ghmclip.data.data_random_GHM import vlm_guide_planes
     tl, il, _ = s.draw_numpy(B)
     post, _, tg, ig = s.posterior(tl, il, guide=True)
-    tr.set_batch(torch.from_numpy(np.ascontiguousarray(tl[:, :-1])), torch.from_numpy(np.ascontiguousarray(tl[:, 1:])),
-                 torch.from_numpy(post), torch.from_numpy(il), torch.from_numpy(vlm_guide_planes(tg, ig, 10)))
+    planes = vlm_guide_planes(tg, ig, 10)
+    for tr in (trs if isinstance(trs, (list, tuple)) else [trs]):
+        tr.set_batch(torch.from_numpy(np.ascontiguousarray(tl[:, :-1])), torch.from_numpy(np.ascontiguousarray(tl[:, 1:])),
+                     torch.from_numpy(post), torch.from_numpy(il), torch.from_numpy(planes))
     return tl, il
 
 
@@ -109,12 +113,11 @@ def test_guided_vlm_module_api_first_step_gradients():
 
 
 def test_guided_vlm_graph_replay_bit_identical():
-    s1, t1 = _trainer(4)
+    _, t1 = _trainer(4)
     s2, t2 = _trainer(4)
     for k in range(4):
-        _stage(s1, t1, 4)
+        _stage(s2, [t1, t2], 4)
         t1.step()
-        _stage(s2, t2, 4)
         t2.step()
         if k == 1:
             t2.capture()
