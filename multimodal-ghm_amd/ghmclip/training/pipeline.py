@@ -10,6 +10,13 @@ import numpy as np
 import torch
 
 
+def _host_buffer(shape, dtype):
+    """A page-locked host buffer for the async H2D copies (plain memory when no
+    device is present: the producer side is tested on the CPU)."""
+    t = torch.empty(*shape, dtype=dtype)
+    return t.pin_memory() if torch.cuda.is_available() else t
+
+
 def shard_rows(block_rows, n_blocks, rank, world):
     """Row indices rank `rank` of `world` keeps from a CLIP batch laid out as
     n_blocks blocks of block_rows rows: a contiguous slice of the within-block
@@ -64,10 +71,10 @@ class BatchPipeline:
             br, rank, world = self.slice
             if br != self.B or br % world:
                 raise ValueError("row_slice must be (batch_size, rank, world) with world | batch_size")
-            self.lo, self.n = rank * (br // world), br // world
-            rows = (self.s.K + 1) * self.n
-        self.slots = [(torch.empty(rows, T, dtype=torch.uint8).pin_memory(),
-                       torch.empty(rows, T, dtype=torch.uint8).pin_memory()) for _ in range(n_slots)]
+            self.shard_lo, self.shard_n = rank * (br // world), br // world
+            rows = (self.s.K + 1) * self.shard_n
+        self.slots = [(_host_buffer((rows, T), torch.uint8), _host_buffer((rows, T), torch.uint8))
+                      for _ in range(n_slots)]
 
     def _fill(self, i):
         """One draw of the global batch (the MT stream advances by all of it; only
@@ -75,7 +82,7 @@ class BatchPipeline:
         full draw)."""
         t, im = self.slots[i]
         if self.slice is not None:
-            self.s.next_shard_into(self.B, self.lo, self.n, t.numpy(), im.numpy())
+            self.s.next_shard_into(self.B, self.shard_lo, self.shard_n, t.numpy(), im.numpy())
         else:
             self.s.next_into(self.B, t.numpy(), im.numpy())
 
@@ -138,8 +145,8 @@ class CdmBatchPipeline(BatchPipeline):
         self.T = T
 
         def slot():
-            return (torch.empty(B, T, dtype=torch.uint8).pin_memory(), torch.empty(B, T, dtype=torch.uint8).pin_memory(),
-                    torch.empty(B, T, dtype=torch.float64).pin_memory())
+            return (_host_buffer((B, T), torch.uint8), _host_buffer((B, T), torch.uint8),
+                    _host_buffer((B, T), torch.float64))
         self.slots = [slot() for _ in range(n_slots)]
         if self.slice is not None:
             self.rows = shard_samples(B, *self.slice)
@@ -177,11 +184,9 @@ class NwpBatchPipeline(BatchPipeline):
         ng = (T - 1) * V * (3 * L[0] + 1) + T * V * L[1] if self.guide else 0
 
         def slot():
-            return (torch.empty(B, T - 1, dtype=torch.uint8).pin_memory(),
-                    torch.empty(B, T - 1, dtype=torch.uint8).pin_memory(),
-                    torch.empty(B, T - 1, V, dtype=torch.float32).pin_memory(),
-                    torch.empty(B, T, dtype=torch.uint8).pin_memory(),
-                    torch.empty(B, ng, dtype=torch.float32).pin_memory() if ng else None)
+            return (_host_buffer((B, T - 1), torch.uint8), _host_buffer((B, T - 1), torch.uint8),
+                    _host_buffer((B, T - 1, V), torch.float32), _host_buffer((B, T), torch.uint8),
+                    _host_buffer((B, ng), torch.float32) if ng else None)
         self.slots = [slot() for _ in range(n_slots)]
         self.tl = np.empty((B, T), np.uint8)
         self.root = np.empty(B, np.uint8)
@@ -208,4 +213,4 @@ class NwpBatchPipeline(BatchPipeline):
             a, b = self.rows
             xt, yt, post, il = xt[a:b], yt[a:b], post[a:b], il[a:b]
             gt = None if gt is None else gt[a:b]
-        trainer.set_batch(xt, yt, post, il, gt)
+        trainer.set_batch(xt, yt, post, il, *(() if gt is None else (gt,)))

@@ -181,3 +181,36 @@ def test_sampler_shard_equals_row_slice():
     k1, p1 = full.native.get_state()
     k2, p2 = part.native.get_state()
     assert p1 == p2 and (k1 == k2).all()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_batch_pipeline_producer_shards(world):
+    """BatchPipeline(row_slice=(B, rank, world)) — the producer train_CLIP runs
+    on every rank — fills its slots with exactly shard_rows of the global draws,
+    in order, for every rank."""
+    from ghmclip import ClipSampler
+    from ghmclip.training.pipeline import BatchPipeline, shard_rows
+    p_y = np.ones(10) / 10
+    B = 16
+    full = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    full.native.seed(5)
+    t = np.empty((5 * B, 81), np.uint8)
+    i = np.empty((5 * B, 81), np.uint8)
+    draws = []
+    for _ in range(2):
+        full.native.next_into(B, t, i)
+        draws.append((t.copy(), i.copy()))
+    for rank in range(world):
+        s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+        s.native.seed(5)
+        pipe = BatchPipeline(s.native, B, n_slots=2, row_slice=(B, rank, world))
+        try:
+            idx = shard_rows(B, 5, rank, world)
+            for k in range(2):
+                assert pipe.ready[k].wait(timeout=30)
+                ts, is_ = pipe.slots[k]
+                assert ts.shape == (5 * B // world, 81)
+                np.testing.assert_array_equal(ts.numpy(), draws[k][0][idx])
+                np.testing.assert_array_equal(is_.numpy(), draws[k][1][idx])
+        finally:
+            pipe.close()
