@@ -346,7 +346,15 @@ def final_risk(a, ws):
             d = json.load(f)
         pub = d[arch][d["p_flip"].index(20)]
     hist = r["loss_history"]
-    return {"value": round(r["final_risk"], 6), "published": pub, "arch": arch, "p_flip": 0.2,
+    # the reference's own code run for all 3001 steps on the CPU (same seeds and
+    # draws; tests/golden/make_golden.py --curve-steps 3001): the number this run
+    # must reproduce (the published value comes from another software stack)
+    ref_run = None
+    path = os.path.join(ROOT, "tests", "golden", "clip_default_curve3001.npz")
+    if not a.guide and a.risk_iters == 3000 and os.path.exists(path):
+        ref_run = round(float(np.load(path)["loss_history"][-100:].mean()), 6)
+    return {"value": round(r["final_risk"], 6), "published": pub, "reference_code_cpu_run": ref_run,
+            "arch": arch, "p_flip": 0.2,
             "bayes": round(float(r["bayes"]), 6), "total_iters": a.risk_iters,
             "definition": "mean(loss_history[-100:]) (figures/eval-clip-risk.py:29)",
             "global_batch_rows": 128, "parallelism": f"dp{ws} (strong: 128 rows split over the ranks)",

@@ -926,8 +926,19 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   __shared__ __attribute__((aligned(16))) __bf16 sBl[2][IMG];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
-  const int a_blk = blockIdx.x * 128, b_blk = blockIdx.y * 128;
-  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * tok_per_split;
+  // XCD-aware order (linear id w runs on XCD w % 8): each XCD walks a contiguous
+  // run of (tile, split) pairs, tiles fastest, so the tiles of one token range
+  // read their shared operand through the same L2
+  int lin = static_cast<int>(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  {
+    const int full = static_cast<int>(gridDim.x * gridDim.y * gridDim.z) / 8 * 8;
+    if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
+  }
+  const int tbx = lin % static_cast<int>(gridDim.x);
+  const int tby = (lin / static_cast<int>(gridDim.x)) % static_cast<int>(gridDim.y);
+  const int tbz = lin / static_cast<int>(gridDim.x * gridDim.y);
+  const int a_blk = tbx * 128, b_blk = tby * 128;
+  const int64_t m_begin = static_cast<int64_t>(tbz) * tok_per_split;
   int64_t m_end = m_begin + tok_per_split;
   if (m_end > M) m_end = M;
   const int nsteps = static_cast<int>((m_end - m_begin + KT - 1) / KT);
@@ -1012,7 +1023,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
     if (st + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
   }
-  float* pz = part + static_cast<int64_t>(blockIdx.z) * Acols * Bcols;
+  float* pz = part + static_cast<int64_t>(tbz) * Acols * Bcols;
   const int a_base = a_blk + wa, b_base = b_blk + wb;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -1022,11 +1033,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
 #pragma unroll
       for (int k = 0; k < 2; ++k) pz[(ra + 32 * i) * Bcols + b_base + 32 * k + j] = acc[i][k][r];
   }
-  if (bias_part && blockIdx.y == 0) {
+  if (bias_part && tby == 0) {
     float* red = reinterpret_cast<float*>(&sAh[0][0]);  // the ring is idle after the last barrier
     red[th * 128 + c] = bsum;
     __syncthreads();
-    if (th == 0) bias_part[static_cast<int64_t>(blockIdx.z) * Acols + a_blk + c] = red[c] + red[128 + c];
+    if (th == 0) bias_part[static_cast<int64_t>(tbz) * Acols + a_blk + c] = red[c] + red[128 + c];
   }
 }
 
