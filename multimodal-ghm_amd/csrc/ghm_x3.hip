@@ -1073,23 +1073,33 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int r0, int r1, int
   return v;
 }
 
-// stage the feature half c of a [T][384]-strided operand (columns col0 + 64hh +
-// 32c + 0..31, hh = 0,1) as a split [row][hh][32] image; rows >= T clamp
+// Staging is split into a global->register half (*_load) and a register->LDS
+// half (*_store) so a kernel can issue the next operand's loads before the
+// barrier and MFMAs of the current one: plain loads stay in flight across
+// __syncthreads() (no LDS-DMA is outstanding in these kernels), and each
+// sequence's chain of dependent HBM round trips shrinks to about two.
+constexpr int HALF_NIT = 8;  // float4 per thread: TP rows x 16 float4 over NKT * 64 threads
+constexpr int COLS_NIT = 4;  // float4 per thread: TP rows x 8 float4 over NKT * 64 threads
+
+// the feature half c of a [T][384]-strided operand (columns col0 + 64hh + 32c +
+// 0..31, hh = 0,1), rows >= T clamped; stored as a split [row][hh][32] image
 template <int NKT>
-__device__ __forceinline__ void stage_half_x3(const float* __restrict__ seq, int T, int c, int col0,
-                                              __bf16* ih, __bf16* il) {
-  constexpr int NT = NKT * 64, NIT = NKT * 32 * 16 / NT;
-  float4 v[NIT];
+__device__ __forceinline__ void half_load(const float* __restrict__ seq, int T, int c, int col0, float4* v) {
+  constexpr int NT = NKT * 64;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < HALF_NIT; ++k) {
     const int idx = threadIdx.x + NT * k;
     const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
     const int rc = row < T ? row : T - 1;
     v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * (3 * GHM_D) + col0 + 64 * hh +
                                             32 * c + 4 * q4);
   }
+}
+template <int NKT>
+__device__ __forceinline__ void half_store(const float4* v, __bf16* ih, __bf16* il) {
+  constexpr int NT = NKT * 64;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < HALF_NIT; ++k) {
     const int idx = threadIdx.x + NT * k;
     const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
     bf16x4 a, b;
@@ -1099,22 +1109,24 @@ __device__ __forceinline__ void stage_half_x3(const float* __restrict__ seq, int
   }
 }
 
-// stage columns col .. col+31 of rows 0..TP-1 (row pitch ld floats) as a split
-// [row][32] image for transposed reads; rows >= T clamp
+// columns col .. col+31 of rows 0..TP-1 (row pitch ld floats), rows >= T
+// clamped; stored as a split [row][32] image for transposed reads
 template <int NKT>
-__device__ __forceinline__ void stage_cols_x3(const float* __restrict__ base, int ld, int T, int col,
-                                              __bf16* ih, __bf16* il) {
-  constexpr int NT = NKT * 64, NIT = NKT * 32 * 8 / NT;
-  float4 v[NIT];
+__device__ __forceinline__ void cols_load(const float* __restrict__ base, int ld, int T, int col, float4* v) {
+  constexpr int NT = NKT * 64;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < COLS_NIT; ++k) {
     const int idx = threadIdx.x + NT * k;
     const int row = idx >> 3, q4 = idx & 7;
     const int rc = row < T ? row : T - 1;
     v[k] = *reinterpret_cast<const float4*>(base + static_cast<int64_t>(rc) * ld + col + 4 * q4);
   }
+}
+template <int NKT>
+__device__ __forceinline__ void cols_store(const float4* v, __bf16* ih, __bf16* il) {
+  constexpr int NT = NKT * 64;
 #pragma unroll
-  for (int k = 0; k < NIT; ++k) {
+  for (int k = 0; k < COLS_NIT; ++k) {
     const int idx = threadIdx.x + NT * k;
     bf16x4 a, b;
     split4(v[k], a, b);
@@ -1153,18 +1165,23 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   const int q = 32 * w + j;
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
+  float4 kst[HALF_NIT];
+  half_load<NKT>(seq, T, 0, GHM_D, kst);  // K, feature half 0 (same round trip as Q)
   bf16x8 qh[8], ql[8];
   load_split64(seq + static_cast<int64_t>(qc) * (3 * GHM_D) + 64 * h, true, qh, ql);  // Q[q][64h + 8t + i]
   f32x16 s[NKT];
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    stage_half_x3<NKT>(seq, T, c, GHM_D, sh, sl);  // K
-    __syncthreads();
-    rows_dot_half<NKT>(sh, sl, qh, ql, c, j, h, s);
-    __syncthreads();
-  }
+  half_store<NKT>(kst, sh, sl);
+  half_load<NKT>(seq, T, 1, GHM_D, kst);  // K half 1 in flight across the first half's MFMAs
+  __syncthreads();
+  rows_dot_half<NKT>(sh, sl, qh, ql, 0, j, h, s);
+  __syncthreads();
+  half_store<NKT>(kst, sh, sl);
+  float4 vst[COLS_NIT];
+  cols_load<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D, vst);  // V column block 0 in flight across softmax
+  __syncthreads();
+  rows_dot_half<NKT>(sh, sl, qh, ql, 1, j, h, s);
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -1208,7 +1225,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   // A fragment of k-step (kt, s) = keys 32kt + 16s + 4h + 0..3 and + 8
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    stage_cols_x3<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D + 32 * dt, sh, sl);
+    __syncthreads();  // the previous phase's LDS reads are done
+    cols_store<NKT>(vst, sh, sl);
+    if (dt < 3) cols_load<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D + 32 * (dt + 1), vst);
+    const int64_t row = (base + qc) * GHM_D + 32 * dt;
+    float4 hv[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
     __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
@@ -1220,12 +1243,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
                       pl[2 * kt + ss], acc);
       }
     }
-    __syncthreads();
     if (qv) {
-      const int64_t row = (base + q) * GHM_D + 32 * dt;
-      float4 hv[4];
-#pragma unroll
-      for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd)
         st4(Hmid + row + quad_off(qd, h), hv[qd].x + acc[4 * qd], hv[qd].y + acc[4 * qd + 1],
@@ -1251,21 +1269,26 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __re
   const int q = 32 * w + j;
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
+  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
   f32x16 dp[NKT];
+  float4 kc[COLS_NIT];
   {
+    float4 vst[HALF_NIT];
+    half_load<NKT>(seq, T, 0, 2 * GHM_D, vst);  // V, feature half 0 (same round trip as dO)
     bf16x8 oh[8], ol[8];
     load_split64(dHmid + (base + qc) * GHM_D + 64 * h, true, oh, ol);  // dO[q][64h + 8t + i]
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) dp[kt] = zero16();
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      stage_half_x3<NKT>(seq, T, c, 2 * GHM_D, sh, sl);  // V
-      __syncthreads();
-      rows_dot_half<NKT>(sh, sl, oh, ol, c, j, h, dp);
-      __syncthreads();
-    }
+    half_store<NKT>(vst, sh, sl);
+    half_load<NKT>(seq, T, 1, 2 * GHM_D, vst);  // V half 1 in flight across the first half's MFMAs
+    __syncthreads();
+    rows_dot_half<NKT>(sh, sl, oh, ol, 0, j, h, dp);
+    __syncthreads();
+    half_store<NKT>(vst, sh, sl);
+    cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D, kc);  // K column block 0 in flight across dS
+    __syncthreads();
+    rows_dot_half<NKT>(sh, sl, oh, ol, 1, j, h, dp);
   }
-  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
   float delta = 0.f;
   f32x16 p[NKT];
 #pragma unroll
@@ -1298,7 +1321,9 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __re
   // dQ^T[d][q] = sum_key K[key][d] dS[q][key], K column block [key][32] in LDS
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    stage_cols_x3<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * dt, sh, sl);
+    __syncthreads();  // the previous phase's LDS reads are done
+    cols_store<NKT>(kc, sh, sl);
+    if (dt < 3) cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * (dt + 1), kc);
     __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
@@ -1310,7 +1335,6 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __re
                       dl[2 * kt + ss], acc);
       }
     }
-    __syncthreads();
     if (qv) {
       float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
 #pragma unroll
@@ -1339,6 +1363,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __r
   const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
   const int key = 32 * w + j;
   const bool kv = key < T;
+  const float* dO = dHmid + base * GHM_D;
+  const float* sq = qkv + base * (3 * GHM_D);
+  // column block 0 of dO^T and Q^T: issued first, in flight while P / dS are split
+  float4 ost[COLS_NIT], qst[COLS_NIT];
+  cols_load<NKT>(dO, GHM_D, T, 0, ost);
+  cols_load<NKT>(sq, 3 * GHM_D, T, 0, qst);
   // B fragments: P[16s + 8h + i][key] and dS[...][key], i = 0..7
   const float* pc = P + static_cast<int64_t>(blockIdx.x) * AT_PAD * AT_PAD + key;
   const float* sc = dS + static_cast<int64_t>(blockIdx.x) * AT_PAD * AT_PAD + key;
@@ -1357,8 +1387,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __r
   }
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    stage_cols_x3<NKT>(dHmid + base * GHM_D, GHM_D, T, 32 * dt, soh, sol);
-    stage_cols_x3<NKT>(qkv + base * (3 * GHM_D), 3 * GHM_D, T, 32 * dt, sqh, sql);
+    if (dt) __syncthreads();  // the previous phase's LDS reads are done
+    cols_store<NKT>(ost, soh, sol);
+    cols_store<NKT>(qst, sqh, sql);
+    if (dt < 3) {
+      cols_load<NKT>(dO, GHM_D, T, 32 * (dt + 1), ost);
+      cols_load<NKT>(sq, 3 * GHM_D, T, 32 * (dt + 1), qst);
+    }
     __syncthreads();
     f32x16 aV = zero16(), aK = zero16();
 #pragma unroll
@@ -1367,7 +1402,6 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __r
       aV = mfma_x3(tr_frag(soh, r0, r0 + 4, lane), tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
       aK = mfma_x3(tr_frag(sqh, r0, r0 + 4, lane), tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
     }
-    __syncthreads();
     if (kv) {
       float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
 #pragma unroll

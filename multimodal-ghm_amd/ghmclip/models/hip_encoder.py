@@ -78,7 +78,7 @@ def require_hip(t):
 
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", wgrad_target_blocks=512, precision=None,
+                 normalize_attn=True, device="cuda", wgrad_target_blocks=256, precision=None,
                  wgrad_min_tokens=None):
         if n_embd != D_MODEL:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
@@ -132,6 +132,7 @@ class EncoderPlan:
         # workgroups of at least wgrad_min_tokens tokens per split (measured on the
         # CDM's 10.5 K tokens: 32 -> 3.01 ms/step, 256 -> 3.09, 512 -> 3.50: the
         # extra parallelism outweighs the larger partial reduction)
+        wgrad_target_blocks = int(os.environ.get("GHM_WGRAD_BLOCKS", wgrad_target_blocks))
         if wgrad_min_tokens is None:
             wgrad_min_tokens = int(os.environ.get("GHM_WGRAD_MIN_TOKENS", "32"))
         self.wg = {}

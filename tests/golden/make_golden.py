@@ -254,8 +254,11 @@ def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, 
     print("wrote", name)
 
 
-def guide_curve_fixture(steps, p=0.2, B=128, total_iters=3000, penalty=1e-3, lr_max=1e-3, lr_min=1e-6):
-    """Guided default config (exp_clip_guidedTF.sh) ploss/loss history."""
+def guide_curve_fixture(steps, p=0.2, B=128, total_iters=3000, penalty=1e-3, lr_max=1e-3, lr_min=1e-6,
+                        out="guide_curve.npz"):
+    """Guided default config (exp_clip_guidedTF.sh) ploss/loss history.  With
+    steps = total_iters + 1 this is the whole reference run (final risk =
+    mean(loss_history[-100:]), figures/eval-clip-risk.py:29)."""
     s = make_sampler(p)
     seed_everything(224)
     tm, im = build_guided(81, 5, 128)
@@ -279,10 +282,10 @@ def guide_curve_fixture(steps, p=0.2, B=128, total_iters=3000, penalty=1e-3, lr_
         if it % 20 == 0:
             print(f"guide curve step {it} ploss {phist[it]:.6f} loss {hist[it]:.6f} ({time.time()-t0:.0f}s)",
                   flush=True)
-    np.savez_compressed(os.path.join(HERE, "guide_curve.npz"), loss_history=hist, ploss_history=phist,
+    np.savez_compressed(os.path.join(HERE, out), loss_history=hist, ploss_history=phist,
                         penalty=pen, p=p, B=B, total_iters=total_iters,
                         hyper=np.array([penalty, lr_max, lr_min]), threads=torch.get_num_threads())
-    print("wrote guide_curve.npz")
+    print("wrote", out)
 
 
 def bayes_fixture():
@@ -303,6 +306,7 @@ if __name__ == "__main__":
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--only", default="")
     ap.add_argument("--guide-steps", type=int, default=100)
+    ap.add_argument("--guide-out", default="guide_curve.npz")
     a = ap.parse_args()
     if a.threads:
         torch.set_num_threads(a.threads)
@@ -323,4 +327,4 @@ if __name__ == "__main__":
     if "guide_tiny" in jobs:
         guide_step_fixture("guide_tiny.npz")
     if "guide_curve" in jobs:
-        guide_curve_fixture(a.guide_steps)
+        guide_curve_fixture(a.guide_steps, out=a.guide_out)
