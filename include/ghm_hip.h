@@ -402,6 +402,17 @@ int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* 
 int64_t ghm_colsum_part_elems(int64_t M, int64_t N);
 int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, float* part, void* stream);
 
+/* ---- zero-shot classification (figures/eval-zsc-risk.py:107-118) --------
+ * logits[q][r][c] = log( mean_{k < n_list[q]} exp(<i_emb[r], t_emb[proto_idx[c][k]]>) )
+ * for every image row r < n_rows and class c < n_class: the reference's
+ * torch.log(exp(i_embeddings @ t_embeddings.T)[:, index].mean(dim=1)) for the
+ * first n_list[q] text samples of class c, without forming the N x N matrix.
+ * i_emb [n_rows][D], t_emb [*][D] fp32 (D <= 16); proto_idx int32
+ * [n_class][n_proto] (rows of t_emb); n_list int32 [n_j] (n_j <= 8, each in
+ * 1..n_proto); logits fp32 [n_j][n_rows][n_class].  Exact f32 MFMA products. */
+int ghm_zsc_logits(const float* i_emb, int64_t n_rows, const float* t_emb, int D, const int32_t* proto_idx,
+                   int n_class, int n_proto, const int32_t* n_list, int n_j, float* logits, void* stream);
+
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);

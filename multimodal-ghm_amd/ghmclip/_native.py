@@ -109,9 +109,10 @@ HIP_SIGNATURES = {
     "ghm_scaled_diff": [_p, _p, _p, _f, _p, _i64, _p],
     "ghm_add_cols": [_p, _p, _i64, _i, _p],
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
+    "ghm_zsc_logits": [_p, _i64, _p, _i, _p, _i, _i, _p, _i, _p, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64, "ghm_ln_rows_blocks": _i64,
-            "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
+            "ghm_ln_rows_blocks": _i64, "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
             "ghm_ce_kl_out_elems": _i64}
 
 HOST_SIGNATURES = {

@@ -249,6 +249,32 @@ class DoubleSampler:
                                           translation_invariance=translation_invariance)
         self.i_transition = GenTransition(n_layers[1], n_childs[1], variable_type, p_flips[1], flip_scale,
                                           translation_invariance=translation_invariance)
+        self._zs = None
+
+    def get_zeroshot_batch(self, batch_size=128, return_tree=False):
+        """:670-683: text and image trees sharing one root per sample (the draw of
+        figures/eval-zsc-risk.py:66).  Returns text leaves, image leaves (int64
+        [B, T]), their BP_CLS root posteriors (float64 [B, V]) and the roots (int64
+        [B]); the trees come from the native sampler on numpy's global stream
+        (root choice, then the text tree, then the image tree, as GHMTree draws
+        them)."""
+        if return_tree:
+            raise NotImplementedError("return_tree: the trees are drawn natively, no GHMTree objects exist")
+        if getattr(self, "_zs", None) is None:
+            t_templ = _templates(self.t_transition, self.n_childs[0])
+            i_templ = _templates(self.i_transition, self.n_childs[1])
+            self._zs = (t_templ, i_templ, NativeClipSampler(t_templ, i_templ, self.variable_type, 2))
+        t_templ, i_templ, nat = self._zs
+        B = batch_size
+        tl = np.empty((B, nat.T), np.uint8)
+        il = np.empty((B, nat.T), np.uint8)
+        root = np.empty(B, np.uint8)
+        nat.pull_numpy_state()
+        nat.next_cdm_into(B, 0.0, tl, il, None, root)
+        nat.push_numpy_state()
+        t_pp = bp_cls_posterior(t_templ, tl, np.asarray(self.p_ys[0], np.float64))
+        i_pp = bp_cls_posterior(i_templ, il, np.asarray(self.p_ys[1], np.float64))
+        return tl.astype(np.int64), il.astype(np.int64), t_pp, i_pp, root.astype(np.int64)
 
 
 class ClipSampler(DoubleSampler):
