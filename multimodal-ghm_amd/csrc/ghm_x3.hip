@@ -942,8 +942,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   int64_t m_end = m_begin + tok_per_split;
   if (m_end > M) m_end = M;
   const int nsteps = static_cast<int>((m_end - m_begin + KT - 1) / KT);
-  // staging role: column c of the tile, tokens 16*th .. 16*th + 15 of the step
-  const int c = threadIdx.x & 127, th = threadIdx.x >> 7;
+  // staging role: column c of the tile, tokens 16*th .. 16*th + 15 of the step.
+  // th is wave-uniform: readfirstlane makes every row index and row pointer
+  // scalar, so a load is one global_load_dword (SGPR row base + the lane's
+  // column offset) with no per-lane 64-bit address arithmetic or clamping.
+  const int c = threadIdx.x & 127, th = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
   float gam = 1.f, bet = 0.f;
   if (MODE == 2) {
     gam = lnw[b_blk + c];
@@ -956,21 +959,32 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   float va[16], vb[16];
   int nvalid = 0;
   float bsum = 0.f;
+  const int ca = a_blk + c, cb = b_blk + c;
   auto load = [&](int step) {
-    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;
+    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;  // uniform
     const int64_t left = m_end - mb;
     nvalid = left < 0 ? 0 : (left > 16 ? 16 : static_cast<int>(left));
+    // rows past m_end re-read the last valid row (masked in store()): the row
+    // step is a uniform select, the lane pointers advance by one add per row
+    const int64_t r0 = nvalid ? mb : m_begin;
+    const float* pa = A + r0 * lda + ca;
+    const float* pb = Bs + r0 * ldb + cb;
+    const float2* sp = stats + r0;  // uniform: scalar loads
+    const int nv = __builtin_amdgcn_readfirstlane(nvalid);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int64_t mt = mb + i;
-      const int64_t mcl = mt < m_end ? mt : m_begin;
-      va[i] = A[mcl * lda + a_blk + c];
-      float b = Bs[mcl * ldb + b_blk + c];
+      va[i] = *pa;
+      float b = *pb;
       if (MODE == 2) {
-        const float2 sv = stats[mcl];
+        const float2 sv = *sp;
         b = (b - sv.x) * sv.y * gam + bet;
       }
       vb[i] = b;
+      if (i + 1 < nv) {  // uniform
+        pa += lda;
+        pb += ldb;
+        sp += 1;
+      }
     }
     if (MODE == 0) issue_fence();
   };
