@@ -187,24 +187,27 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
   const int nk = vx_key_tiles(NW * (static_cast<int>(blockIdx.y) + 1), T, npre);
   f32x16 s[NKT];
   vx_scores<NKT, DD, NW>(seq, LD, DD, seq + qc * LD, T, j, h, nk, sh, sl, s);
+  // one reciprocal and a base-2 exponent per score (as k_attn_fwd_x3)
+  const float inv_scale = 1.f / scale_div, l2e = 1.4426950408889634f;
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * kt + acc_row(r, h);
-      const float v = (key < T && vx_allowed(qc, key, npre)) ? s[kt][r] / scale_div : -INFINITY;
+      const float v = (key < T && vx_allowed(qc, key, npre)) ? s[kt][r] * inv_scale : -INFINITY;
       s[kt][r] = v;
       mx = fmaxf(mx, v);
     }
   }
   mx = fmaxf(mx, xhalf(mx));
+  const float mx2 = mx * l2e;
   float sum = 0.f;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = expf(s[kt][r] - mx);
+      const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
       s[kt][r] = e;
       sum += e;
     }
@@ -282,6 +285,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
   f32x16 dp[NKT];
   vx_scores<NKT, DD, NW>(seq, LD, 2 * DD, dHmid + (base + qc) * DD, T, j, h, nk, sh, sl, dp);
   const float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
+  const float inv_scale = 1.f / scale_div;
   float delta = 0.f;
   f32x16 p[NKT];
 #pragma unroll
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
   for (int kt = 0; kt < NKT; ++kt) {
     float dv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);

@@ -1196,24 +1196,29 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   cols_load<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D, vst);  // V column block 0 in flight across softmax
   __syncthreads();
   rows_dot_half<NKT>(sh, sl, qh, ql, 1, j, h, s);
+  // scores scaled by one reciprocal and exponentiated as exp2 of a base-2
+  // argument: two VALU ops per score instead of an IEEE divide and a libm expf
+  // (each ~10); both within 2 ulp, far below the split products' 2^-16
+  const float inv_scale = 1.f / scale_div, l2e = 1.4426950408889634f;
   float mx = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = 32 * kt + acc_row(r, h);
-      const float v = key < T ? s[kt][r] / scale_div : -INFINITY;
+      const float v = key < T ? s[kt][r] * inv_scale : -INFINITY;
       s[kt][r] = v;
       mx = fmaxf(mx, v);
     }
   }
   mx = fmaxf(mx, xhalf(mx));
+  const float mx2 = mx * l2e;
   float sum = 0.f;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = expf(s[kt][r] - mx);
+      const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
       s[kt][r] = e;
       sum += e;
     }
@@ -1303,6 +1308,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __re
     __syncthreads();
     rows_dot_half<NKT>(sh, sl, oh, ol, 1, j, h, dp);
   }
+  const float inv_scale = 1.f / scale_div;
   float delta = 0.f;
   f32x16 p[NKT];
 #pragma unroll
@@ -1325,7 +1331,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q_x3(const float* __re
   for (int kt = 0; kt < NKT; ++kt) {
     float dv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);

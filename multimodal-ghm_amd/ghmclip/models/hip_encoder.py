@@ -60,10 +60,11 @@ PRECISIONS = ("f32", "x3")
 
 def default_precision(fallback="x3"):
     """GHM_PRECISION env var: "x3" (split-bf16 MFMA, fp32-accurate to ~1e-5
-    relative per product; the CLIP and VLM default: the reference's CLIP curve
-    within 6e-6 over 1400 steps) or "f32" (exact-f32 MFMA; the joint CDM default,
-    whose lr-1e-2 guided run amplifies x3 rounding past the reference's own
-    thread-count spread)."""
+    relative per product; the CLIP and VLM default: the reference code's whole
+    3001-step CLIP run within 1.4e-6) or "f32" (exact-f32 MFMA for the
+    projections and the MLP; the joint CDM default, whose lr-1e-2 guided run
+    amplifies x3 rounding past the reference's own thread-count spread,
+    DESIGN.md §2)."""
     p = os.environ.get("GHM_PRECISION", fallback)
     if p not in PRECISIONS:
         raise ValueError(f"GHM_PRECISION must be one of {PRECISIONS} (got {p!r})")
@@ -111,7 +112,12 @@ class EncoderPlan:
         # x3: the MLP forward saves nothing and its backward recomputes U
         # (GHM_MLP_RECOMPUTE=1, default) or the forward saves G and GELU'(U) (=0)
         self.mlp_rc = self.precision == "x3" and os.environ.get("GHM_MLP_RECOMPUTE", "1") != "0"
-        self.attn_f32 = self.long_attn and self.precision == "f32"
+        # past 96 tokens the f32 plan runs the attention core on the split-bf16
+        # ghm_attn_ext kernels (the joint CDM's curves stay inside the reference's
+        # own thread-count spread with them: DESIGN.md §2); GHM_LONG_ATTN=f32
+        # selects the exact-f32 torch validation path instead
+        self.attn_f32 = (self.long_attn and self.precision == "f32"
+                         and os.environ.get("GHM_LONG_ATTN", "x3") == "f32")
         if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2)
             self.G, self.Dg = e(M, D_HIDDEN), None
         else:
@@ -214,8 +220,11 @@ class EncoderPlan:
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-            if self.long_attn:
+            if self.attn_f32:
                 self._attn_fwd_f32(l)
+            elif self.long_attn:
+                c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                  _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
             else:
                 c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   N, T, D_MODEL, self.scale_div, s)

@@ -2,8 +2,9 @@
 leaves through t_embedding, T = 162) on the HIP path vs the CPU oracle and the
 reference's own fixtures (tests/golden/make_golden_cdm_joint.py).
 
-Sequences past 96 tokens run on the split-bf16 attention kernels; the exact-f32
-mode ("f32") takes the validation attention of EncoderPlan._attn_fwd_f32.
+Sequences past 96 tokens run on the split-bf16 attention kernels in both modes
+(the exact-f32 torch attention, EncoderPlan._attn_fwd_f32, is the
+GHM_LONG_ATTN=f32 validation path; test_f32_validation_attention_matches).
 Tolerances as tests/test_gpu_cdm.py for x3: forward 1e-4 and gradients 5e-4
 relative to the tensor's max-abs; losses 1e-4 relative; curves 1e-4 or twice the
 reference's own 2-vs-8-thread spread (conftest.curve_bound)."""
@@ -37,11 +38,16 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-@pytest.mark.parametrize("B", [3, 8])
-def test_joint_cdm_module_forward_backward(B):
+@pytest.mark.parametrize("B,mode", [(3, "x3"), (8, "x3"), (8, "f32"), (8, "f32_exact_attn")])
+def test_joint_cdm_module_forward_backward(B, mode, monkeypatch):
     """ConditionalDenoiseEncoderTransformer(sequential=False) forward and every
-    parameter gradient (t_embedding included) vs the oracle restatement."""
+    parameter gradient (t_embedding included) vs the oracle restatement, in
+    the split-bf16 mode, the f32 mode (the joint default: exact projections and
+    MLP, split-bf16 attention core past 96 tokens) and the f32 mode's exact
+    torch attention (GHM_LONG_ATTN=f32, the validation path)."""
     from ghmclip import ConditionalDenoiseEncoderTransformer
+    if mode == "f32_exact_attn":
+        monkeypatch.setenv("GHM_LONG_ATTN", "f32")
     torch.manual_seed(11)
     prod = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 2, [4, 4], 4, 512, sequential=False)
     torch.manual_seed(11)
@@ -54,7 +60,7 @@ def test_joint_cdm_module_forward_backward(B):
                 d = 0.1 * torch.randn(vp.shape, generator=g)
                 vp.add_(d)
                 vr.add_(d)
-    prod.precision = "x3"
+    prod.precision = "x3" if mode == "x3" else "f32"
     prod = prod.to(DEV)
     xt = torch.randint(0, 10, (B, 81), generator=g)
     z = torch.randint(0, 10, (B, 81), generator=g).float() + torch.randn(B, 81, generator=g)
