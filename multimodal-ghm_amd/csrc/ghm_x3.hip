@@ -952,51 +952,73 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
     gam = lnw[b_blk + c];
     bet = lnb[b_blk + c];
   }
-  // MODE 0: raw prefetch registers, the token mask applied in store(), so the
-  // loads stay in flight across the compute.  MODE 2: the LayerNorm transform
-  // is applied at load time (its per-token statistics would otherwise hold 32
-  // more registers across the compute, which measured slower).
-  float va[16], vb[16];
-  int nvalid = 0;
+  // Raw prefetch registers: the token mask and (MODE 2) the LayerNorm transform
+  // are applied in store(), so the loads stay in flight across the compute.
+  // (Round 1 applied the transform at load time; the ISA then waited for every
+  // prefetch load before the step's MFMAs -- no latency hiding: 59 us vs 41 us
+  // for MODE 0.)  The per-token statistics travel with the slot: lane l loads
+  // row l's pair, store() broadcasts them with v_readlane (scalar loads there
+  // serialised four K$-miss round trips per step: MODE 2 ran 2.4 us/step vs
+  // 1.65 for MODE 0).
+  // Two register slots: the loads of step st + 2 are issued while step st is
+  // computed and step st + 1's loads (issued one step earlier) are consumed, so
+  // each load has two compute phases to land (one phase, ~0.4 us of MFMAs, is
+  // well under the loaded HBM latency).
+  struct Slot {
+    float va[16], vb[16];
+    float2 st;  // MODE 2: LayerNorm statistics of the slot's row (lane & 15)
+    int nvalid;
+  };
+  Slot S0, S1;
   float bsum = 0.f;
   const int ca = a_blk + c, cb = b_blk + c;
-  auto load = [&](int step) {
+  // Buffer loads: SGPR descriptor + SGPR row offset (soffset) + the lane's
+  // column offset (voffset), one instruction per row and no VGPR address
+  // arithmetic.  The host checks that both operands fit a 31-bit byte range.
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), static_cast<short>(0),
+                                                     0x7fffffff, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bs), static_cast<short>(0),
+                                                     0x7fffffff, 0x00020000);
+  const int voa = 4 * ca, vob = 4 * cb;
+  auto load = [&](Slot& S, int step) {
     const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;  // uniform
     const int64_t left = m_end - mb;
-    nvalid = left < 0 ? 0 : (left > 16 ? 16 : static_cast<int>(left));
-    // rows past m_end re-read the last valid row (masked in store()): the row
-    // step is a uniform select, the lane pointers advance by one add per row
-    const int64_t r0 = nvalid ? mb : m_begin;
-    const float* pa = A + r0 * lda + ca;
-    const float* pb = Bs + r0 * ldb + cb;
-    const float2* sp = stats + r0;  // uniform: scalar loads
-    const int nv = __builtin_amdgcn_readfirstlane(nvalid);
+    S.nvalid = left < 0 ? 0 : (left > 16 ? 16 : static_cast<int>(left));
+    // rows past m_end re-read the last valid row (masked in store())
+    const int64_t r0 = S.nvalid ? mb : m_begin;
+    const int nv = __builtin_amdgcn_readfirstlane(S.nvalid > 0 ? S.nvalid : 1);
+    if (MODE == 2) {  // one vector load: lane l holds row (l & 15)'s (mean, rstd)
+      const int li = lane & 15;
+      S.st = stats[r0 + (li < nv ? li : nv - 1)];
+    }
+    const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * lda * 4));
+    const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * ldb * 4));
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      va[i] = *pa;
-      float b = *pb;
-      if (MODE == 2) {
-        const float2 sv = *sp;
-        b = (b - sv.x) * sv.y * gam + bet;
-      }
-      vb[i] = b;
-      if (i + 1 < nv) {  // uniform
-        pa += lda;
-        pb += ldb;
-        sp += 1;
+      const int ri = i < nv ? i : nv - 1;  // uniform
+      S.va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, voa, sa + ri * lda * 4, 0));
+      S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob, sb + ri * ldb * 4, 0));
+    }
+    issue_fence();
+  };
+  auto store = [&](Slot& S, int buf) {
+    if (MODE == 2) {  // row i's statistics broadcast from lane i (v_readlane)
+      const int mx = __float_as_int(S.st.x), rx = __float_as_int(S.st.y);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float mean = __int_as_float(__builtin_amdgcn_readlane(mx, i));
+        const float rstd = __int_as_float(__builtin_amdgcn_readlane(rx, i));
+        S.vb[i] = (S.vb[i] - mean) * rstd * gam + bet;
       }
     }
-    if (MODE == 0) issue_fence();
-  };
-  auto store = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (i >= nvalid) va[i] = 0.f;
+      if (i >= S.nvalid) S.va[i] = 0.f;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       bf16x8 ah, al, bh, bl;
-      split8(va + 8 * half, ah, al);
-      split8(vb + 8 * half, bh, bl);
+      split8(S.va + 8 * half, ah, al);
+      split8(S.vb + 8 * half, bh, bl);
       const int off = wg_img(c, 2 * th + half);
       *reinterpret_cast<bf16x8*>(sAh[buf] + off) = ah;
       *reinterpret_cast<bf16x8*>(sAl[buf] + off) = al;
@@ -1004,20 +1026,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
       *reinterpret_cast<bf16x8*>(sBl[buf] + off) = bl;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bsum += va[i];
+    for (int i = 0; i < 16; ++i) bsum += S.va[i];
   };
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int k = 0; k < 2; ++k) acc[i][k] = zero16();
-  load(0);
-  store(0);
-  __syncthreads();
-#pragma unroll 1
-  for (int st = 0; st < nsteps; ++st) {
-    const int cur = st & 1;
-    if (st + 1 < nsteps) load(st + 1);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
@@ -1034,7 +1050,26 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
 #pragma unroll
         for (int k = 0; k < 2; ++k) acc[i][k] = mfma_x3(ah[i], al[i], bh[k], bl[k], acc[i][k]);
     }
-    if (st + 1 < nsteps) store(cur ^ 1);
+  };
+  // The loads are unconditional (past the last step they re-read it, L2-hot)
+  // so the vmcnt bookkeeping is static: a store waits only for its own slot.
+  const int last = nsteps - 1;
+  load(S0, 0);
+  store(S0, 0);
+  load(S1, 1 < last ? 1 : last);
+  __syncthreads();
+#pragma unroll 1
+  for (int st = 0; st < nsteps; st += 2) {
+    // LDS buffer 0 holds step st; S1 holds step st + 1 (in flight)
+    load(S0, st + 2 < last ? st + 2 : last);
+    compute(0);
+    if (st + 1 < nsteps) store(S1, 1);
+    __syncthreads();
+    if (st + 1 >= nsteps) break;
+    // LDS buffer 1 holds step st + 1; S0 holds step st + 2 (in flight)
+    load(S1, st + 3 < last ? st + 3 : last);
+    compute(1);
+    if (st + 2 < nsteps) store(S0, 0);
     __syncthreads();
   }
   float* pz = part + static_cast<int64_t>(tbz) * Acols * Bcols;
@@ -1514,6 +1549,8 @@ extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B,
   GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
   GHM_CHECK(tok_per_split > 0 && tok_per_split % 32 == 0, "tok_per_split must be a positive multiple of 32");
   GHM_CHECK(b_mode == 0 || b_mode == 2, "b_mode (split path: 0 plain, 2 layernorm)");
+  GHM_CHECK(M * lda * 4 < (int64_t(1) << 31) && M * ldb * 4 < (int64_t(1) << 31),
+            "operands must fit a 31-bit byte range (buffer-load row offsets)");
   GHM_CHECK(b_mode != 2 || (stats && ln_w && ln_b), "layernorm mode needs stats/ln_w/ln_b");
   const int64_t nsplit = (M + tok_per_split - 1) / tok_per_split;
   GHM_CHECK(nsplit <= 65535, "too many splits");
