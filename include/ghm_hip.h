@@ -183,7 +183,7 @@ int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, 
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),
  * dH_mid = dH_out + dLN2 (must not alias dH_out) and part_ln as ghm_mlp_bwd
- * (n_blocks = ghm_token_blocks(M))  —  backward of model.py:741-747,784-788. */
+ * (n_blocks = ghm_mlp_bwd_rc_x3_blocks(M))  —  backward of model.py:741-747,784-788. */
 int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                       const float* ln_b, const void* pack, const float* b1, float* G, float* dU, float* dH_mid,
                       float* part_ln, int64_t M, int D, int F, void* stream);
@@ -416,6 +416,8 @@ int ghm_zsc_logits(const float* i_emb, int64_t n_rows, const float* t_emb, int D
 /* ---- helpers ----------------------------------------------------------- */
 /* number of 128-token blocks the token-parallel kernels use for M tokens */
 int64_t ghm_token_blocks(int64_t M);
+/* number of LN-partial rows (token workgroups) ghm_mlp_bwd_rc_x3 writes for M tokens */
+int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M);
 
 #ifdef __cplusplus
 }

@@ -571,32 +571,71 @@ __device__ __forceinline__ float2 reduce_scatter32_t16(float* v, int t) {
   return make_float2(v[0], v[1]);
 }
 
-__global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
+// W1 chunk image shared by row reads and transposed reads: [32 rows][128]
+// (256-B rows), 16-B chunk c of row r at c ^ 2(r & 7).  Row reads (16x16x32
+// operand: lane t -> row 16 jt + t, chunk 4 s2 + g) hit 16 distinct chunks per
+// ds_read_b128 lane group; a transposed read's 32-lane half (rows of one
+// aligned 8-row block x the two chunks of 16 columns) hits all 64 banks once.
+__device__ __forceinline__ int r32t_off(int row, int lc) { return row * 128 + 8 * (lc ^ (2 * (row & 7))); }
+template <int NW>
+__device__ __forceinline__ void fill_r32t_w8(const __bf16* g, int ldg, int lo_off, __bf16* ih, __bf16* il) {
+  const int L = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < (8 + NW - 1) / NW; ++k) {
+    const int b = (threadIdx.x >> 6) + NW * k;
+    if (8 % NW == 0 || b < 8) {
+      const int row = 4 * b + (L >> 4), lc = (L & 15) ^ (2 * (row & 7));
+      const __bf16* src = g + row * ldg + 8 * lc;
+      glds16(src, ih + 512 * b);
+      glds16(src + lo_off, il + 512 * b);
+    }
+  }
+}
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+__device__ __forceinline__ bf16x4 ldtr(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+}
+// element offset of lane (g, q, p)'s transposed-read address for dX2 tile j:
+// row 4 g + q, columns 16 j + 4 p .. + 3 (the second read: row + 16, same
+// swizzle since (row + 16) & 7 == row & 7)
+__device__ __forceinline__ int w1t_tr_off(int j, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, row = 4 * g + q;
+  return row * 128 + 8 * ((2 * j + (p >> 1)) ^ (2 * (row & 7))) + 4 * (p & 1);
+}
+__device__ __forceinline__ bf16x8 tr_pair(const __bf16* p) {
+  const bf16x4 a = ldtr(p), b = ldtr(p + 16 * 128);
+  bf16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return v;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
     const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
     float* __restrict__ Gout, float* __restrict__ dU, float* __restrict__ dHmid, float* __restrict__ part_ln,
     int64_t M) {
-  constexpr int NW = 8, NC = GHM_F / 32;
-  // [W1 hi|lo][W2^T hi|lo][W1^T hi|lo] x 2 buffers (96 KB); the LN partial
-  // buffer aliases it after the loop
-  __shared__ __attribute__((aligned(16))) __bf16 lds[12 * PLANE + 2 * GHM_F];
-  float* sb1 = reinterpret_cast<float*>(lds + 12 * PLANE);  // read before the fills: see k_ln_mlp_fwd_x3b
-  auto sw1h = [&](int b) { return lds + 6 * PLANE * b; };
-  auto sw1l = [&](int b) { return lds + 6 * PLANE * b + PLANE; };
-  auto sw2h = [&](int b) { return lds + 6 * PLANE * b + 2 * PLANE; };
-  auto sw2l = [&](int b) { return lds + 6 * PLANE * b + 3 * PLANE; };
-  auto sw3h = [&](int b) { return lds + 6 * PLANE * b + 4 * PLANE; };
-  auto sw3l = [&](int b) { return lds + 6 * PLANE * b + 5 * PLANE; };
+  constexpr int NC = GHM_F / 32;
+  // [W1 hi|lo][W2^T hi|lo] x 2 buffers (64 KB: two workgroups per CU); the LN
+  // partial buffer aliases it after the loop.  The W1 chunk serves both the U
+  // recompute (row reads) and, through ds_read_b64_tr_b16, the dX2 product's
+  // W1^T operand (round 1 staged a third, transposed W1^T image: 96 KB, one
+  // workgroup per CU).
+  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE + 2 * GHM_F];
+  float* sb1 = reinterpret_cast<float*>(lds + 8 * PLANE);  // read before the fills: see k_ln_mlp_fwd_x3b
+  auto sw1h = [&](int b) { return lds + 4 * PLANE * b; };
+  auto sw1l = [&](int b) { return lds + 4 * PLANE * b + PLANE; };
+  auto sw2h = [&](int b) { return lds + 4 * PLANE * b + 2 * PLANE; };
+  auto sw2l = [&](int b) { return lds + 4 * PLANE * b + 3 * PLANE; };
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
   const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + wave) * 16 + t;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
   const __bf16* W1 = pack + PK_W1_N;    // [512 f][128 d]
   const __bf16* W2T = pack + PK_W2_T;   // [512 f][128 o]
-  const __bf16* W1T = pack + PK_W1_T32; // [128 d][512 q], q perm32
-  fill_r32_w8<NW>(W1, GHM_D, PK_W, sw1h(0), sw1l(0));
+  fill_r32t_w8<NW>(W1, GHM_D, PK_W, sw1h(0), sw1l(0));
   fill_r32_w8<NW>(W2T, GHM_D, PK_W, sw2h(0), sw2l(0));
-  fill_r128_w8<NW>(W1T, GHM_F, PK_W, sw3h(0), sw3l(0));
   if (threadIdx.x < GHM_F / 4)
     reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
   // B operands: LN2(Hmid) and dY of the token, lane holds features 32 s2 + 8 g + i
@@ -639,9 +678,8 @@ __global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
     issue_fence();
     {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
       const int cn = c + 1 < NC ? c + 1 : NC - 1;
-      fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, sw1h(cur ^ 1), sw1l(cur ^ 1));
+      fill_r32t_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, sw1h(cur ^ 1), sw1l(cur ^ 1));
       fill_r32_w8<NW>(W2T + cn * 32 * GHM_D, GHM_D, PK_W, sw2h(cur ^ 1), sw2l(cur ^ 1));
-      fill_r128_w8<NW>(W1T + cn * 32, GHM_F, PK_W, sw3h(cur ^ 1), sw3l(cur ^ 1));
     }
     f32x4 u[2], dg[2];
 #pragma unroll
@@ -650,8 +688,8 @@ __global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
       dg[jt] = zero4();
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
-        const int o = r32_off(16 * jt + t, 4 * s2 + g);
-        u[jt] = mfma16_x3(ldsb8(sw1h(cur) + o), ldsb8(sw1l(cur) + o), xh[s2], xl[s2], u[jt]);
+        const int o1 = r32t_off(16 * jt + t, 4 * s2 + g), o = r32_off(16 * jt + t, 4 * s2 + g);
+        u[jt] = mfma16_x3(ldsb8(sw1h(cur) + o1), ldsb8(sw1l(cur) + o1), xh[s2], xl[s2], u[jt]);
         dg[jt] = mfma16_x3(ldsb8(sw2h(cur) + o), ldsb8(sw2l(cur) + o), yh[s2], yl[s2], dg[jt]);
       }
     }
@@ -676,12 +714,15 @@ __global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
     }
     bf16x8 dh, dl;
     split8(du, dh, dl);
+    // dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
+    // i.e. rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of the W1 chunk at
+    // column 16 j + t: two transposed reads per plane
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int o = r128_off(16 * j + t, g);
-      dx[j] = mfma16_x3(ldsb8(sw3h(cur) + o), ldsb8(sw3l(cur) + o), dh, dl, dx[j]);
+      const int o = w1t_tr_off(j, lane);
+      dx[j] = mfma16_x3(tr_pair(sw1h(cur) + o), tr_pair(sw1l(cur) + o), dh, dl, dx[j]);
     }
-    // retire this iteration's 6 LDS-DMA fills (issued before the 4 stores)
+    // retire this iteration's 4 LDS-DMA fills (issued before the 4 stores)
     asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // LN2 backward: lane holds dX2 of features d = 16 j + 4 g + r
@@ -751,8 +792,12 @@ __global__ __launch_bounds__(512, 2) void k_mlp_bwd_rc_x3(
   if (threadIdx.x < 2 * GHM_D) {
     const int q = threadIdx.x >> 7, f = threadIdx.x & 127;
     const float* rr = red + q * NW * GHM_D + f;
-    const float sum = ((rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D])) +
-                      ((rr[4 * GHM_D] + rr[5 * GHM_D]) + (rr[6 * GHM_D] + rr[7 * GHM_D]));
+    float sum;
+    if (NW == 8)
+      sum = ((rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D])) +
+            ((rr[4 * GHM_D] + rr[5 * GHM_D]) + (rr[6 * GHM_D] + rr[7 * GHM_D]));
+    else
+      sum = (rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D]);
     part_ln[static_cast<int64_t>(blockIdx.x) * 2 * GHM_D + q * GHM_D + f] = sum;
   }
 }
@@ -1103,10 +1148,6 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
 constexpr int AT_PAD = 96;         // padded sequence length of the P / dS layouts
 constexpr int AH_PITCH = 64 + 8;   // [row][h][32] half image row (bf16): 144 B, b128 reads conflict-free
 
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-__device__ __forceinline__ bf16x4 ldtr(const __bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
-}
 // 8-row transposed fragment from a [row][32] image (pitch 32 bf16 = 64 B: the
 // 2 x 4 rows x 32 B a 32-lane half reads fall on 64 distinct banks).  Lane l of
 // group g = l >> 4 receives column 16(g & 1) + (l & 15) of rows r0, r0 + 1,
@@ -1518,15 +1559,25 @@ extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const flo
   return ghm_launch_status();
 }
 
+// waves per workgroup of k_mlp_bwd_rc_x3 (16 tokens each).  Measured (one
+// box, alternating 200-step benches): 8 waves 4.42 ms/step, 4 waves (two
+// workgroups per CU, 64 KB of LDS each) 4.43-4.48.
+constexpr int RC_NW = 8;
+extern "C" int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M) {
+  const int64_t tok = 16 * RC_NW;
+  return (M + tok - 1) / tok;
+}
+
 extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                                  const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
                                  float* dH_mid, float* part_ln, int64_t M, int D, int F, void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln, "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
-  hipLaunchKernelGGL(k_mlp_bwd_rc_x3, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
-                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w, ln_b,
-                     reinterpret_cast<const __bf16*>(pack), b1, G, dU, dH_mid, part_ln, M);
+  const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
+  hipLaunchKernelGGL(k_mlp_bwd_rc_x3<RC_NW>, dim3(nblk), dim3(64 * RC_NW), 0, ghm_stream(stream), dH_out, H_mid,
+                     reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                     G, dU, dH_mid, part_ln, M);
   return ghm_launch_status();
 }
 

@@ -40,6 +40,7 @@ HIP_SIGNATURES = {
     "ghm_last_error_string": [],
     "ghm_device_ok": [],
     "ghm_token_blocks": [_i64],
+    "ghm_mlp_bwd_rc_x3_blocks": [_i64],
     "ghm_embed_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ln_qkv_fwd": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_attn_fwd": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
@@ -112,6 +113,7 @@ HIP_SIGNATURES = {
     "ghm_zsc_logits": [_p, _i64, _p, _i, _p, _i, _i, _p, _i, _p, _p],
 }
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
+            "ghm_mlp_bwd_rc_x3_blocks": _i64,
             "ghm_ln_rows_blocks": _i64, "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
             "ghm_ce_kl_out_elems": _i64}
 

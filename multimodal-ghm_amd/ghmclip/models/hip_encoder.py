@@ -133,7 +133,8 @@ class EncoderPlan:
         self.dS = torch.zeros(N, pad, pad, dtype=f32, device=dev)
         self.nblk = int(_native.hip_lib().ghm_token_blocks(M))
         self.part_ln = e(self.nblk, 2, D_MODEL)
-        self.part_ln2 = e(self.nblk, 2, D_MODEL)
+        self.nblk_rc = int(_native.hip_lib().ghm_mlp_bwd_rc_x3_blocks(M))
+        self.part_ln2 = e(max(self.nblk, self.nblk_rc), 2, D_MODEL)
         # split-K plans (A_cols x B_cols output tiles of 128x128): ~wgrad_target_blocks
         # workgroups of at least wgrad_min_tokens tokens per split (measured on the
         # CDM's 10.5 K tokens: 32 -> 3.01 ms/step, 256 -> 3.09, 512 -> 3.50: the
@@ -358,7 +359,8 @@ class EncoderPlan:
                 c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
                   _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
-            jobs.append(J(self.part_ln2, self.nblk, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
+            nb2 = self.nblk_rc if (x3 and self.mlp_rc) else self.nblk
+            jobs.append(J(self.part_ln2, nb2, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
             c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G if self.mlp_rc else self.G[l]), D_HIDDEN, D_HIDDEN, 0,
               None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)

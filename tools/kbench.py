@@ -90,7 +90,7 @@ def main():
                                               P(xo["st"]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
             "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
-                                        P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln), M, 128, 512, sp),
+                                        P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512, sp),
                               gf(6 * M * 128 * 512)),
             "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                      P(p["_lns_2.0.weight"]), pk, P(xo["Dg"]), P(plan.dU), P(xo["dHm"]),
