@@ -454,11 +454,16 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, i
 // ---------------------------------------------------------------------------
 // Readout backward, one workgroup per sequence                 (model.py:802-805)
 // The sequence's rows of H are staged once into LDS (coalesced float4 loads);
-// every later access (P recompute, dW_ro partial, dH) reads LDS.
+// every later access (P recompute, dW_ro partial, dH) reads LDS.  All 256
+// threads work in every phase: the P recompute takes 4 lanes per token (each a
+// quarter of the features, combined with two xor-shuffles), the dW_ro partial
+// 2 threads per feature (token halves, combined through LDS).  Row pitch 144
+// floats (16 dwords mod 64): the 16 lanes of a ds_read_b128 group (4 tokens x 4
+// quarters) hit 16 distinct 4-bank slots.
 // ---------------------------------------------------------------------------
-constexpr int RO_PITCH = GHM_D + 4;  // 16-B aligned rows; float4 reads of distinct rows conflict-free
+constexpr int RO_PITCH = GHM_D + 16;
 template <int NC>
-__global__ __launch_bounds__(256) void k_readout_bwd(
+__global__ __launch_bounds__(256, 2) void k_readout_bwd(
     const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
     const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
     float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
@@ -466,6 +471,7 @@ __global__ __launch_bounds__(256) void k_readout_bwd(
   __shared__ __attribute__((aligned(16))) float sW[NC * GHM_D];
   __shared__ __attribute__((aligned(16))) float sH[GHM_MAXT * RO_PITCH];
   __shared__ float sdP[GHM_MAXT][NC + 1];
+  __shared__ float sred[NC][GHM_D];
   const int tid = threadIdx.x, n = blockIdx.x;
   const int64_t base = static_cast<int64_t>(n) * T;
   for (int i = tid; i < NC * GHM_D; i += 256) sW[i] = Wro[i];
@@ -489,53 +495,72 @@ __global__ __launch_bounds__(256) void k_readout_bwd(
 #pragma unroll
   for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
   __syncthreads();
-  if (tid < T) {  // thread = token: recompute P[t][c], dP, dw_out partial
-    const int t = tid;
-    float p[NC];
+  {  // P[t][c] recompute, dP, dw_out partial: lane quarter qq holds features 4 qq + 16 k + 0..3
+    const int qq = tid & 3;
+#pragma unroll 1
+    for (int t = tid >> 2; t < GHM_MAXT; t += 64) {  // uniform trip count (96 / 64): shuffles stay converged
+      const int tr = t < T ? t : T - 1;
+      float p[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) p[c] = 0.f;
-#pragma unroll 4
-    for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
-      const float4 hv = lds4(sH + t * RO_PITCH + 4 * d4);
+      for (int c = 0; c < NC; ++c) p[c] = 0.f;
+#pragma unroll 2
+      for (int k = 0; k < GHM_D / 16; ++k) {
+        const float4 hv = lds4(sH + tr * RO_PITCH + 4 * qq + 16 * k);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const float4 wv = lds4(sW + c * GHM_D + 4 * qq + 16 * k);
+          p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
+        }
+      }
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const float4 wv = lds4(sW + c * GHM_D + 4 * d4);
-        p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
+        p[c] += __shfl_xor(p[c], 1, 64);
+        p[c] += __shfl_xor(p[c], 2, 64);
+      }
+      if (qq == 0 && t < T) {
+        float dw = 0.f;
+        const float wt = wout[t];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          dw += de[c] * (p[c] + bro[c]);
+          sdP[t][c] = de[c] * wt;
+        }
+        part_wout[base + t] = dw;
       }
     }
-    float dw = 0.f;
-    const float wt = wout[t];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      dw += de[c] * (p[c] + bro[c]);
-      sdP[t][c] = de[c] * wt;
-    }
-    part_wout[base + t] = dw;
   }
   __syncthreads();
-  if (tid < GHM_D) {  // thread = feature d: partial dW_ro[c][d]
-    const int d = tid;
+  {  // partial dW_ro[c][d]: thread = (feature d, token half hf)
+    const int d = tid & 127, hf = tid >> 7;
+    const int t0 = hf ? (T + 1) / 2 : 0, t1 = hf ? T : (T + 1) / 2;
     float aw[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) aw[c] = 0.f;
 #pragma unroll 3
-    for (int t = 0; t < T; ++t) {
+    for (int t = t0; t < t1; ++t) {
       const float hv = sH[t * RO_PITCH + d];
 #pragma unroll
       for (int c = 0; c < NC; ++c) aw[c] += sdP[t][c] * hv;
     }
+    if (hf) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) part_wro[(static_cast<int64_t>(n) * NC + c) * GHM_D + d] = aw[c];
-  } else if (tid < GHM_D + NC) {
-    const int c = tid - GHM_D;
-    float sacc = 0.f;
-    for (int t = 0; t < T; ++t) sacc += sdP[t][c];
-    part_bro[static_cast<int64_t>(n) * NC + c] = sacc;
-    if (c == 0) {
-      float sbo = 0.f;
+      for (int c = 0; c < NC; ++c) sred[c][d] = aw[c];
+    }
+    __syncthreads();
+    if (!hf) {
 #pragma unroll
-      for (int k = 0; k < NC; ++k) sbo += de[k];
-      part_bout[n] = sbo;
+      for (int c = 0; c < NC; ++c) part_wro[(static_cast<int64_t>(n) * NC + c) * GHM_D + d] = aw[c] + sred[c][d];
+    } else if (d < NC) {
+      const int c = d;
+      float sacc = 0.f;
+      for (int t = 0; t < T; ++t) sacc += sdP[t][c];
+      part_bro[static_cast<int64_t>(n) * NC + c] = sacc;
+      if (c == 0) {
+        float sbo = 0.f;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) sbo += de[k];
+        part_bout[n] = sbo;
+      }
     }
   }
   // dH[t][d] = sum_c dP[t][c] W_ro[c][d]: float4 per thread, coalesced rows

@@ -45,8 +45,13 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
 
-// lane-pair (l, l^32) exchange
-__device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32, 64); }
+// lane-pair (l, l^32) exchange on the VALU (v_permlane32_swap: the lower half
+// of one copy trades places with the upper half of the other), not through the
+// LDS crossbar (ds_bpermute)
+__device__ __forceinline__ float xhalf(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((__lane_id() & 32) ? r[0] : r[1]);
+}
 
 // sum over the 32 lanes of one half (lanes j = 0..31 for fixed h)
 __device__ __forceinline__ float sum32(float v) {

@@ -953,7 +953,13 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 // lane's 8-token operand fragment is one ds_read_b128.  Workgroup = 128 x 128
 // output tile, 4 waves as 2 x 2 of 64 x 64.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (ch ^ ((row >> 2) & 3)); }
+// 16-B chunk ch of image row r at ch ^ s(r), s(r) = bit 2 of r | (bit 1 ^ bit 3) << 1:
+// the operand reads (ds_read_b128, rows 32n + j) stay conflict-free and the
+// staging stores (ds_write_b128, 8 consecutive rows per LDS cycle, 32 banks)
+// become so (s(r) = (r >> 2) & 3 left them 2-way: SQ_LDS_BANK_CONFLICT 1.66 M
+// per dW2 launch).
+__device__ __forceinline__ int wg_swz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
+__device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (ch ^ wg_swz(row)); }
 
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A, int lda,

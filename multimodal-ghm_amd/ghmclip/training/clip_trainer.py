@@ -17,6 +17,7 @@ Design:
   optimizer graph.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -169,7 +170,7 @@ class ClipTrainer:
         join through stream waits, which graph capture records as edges), so the
         two towers' launches overlap and fill each other's tails."""
         main = torch.cuda.current_stream()
-        side = self.side
+        side = main if os.environ.get("GHM_SERIAL_TOWERS") == "1" else self.side
         pt, pi = self.plans
         (tp, tg, _, _), (ip, ig, _, _) = self.views
         side.wait_stream(main)
