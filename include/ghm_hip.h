@@ -187,9 +187,11 @@ int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, 
 int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                       const float* ln_b, const void* pack, const float* b1, float* G, float* dU, float* dH_mid,
                       float* part_ln, int64_t M, int D, int F, void* stream);
-/* As ghm_qkv_bwd (backward of model.py:772-775). */
-int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
-                   const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, void* stream);
+/* As ghm_qkv_bwd (backward of model.py:772-775), with the LN1 statistics
+ * recomputed from H (as the forward computed them, eps = the LayerNorm eps)
+ * instead of read from the forward's stats buffer. */
+int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* ln_w, const void* pack, const float* dH_mid,
+                   float* dH, float* part_ln, int64_t M, int D, float eps, void* stream);
 
 /* As ghm_attn_fwd / ghm_attn_bwd (model.py:778-782 and its backward); P and dS
  * are stored fp32 in the same dense padded layout. */

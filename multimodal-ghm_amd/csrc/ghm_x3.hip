@@ -897,9 +897,9 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
 //   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
-    const float* __restrict__ dqkv, const float* __restrict__ H, const float2* __restrict__ stats,
-    const float* __restrict__ lnw, const __bf16* __restrict__ pack, const float* __restrict__ dHmid,
-    float* __restrict__ dH, float* __restrict__ part_ln, int64_t M) {
+    const float* __restrict__ dqkv, const float* __restrict__ H, const float* __restrict__ lnw,
+    const __bf16* __restrict__ pack, const float* __restrict__ dHmid, float* __restrict__ dH,
+    float* __restrict__ part_ln, int64_t M, float eps) {
   __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
   __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
   __shared__ float red[2 * 4 * GHM_D];
@@ -912,6 +912,18 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
+  // LN1 statistics recomputed from the row exactly as the forward computed them
+  // (ln_row: the lane pair's 64 contiguous features, ln_stats64), not loaded
+  // from the forward's [M][2] buffer: a workgroup reading that buffer while a
+  // k_wgrad_x3 or k_ln_mlp_fwd_x3b workgroup shared its CU received wrong
+  // values for whole 16-token (128-byte) groups (tools/race_probe.py;
+  // DESIGN.md §4 "Determinism").  Bit-identical to the stored statistics.
+  float2 lnst;
+  {
+    float x[64];
+    load64(H + mc * GHM_D + 64 * h, x);
+    ln_stats64(x, eps, lnst.x, lnst.y);
+  }
   f32x16 dx[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) dx[it] = zero16();
@@ -937,7 +949,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
     }
   }
   if (active)
-    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, H + mc * GHM_D, lnst, gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -1587,14 +1599,14 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
   return ghm_launch_status();
 }
 
-extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w,
-                              const void* pack, const float* dH_mid, float* dH, float* part_ln, int64_t M,
-                              int D, void* stream) {
-  GHM_CHECK(dqkv && H && stats && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
+extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* ln_w, const void* pack,
+                              const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, float eps,
+                              void* stream) {
+  GHM_CHECK(dqkv && H && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
   hipLaunchKernelGGL(k_qkv_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), dqkv, H, reinterpret_cast<const float2*>(stats), ln_w,
-                     reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln, M);
+                     ghm_stream(stream), dqkv, H, ln_w, reinterpret_cast<const __bf16*>(pack), dH_mid, dH,
+                     part_ln, M, eps);
   return ghm_launch_status();
 }
 

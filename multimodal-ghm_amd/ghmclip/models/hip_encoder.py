@@ -386,9 +386,8 @@ class EncoderPlan:
             jobs.append(J(self.part_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
                                              g[f"_values.{l}.weight"]]))
             if x3:
-                c("ghm_qkv_bwd_x3", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]),
-                  _ptr(p[f"_lns_1.{l}.weight"]), _ptr(self.pack[l]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M,
-                  D_MODEL, s)
+                c("ghm_qkv_bwd_x3", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+                  _ptr(self.pack[l]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, self.eps, s)
             else:
                 c("ghm_qkv_bwd", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
                   _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),

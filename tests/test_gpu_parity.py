@@ -369,6 +369,32 @@ def test_guided_curve_vs_reference(precision):
     assert pdev.max() <= 1e-4
 
 
+def test_guided_full_run_final_risk_vs_reference_cpu_run():
+    """The whole guided run (exp_clip_guidedTF.sh: lr 1e-3 -> 1e-6, penalty 1e-3,
+    total_iters=3000, 3001 steps, split-bf16) against the reference's own code run
+    here on the CPU for all 3001 steps (clip_guided_curve3001.npz, 5 threads,
+    make_golden.py --only guide_curve --guide-steps 3001): the final risk
+    mean(loss_history[-100:]) of the penalty-free loss within 3e-4 relative
+    (measured 1.2e-4) and the first 100 steps within 1e-4 (as
+    test_guided_curve_vs_reference).  Step-wise the guided run drifts further
+    in its middle (measured max |dloss| 3e-2 near step 1000: lr 1e-3 and the
+    BP-penalty gradients amplify rounding), so later steps are not bounded."""
+    g = np.load(os.path.join(GOLDEN, "clip_guided_curve3001.npz"))
+    ref, pref = g["loss_history"], g["ploss_history"]
+    assert len(ref) == 3001 and (ref != 0).all()
+    sampler, tr = _guided_trainer(5, 128, "x3")
+    hist = _run(sampler, tr, 128, 3001, graph_after=3)
+    ph = tr.ploss_history()
+    risk, ref_risk = hist[-100:].mean(), ref[-100:].mean()
+    dev = np.abs(hist - ref)
+    pdev = np.abs(ph - pref) / np.abs(pref)
+    print(f"guided 3001-step run: final risk {risk:.7f} vs reference CPU run {ref_risk:.7f} "
+          f"(rel {abs(risk - ref_risk) / ref_risk:.2e}); max |dloss| {dev.max():.3e} at step {dev.argmax()}; "
+          f"max rel |dploss| {pdev.max():.3e}")
+    assert abs(risk - ref_risk) <= 3e-4 * ref_risk
+    assert dev[:100].max() <= 1e-4
+
+
 def test_guided_module_api():
     """EncoderTransformer(guide=True) returns H_{l+1}[:, :, :10] of the flagged
     layers, and GuidedClipLoss(guide=True) matches the oracle's value and grads."""

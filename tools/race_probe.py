@@ -57,8 +57,8 @@ def main():
 
     def run_victim():
         if victim == "qkv_bwd":
-            c("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]),
-              P(dHmid), P(outH), P(outP), M, 128, A)
+            c("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]),
+              P(dHmid), P(outH), P(outP), M, 128, p0.eps, A)
             return [outH, outP]
         if victim == "wgrad":
             tps, ns = p0.wg["w1"]
@@ -164,6 +164,22 @@ def main():
                               f"max |d| {diff.max().item():.3e}, |ref| max {a.abs().max().item():.3e}, "
                               f"nan {torch.isnan(b).sum().item()}")
     print(f"victim {victim} aggressor {aggr}: {bad}/{reps - 1} repetitions differ")
+    if os.environ.get("GHM_PROBE_STATS") == "1" and victim == "qkv_bwd":
+        # debug build GHM_QKV_DBG=13: dH[m][0:2] holds the (mean, rstd) the kernel read
+        got = outH[:, :2]
+        true = p0.st1[l]
+        bad_rows = torch.nonzero((got != true).any(1)).flatten()
+        print(f"stats read wrong for {len(bad_rows)} tokens: {bad_rows[:20].tolist()}")
+        for m in bad_rows[:4].tolist():
+            v = got[m]
+            # where else does this value live?
+            hits = []
+            for name, t in (("p0.st1", p0.st1), ("p0.st2", p0.st2), ("p1.st1", p1.st1), ("p1.st2", p1.st2)):
+                flat = t.reshape(-1, 2)
+                idx = torch.nonzero((flat == v).all(1)).flatten()
+                if len(idx):
+                    hits.append(f"{name}[{idx[:3].tolist()}]")
+            print(f"  token {m}: read {v.tolist()} true {true[m].tolist()} found in {hits}")
 
 
 if __name__ == "__main__":
