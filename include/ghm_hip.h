@@ -188,8 +188,8 @@ int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stat
                       const float* ln_b, const void* pack, const float* b1, float* G, float* dU, float* dH_mid,
                       float* part_ln, int64_t M, int D, int F, void* stream);
 /* As ghm_qkv_bwd (backward of model.py:772-775), with the LN1 statistics
- * recomputed from H (as the forward computed them, eps = the LayerNorm eps)
- * instead of read from the forward's stats buffer. */
+ * recomputed from H exactly as the forward computed them (eps = the LayerNorm
+ * eps) instead of read from the forward's stats buffer. */
 int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* ln_w, const void* pack, const float* dH_mid,
                    float* dH, float* part_ln, int64_t M, int D, float eps, void* stream);
 

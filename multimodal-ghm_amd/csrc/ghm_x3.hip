@@ -609,7 +609,6 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p) {
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
   return v;
 }
-
 template <int NW>
 __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
@@ -913,11 +912,12 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
   // LN1 statistics recomputed from the row exactly as the forward computed them
-  // (ln_row: the lane pair's 64 contiguous features, ln_stats64), not loaded
-  // from the forward's [M][2] buffer: a workgroup reading that buffer while a
-  // k_wgrad_x3 or k_ln_mlp_fwd_x3b workgroup shared its CU received wrong
-  // values for whole 16-token (128-byte) groups (tools/race_probe.py;
-  // DESIGN.md §4 "Determinism").  Bit-identical to the stored statistics.
+  // (ln_row: the lane pair's 64 contiguous features, ln_stats64; bit-identical
+  // to the forward's), not loaded from the forward's [M][2] buffer: a
+  // workgroup reading that buffer while a k_wgrad_x3 or k_ln_mlp_fwd_x3b
+  // workgroup shared its CU received wrong values for whole 16-token
+  // (128-byte) groups (tools/race_probe.py; DESIGN.md §4 "Determinism").
+  // Measured: 43 -> 50 us per launch (the row is read once more).
   float2 lnst;
   {
     float x[64];

@@ -220,6 +220,25 @@ def _run(sampler, tr, B, steps, graph_after=None):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
+def test_step_bit_identical_across_runs(precision):
+    """Two fresh trainers on the same draws give bit-identical loss histories,
+    parameters and Adam moments after 12 steps (graph captured after 3), with the
+    two towers running concurrently on two streams: fixed reduction trees, no
+    atomics, and no read that depends on which workgroups share a CU (the QKV
+    backward once read its LN statistics wrong beside the weight-gradient
+    kernel: DESIGN.md section 4 "Determinism")."""
+    outs = []
+    for _ in range(2):
+        sampler, tr = _trainer(5, 128, 0.2, precision=precision)
+        hist = _run(sampler, tr, 128, 12, graph_after=3)
+        outs.append((hist.copy(), tr.pflat.cpu().clone(), tr.mflat.cpu().clone(), tr.vflat.cpu().clone()))
+        del tr
+    (h0, p0, m0, v0), (h1, p1, m1, v1) = outs
+    assert np.array_equal(h0, h1)
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 def test_train_steps_vs_reference_fixture(precision):
     """Two full steps of the d=128, L=2, B=8 config against the reference's own
     numbers (tests/golden/clip_d128.npz)."""
