@@ -258,9 +258,9 @@ class CdmTrainer:
         dp = self.pg is not None or distributed.is_on()
         if self.graphs is not None:
             self.graphs[0].replay()
-            if dp:
+            if len(self.graphs) > 1:
                 self._allreduce()
-            self.graphs[1].replay()
+                self.graphs[1].replay()
         else:
             self._fwd_bwd()
             if dp:
@@ -269,17 +269,28 @@ class CdmTrainer:
         self.steps_done += 1
 
     def capture(self):
-        """Capture the step into HIP graphs (after >= 1 eager step)."""
+        """Capture the step into HIP graphs (after >= 1 eager step): one graph in
+        a single process, fwd/bwd and optimizer graphs around the gradient
+        all-reduce under data parallelism."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        dp = self.pg is not None or distributed.is_on()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
-                self._fwd_bwd()
-            with torch.cuda.graph(g2, stream=s):
-                self._optim()
+            if dp:
+                g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1, stream=s):
+                    self._fwd_bwd()
+                with torch.cuda.graph(g2, stream=s):
+                    self._optim()
+                graphs = (g1, g2)
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self._fwd_bwd()
+                    self._optim()
+                graphs = (g,)
         torch.cuda.current_stream().wait_stream(s)
-        self.graphs = (g1, g2)
+        self.graphs = graphs
 
     # -- host-side views -----------------------------------------------------------
     def loss_history(self, upto=None):

@@ -218,9 +218,9 @@ class ClipTrainer:
             raise RuntimeError("schedule exhausted")
         if self.graphs is not None:
             self.graphs[0].replay()
-            if self.pg is not None or distributed.is_on():
+            if len(self.graphs) > 1:
                 self._allreduce()
-            self.graphs[1].replay()
+                self.graphs[1].replay()
         else:
             self._fwd_bwd()
             if self.pg is not None or distributed.is_on():
@@ -230,17 +230,29 @@ class ClipTrainer:
 
     def capture(self):
         """Capture the step into HIP graphs (call after >= 1 eager step so all
-        lazy initialisation has happened).  Replays reuse the staged tokens."""
+        lazy initialisation has happened).  Replays reuse the staged tokens.
+        One process: fwd/bwd and the optimizer are one graph (one launch, no
+        host gap between them).  Data parallel: two graphs with the gradient
+        all-reduce between them."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        dp = self.pg is not None or distributed.is_on()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
-                self._fwd_bwd()
-            with torch.cuda.graph(g2, stream=s):
-                self._optim()
+            if dp:
+                g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1, stream=s):
+                    self._fwd_bwd()
+                with torch.cuda.graph(g2, stream=s):
+                    self._optim()
+                graphs = (g1, g2)
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    self._fwd_bwd()
+                    self._optim()
+                graphs = (g,)
         torch.cuda.current_stream().wait_stream(s)
-        self.graphs = (g1, g2)
+        self.graphs = graphs
 
     # -- host-side views -----------------------------------------------------------
     def loss_history(self, upto=None):
