@@ -604,28 +604,61 @@ __global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0
 }
 
 // ---------------------------------------------------------------------------
-// Deterministic partial reductions, several jobs per launch.
-// 1024 threads = 64 consecutive outputs x 16 split groups; group g sums splits
-// g, g+16, ... in order, then the 16 group sums are added in order: a fixed
-// summation tree independent of timing.  Block b serves the job whose block
-// range contains b.
+// Deterministic partial reductions, several jobs per launch.  Wide, shallow jobs
+// (the weight-gradient partials): thread = one output, its splits summed in 8
+// interleaved partial sums and a balanced tree, 256 outputs per block.  The others (LayerNorm / readout /
+// embedding partials: up to 10 K outputs over hundreds of splits): 16
+// outputs x 16 split groups per block, group g summing splits g, g+16, ... in
+// order and the 16 group sums added in order.  Either way a fixed summation
+// order independent of timing.  Block b serves the job whose block range
+// contains b.
 // ---------------------------------------------------------------------------
 #define GHM_MAX_JOBS 8
+// a job takes one thread per output when it is wide and shallow (the split-K
+// weight partials: 49 K - 66 K outputs x 64 - 85 splits)
+__host__ __device__ __forceinline__ bool red_wide(int64_t n, int n_split) { return n >= 8192 && n_split <= 256; }
 struct ReduceJobs {
   ghm_reduce_job job[GHM_MAX_JOBS];
   int64_t blk_end[GHM_MAX_JOBS];  // cumulative block counts
   int n_jobs;
 };
 
-__global__ __launch_bounds__(1024) void k_reduce(ReduceJobs J) {
-  __shared__ float red[16][64];
+__device__ __forceinline__ void red_store(const ghm_reduce_job& jb, int64_t i, float t) {
+  int d = 0;
+  while (d + 1 < jb.n_seg && i >= jb.off[d + 1]) ++d;
+  jb.dst[d][i - jb.off[d]] = t;
+}
+
+__global__ __launch_bounds__(256) void k_reduce(ReduceJobs J) {
+  __shared__ float red[16][17];
   int q = 0;
   while (q + 1 < J.n_jobs && static_cast<int64_t>(blockIdx.x) >= J.blk_end[q]) ++q;
   const ghm_reduce_job& jb = J.job[q];
   const int64_t blk = static_cast<int64_t>(blockIdx.x) - (q ? J.blk_end[q - 1] : 0);
-  const int e = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t i = blk * 64 + e;
   const int64_t n = jb.n;
+  if (red_wide(n, jb.n_split)) {
+    const int64_t i = blk * 256 + threadIdx.x;
+    if (i >= n) return;
+    // 8 interleaved partial sums (split k goes to sum k % 8), combined as a
+    // balanced tree: as accurate as the round-1 16-group tree, more loads in flight
+    const float* p = jb.part + i;
+    float a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = 0.f;
+    int k = 0;
+    for (; k + 8 <= jb.n_split; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[static_cast<int64_t>(k + u) * n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += v[u];
+    }
+    for (int u = 0; k < jb.n_split; ++k, ++u) a[u] += p[static_cast<int64_t>(k) * n];
+    red_store(jb, i, ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
+    return;
+  }
+  const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t i = blk * 16 + e;
   float s = 0.f;
   if (i < n) {
 #pragma unroll 4
@@ -637,9 +670,7 @@ __global__ __launch_bounds__(1024) void k_reduce(ReduceJobs J) {
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) t += red[k][e];
-    int d = 0;
-    while (d + 1 < jb.n_seg && i >= jb.off[d + 1]) ++d;
-    jb.dst[d][i - jb.off[d]] = t;
+    red_store(jb, i, t);
   }
 }
 
@@ -754,13 +785,13 @@ extern "C" int ghm_reduce_batch(const ghm_reduce_job* jobs, int n_jobs, void* st
       const int rc = validate_job(jobs[q]);
       if (rc) return rc;
       J.job[q] = jobs[q];
-      blocks += (jobs[q].n + 63) / 64;
+      blocks += red_wide(jobs[q].n, jobs[q].n_split) ? (jobs[q].n + 255) / 256 : (jobs[q].n + 15) / 16;
     } else {
       J.job[q] = jobs[n_jobs - 1];
     }
     J.blk_end[q] = blocks;
   }
-  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>(blocks)), dim3(1024), 0, ghm_stream(stream), J);
+  hipLaunchKernelGGL(k_reduce, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, ghm_stream(stream), J);
   return ghm_launch_status();
 }
 
