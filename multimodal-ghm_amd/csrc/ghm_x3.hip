@@ -1577,12 +1577,13 @@ extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const flo
   return ghm_launch_status();
 }
 
-// waves per workgroup of k_mlp_bwd_rc_x3 (16 tokens each).  Measured (one
-// box, alternating 200-step benches): 8 waves 4.42 ms/step, 4 waves (two
-// workgroups per CU, 64 KB of LDS each) 4.43-4.48.
-constexpr int RC_NW = 8;
+// waves per workgroup of k_mlp_bwd_rc_x3 (16 tokens each): 8 when M gives every
+// CU a 128-token workgroup (the CLIP's 51,840 tokens: measured 4.42 ms/step vs
+// 4.43-4.48 for 4 waves), else 4 (the CDM's 10,496 tokens: 164 workgroups
+// instead of 82), the rule of ghm_ln_mlp_fwd_x3b
+static int rc_waves(int64_t M) { return (M + 127) / 128 >= 256 ? 8 : 4; }
 extern "C" int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M) {
-  const int64_t tok = 16 * RC_NW;
+  const int64_t tok = 16 * rc_waves(M);
   return (M + tok - 1) / tok;
 }
 
@@ -1593,9 +1594,14 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
   const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
-  hipLaunchKernelGGL(k_mlp_bwd_rc_x3<RC_NW>, dim3(nblk), dim3(64 * RC_NW), 0, ghm_stream(stream), dH_out, H_mid,
-                     reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
-                     G, dU, dH_mid, part_ln, M);
+  if (rc_waves(M) == 8)
+    hipLaunchKernelGGL(k_mlp_bwd_rc_x3<8>, dim3(nblk), dim3(512), 0, ghm_stream(stream), dH_out, H_mid,
+                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                       G, dU, dH_mid, part_ln, M);
+  else
+    hipLaunchKernelGGL(k_mlp_bwd_rc_x3<4>, dim3(nblk), dim3(256), 0, ghm_stream(stream), dH_out, H_mid,
+                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                       G, dU, dH_mid, part_ln, M);
   return ghm_launch_status();
 }
 
