@@ -238,6 +238,46 @@ def test_step_bit_identical_across_runs(precision):
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
+def test_qkv_backward_unperturbed_beside_weight_gradient():
+    """The QKV backward on fixed inputs gives bit-identical outputs while the
+    weight-gradient kernel runs on another stream (before the fix its LN
+    statistics were read wrong for 16-token groups in every repetition:
+    tools/race_probe.py, DESIGN.md section 4 "Determinism")."""
+    import ctypes
+    from ghmclip import _native
+    sampler, tr = _trainer(5, 128, 0.2, precision="x3")
+    _run(sampler, tr, 128, 1)
+    p0, p1 = tr.plans
+    w0, w1 = tr.views[0][0], tr.views[1][0]
+    M, l = p0.M, 2
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dHmid = torch.randn(M, 128, device=DEV, generator=g) * 1e-3
+    dqkv = torch.randn(M, 384, device=DEV, generator=g) * 1e-3
+    outH, outP = torch.empty(M, 128, device=DEV), torch.empty_like(p0.part_ln)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    A, B = ctypes.c_void_p(sa.cuda_stream), ctypes.c_void_p(sb.cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    tps, _ = p1.wg["w2"]
+    ref = None
+    for _ in range(6):
+        sa.wait_stream(torch.cuda.current_stream())
+        sb.wait_stream(torch.cuda.current_stream())
+        for _ in range(3):
+            _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
+                         P(p1.part_w2), P(p1.part_b2), M, tps, B)
+        _native.call("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]), P(dHmid),
+                     P(outH), P(outP), M, 128, p0.eps, A)
+        for _ in range(3):
+            _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
+                         P(p1.part_w2), P(p1.part_b2), M, tps, B)
+        torch.cuda.synchronize()
+        got = (outH.clone(), outP.clone())
+        if ref is None:
+            ref = got
+        else:
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_train_steps_vs_reference_fixture(precision):
     """Two full steps of the d=128, L=2, B=8 config against the reference's own
