@@ -5,15 +5,23 @@ HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 LIBDIR := multimodal-ghm_amd/ghmclip/_lib
 SRC := multimodal-ghm_amd/csrc
-HIPFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result
+HIPOBJFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 HIP_SRCS := $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_x3.hip $(SRC)/ghm_guide.hip $(SRC)/ghm_cdm.hip $(SRC)/ghm_vlm.hip $(SRC)/ghm_gemm.hip $(SRC)/ghm_vlm_x3.hip $(SRC)/ghm_optim.hip $(SRC)/ghm_eval.hip
 HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h $(SRC)/ghm_split.h $(SRC)/ghm_ln.h include/ghm_hip.h
 
 all: $(LIBDIR)/libghm_hip.so $(LIBDIR)/libghm_host.so
 
-$(LIBDIR)/libghm_hip.so: $(HIP_SRCS) $(HIP_HDRS)
+OBJDIR := build/obj
+HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+
+# one object per translation unit (parallel, incremental), linked into one library
+$(OBJDIR)/%.o: $(SRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPOBJFLAGS) -c -o $@ $<
+
+$(LIBDIR)/libghm_hip.so: $(HIP_OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -o $@ $(HIP_SRCS)
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS)
 
 $(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h
 	@mkdir -p $(LIBDIR)
@@ -25,6 +33,6 @@ resource-usage: $(HIP_SRCS) $(HIP_HDRS)
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_x3.hip -o /tmp/ghm_x3.o
 
 clean:
-	rm -f $(LIBDIR)/*.so
+	rm -f $(LIBDIR)/*.so $(OBJDIR)/*.o
 
 .PHONY: all clean resource-usage

@@ -10,7 +10,9 @@
  * Ownership: the handle owns only host memory; output buffers are caller-owned.
  * Errors: int return, 0 = success, negative GHM_E* on bad arguments.
  * Threading: one handle per calling thread (each handle owns a small worker pool
- * for the tree expansion); no global state.
+ * for the tree expansion); no global state.  Fork: a handle used in a child
+ * process (fork after ghm_sampler_create) expands serially on the calling
+ * thread — same draws, no deadlock on the parent's absent workers.
  */
 #ifndef GHM_SAMPLER_H
 #define GHM_SAMPLER_H

@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 namespace {
@@ -118,12 +119,20 @@ struct MT19937 {
 // Fixed worker pool for the tree expansion (the MT stream itself is serial).
 // Workers park on a condition variable between batches; run(f) calls f(w) for
 // w = 0..n-1, w = 0 on the calling thread, and returns when all are done.
+// Fork safety: a child process inherits the pool object but not its threads,
+// so in any process other than the creating one run() calls f(0..n-1) serially
+// on the calling thread (same results: the partition of the work is unchanged)
+// and the destructor neither signals nor joins the absent workers.
 class Pool {
  public:
-  explicit Pool(int n) : n_(n < 1 ? 1 : n) {
+  explicit Pool(int n) : n_(n < 1 ? 1 : n), pid_(getpid()) {
     for (int w = 1; w < n_; ++w) th_.emplace_back([this, w] { loop(w); });
   }
   ~Pool() {
+    if (getpid() != pid_) {  // forked child: the workers do not exist here
+      new std::vector<std::thread>(std::move(th_));  // leaked on purpose: never joined
+      return;
+    }
     {
       std::lock_guard<std::mutex> g(mu_);
       stop_ = true;
@@ -133,8 +142,8 @@ class Pool {
   }
   int size() const { return n_; }
   void run(const std::function<void(int)>& f) {
-    if (n_ == 1) {
-      f(0);
+    if (n_ == 1 || getpid() != pid_) {
+      for (int w = 0; w < n_; ++w) f(w);
       return;
     }
     {
@@ -168,6 +177,7 @@ class Pool {
     }
   }
   int n_;
+  pid_t pid_;
   std::vector<std::thread> th_;
   std::mutex mu_;
   std::condition_variable cv_, done_;

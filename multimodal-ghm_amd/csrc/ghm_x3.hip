@@ -19,6 +19,9 @@
 #ifndef GHM_ABL
 #define GHM_ABL 0
 #endif
+#if GHM_ABL != 0 && !defined(GHM_ABLATION_BUILD)
+#error "GHM_ABL timing ablations give wrong results: only with -DGHM_ABLATION_BUILD (tools/, never the product library)"
+#endif
 
 // ---------------------------------------------------------------------------
 // Weight pack (bf16 elements per layer; each region = hi plane then lo plane)

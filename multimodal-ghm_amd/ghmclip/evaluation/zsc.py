@@ -61,10 +61,22 @@ def _embed(model, leaves, n_valid, device, D=10):
 
 
 def zsc_logits(i_emb, t_emb, proto_idx, n_list):
-    """[len(n_list), rows, n_class] device logits (ghm_zsc_logits)."""
+    """[len(n_list), rows, n_class] device logits (ghm_zsc_logits).
+    Every support size must lie in 1..n_proto (the kernel divides the first n
+    prototypes' sum by n) and at most 8 sizes are scored per launch; the
+    prototype indices must address rows of t_emb."""
     require_hip(i_emb)
     n_rows, D = i_emb.shape
     n_class, n_proto = proto_idx.shape
+    n_list = [int(n) for n in n_list]
+    if not 1 <= len(n_list) <= 8:
+        raise ValueError(f"zsc_logits scores 1..8 support sizes per call, got {len(n_list)}")
+    if any(n < 1 or n > n_proto for n in n_list):
+        raise ValueError(f"support sizes {n_list} must lie in 1..{n_proto} (prototypes per class)")
+    if t_emb.shape[1] != D or D > 16:
+        raise ValueError(f"embedding widths {D} / {t_emb.shape[1]} must match and be <= 16")
+    if proto_idx.numel() and (int(proto_idx.min()) < 0 or int(proto_idx.max()) >= t_emb.shape[0]):
+        raise ValueError("prototype indices must address rows of t_emb")
     out = torch.empty(len(n_list), n_rows, n_class, dtype=torch.float32, device=i_emb.device)
     nl = torch.tensor(n_list, dtype=torch.int32, device=i_emb.device)
     ie, te = i_emb.contiguous(), t_emb.contiguous()

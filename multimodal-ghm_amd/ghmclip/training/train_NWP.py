@@ -149,7 +149,10 @@ def main(argv=None):
                 sync_hist(iter_num + 1)
                 finish_time = time.time()
                 h = iter_num // 2
-                pen = trainer.guide_penalties()  # this rank's last step: output[1:5] of the reference
+                # the last step's output[1:5] of the reference; under DP averaged over
+                # the ranks like the histories beside it (a collective: every rank logs)
+                pen = distributed.mean_histories([trainer.guide_penalties()], device)[0] if c.guide \
+                    else [0.0, 0.0, 0.0, 0.0]
                 logger.info(f'Iter: {iter_num},Penalty train loss: {np.mean(ploss_history[h:iter_num]):.4f}, '
                             f'Train loss: {np.mean(loss_history[h:iter_num]):.4f}, '
                             f'Compare: {np.mean(compare_history[h:iter_num]):.4f}, '

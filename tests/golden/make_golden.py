@@ -141,13 +141,14 @@ def step_fixture(name, L, d, B, nsteps, p=0.2, total_iters=3000, checksum_only=F
     print("wrote", name)
 
 
-def curve_fixture(steps, p=0.2, B=128, total_iters=3000, out="clip_default_curve.npz"):
+def curve_fixture(steps, p=0.2, B=128, total_iters=3000, out="clip_default_curve.npz", n_layer=5):
     """Default CLIP config (scripts/experiments/exp_clip_standardTF.sh:15-40).
     With steps = total_iters + 1 this is the whole reference run (F5): its final
-    risk is mean(loss_history[-100:]) (figures/eval-clip-risk.py:29)."""
+    risk is mean(loss_history[-100:]) (figures/eval-clip-risk.py:29).
+    n_layer=1 is the Shallow TF architecture (exp_clip_shallowTF.sh:19-36)."""
     s = make_sampler(p)
     seed_everything(224)
-    tm, im = build_models(81, 5, 128)
+    tm, im = build_models(81, n_layer, 128)
     loss_nop = GuidedClipLoss(4, B, penalty=0, guide=False)
     loss = GuidedClipLoss(4, B, penalty=1e-3, guide=False)
     params = list(tm.parameters()) + list(im.parameters())
@@ -171,9 +172,10 @@ def curve_fixture(steps, p=0.2, B=128, total_iters=3000, out="clip_default_curve
             print(f"curve step {it} loss {hist[it]:.6f} ({time.time()-t0:.0f}s)", flush=True)
         if it % 200 == 0 and steps > 1000:  # checkpoint the long run
             np.savez_compressed(os.path.join(HERE, out), loss_history=hist[:it + 1], grad_norm=norms[:it + 1],
-                                p=p, B=B, total_iters=total_iters, threads=torch.get_num_threads())
+                                p=p, B=B, total_iters=total_iters, n_layer=n_layer,
+                                threads=torch.get_num_threads())
     np.savez_compressed(os.path.join(HERE, out), loss_history=hist,
-                        grad_norm=norms, p=p, B=B, total_iters=total_iters,
+                        grad_norm=norms, p=p, B=B, total_iters=total_iters, n_layer=n_layer,
                         threads=torch.get_num_threads())
     print("wrote", out)
 
@@ -282,6 +284,10 @@ def guide_curve_fixture(steps, p=0.2, B=128, total_iters=3000, penalty=1e-3, lr_
         if it % 20 == 0:
             print(f"guide curve step {it} ploss {phist[it]:.6f} loss {hist[it]:.6f} ({time.time()-t0:.0f}s)",
                   flush=True)
+        if it % 100 == 0 and steps > 1000:  # checkpoint the long run (partial prefix)
+            np.savez_compressed(os.path.join(HERE, out), loss_history=hist[:it + 1], ploss_history=phist[:it + 1],
+                                penalty=pen[:it + 1], p=p, B=B, total_iters=total_iters,
+                                hyper=np.array([penalty, lr_max, lr_min]), threads=torch.get_num_threads())
     np.savez_compressed(os.path.join(HERE, out), loss_history=hist, ploss_history=phist,
                         penalty=pen, p=p, B=B, total_iters=total_iters,
                         hyper=np.array([penalty, lr_max, lr_min]), threads=torch.get_num_threads())
@@ -303,6 +309,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--curve-steps", type=int, default=200)
     ap.add_argument("--curve-out", default="clip_default_curve.npz")
+    ap.add_argument("--curve-layers", type=int, default=5)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--only", default="")
     ap.add_argument("--guide-steps", type=int, default=100)
@@ -321,7 +328,7 @@ if __name__ == "__main__":
     if "bayes" in jobs:
         bayes_fixture()
     if "curve" in jobs:
-        curve_fixture(a.curve_steps, out=a.curve_out)
+        curve_fixture(a.curve_steps, out=a.curve_out, n_layer=a.curve_layers)
     if "guide_bp" in jobs:
         guide_bp_fixture()
     if "guide_tiny" in jobs:

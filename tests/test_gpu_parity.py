@@ -329,8 +329,8 @@ def test_full_run_final_risk_vs_reference_cpu_run():
     run here on the CPU for all 3001 steps (clip_default_curve3001.npz, 6
     threads, make_golden.py --curve-steps 3001): final risk
     mean(loss_history[-100:]) (figures/eval-clip-risk.py:29) within 1e-5
-    relative, every step within 1e-3 absolute (the reference's reduction-order
-    noise and ours both grow along 3000 AdamW steps)."""
+    relative, every step within 1e-4 absolute (the north_star's curve bound;
+    measured 1.4e-6)."""
     g = np.load(os.path.join(GOLDEN, "clip_default_curve3001.npz"))
     ref = g["loss_history"]
     assert len(ref) == 3001 and (ref != 0).all()
@@ -342,7 +342,7 @@ def test_full_run_final_risk_vs_reference_cpu_run():
           f"(rel {abs(risk - ref_risk) / ref_risk:.2e}); max |dloss| {dev.max():.3e} at step {dev.argmax()}, "
           f"first 1000 steps {dev[:1000].max():.3e}")
     assert abs(risk - ref_risk) <= 1e-5 * ref_risk
-    assert dev.max() <= 1e-3
+    assert dev.max() <= 1e-4
 
 
 # ----------------------------------------------------------------------------

@@ -214,3 +214,36 @@ def test_batch_pipeline_producer_shards(world):
                 np.testing.assert_array_equal(is_.numpy(), draws[k][1][idx])
         finally:
             pipe.close()
+
+
+def test_sampler_usable_after_fork():
+    """A handle created before fork() draws in the child (serially: the parent's
+    worker threads do not exist there) the same batch the parent draws from
+    the same state — no deadlock (ghm_sampler.h, fork note)."""
+    import os
+    from ghmclip import ClipSampler
+    p_y = np.ones(10) / 10
+    s = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+    s.native.seed(3)
+    B = 32
+    t = np.empty((5 * B, 81), np.uint8)
+    i = np.empty((5 * B, 81), np.uint8)
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # child: draw, send, exit without running the parent's atexit handlers
+        try:
+            s.native.next_into(B, t, i)
+            os.write(w, t.tobytes() + i.tobytes())
+        finally:
+            os._exit(0)
+    os.close(w)
+    buf = b""
+    while True:
+        chunk = os.read(r, 1 << 16)
+        if not chunk:
+            break
+        buf += chunk
+    os.close(r)
+    os.waitpid(pid, 0)
+    s.native.next_into(B, t, i)
+    assert buf == t.tobytes() + i.tobytes()

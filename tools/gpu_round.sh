@@ -6,7 +6,7 @@ TAG=${1:-r1}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 ok() { r=$1; [ $r -eq 0 ] || [ $r -eq 1 ]; }
-timeout -k 10 700 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $OUT/gpu_tests.log
 grep -E "^FAILED|^ERROR|passed|failed" $OUT/gpu_tests.log | tail -12
