@@ -10,7 +10,8 @@ ConditionalGuidedCELoss, model.py:1080-1149, in the loops of train_CDNS.py:
 contiguous 1/world of every global batch's samples (CdmBatchPipeline /
 NwpBatchPipeline row_slice) and the flat gradient is averaged, so rank 0's
 loss_history (the rank mean of the shard losses) equals the single-rank run's
-up to reduction order.  --raw=False --eval_interval=2 exercises the collective
+up to reduction order (measured: <= 2.4e-7 absolute for the VLM CLIs, <= 2e-7
+relative for the CDM CLIs, whose losses are 1e2..1e5).  --raw=False --eval_interval=2 exercises the collective
 schedule that deadlocked in round 1 (history syncs before each rank-0 save).
 
 Also the bench line: bench.py --workload cdm --gpus 2 under torch.distributed.run.
@@ -132,9 +133,11 @@ def test_cli_dp2_equals_single_rank(case, tmp_path, clip_logs):
         np.testing.assert_array_equal(a, b)
     dev = [float(np.abs(a - b).max()) for a, b in zip(two[0], one)]
     print(f"{case}: dp2 vs single-rank max |d| per history (loss, compare) = {dev}")
-    np.testing.assert_allclose(loss2, loss1, rtol=0, atol=1e-6)
+    # 1e-6 relative: the CDM's LS losses run to 1e5 (guided, lr 1e-2), where one
+    # float32 ulp of the shard-mean order is ~1e-7 relative (measured <= 2e-7)
+    np.testing.assert_allclose(loss2, loss1, rtol=1e-6, atol=1e-6)
     if len(one) > 1:  # Compare (the BP-posterior gap) is a sample mean too
-        np.testing.assert_allclose(two[0][1], one[1], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(two[0][1], one[1], rtol=1e-6, atol=1e-6)
     job = "CDM" if "DNS" in cli else "VLM"
     ck = glob.glob(str(tmp_path / f"two/logs/{job}/*/*/*/checkpoint.pth"))
     assert len(ck) == 1, ck  # rank 0 saves, rank 1 is raw
