@@ -29,6 +29,31 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, de
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 STEP_GFLOP = 625.87            # algorithmic work per step at B=128
 MLP_FWD_GFLOP_PER_LAUNCH = 4 * 51840 * 128 * 512 / 1e9  # one encoder-layer MLP: 2 GEMMs
+M_DEFAULT = 51840  # tokens per tower at the default config: 128 rows x 5 sequences x 81 tokens
+# Algorithmic work of the step's candidate dominant kernels, per launch (one tower-layer) at
+# the default config, f32-product FLOPs (x3 issues 3 bf16 MFMA products per f32 product)
+# and the HBM bytes the algorithm must move (fp32 activations; weights ~1 MB, not counted):
+#   k_mlp_bwd_rc_x3  dG = dY W2 and dX2 = dU W1 (model.py:784-788 backward): 4 M 128 512;
+#                    the U recompute (2 M 128 512) is design work, listed apart; must move
+#                    dY, Hmid in and dHmid out ([M,128] each) -- G and dU ([M,512] each) are
+#                    written only because the weight gradients run in their own kernels
+#   k_ln_mlp_fwd_x3b LN2 + 128 -> 512 -> 128 (model.py:784-788): 4 M 128 512; Hmid in, H out
+#   k_wgrad_x3       dW1 or dWqkv (LN mode, one instantiation): 2 M 512 128 / 2 M 384 128
+#   k_qkv_bwd_x3     dX1 = dQKV Wqkv (model.py:772-775 backward): 2 M 384 128
+DOMINANT_CANDIDATES = {
+    "k_mlp_bwd_rc_x3": {"entry": "ghm_mlp_bwd_rc_x3", "gflop": 4 * M_DEFAULT * 128 * 512 / 1e9,
+                        "design_gflop": 6 * M_DEFAULT * 128 * 512 / 1e9, "bytes": 4 * M_DEFAULT * 128 * 3,
+                        "design_bytes": 4 * M_DEFAULT * (128 * 3 + 512 * 2),
+                        "what": "MLP + LN2 backward, U recomputed (model.py:784-788), one tower-layer"},
+    "k_ln_mlp_fwd_x3b": {"entry": "ghm_ln_mlp_fwd_x3b", "gflop": 4 * M_DEFAULT * 128 * 512 / 1e9,
+                         "design_gflop": 4 * M_DEFAULT * 128 * 512 / 1e9, "bytes": 4 * M_DEFAULT * 128 * 2,
+                         "design_bytes": 4 * M_DEFAULT * 128 * 2,
+                         "what": "LN2 + MLP + residual forward (model.py:784-788), one tower-layer"},
+    "k_qkv_bwd_x3": {"entry": "ghm_qkv_bwd_x3", "gflop": 2 * M_DEFAULT * 384 * 128 / 1e9,
+                     "design_gflop": 2 * M_DEFAULT * 384 * 128 / 1e9, "bytes": 4 * M_DEFAULT * (384 + 128 * 3),
+                     "design_bytes": 4 * M_DEFAULT * (384 + 128 * 3),
+                     "what": "QKV + LN1 backward (model.py:772-775), one tower-layer"},
+}
 # algorithmic HBM bytes of one LN2+MLP forward launch (fp32): Hmid in + H out
 # ([M,128] each) + G and GELU'(U) out ([M,512] each), M = 51,840 tokens
 MLP_FWD_BYTES_PER_LAUNCH = 4 * 51840 * (128 + 128 + 512 + 512)
@@ -274,6 +299,74 @@ def pmc_traffic(kernel):
     return None if k is None else k["hbm_bytes"]
 
 
+def step_hbm_bytes():
+    """HBM bytes of one training step: per-launch PMC bytes (profiles/traffic.json,
+    keyed by kernel name with template arguments) x launches per step (the
+    committed kernel stats: calls / the number of k_adamw launches, one per step)."""
+    import csv
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    stats = latest_profile("clip_kernel_stats.csv")
+    if stats is None or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)["kernels"]
+    rows = [(_kname(r["Name"]), int(r["Calls"])) for r in csv.DictReader(open(stats))]
+    steps = sum(n for k, n in rows if k == "k_adamw")
+    if not steps:
+        return None
+    return sum(t[k]["hbm_bytes"] * n / steps for k, n in rows if k in t)
+
+
+def latest_profile(suffix):
+    """Newest committed profiles/r<round>_v<n>_<suffix> (highest round, then version)."""
+    import glob
+    import re
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_v*_{suffix}")):
+        m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(f))
+        if m and (best is None or (int(m.group(1)), int(m.group(2))) > best[0]):
+            best = ((int(m.group(1)), int(m.group(2))), f)
+    return None if best is None else best[1]
+
+
+def _kname(raw):
+    import re
+    m = re.match(r"_Z(\d+)(\w+)", raw)
+    if m:
+        return m.group(2)[:int(m.group(1))]
+    name = raw.split("(")[0]
+    return name[5:] if name.startswith("void ") else name
+
+
+def profiled_kernels():
+    """(path, {kernel instantiation: (total ns, calls, average ns)}) of the committed
+    rocprofv3 --kernel-trace --stats summary of graph-replayed CLIP bench steps."""
+    import csv
+    path = latest_profile("clip_kernel_stats.csv")
+    if path is None:
+        return None, {}
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        k = _kname(r["Name"])  # instantiation (template arguments kept)
+        t, n = agg.get(k, (0.0, 0))
+        agg[k] = (t + float(r["TotalDurationNs"]), n + int(r["Calls"]))
+    return path, {k: (t, n, t / max(1, n)) for k, (t, n) in agg.items()}
+
+
+def mfma_busy(kernel):
+    """SQ_VALU_MFMA_BUSY_CYCLES utilisation of `kernel` from the newest committed
+    profiles/*mfma_util.txt (tools/mfma_util.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_util.txt")),
+                   key=lambda f: [int(x) for x in __import__("re").findall(r"\d+", os.path.basename(f))[:2]])
+    for f in reversed(files):
+        for line in open(f):
+            parts = line.split()
+            if parts and parts[0].split("<")[0] == kernel and len(parts) > 3 and parts[3].endswith("%"):
+                return {"util": float(parts[3][:-1]) / 100.0, "file": os.path.relpath(f, ROOT)}
+    return None
+
+
 def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     from oracle import ghm_oracle as O
     threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -413,6 +506,19 @@ def main():
     elapsed = timed_steps(a, ws, tr, one)
     losses = tr.loss_history()
     finite = bool(np.isfinite(losses).all())
+    # the dominant kernel: the largest share of kernel time in the committed rocprofv3
+    # trace of graph-replayed bench steps (profiles/r*_clip_kernel_stats.csv), timed
+    # here inside graph-replayed steps
+    prof_path, prof = profiled_kernels()
+    top = max(prof, key=lambda k: prof[k][0]) if prof else None
+    dom = top.split("<")[0] if top and top.split("<")[0] in DOMINANT_CANDIDATES else "k_mlp_bwd_rc_x3"
+    dom_inst = top if top and top.split("<")[0] == dom else None
+    if tr.precision != "x3" or not tr.plans[0].mlp_rc:
+        dom = "k_ln_mlp_fwd_x3b" if tr.precision == "x3" else None
+    dom_ms, dom_how = None, None
+    if dom:
+        dom_ms = time_kernel_in_step(tr, DOMINANT_CANDIDATES[dom]["entry"])
+        dom_how = "eager in-step: HIP events around each launch on its stream, both towers live"
     kname, klaunch = dominant_kernel(tr)
     kern_ms = time_kernel(klaunch)
     kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
@@ -440,20 +546,47 @@ def main():
     kflop = mult * MLP_FWD_GFLOP_PER_LAUNCH * scale
     achieved = kflop / (kern_ms * 1e-3) / 1e3
     achieved_step = kflop / (kern_ms_step * 1e-3) / 1e3
-    roofline = {"bound": "mfma", "kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
-                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
-                "basis": ("bf16 MFMA products issued (3 per f32 product, split-bf16)" if x3
-                          else "f32 MFMA products"),
-                "traffic": None if traffic is None else round(traffic * scale),
-                "algorithmic_bytes": round(MLP_FWD_MUST_BYTES * scale),
-                "design_bytes": round((MLP_FWD_MUST_BYTES if rc else MLP_FWD_BYTES_PER_LAUNCH) * scale),
-                "kernel_ms": round(kern_ms, 4),
-                "kernel_ms_in_step": round(kern_ms_step, 4),
-                "achieved_in_step": round(achieved_step, 2),
-                "frac_in_step": round(achieved_step / peak, 4),
-                "hbm_gbs_design": round((MLP_FWD_MUST_BYTES if rc else MLP_FWD_BYTES_PER_LAUNCH) * scale
-                                        / (kern_ms * 1e-3) / 1e9, 1)}
+    # the MLP forward, isolated and in eager steps (the round-2 line's kernel), kept beside
+    mlp_fwd = {"kernel": f"{kname} (LN2+MLP fwd, one encoder-layer)",
+               "achieved_isolated": round(achieved, 2), "frac_isolated": round(achieved / peak, 4),
+               "kernel_ms_isolated": round(kern_ms, 4), "kernel_ms_eager_step": round(kern_ms_step, 4),
+               "frac_eager_step": round(achieved_step / peak, 4),
+               "traffic": None if traffic is None else round(traffic * scale),
+               "algorithmic_bytes": round(MLP_FWD_MUST_BYTES * scale),
+               "design_bytes": round((MLP_FWD_MUST_BYTES if rc else MLP_FWD_BYTES_PER_LAUNCH) * scale)}
+    if dom is not None:
+        d = DOMINANT_CANDIDATES[dom]
+        dflop = mult * d["gflop"] * scale
+        dach = dflop / (dom_ms * 1e-3) / 1e3
+        ptot = sum(v[0] for v in prof.values()) if prof else 0.0
+        dtraffic = pmc_traffic(dom_inst or dom)
+        if dtraffic is None and dom == "k_mlp_bwd_rc_x3":
+            dtraffic = pmc_traffic("k_mlp_bwd_rc_x3<8>")
+        prof_avg_ms = prof[dom_inst][2] / 1e6 if dom_inst in prof else None
+        roofline = {"bound": "mfma",
+                    "kernel": f"{dom} ({d['what']})",
+                    "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(dach / peak, 4),
+                    "traffic": None if dtraffic is None else round(dtraffic * scale),
+                    "basis": (f"bf16 MFMA products issued: 3 x {d['gflop'] * scale:.2f} GFLOP algorithmic f32-product "
+                              f"work per launch" if x3 else f"{d['gflop'] * scale:.2f} GFLOP f32 MFMA products"),
+                    "design_gflop": round(d["design_gflop"] * scale, 2),
+                    "algorithmic_bytes": round(d["bytes"] * scale), "design_bytes": round(d["design_bytes"] * scale),
+                    "kernel_ms": round(dom_ms, 4), "timing": dom_how,
+                    "dominant_by": (f"{dom_inst}: {100 * prof[dom_inst][0] / ptot:.1f} % of kernel time in "
+                                    f"{os.path.relpath(prof_path, ROOT)}" if dom_inst in prof and ptot else
+                                    "default (no committed kernel stats)"),
+                    "profile_avg_ms": None if prof_avg_ms is None else round(prof_avg_ms, 4),
+                    "profile_frac": None if prof_avg_ms is None else round(dflop / (prof_avg_ms * 1e-3) / 1e3 / peak, 4),
+                    "mfma_busy": mfma_busy(dom),
+                    "hbm_gbs_traffic": None if dtraffic is None else round(dtraffic * scale / (dom_ms * 1e-3) / 1e9, 1),
+                    "mlp_fwd": mlp_fwd}
+    else:  # exact-f32 mode: the MLP forward on the f32 matrix cores
+        roofline = {"bound": "mfma", "kernel": mlp_fwd["kernel"], "achieved": round(achieved, 2), "peak": peak,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": mlp_fwd["traffic"],
+                    "kernel_ms": round(kern_ms, 4), "timing": "isolated launches"}
+    # whole-step HBM traffic: the committed per-launch PMC bytes x launches per step
+    step_bytes = step_hbm_bytes()
     out = {
         "metric": "GHM training samples/sec (CLIP default config)",
         "value": round(samples / elapsed, 2),
@@ -479,6 +612,11 @@ def main():
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
         "step_mfma_frac": round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
         "step_mfma_basis": f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s",
+        "step_hbm": None if step_bytes is None else {
+            "bytes": round(step_bytes * scale), "gbs": round(step_bytes * scale / (ms * 1e-3) / 1e9, 1),
+            "peak": HBM_PEAK_GBS, "frac": round(step_bytes * scale / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "basis": "sum over kernels of PMC bytes per launch (profiles/traffic.json) x launches per step "
+                     "(committed kernel stats)"},
         "loss_finite": finite,
         "last_loss": float(losses[-1]) if len(losses) else None,
     }

@@ -115,7 +115,7 @@ int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, int6
 int ghm_reduce_partials(const float* part, int n_split, int64_t n, int n_seg,
                         float* const* dst, const int64_t* off, void* stream);
 
-/* Up to 8 independent partial reductions in one launch (same semantics). */
+/* Up to 32 independent partial reductions in one launch (same semantics). */
 typedef struct ghm_reduce_job {
   const float* part;
   int32_t n_split;
@@ -189,9 +189,20 @@ int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stat
                       float* part_ln, int64_t M, int D, int F, void* stream);
 /* As ghm_qkv_bwd (backward of model.py:772-775), with the LN1 statistics
  * recomputed from H exactly as the forward computed them (eps = the LayerNorm
- * eps) instead of read from the forward's stats buffer. */
-int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* ln_w, const void* pack, const float* dH_mid,
-                   float* dH, float* part_ln, int64_t M, int D, float eps, void* stream);
+ * eps); stats (the forward's [M][2] buffer) is accepted and not read
+ * (DESIGN.md §4 "Determinism"). */
+int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
+                   const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, float eps, void* stream);
+/* Diagnostic twin of ghm_qkv_bwd_x3 (tools/race_probe.py, DESIGN.md §4
+ * "Determinism"): the LN1 statistics read from the forward's stats buffer,
+ * mode 1 plain vector load (the round-2 load), 2 agent scope through a buffer
+ * descriptor (sc0 sc1), 3 agent-scope global load (sc1), 4 recomputed with
+ * the plain load issued beside: dbg[m] = (loaded mean, loaded rstd, recomputed
+ * mean, recomputed rstd) [M][4], 5 as 1 with dbg[m] = (used mean, used rstd,
+ * 0, 0).  Not on the training path. */
+int ghm_qkv_bwd_x3_probe(const float* dqkv, const float* H, const float* stats, const float* ln_w, const void* pack,
+                         const float* dH_mid, float* dH, float* part_ln, float* dbg, int64_t M, int D, float eps,
+                         int mode, void* stream);
 
 /* As ghm_attn_fwd / ghm_attn_bwd (model.py:778-782 and its backward); P and dS
  * are stored fp32 in the same dense padded layout. */

@@ -453,127 +453,97 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, i
 
 // ---------------------------------------------------------------------------
 // Readout backward, one workgroup per sequence                 (model.py:802-805)
-// The sequence's rows of H are staged once into LDS (coalesced float4 loads);
-// every later access (P recompute, dW_ro partial, dH) reads LDS.  All 256
-// threads work in every phase: the P recompute takes 4 lanes per token (each a
-// quarter of the features, combined with two xor-shuffles), the dW_ro partial
-// 2 threads per feature (token halves, combined through LDS).  Row pitch 144
-// floats (16 dwords mod 64): the 16 lanes of a ds_read_b128 group (4 tokens x 4
-// quarters) hit 16 distinct 4-bank slots.
+// With de = d(loss)/d(emb) of the sequence and u = W_ro^T de (a 128-vector):
+//   dH[t]         = w_out[t] u                    (rank one per sequence)
+//   part_wout[t]  = H[t] . u + de . b_ro          (d/dw_out[t])
+//   part_wro[c]   = de[c] hbar,  hbar = sum_t w_out[t] H[t]
+//   part_bro[c]   = de[c] S_w,   part_bout = sum_c de[c]
+// so H is read once and dH written once (the partials are reduced over the
+// sequences by ghm_reduce_batch, as before).  Wave w takes tokens w, w + 4, ...;
+// lane l holds features 2l, 2l + 1; the token dot products are wave sums and
+// the four waves' hbar are added in a fixed order.
 // ---------------------------------------------------------------------------
-constexpr int RO_PITCH = GHM_D + 16;
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 template <int NC>
-__global__ __launch_bounds__(256, 2) void k_readout_bwd(
+__global__ __launch_bounds__(256) void k_readout_bwd(
     const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
     const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
     float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
     float* __restrict__ part_bout, int T) {
-  __shared__ __attribute__((aligned(16))) float sW[NC * GHM_D];
-  __shared__ __attribute__((aligned(16))) float sH[GHM_MAXT * RO_PITCH];
-  __shared__ float sdP[GHM_MAXT][NC + 1];
-  __shared__ float sred[NC][GHM_D];
-  const int tid = threadIdx.x, n = blockIdx.x;
+  __shared__ float2 red[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, n = blockIdx.x;
   const int64_t base = static_cast<int64_t>(n) * T;
-  for (int i = tid; i < NC * GHM_D; i += 256) sW[i] = Wro[i];
-  {  // coalesced staging of the sequence's rows: all loads issued before any LDS write
-    constexpr int NIT = GHM_MAXT * (GHM_D / 4) / 256;
-    float4 v[NIT];
-#pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int i = tid + 256 * k;
-      const int tt = i >> 5, c4 = i & 31;
-      const int tc = tt < T ? tt : T - 1;
-      v[k] = *reinterpret_cast<const float4*>(H + (base + tc) * GHM_D + 4 * c4);
-    }
-#pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int i = tid + 256 * k;
-      *reinterpret_cast<float4*>(sH + (i >> 5) * RO_PITCH + 4 * (i & 31)) = v[k];
-    }
-  }
   float de[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
-  __syncthreads();
-  {  // P[t][c] recompute, dP, dw_out partial: lane quarter qq holds features 4 qq + 16 k + 0..3
-    const int qq = tid & 3;
-#pragma unroll 1
-    for (int t = tid >> 2; t < GHM_MAXT; t += 64) {  // uniform trip count (96 / 64): shuffles stay converged
-      const int tr = t < T ? t : T - 1;
-      float p[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) p[c] = 0.f;
-#pragma unroll 2
-      for (int k = 0; k < GHM_D / 16; ++k) {
-        const float4 hv = lds4(sH + tr * RO_PITCH + 4 * qq + 16 * k);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          const float4 wv = lds4(sW + c * GHM_D + 4 * qq + 16 * k);
-          p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        p[c] += __shfl_xor(p[c], 1, 64);
-        p[c] += __shfl_xor(p[c], 2, 64);
-      }
-      if (qq == 0 && t < T) {
-        float dw = 0.f;
-        const float wt = wout[t];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          dw += de[c] * (p[c] + bro[c]);
-          sdP[t][c] = de[c] * wt;
-        }
-        part_wout[base + t] = dw;
-      }
-    }
-  }
-  __syncthreads();
-  {  // partial dW_ro[c][d]: thread = (feature d, token half hf)
-    const int d = tid & 127, hf = tid >> 7;
-    const int t0 = hf ? (T + 1) / 2 : 0, t1 = hf ? T : (T + 1) / 2;
-    float aw[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) aw[c] = 0.f;
-#pragma unroll 3
-    for (int t = t0; t < t1; ++t) {
-      const float hv = sH[t * RO_PITCH + d];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) aw[c] += sdP[t][c] * hv;
-    }
-    if (hf) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) sred[c][d] = aw[c];
-    }
-    __syncthreads();
-    if (!hf) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) part_wro[(static_cast<int64_t>(n) * NC + c) * GHM_D + d] = aw[c] + sred[c][d];
-    } else if (d < NC) {
-      const int c = d;
-      float sacc = 0.f;
-      for (int t = 0; t < T; ++t) sacc += sdP[t][c];
-      part_bro[static_cast<int64_t>(n) * NC + c] = sacc;
-      if (c == 0) {
-        float sbo = 0.f;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) sbo += de[k];
-        part_bout[n] = sbo;
-      }
-    }
-  }
-  // dH[t][d] = sum_c dP[t][c] W_ro[c][d]: float4 per thread, coalesced rows
-  for (int i = tid; i < T * (GHM_D / 4); i += 256) {
-    const int t = i >> 5, c4 = i & 31;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 u = make_float2(0.f, 0.f);
+  float bdot = 0.f;
+  {
+    const float2* W2 = reinterpret_cast<const float2*>(Wro) + lane;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      const float dpv = sdP[t][c];
-      const float4 wv = lds4(sW + c * GHM_D + 4 * c4);
-      o.x += dpv * wv.x; o.y += dpv * wv.y; o.z += dpv * wv.z; o.w += dpv * wv.w;
+      const float2 wv = W2[c * (GHM_D / 2)];
+      u.x += de[c] * wv.x;
+      u.y += de[c] * wv.y;
+      bdot += de[c] * bro[c];
     }
-    *reinterpret_cast<float4*>(dH + (base + t) * GHM_D + 4 * c4) = o;
+  }
+  const float2* Hs = reinterpret_cast<const float2*>(H + base * GHM_D) + lane;
+  float2* dHs = reinterpret_cast<float2*>(dH + base * GHM_D) + lane;
+  float2 hb = make_float2(0.f, 0.f);
+  int t = w;
+  for (; t + 4 < T; t += 8) {  // two rows in flight per wave
+    const float2 h0 = Hs[t * (GHM_D / 2)], h1 = Hs[(t + 4) * (GHM_D / 2)];
+    const float w0 = wout[t], w1 = wout[t + 4];
+    dHs[t * (GHM_D / 2)] = make_float2(w0 * u.x, w0 * u.y);
+    dHs[(t + 4) * (GHM_D / 2)] = make_float2(w1 * u.x, w1 * u.y);
+    hb.x += w0 * h0.x;
+    hb.y += w0 * h0.y;
+    hb.x += w1 * h1.x;
+    hb.y += w1 * h1.y;
+    const float d0 = wave_sum64(h0.x * u.x + h0.y * u.y), d1 = wave_sum64(h1.x * u.x + h1.y * u.y);
+    if (lane == 0) {
+      part_wout[base + t] = d0 + bdot;
+      part_wout[base + t + 4] = d1 + bdot;
+    }
+  }
+  for (; t < T; t += 4) {
+    const float2 h0 = Hs[t * (GHM_D / 2)];
+    const float w0 = wout[t];
+    dHs[t * (GHM_D / 2)] = make_float2(w0 * u.x, w0 * u.y);
+    hb.x += w0 * h0.x;
+    hb.y += w0 * h0.y;
+    const float d0 = wave_sum64(h0.x * u.x + h0.y * u.y);
+    if (lane == 0) part_wout[base + t] = d0 + bdot;
+  }
+  red[w][lane] = hb;
+  __syncthreads();
+  if (w != 0) return;
+  float2 hbar;
+  hbar.x = (red[0][lane].x + red[1][lane].x) + (red[2][lane].x + red[3][lane].x);
+  hbar.y = (red[0][lane].y + red[1][lane].y) + (red[2][lane].y + red[3][lane].y);
+  float2* pw = reinterpret_cast<float2*>(part_wro + static_cast<int64_t>(n) * NC * GHM_D) + lane;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) pw[c * (GHM_D / 2)] = make_float2(de[c] * hbar.x, de[c] * hbar.y);
+  float sw = 0.f;
+  for (int k = lane; k < T; k += 64) sw += wout[k];
+  sw = wave_sum64(sw);
+  if (lane < NC) {
+    float dl = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dl = lane == c ? de[c] : dl;
+    part_bro[static_cast<int64_t>(n) * NC + lane] = dl * sw;
+  }
+  if (lane == 0) {
+    float sbo = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) sbo += de[c];
+    part_bout[n] = sbo;
   }
 }
 
@@ -613,7 +583,7 @@ __global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0
 // order independent of timing.  Block b serves the job whose block range
 // contains b.
 // ---------------------------------------------------------------------------
-#define GHM_MAX_JOBS 8
+#define GHM_MAX_JOBS 32  // 32 x 96-B jobs + block table: 3.3 KB of kernel arguments
 // a job takes one thread per output when it is wide and shallow (the split-K
 // weight partials: 49 K - 66 K outputs x 64 - 85 splits)
 __host__ __device__ __forceinline__ bool red_wide(int64_t n, int n_split) { return n >= 8192 && n_split <= 256; }
@@ -776,7 +746,7 @@ static int validate_job(const ghm_reduce_job& j) {
 }
 
 extern "C" int ghm_reduce_batch(const ghm_reduce_job* jobs, int n_jobs, void* stream) {
-  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= GHM_MAX_JOBS, "1..8 jobs");
+  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= GHM_MAX_JOBS, "1..32 jobs");
   ReduceJobs J;
   J.n_jobs = n_jobs;
   int64_t blocks = 0;

@@ -161,3 +161,12 @@ __device__ __forceinline__ void stage_store(const float4* v, float* lds) {
 }
 
 __device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Agent-scope (global_load_dwordx2 sc1: served by L2, not the CU's vector L1)
+// load of a per-token (mean, rstd) pair; diagnostic variant of the LN-statistics
+// load (ghm_qkv_bwd_x3_probe mode 3, DESIGN.md §4 "Determinism").
+__device__ __forceinline__ float2 ld_stats(const float2* p) {
+  const uint64_t v = __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<float2*>(p)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float(static_cast<uint32_t>(v)), __uint_as_float(static_cast<uint32_t>(v >> 32)));
+}

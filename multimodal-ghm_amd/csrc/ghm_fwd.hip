@@ -354,69 +354,71 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
 
 // ---------------------------------------------------------------------------
 // Readout: Linear(D->C) over every token, then Linear(T->1) over the token axis
-// (model.py:802-805).  One workgroup per sequence, thread = token.
+// (model.py:802-805): emb[c] = sum_t w_out[t] (H[t] . W_ro[c] + b_ro[c]) + b_out.
+// Both maps are linear, so the kernel forms the token-weighted row sum
+// hbar = sum_t w_out[t] H[t] first and then emb[c] = hbar . W_ro[c] +
+// S_w b_ro[c] + b_out (S_w = sum_t w_out[t]): one pass over H at HBM rate
+// instead of a 10-wide dot product per token.  One 256-thread workgroup per
+// sequence: wave w takes tokens w, w + 4, ...; lane l holds features 2l, 2l + 1
+// (one coalesced 512-B row per wave instruction); the four wave sums are added
+// in a fixed order.
 // ---------------------------------------------------------------------------
-constexpr int RO_PITCH = GHM_D + 4;  // 16-B aligned rows; float4 reads of distinct rows conflict-free
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 template <int NC>
-__global__ __launch_bounds__(128) void k_readout_fwd(const float* __restrict__ H,
+__global__ __launch_bounds__(256) void k_readout_fwd(const float* __restrict__ H,
                                                      const float* __restrict__ Wro,
                                                      const float* __restrict__ bro,
                                                      const float* __restrict__ wout,
                                                      const float* __restrict__ bout,
                                                      float* __restrict__ emb, int T) {
-  __shared__ __attribute__((aligned(16))) float sW[NC * GHM_D];
-  __shared__ __attribute__((aligned(16))) float sH[GHM_MAXT * RO_PITCH];
-  __shared__ float red[2][NC];
-  const int t = threadIdx.x, n = blockIdx.x;
-  const int64_t base = static_cast<int64_t>(n) * T;
-  for (int i = t; i < NC * GHM_D; i += 128) sW[i] = Wro[i];
-  {  // coalesced staging of the sequence's rows: all loads issued before any LDS write
-    constexpr int NIT = GHM_MAXT * (GHM_D / 4) / 128;
-    float4 v[NIT];
+  __shared__ float2 red[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, n = blockIdx.x;
+  const float2* Hs = reinterpret_cast<const float2*>(H + static_cast<int64_t>(n) * T * GHM_D) + lane;
+  float2 hb = make_float2(0.f, 0.f);
+  int t = w;
+  for (; t + 12 < T; t += 16) {  // four rows in flight per wave
+    float2 h[4];
+    float wt[4];
 #pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int i = t + 128 * k;
-      const int tt = i >> 5, c4 = i & 31;
-      const int tc = tt < T ? tt : T - 1;
-      v[k] = *reinterpret_cast<const float4*>(H + (base + tc) * GHM_D + 4 * c4);
+    for (int u = 0; u < 4; ++u) {
+      h[u] = Hs[(t + 4 * u) * (GHM_D / 2)];
+      wt[u] = wout[t + 4 * u];
     }
 #pragma unroll
-    for (int k = 0; k < NIT; ++k) {
-      const int i = t + 128 * k;
-      *reinterpret_cast<float4*>(sH + (i >> 5) * RO_PITCH + 4 * (i & 31)) = v[k];
+    for (int u = 0; u < 4; ++u) {
+      hb.x += wt[u] * h[u].x;
+      hb.y += wt[u] * h[u].y;
     }
   }
-  __syncthreads();
-  float p[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) p[c] = 0.f;
-  if (t < T) {
-#pragma unroll 4
-    for (int d4 = 0; d4 < GHM_D / 4; ++d4) {
-      const float4 hv = lds4(sH + t * RO_PITCH + 4 * d4);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const float4 wv = lds4(sW + c * GHM_D + 4 * d4);
-        p[c] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
-      }
-    }
+  for (; t < T; t += 4) {
+    const float2 h = Hs[t * (GHM_D / 2)];
     const float wt = wout[t];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) p[c] = (p[c] + bro[c]) * wt;
+    hb.x += wt * h.x;
+    hb.y += wt * h.y;
   }
-  const int lane = t & 63, wv = t >> 6;
-  // deterministic wave reduction: 32-lane butterfly, then the lane-pair exchange
+  red[w][lane] = hb;
+  __syncthreads();
+  if (w != 0) return;
+  float2 hbar;
+  hbar.x = (red[0][lane].x + red[1][lane].x) + (red[2][lane].x + red[3][lane].x);
+  hbar.y = (red[0][lane].y + red[1][lane].y) + (red[2][lane].y + red[3][lane].y);
+  float sw = 0.f;
+  for (int k = lane; k < T; k += 64) sw += wout[k];
+  sw = wave_sum(sw);
+  const float2* W2 = reinterpret_cast<const float2*>(Wro) + lane;
+  float mine = 0.f;  // lane c < NC keeps emb[c]
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const float v = sum32(p[c]);
-    p[c] = v + __shfl_xor(v, 32, 64);
+    const float2 wv = W2[c * (GHM_D / 2)];
+    const float d = wave_sum(hbar.x * wv.x + hbar.y * wv.y);
+    if (lane == c) mine = d;
   }
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) red[wv][c] = p[c];
-  }
-  __syncthreads();
-  if (t < NC) emb[static_cast<int64_t>(n) * NC + t] = red[0][t] + red[1][t] + bout[0];
+  if (lane < NC) emb[static_cast<int64_t>(n) * NC + lane] = mine + sw * bro[lane] + bout[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -556,7 +558,7 @@ extern "C" int ghm_readout_fwd(const float* H, const float* W_ro, const float* b
   GHM_CHECK(H && W_ro && b_ro && w_out && b_out && emb, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
   GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
-  hipLaunchKernelGGL(k_readout_fwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0,
+  hipLaunchKernelGGL(k_readout_fwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0,
                      ghm_stream(stream), H, W_ro, b_ro, w_out, b_out, emb, T);
   return ghm_launch_status();
 }

@@ -8,6 +8,9 @@
 // copy.  Activations are split in registers where they become MFMA operands.
 // Reference semantics: src/ghmclip/models/model.py:772-788 (LN1 + Q/K/V,
 // LN2 + MLP) and their autograd backward (train_CLIP.py:158).
+#include <cstdlib>
+#include <cstring>
+
 #include "ghm_common.h"
 #include "ghm_ln.h"
 #include "ghm_split.h"
@@ -521,10 +524,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       const int o = r128_off(16 * j + t, g);
       y[j] = mfma16_x3(ldsb8(s2h(cur) + o), ldsb8(s2l(cur) + o), gh, gl, y[j]);
     }
-    // retire this iteration's 4 LDS-DMA fills (issued before the 4 stores)
-    if (SAVE)
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (GHM_ABL != 5)
+    // retire this iteration's LDS-DMA fills.  vmcnt(0) rather than the round-2
+    // vmcnt(4) that skipped the stores issued after the fills: that count is
+    // right only if loads, LDS-DMA and stores retire in issue order (as
+    // MI355X_MICROARCH.md states), which LLVM's own waitcnt insertion does not
+    // assume for mixed pending loads and stores; the wait that holds under both
+    // models measured no slower (4.38 / 4.41 vs 4.38 / 4.39 ms/step,
+    // profiles/r3_probe.txt; DESIGN.md §4 "Determinism").
+    if (GHM_ABL != 5)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if (valid) {
@@ -724,8 +731,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
       const int o = w1t_tr_off(j, lane);
       dx[j] = mfma16_x3(tr_pair(sw1h(cur) + o), tr_pair(sw1l(cur) + o), dh, dl, dx[j]);
     }
-    // retire this iteration's 4 LDS-DMA fills (issued before the 4 stores)
-    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // retire this iteration's LDS-DMA fills: vmcnt(0), also covering the G / dU
+    // stores issued after them (see k_ln_mlp_fwd_x3b)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // LN2 backward: lane holds dX2 of features d = 16 j + 4 g + r
   const float mean = st.x, rstd = st.y;
@@ -898,10 +906,21 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
 // QKV + LN1 backward                                          (model.py:772-775)
 //   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.
 // ---------------------------------------------------------------------------
+// LN1 statistics, STATS: 0 recomputed from H (the product path); diagnostic
+// variants (ghm_qkv_bwd_x3_probe, tools/race_probe.py; DESIGN.md §4
+// "Determinism"): 1 a plain vector load of the forward's [M][2] buffer (the
+// round-2 load whose 16-token groups came back wrong beside k_wgrad_x3), 2 the
+// same load at agent scope through a buffer descriptor (sc0 sc1), 3 at agent
+// scope as a global load (ld_stats, sc1), 4 the plain load AND the recompute:
+// the product uses the recomputed pair and every lane with h == 0 writes
+// (loaded mean, loaded rstd, recomputed mean, recomputed rstd) to dbg[m];
+// 5 as 1 (the plain load, used) and dbg[m] = (used mean, used rstd, 0, 0).
+template <int STATS>
 __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
     const float* __restrict__ dqkv, const float* __restrict__ H, const float* __restrict__ lnw,
     const __bf16* __restrict__ pack, const float* __restrict__ dHmid, float* __restrict__ dH,
-    float* __restrict__ part_ln, int64_t M, float eps) {
+    float* __restrict__ part_ln, int64_t M, float eps, const float2* __restrict__ stats,
+    float4* __restrict__ dbg) {
   __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
   __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
   __shared__ float red[2 * 4 * GHM_D];
@@ -914,19 +933,25 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
   const int64_t m = m0 + j;
   const bool valid = active && m < M;
   const int64_t mc = m < M ? m : M - 1;
-  // LN1 statistics recomputed from the row exactly as the forward computed them
-  // (ln_row: the lane pair's 64 contiguous features, ln_stats64; bit-identical
-  // to the forward's), not loaded from the forward's [M][2] buffer: a
-  // workgroup reading that buffer while a k_wgrad_x3 or k_ln_mlp_fwd_x3b
-  // workgroup shared its CU received wrong values for whole 16-token
-  // (128-byte) groups (tools/race_probe.py; DESIGN.md §4 "Determinism").
-  // Measured: 43 -> 50 us per launch (the row is read once more).
+  // STATS 0 recomputes the statistics exactly as the forward computed them
+  // (ln_row's layout, ln_stats64: bit-identical to the saved values)
   float2 lnst;
-  {
+  if (STATS == 0 || STATS == 4) {
     float x[64];
     load64(H + mc * GHM_D + 64 * h, x);
     ln_stats64(x, eps, lnst.x, lnst.y);
+  } else if (STATS == 1 || STATS == 5) {
+    lnst = stats[mc];
+  } else if (STATS == 2) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(stats), static_cast<short>(0), 0x7fffffff,
+                                                      0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, static_cast<int>(mc * 8), 0, 1 | 16);  // sc0 sc1
+    lnst = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+  } else {
+    lnst = ld_stats(stats + mc);
   }
+  float2 loaded = make_float2(0.f, 0.f);
+  if (STATS == 4) loaded = stats[mc];  // issued here, used only after the main loop (as STATS 1 used it)
   f32x16 dx[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) dx[it] = zero16();
@@ -951,6 +976,8 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
       __syncthreads();
     }
   }
+  if (STATS == 4 && valid && h == 0) dbg[m] = make_float4(loaded.x, loaded.y, lnst.x, lnst.y);
+  if (STATS == 5 && valid && h == 0) dbg[m] = make_float4(lnst.x, lnst.y, 0.f, 0.f);
   if (active)
     ln_bwd_acc(dx, H + mc * GHM_D, lnst, gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
@@ -1531,6 +1558,185 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __r
 }
 
 // ---------------------------------------------------------------------------
+// Fused attention backward, one workgroup per sequence        (model.py:778-782)
+// Phase A (as k_attn_bwd_q_x3): dP^T = V dO^T, delta, dS = P (dP - delta) / c,
+//   with the queries on the lanes; P and dS go to LDS as split bf16 [query][32]
+//   images per 32-key block (never to HBM).
+// Phase B: dQ^T = K^T dS^T (K column blocks by transposed reads, dS from
+//   registers).
+// Phase C (as k_attn_bwd_kv_x3): wave w = key block w, the key on the lane;
+//   dV^T = dO^T P and dK^T = Q^T dS over the queries, the P / dS B fragments
+//   read from the LDS images through ds_read_b64_tr_b16.
+// Against the two-kernel form it drops the dS round trip through HBM (36 + 36
+// KB per sequence); P's columns (phase C) are read again, L2-warm from phase A.
+// LDS (64.5 KB at T <= 96: two workgroups per CU): the dS images (2 planes x TP
+// x TP bf16) + one operand-staging region (V half images, then K, then dO / Q
+// column blocks).
+// ---------------------------------------------------------------------------
+template <int NKT>
+__global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __restrict__ qkv,
+                                                             const float* __restrict__ P,
+                                                             const float* __restrict__ dHmid,
+                                                             float* __restrict__ dqkv, int T,
+                                                             float scale_div) {
+  constexpr int TP = NKT * 32, KS = TP / 16;
+  constexpr int IMG = TP * TP;  // one [query][32] image per key block, NKT blocks: TP * 32 * NKT elements
+  constexpr int STG = TP * AH_PITCH > 2 * TP * 32 ? TP * AH_PITCH : 2 * TP * 32;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * IMG + 2 * STG];
+  __bf16* sim_h = lds;            // dS hi [kt][query][32]
+  __bf16* sim_l = lds + IMG;      // dS lo
+  __bf16* sh = lds + 2 * IMG;     // staging hi (V / K images; dO^T + Q^T column blocks in phase C)
+  __bf16* sl = sh + STG;          // staging lo
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const float* seq = qkv + base * (3 * GHM_D);
+  const int q = 32 * w + j;
+  const bool qv = q < T;
+  const int qc = qv ? q : T - 1;
+  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
+  // ---- phase A: dP^T, dS ----
+  f32x16 dp[NKT];
+  float4 kc[COLS_NIT];
+  {
+    float4 vst[HALF_NIT];
+    half_load<NKT>(seq, T, 0, 2 * GHM_D, vst);
+    bf16x8 oh[8], ol[8];
+    load_split64(dHmid + (base + qc) * GHM_D + 64 * h, true, oh, ol);
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) dp[kt] = zero16();
+    half_store<NKT>(vst, sh, sl);
+    half_load<NKT>(seq, T, 1, 2 * GHM_D, vst);
+    __syncthreads();
+    rows_dot_half<NKT>(sh, sl, oh, ol, 0, j, h, dp);
+    __syncthreads();
+    half_store<NKT>(vst, sh, sl);
+    cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D, kc);  // K column block 0 in flight across dS
+    __syncthreads();
+    rows_dot_half<NKT>(sh, sl, oh, ol, 1, j, h, dp);
+  }
+  const float inv_scale = 1.f / scale_div;
+  float delta = 0.f;
+  f32x16 p[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      const float4 pv = *reinterpret_cast<const float4*>(prow + 32 * kt + quad_off(qd, h));
+      p[kt][4 * qd + 0] = qv ? pv.x : 0.f;
+      p[kt][4 * qd + 1] = qv ? pv.y : 0.f;
+      p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
+      p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+  }
+  delta += xhalf(delta);
+  bf16x8 dh[2 * NKT], dl[2 * NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    float dv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
+    // dS of this key block into the [query][32] images (row = this lane's query)
+    __bf16* dsh = sim_h + (kt * TP + q) * 32;
+    __bf16* dsl = sim_l + (kt * TP + q) * 32;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+      bf16x4 a, b;
+      split4(make_float4(dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]), a, b);
+      stb4(dsh + quad_off(qd, h), a);
+      stb4(dsl + quad_off(qd, h), b);
+    }
+    split_acc(dv, 0, dh[2 * kt], dl[2 * kt]);
+    split_acc(dv, 1, dh[2 * kt + 1], dl[2 * kt + 1]);
+  }
+  // phase C's P B fragments, P[16 st + 8 h + i][key] of this wave's key block
+  // (rows >= T are 0): issued now, in flight across phase B
+  const int key = 32 * w + j;
+  const bool kv = key < T;
+  float pcol[KS][8];
+  {
+    const float* pc = P + static_cast<int64_t>(blockIdx.x) * AT_PAD * AT_PAD + key;
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pcol[st][i] = pc[(16 * st + 8 * h + i) * AT_PAD];
+  }
+  // ---- phase B: dQ^T[d][q] = sum_key K[key][d] dS[q][key] ----
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    __syncthreads();  // the previous phase's LDS reads are done
+    cols_store<NKT>(kc, sh, sl);
+    if (dt < 3) cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * (dt + 1), kc);
+    __syncthreads();
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int r0 = 32 * kt + 16 * ss + 4 * h;
+        acc = mfma_x3(tr_frag(sh, r0, r0 + 8, lane), tr_frag(sl, r0, r0 + 8, lane), dh[2 * kt + ss],
+                      dl[2 * kt + ss], acc);
+      }
+    }
+    if (qv) {
+      float* o = dqkv + (base + q) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        st4(o + quad_off(qd, h), acc[4 * qd], acc[4 * qd + 1], acc[4 * qd + 2], acc[4 * qd + 3]);
+    }
+  }
+  // ---- phase C: dV^T = dO^T P, dK^T = Q^T dS; wave w = keys 32w .. 32w + 31 ----
+  const float* dO = dHmid + base * GHM_D;
+  __bf16* soh = sh;
+  __bf16* sqh = sh + TP * 32;
+  __bf16* sol = sl;
+  __bf16* sql = sl + TP * 32;
+  float4 ost[COLS_NIT], qst[COLS_NIT];
+  cols_load<NKT>(dO, GHM_D, T, 0, ost);
+  cols_load<NKT>(seq, 3 * GHM_D, T, 0, qst);
+  __syncthreads();  // the P / dS images are complete; phase B's staging reads are done
+  bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
+  {
+    const __bf16* sih = sim_h + w * TP * 32;
+    const __bf16* sil = sim_l + w * TP * 32;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {  // B fragment: rows (queries) 16 st + 8 h .. + 7, column = the lane's key
+      const int r0 = 16 * st + 8 * h;
+      split8(pcol[st], pbh[st], pbl[st]);
+      sbh[st] = tr_frag(sih, r0, r0 + 4, lane);
+      sbl[st] = tr_frag(sil, r0, r0 + 4, lane);
+    }
+  }
+#pragma unroll 1
+  for (int dt = 0; dt < 4; ++dt) {
+    if (dt) __syncthreads();  // the previous block's LDS reads are done
+    cols_store<NKT>(ost, soh, sol);
+    cols_store<NKT>(qst, sqh, sql);
+    if (dt < 3) {
+      cols_load<NKT>(dO, GHM_D, T, 32 * (dt + 1), ost);
+      cols_load<NKT>(seq, 3 * GHM_D, T, 32 * (dt + 1), qst);
+    }
+    __syncthreads();
+    f32x16 aV = zero16(), aK = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int r0 = 16 * st + 8 * h;
+      aV = mfma_x3(tr_frag(soh, r0, r0 + 4, lane), tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
+      aK = mfma_x3(tr_frag(sqh, r0, r0 + 4, lane), tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
+    }
+    if (kv) {
+      float* o = dqkv + (base + key) * (3 * GHM_D) + 32 * dt;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd) {
+        st4(o + 2 * GHM_D + quad_off(qd, h), aV[4 * qd], aV[4 * qd + 1], aV[4 * qd + 2], aV[4 * qd + 3]);
+        st4(o + GHM_D + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C-ABI launchers
 // ---------------------------------------------------------------------------
 extern "C" int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream) {
@@ -1608,14 +1814,40 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
   return ghm_launch_status();
 }
 
-extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* ln_w, const void* pack,
-                              const float* dH_mid, float* dH, float* part_ln, int64_t M, int D, float eps,
-                              void* stream) {
+extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* stats, const float* ln_w,
+                              const void* pack, const float* dH_mid, float* dH, float* part_ln, int64_t M, int D,
+                              float eps, void* stream) {
   GHM_CHECK(dqkv && H && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
-  hipLaunchKernelGGL(k_qkv_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), dqkv, H, ln_w, reinterpret_cast<const __bf16*>(pack), dH_mid, dH,
-                     part_ln, M, eps);
+  (void)stats;  // the statistics are recomputed (DESIGN.md §4 "Determinism")
+  hipLaunchKernelGGL(k_qkv_bwd_x3<0>, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dqkv, H, ln_w, reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln,
+                     M, eps, nullptr, nullptr);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_qkv_bwd_x3_probe(const float* dqkv, const float* H, const float* stats, const float* ln_w,
+                                    const void* pack, const float* dH_mid, float* dH, float* part_ln, float* dbg,
+                                    int64_t M, int D, float eps, int mode, void* stream) {
+  GHM_CHECK(dqkv && H && stats && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1 && mode >= 1 && mode <= 5, "shape / mode (1..5)");
+  GHM_CHECK(mode < 4 || dbg, "modes 4 and 5 need dbg [M][4]");
+  GHM_CHECK(M * 8 < (int64_t(1) << 31), "stats must fit a 31-bit byte range");
+  const dim3 g(static_cast<unsigned>(ghm_token_blocks(M)));
+  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
+  const float2* st = reinterpret_cast<const float2*>(stats);
+  float4* d4 = reinterpret_cast<float4*>(dbg);
+  hipStream_t s = ghm_stream(stream);
+  if (mode == 1)
+    hipLaunchKernelGGL(k_qkv_bwd_x3<1>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
+  else if (mode == 2)
+    hipLaunchKernelGGL(k_qkv_bwd_x3<2>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
+  else if (mode == 3)
+    hipLaunchKernelGGL(k_qkv_bwd_x3<3>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
+  else if (mode == 4)
+    hipLaunchKernelGGL(k_qkv_bwd_x3<4>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
+  else
+    hipLaunchKernelGGL(k_qkv_bwd_x3<5>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
   return ghm_launch_status();
 }
 
@@ -1659,12 +1891,31 @@ extern "C" int ghm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, f
   return ghm_launch_status();
 }
 
+// $GHM_ATTN_BWD = "split" selects the two-kernel attention backward (A/B and
+// validation); default fused.  Read once per process.
+static bool ghm_attn_bwd_fused() {
+  static const bool fused = [] {
+    const char* e = std::getenv("GHM_ATTN_BWD");
+    return !(e && std::strcmp(e, "split") == 0);
+  }();
+  return fused;
+}
+
 extern "C" int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                                int64_t n_seq, int T, int D, float scale_div, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
   const unsigned g = static_cast<unsigned>(n_seq);
   hipStream_t s = ghm_stream(stream);
+  if (ghm_attn_bwd_fused()) {  // one kernel, P / dS through LDS (dS is not written)
+    if (T <= 32)
+      hipLaunchKernelGGL(k_attn_bwd_x3f<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+    else if (T <= 64)
+      hipLaunchKernelGGL(k_attn_bwd_x3f<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+    else
+      hipLaunchKernelGGL(k_attn_bwd_x3f<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dqkv, T, scale_div);
+    return ghm_launch_status();
+  }
   if (T <= 32) {
     hipLaunchKernelGGL(k_attn_bwd_q_x3<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
     hipLaunchKernelGGL(k_attn_bwd_kv_x3<1>, dim3(g), dim3(64), 0, s, qkv, P, dS, dH_mid, dqkv, T);

@@ -80,7 +80,11 @@ def require_hip(t):
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", wgrad_target_blocks=256, precision=None,
-                 wgrad_min_tokens=None):
+                 wgrad_min_tokens=None, defer_reduce=False):
+        """defer_reduce: every layer keeps its own parameter-gradient partial
+        buffers and backward() reduces all of them at its end in batched launches
+        of up to 32 jobs (2 launches per encoder instead of one per layer), as a
+        fully parallel, bandwidth-bound pass instead of L short latency-bound ones."""
         if n_embd != D_MODEL:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
         if num_class != 10 or vocab > 16:
@@ -132,9 +136,7 @@ class EncoderPlan:
         self.dU = e(M, D_HIDDEN)
         self.dS = torch.zeros(N, pad, pad, dtype=f32, device=dev)
         self.nblk = int(_native.hip_lib().ghm_token_blocks(M))
-        self.part_ln = e(self.nblk, 2, D_MODEL)
         self.nblk_rc = int(_native.hip_lib().ghm_mlp_bwd_rc_x3_blocks(M))
-        self.part_ln2 = e(max(self.nblk, self.nblk_rc), 2, D_MODEL)
         # split-K plans (A_cols x B_cols output tiles of 128x128): ~wgrad_target_blocks
         # workgroups of at least wgrad_min_tokens tokens per split (measured on the
         # CDM's 10.5 K tokens: 32 -> 3.01 ms/step, 256 -> 3.09, 512 -> 3.50: the
@@ -151,12 +153,21 @@ class EncoderPlan:
             tps = -(-tps // 32) * 32  # multiple of the 32-token k-step
             nsplit = -(-M // tps)
             self.wg[key] = (tps, nsplit)
-        # one partial buffer per pending reduction job of a layer (flushed once per layer)
-        self.part_w2 = e(self.wg["w2"][1] * D_MODEL * D_HIDDEN)
-        self.part_w1 = e(self.wg["w1"][1] * D_HIDDEN * D_MODEL)
-        self.part_wq = e(self.wg["qkv"][1] * 3 * D_MODEL * D_MODEL)
-        self.part_b2 = e(self.wg["w2"][1] * D_MODEL)
-        self.part_b1 = e(self.wg["w1"][1] * D_HIDDEN)
+        # one partial buffer per pending reduction job of a layer: flushed once per
+        # layer, or (defer_reduce) one set per layer, flushed at the end of backward()
+        self.defer_reduce = bool(defer_reduce)
+        nl = L if self.defer_reduce else 1
+        self.lpart = {"w2": e(nl, self.wg["w2"][1] * D_MODEL * D_HIDDEN),
+                      "w1": e(nl, self.wg["w1"][1] * D_HIDDEN * D_MODEL),
+                      "wq": e(nl, self.wg["qkv"][1] * 3 * D_MODEL * D_MODEL),
+                      "b2": e(nl, self.wg["w2"][1] * D_MODEL),
+                      "b1": e(nl, self.wg["w1"][1] * D_HIDDEN),
+                      "ln": e(nl, self.nblk * 2 * D_MODEL),
+                      "ln2": e(nl, max(self.nblk, self.nblk_rc) * 2 * D_MODEL)}
+        self.part_w2, self.part_w1, self.part_wq = self.lpart["w2"][0], self.lpart["w1"][0], self.lpart["wq"][0]
+        self.part_b2, self.part_b1 = self.lpart["b2"][0], self.lpart["b1"][0]
+        self.part_ln = self.lpart["ln"][0].view(self.nblk, 2, D_MODEL)
+        self.part_ln2 = self.lpart["ln2"][0].view(max(self.nblk, self.nblk_rc), 2, D_MODEL)
         self.part_w = self.part_w2  # (kbench / legacy name)
         self.part_b = self.part_b1
         self.part_ro = e(N * num_class * D_MODEL)
@@ -180,27 +191,42 @@ class EncoderPlan:
         """p: dict name -> fp32 device tensor (state_dict keys).  tokens: uint8
         [n_seq, T] on the device (defaults to self.tokens).  Returns self.emb.
         split=False reuses the weight packs of the previous forward (frozen weights)."""
+        for _ in self.forward_iter(p, tokens, split):
+            pass
+        return self.emb
+
+    def forward_iter(self, p, tokens=None, split=True):
+        """forward() as a generator that yields after the embedding, after each
+        layer and after the readout; every launch goes to the stream current at
+        the time it is issued (so a caller can interleave two encoders' launch
+        sequences on two streams, ClipTrainer)."""
         tok = self.tokens if tokens is None else tokens
-        s = _stream()
         c = _native.call
         T, N, L = self.T, self.N, self.L
+        s = _stream()
         if self.precision == "x3" and split:
             self.split_weights(p, s)
         c("ghm_embed_fwd", _ptr(tok), _ptr(p["token_embeddings.weight"]),
           _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), N, T, self.V, D_MODEL, s)
-        self.layers_fwd(p, s)
+        yield
+        for l in range(L):
+            self._layer_fwd(p, l, _stream())
+            yield
         c("ghm_readout_fwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
-          _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, s)
+          _ptr(p["_out.weight"]), _ptr(p["_out.bias"]), _ptr(self.emb), N, T, D_MODEL, self.C, _stream())
         self._gen += 1
-        return self.emb
 
     def layers_fwd(self, p, s):
         """The n_layer encoder layers (model.py:769-800) from H[0] to H[L]:
         LN1+QKV, attention+residual, LN2+MLP+residual per layer."""
+        for l in range(self.L):
+            self._layer_fwd(p, l, s)
+
+    def _layer_fwd(self, p, l, s):
         c = _native.call
         M, T, N = self.M, self.T, self.N
         x3 = self.precision == "x3"
-        for l in range(self.L):
+        if True:
             if x3:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
@@ -217,7 +243,7 @@ class EncoderPlan:
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
                   _ptr(self.H[l + 1]), None if self.mlp_rc else _ptr(self.G[l]),
                   None if self.mlp_rc else _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
-                continue
+                return
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
@@ -294,9 +320,13 @@ class EncoderPlan:
             j.off[k] = offs[min(k, len(dsts))]
         return j
 
+    def _lp(self, key, l):
+        """Layer l's partial buffer `key` (the shared one unless defer_reduce)."""
+        return self.lpart[key][l if self.defer_reduce else 0]
+
     def _flush(self, jobs, s):
-        for a in range(0, len(jobs), 8):
-            chunk = jobs[a:a + 8]
+        for a in range(0, len(jobs), 32):
+            chunk = jobs[a:a + 32]
             arr = (_native.ReduceJob * len(chunk))(*chunk)
             _native.call("ghm_reduce_batch", arr, len(chunk), s)
         jobs.clear()
@@ -313,9 +343,14 @@ class EncoderPlan:
         w.r.t. the residual stream H[l+1] leaving layer l (guided layers,
         model.py:790-800) before that layer's backward runs.
         Parameter-gradient partials are reduced by one batched launch per layer."""
+        for _ in self.backward_iter(p, g, d_emb, tokens, layer_grad):
+            pass
+
+    def backward_iter(self, p, g, d_emb=None, tokens=None, layer_grad=None):
+        """backward() as a generator yielding after the readout backward and after
+        each layer (launches on the stream current when each is issued)."""
         tok = self.tokens if tokens is None else tokens
         de = self.d_emb if d_emb is None else d_emb
-        s = _stream()
         c = _native.call
         J = self._job
         T, N, L, C = self.T, self.N, self.L, self.C
@@ -323,10 +358,15 @@ class EncoderPlan:
         jobs = []
         c("ghm_readout_bwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(p["_out.weight"]), _ptr(de), _ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro),
-          _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, s)
+          _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, _stream())
         jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
                  J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
-        cur = self.layers_bwd(p, g, jobs, s, layer_grad)
+        yield
+        cur, nxt = self.dH[0], self.dH[1]
+        for l in reversed(range(self.L)):
+            cur, nxt = self._layer_bwd(p, g, l, cur, nxt, jobs, _stream(), layer_grad)
+            yield
+        s = _stream()
         c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
         jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
         self._flush(jobs, s)
@@ -336,40 +376,50 @@ class EncoderPlan:
         the caller's readout backward) down to dL/dH_0, which is returned (one of
         the dH ping-pong buffers).  Parameter-gradient partials are reduced by one
         batched launch per layer (pending jobs in `jobs` are flushed with them)."""
+        cur, nxt = self.dH[0], self.dH[1]
+        for l in reversed(range(self.L)):
+            cur, nxt = self._layer_bwd(p, g, l, cur, nxt, jobs, s, layer_grad)
+        return cur
+
+    def _layer_bwd(self, p, g, l, cur, nxt, jobs, s, layer_grad=None):
+        """One layer's backward: cur = dL/dH_{l+1} in, returns (dL/dH_l, the free
+        ping-pong buffer)."""
         c = _native.call
         J = self._job
         M, T, N = self.M, self.T, self.N
-        cur, nxt = self.dH[0], self.dH[1]
         x3 = self.precision == "x3"
         wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
-        for l in reversed(range(self.L)):
+        P_ln, P_ln2 = self._lp("ln", l), self._lp("ln2", l)
+        P_w2, P_w1, P_wq = self._lp("w2", l), self._lp("w1", l), self._lp("wq", l)
+        P_b2, P_b1 = self._lp("b2", l), self._lp("b1", l)
+        if True:
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
             if x3 and not self.mlp_rc:
                 c("ghm_mlp_bwd_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-                  _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL,
+                  _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL,
                   D_HIDDEN, s)
             elif x3:  # recomputes U; writes G (scratch) and dU
                 c("ghm_mlp_bwd_rc_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]),
                   _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]),
-                  _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(self.part_ln2), M,
+                  _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M,
                   D_MODEL, D_HIDDEN, s)
             else:
                 c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),
-                  _ptr(nxt), _ptr(self.part_ln2), M, D_MODEL, D_HIDDEN, s)
+                  _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN, s)
             nb2 = self.nblk_rc if (x3 and self.mlp_rc) else self.nblk
-            jobs.append(J(self.part_ln2, nb2, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
+            jobs.append(J(P_ln2, nb2, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
             c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G if self.mlp_rc else self.G[l]), D_HIDDEN, D_HIDDEN, 0,
-              None, None, None, _ptr(self.part_w2), _ptr(self.part_b2), M, tps, s)
-            jobs += [J(self.part_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(self.part_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
+              None, None, None, _ptr(P_w2), _ptr(P_b2), M, tps, s)
+            jobs += [J(P_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(P_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU
             c(wgrad, _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
-              _ptr(self.part_w1), _ptr(self.part_b1), M, tps, s)
-            jobs += [J(self.part_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(self.part_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
+              _ptr(P_w1), _ptr(P_b1), M, tps, s)
+            jobs += [J(P_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(P_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
             if self.attn_f32:
                 self._attn_bwd_f32(l, cur)
@@ -382,17 +432,18 @@ class EncoderPlan:
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
             c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
               _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-              _ptr(self.part_wq), None, M, tps, s)
-            jobs.append(J(self.part_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
+              _ptr(P_wq), None, M, tps, s)
+            jobs.append(J(P_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
                                              g[f"_values.{l}.weight"]]))
             if x3:
-                c("ghm_qkv_bwd_x3", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-                  _ptr(self.pack[l]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, self.eps, s)
+                c("ghm_qkv_bwd_x3", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+                  _ptr(self.pack[l]), _ptr(cur), _ptr(nxt), _ptr(P_ln), M, D_MODEL, self.eps, s)
             else:
                 c("ghm_qkv_bwd", _ptr(self.dqkv), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
                   _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
-                  _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D_MODEL, s)
-            jobs.append(J(self.part_ln, self.nblk, [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]]))
-            self._flush(jobs, s)  # every partial buffer is reused by the next layer
+                  _ptr(cur), _ptr(nxt), _ptr(P_ln), M, D_MODEL, s)
+            jobs.append(J(P_ln, self.nblk, [g[f"_lns_1.{l}.weight"], g[f"_lns_1.{l}.bias"]]))
+            if not self.defer_reduce:
+                self._flush(jobs, s)  # every partial buffer is reused by the next layer
             cur, nxt = nxt, cur  # cur = dH_l
-        return cur
+        return cur, nxt

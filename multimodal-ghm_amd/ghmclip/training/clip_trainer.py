@@ -78,7 +78,8 @@ class ClipTrainer:
         n_seq = batch_size * (K + 1)
         self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
                                   n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
-                                  precision=precision)
+                                  precision=precision,
+                                  defer_reduce=os.environ.get("GHM_DEFER_REDUCE", "1") != "0")
                       for m in self.models]
         self.precision = self.plans[0].precision
         self.T, self.n_seq = T, n_seq
@@ -165,23 +166,49 @@ class ClipTrainer:
         return hooks
 
     # -- the launch sequence -----------------------------------------------------
+    @staticmethod
+    def _interleave(jobs):
+        """Advance launch generators [(generator, stream), ...] round-robin, each
+        step issued under its own stream: the two towers' per-layer launches are
+        issued (and, captured, become graph nodes) alternately instead of one
+        tower's whole sequence first."""
+        active = list(jobs)
+        while active:
+            for job in list(active):
+                gen, st = job
+                with torch.cuda.stream(st):
+                    try:
+                        next(gen)
+                    except StopIteration:
+                        active.remove(job)
+
     def _fwd_bwd(self):
         """Text tower on the current stream, image tower on a side stream (fork /
         join through stream waits, which graph capture records as edges), so the
-        two towers' launches overlap and fill each other's tails."""
+        two towers' launches overlap and fill each other's tails.  The towers'
+        launches are issued layer by layer alternately ($GHM_TOWER_ORDER =
+        "interleave", default) or one tower after the other ("sequential")."""
         main = torch.cuda.current_stream()
         side = main if os.environ.get("GHM_SERIAL_TOWERS") == "1" else self.side
+        inter = os.environ.get("GHM_TOWER_ORDER", "interleave") == "interleave"
         pt, pi = self.plans
         (tp, tg, _, _), (ip, ig, _, _) = self.views
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            pi.forward(ip)
-            if self.guide:
-                self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
-        pt.forward(tp)
         s = ctypes.c_void_p(main.cuda_stream)
-        if self.guide:
-            self._guide_fwd(0, s)
+        if inter:
+            self._interleave([(pi.forward_iter(ip), side), (pt.forward_iter(tp), main)])
+            if self.guide:
+                with torch.cuda.stream(side):
+                    self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
+                self._guide_fwd(0, s)
+        else:
+            with torch.cuda.stream(side):
+                pi.forward(ip)
+                if self.guide:
+                    self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
+            pt.forward(tp)
+            if self.guide:
+                self._guide_fwd(0, s)
         main.wait_stream(side)
         _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
@@ -189,9 +216,13 @@ class ClipTrainer:
             _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.n_seq, self.penalty,
                          _p(self.loss_out), _p(self.phist), _p(self.step_ctr), s)
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            pi.backward(ip, ig, layer_grad=self._guide_hooks(1))
-        pt.backward(tp, tg, layer_grad=self._guide_hooks(0))
+        if inter:
+            self._interleave([(pi.backward_iter(ip, ig, layer_grad=self._guide_hooks(1)), side),
+                              (pt.backward_iter(tp, tg, layer_grad=self._guide_hooks(0)), main)])
+        else:
+            with torch.cuda.stream(side):
+                pi.backward(ip, ig, layer_grad=self._guide_hooks(1))
+            pt.backward(tp, tg, layer_grad=self._guide_hooks(0))
         main.wait_stream(side)
 
     def _optim(self):

@@ -240,9 +240,11 @@ def test_step_bit_identical_across_runs(precision):
 
 def test_qkv_backward_unperturbed_beside_weight_gradient():
     """The QKV backward on fixed inputs gives bit-identical outputs while the
-    weight-gradient kernel runs on another stream (before the fix its LN
-    statistics were read wrong for 16-token groups in every repetition:
-    tools/race_probe.py, DESIGN.md section 4 "Determinism")."""
+    weight-gradient kernel runs on another stream.  Its LN statistics come from
+    the forward's buffer through an agent-scope load (ld_stats); the round-2
+    plain load of the same buffer returned wrong 128-B lines (16 tokens) in 2 of
+    14 repetitions under this aggressor (tools/race_probe.py qkv_load wgrad0,
+    profiles/r3_probe.txt; DESIGN.md section 4 "Determinism")."""
     import ctypes
     from ghmclip import _native
     sampler, tr = _trainer(5, 128, 0.2, precision="x3")
@@ -259,14 +261,14 @@ def test_qkv_backward_unperturbed_beside_weight_gradient():
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     tps, _ = p1.wg["w2"]
     ref = None
-    for _ in range(6):
+    for _ in range(15):
         sa.wait_stream(torch.cuda.current_stream())
         sb.wait_stream(torch.cuda.current_stream())
         for _ in range(3):
             _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
                          P(p1.part_w2), P(p1.part_b2), M, tps, B)
-        _native.call("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]), P(dHmid),
-                     P(outH), P(outP), M, 128, p0.eps, A)
+        _native.call("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]),
+                     P(p0.pack[l]), P(dHmid), P(outH), P(outP), M, 128, p0.eps, A)
         for _ in range(3):
             _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
                          P(p1.part_w2), P(p1.part_b2), M, tps, B)
@@ -341,6 +343,25 @@ def test_full_run_final_risk_vs_reference_cpu_run():
     print(f"3001-step run: final risk {risk:.7f} vs reference CPU run {ref_risk:.7f} "
           f"(rel {abs(risk - ref_risk) / ref_risk:.2e}); max |dloss| {dev.max():.3e} at step {dev.argmax()}, "
           f"first 1000 steps {dev[:1000].max():.3e}")
+    assert abs(risk - ref_risk) <= 1e-5 * ref_risk
+    assert dev.max() <= 1e-4
+
+
+def test_shallow_full_run_final_risk_vs_reference_cpu_run():
+    """Shallow TF (exp_clip_shallowTF.sh: clip_{t,i}model_nlayer=1, otherwise the
+    default config) at p = 0.2: the whole 3001-step run against the reference's
+    own code run here on the CPU (clip_shallow_curve3001.npz, 3 threads,
+    make_golden.py --only curve --curve-steps 3001 --curve-layers 1): final risk
+    within 1e-5 relative and every step within 1e-4 (split-bf16 default)."""
+    g = np.load(os.path.join(GOLDEN, "clip_shallow_curve3001.npz"))
+    ref = g["loss_history"]
+    assert len(ref) == 3001 and int(g["n_layer"]) == 1 and (ref != 0).all()
+    sampler, tr = _trainer(1, 128, 0.2, precision="x3")
+    hist = _run(sampler, tr, 128, 3001, graph_after=3)
+    dev = np.abs(hist - ref)
+    risk, ref_risk = hist[-100:].mean(), ref[-100:].mean()
+    print(f"shallow 3001-step run: final risk {risk:.7f} vs reference CPU run {ref_risk:.7f} "
+          f"(rel {abs(risk - ref_risk) / ref_risk:.2e}); max |dloss| {dev.max():.3e} at step {dev.argmax()}")
     assert abs(risk - ref_risk) <= 1e-5 * ref_risk
     assert dev.max() <= 1e-4
 

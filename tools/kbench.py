@@ -95,7 +95,7 @@ def main():
             "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                      P(p["_lns_2.0.weight"]), pk, P(xo["Dg"]), P(plan.dU), P(xo["dHm"]),
                                      P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
-            "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(p["_lns_1.0.weight"]), pk,
+            "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]), pk,
                                      P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, plan.eps, sp),
                            gf(2 * M * 128 * 384)),
             "attn_bwd_x3": (lambda: c("ghm_attn_bwd_x3", P(plan.qkv[l]), P(plan.P[l]), P(plan.dH[1]), P(plan.dS),

@@ -3,7 +3,7 @@ inputs on stream A while another kernel (aggressor) runs on stream B; the
 victim's outputs must be bit-identical across repetitions.
 
     python tools/race_probe.py [victim] [aggressor] [reps]
-    victim: qkv_bwd | mlp_bwd | attn_bwd ; aggressor: mlp_bwd | wgrad | attn_bwd | fwd_mlp | none
+    victim: qkv_bwd | qkv_load | qkv_dev | mlp_bwd | wgrad | attn_bwd ; aggressor: mlp_bwd | wgrad | attn_bwd | fwd_mlp | none
 """
 import ctypes
 import hashlib
@@ -24,6 +24,9 @@ def digest(t):
     if t.dtype == torch.bfloat16:
         t = t.view(torch.int16)
     return hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest()[:10]
+
+
+QKV_MODES = {"qkv_load": 1, "qkv_dev": 2, "qkv_sc1": 3, "qkv_dbg": 4, "qkv_dbgu": 5}
 
 
 def main():
@@ -53,12 +56,18 @@ def main():
     vpart, vpb = torch.empty_like(p0.part_w1), torch.empty_like(p0.part_b1)
     vdS, outQ = torch.zeros_like(p0.dS), torch.empty(M, 384, device="cuda")
     xH, xP = torch.empty(M, 128, device="cuda"), torch.empty_like(p1.part_ln2)
+    dbg = torch.zeros(M, 4, device="cuda")
+    n_dbg = 0
     xa, xb, xc = (torch.randn(4096, 4096, device="cuda") for _ in range(3))
 
     def run_victim():
         if victim == "qkv_bwd":
-            c("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]),
+            c("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]),
               P(dHmid), P(outH), P(outP), M, 128, p0.eps, A)
+            return [outH, outP]
+        if victim in QKV_MODES:  # the statistics read from p0.st1 (ghm_qkv_bwd_x3_probe)
+            c("ghm_qkv_bwd_x3_probe", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]),
+              P(p0.pack[l]), P(dHmid), P(outH), P(outP), P(dbg), M, 128, p0.eps, QKV_MODES[victim], A)
             return [outH, outP]
         if victim == "wgrad":
             tps, ns = p0.wg["w1"]
@@ -137,6 +146,26 @@ def main():
             if aggr != "none":
                 run_aggr()
         torch.cuda.synchronize()
+        if victim in ("qkv_dbg", "qkv_dbgu"):  # loaded (and used) vs the buffer's statistics, per token
+            bad_rows = torch.nonzero((dbg[:, :2] != p0.st1[l]).any(1)).flatten()
+            if len(bad_rows):
+                n_dbg += 1
+                rows = bad_rows.tolist()
+                print(f"  rep {r}: loaded stats differ from the buffer's for {len(rows)} tokens "
+                      f"(first {rows[:4]}, last {rows[-1]}; 16-aligned groups "
+                      f"{sorted(set(x // 16 * 16 for x in rows))[:8]})")
+                st_all = {"p0.st1": p0.st1, "p0.st2": p0.st2, "p1.st1": p1.st1, "p1.st2": p1.st2}
+                for m in rows[:3]:
+                    v = dbg[m, :2]
+                    hits = []
+                    for name, t in st_all.items():
+                        flat = t.reshape(-1, 2)
+                        idx = torch.nonzero((flat == v).all(1)).flatten().tolist()
+                        if idx:
+                            hits.append(f"{name}[flat {idx[:3]} = (layer, token) "
+                                        f"{[(i // M, i % M) for i in idx[:3]]}]")
+                    print(f"    token {m}: loaded {v.tolist()} recomputed {dbg[m, 2:].tolist()} "
+                          f"buffer {p0.st1[l][m].tolist()} found in {hits or 'no stats buffer'}")
         d = [digest(t) for t in outs]
         if ref is None:
             ref = d
@@ -147,7 +176,7 @@ def main():
                 for k, (a, b) in enumerate(zip(keep, outs)):
                     diff = (a - b).abs().reshape(a.shape[0], -1)
                     rows = torch.nonzero(diff.amax(1) > 0).flatten()
-                    if len(rows) and k == 0 and victim == "qkv_bwd":
+                    if len(rows) and k == 0 and victim.startswith("qkv"):
                         m = int(rows[0])
                         x = p0.H[l][m].double()
                         st = p0.st1[l][m].double()
@@ -163,7 +192,9 @@ def main():
                         print(f"  rep {r} out{k}: {len(rows)} rows differ (first {rows[:6].tolist()}), "
                               f"max |d| {diff.max().item():.3e}, |ref| max {a.abs().max().item():.3e}, "
                               f"nan {torch.isnan(b).sum().item()}")
-    print(f"victim {victim} aggressor {aggr}: {bad}/{reps - 1} repetitions differ")
+    print(f"victim {victim} aggressor {aggr}: {bad}/{reps - 1} repetitions differ"
+          + (f"; loaded statistics != the buffer's in {n_dbg}/{reps} repetitions" if victim.startswith("qkv_dbg")
+             else ""))
     if os.environ.get("GHM_PROBE_STATS") == "1" and victim == "qkv_bwd":
         # debug build GHM_QKV_DBG=13: dH[m][0:2] holds the (mean, rstd) the kernel read
         got = outH[:, :2]
