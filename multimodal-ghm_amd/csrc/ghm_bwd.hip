@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd(
     __syncthreads();
   }
   if (active)
-    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, Hmid + mc * GHM_D, ld_stats_sys(stats, mc), gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd(
     }
   }
   if (active)
-    ln_bwd_acc(dx, H + mc * GHM_D, stats[mc], gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, H + mc * GHM_D, ld_stats_sys(stats, mc), gam, dHmid + mc * GHM_D, dH + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const float* __restrict__ A, i
       va[k] = *reinterpret_cast<const float4*>(A + mcl * lda + a_blk + 4 * c4);
       vb[k] = *reinterpret_cast<const float4*>(Bs + mcl * ldb + b_blk + 4 * c4);
       if (!ok) va[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (MODE == 2) vs[k] = stats[mcl];
+      if (MODE == 2) vs[k] = ld_stats_sys(stats, mcl);
     }
   };
   auto store = [&](int buf) {
@@ -665,6 +665,7 @@ extern "C" int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float*
                            float* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
                            void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && W1 && W2 && U && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   hipLaunchKernelGGL(k_mlp_bwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w, W1,
@@ -695,6 +696,7 @@ extern "C" int ghm_qkv_bwd(const float* dqkv, const float* H, const float* stats
                            const float* Wq, const float* Wk, const float* Wv, const float* dH_mid,
                            float* dH, float* part_ln, int64_t M, int D, void* stream) {
   GHM_CHECK(dqkv && H && stats && ln_w && Wq && Wk && Wv && dH_mid && dH && part_ln, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
   hipLaunchKernelGGL(k_qkv_bwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), dqkv, H, reinterpret_cast<const float2*>(stats), ln_w, Wq, Wk, Wv,
@@ -706,6 +708,7 @@ extern "C" int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, in
                          int b_mode, const float* stats, const float* ln_w, const float* ln_b,
                          float* part, float* bias_part, int64_t M, int tok_per_split, void* stream) {
   GHM_CHECK(A && B && part, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(A_cols > 0 && B_cols > 0 && A_cols % 128 == 0 && B_cols % 128 == 0, "A_cols/B_cols % 128");
   GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
   GHM_CHECK(tok_per_split > 0 && tok_per_split % 32 == 0, "tok_per_split must be a positive multiple of 32");

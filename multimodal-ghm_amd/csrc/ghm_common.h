@@ -162,9 +162,21 @@ __device__ __forceinline__ void stage_store(const float4* v, float* lds) {
 
 __device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// Agent-scope (global_load_dwordx2 sc1: served by L2, not the CU's vector L1)
-// load of a per-token (mean, rstd) pair; diagnostic variant of the LN-statistics
-// load (ghm_qkv_bwd_x3_probe mode 3, DESIGN.md §4 "Determinism").
+// Per-token LayerNorm statistics (mean, rstd) written by a forward kernel and
+// read by a backward one.  ld_stats_sys: a system-scope buffer load (sc0 sc1),
+// served past the XCD's L2; ld_stats: agent scope (sc1, served by L2).  The
+// round-2 plain load of this buffer in k_qkv_bwd_x3 returned wrong 128-B lines
+// beside a k_wgrad_x3 workgroup; on the same probe the agent-scope load was
+// wrong in 32 of 39 repetitions and the system-scope load in none of 3 x 39
+// (tools/race_probe.py; DESIGN.md §4 "Determinism").  The backward kernels
+// read the statistics with ld_stats_sys (8 bytes per token: free), and
+// k_qkv_bwd_x3 recomputes them.  Byte offsets must fit 31 bits (host-checked).
+__device__ __forceinline__ float2 ld_stats_sys(const float2* base, int64_t idx) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(base), static_cast<short>(0), 0x7fffffff,
+                                                    0x00020000);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, static_cast<int>(idx * 8), 0, 1 | 16);  // sc0 sc1
+  return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
 __device__ __forceinline__ float2 ld_stats(const float2* p) {
   const uint64_t v = __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<float2*>(p)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_ln_rows_bwd(const float* __restrict__ d
 #pragma unroll
     for (int b = 0; b < LN_BATCH; ++b) {
       const int64_t row = row0 + b < M ? row0 + b : M - 1;  // clamped (unused past M)
-      stv[b] = stats[row];
+      stv[b] = ld_stats_sys(stats, row);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int c = lane + 64 * r;
@@ -565,6 +565,7 @@ extern "C" int64_t ghm_ln_rows_blocks(int64_t M) { return (M + 4 * LN_ROWS_PER_W
 extern "C" int ghm_ln_rows_bwd(const float* dY, const float* X, const float* stats, const float* w, const float* dres,
                                float* dX, float* part, int64_t M, int D, void* stream) {
   GHM_CHECK(dY && X && stats && w && dres && dX && part, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(M >= 1 && (D == 128 || D == 256 || D == 512), "shape (D in {128, 256, 512})");
   const dim3 g(static_cast<unsigned>(ghm_ln_rows_blocks(M)));
   const float2* st = reinterpret_cast<const float2*>(stats);

@@ -649,7 +649,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
   // B operands: LN2(Hmid) and dY of the token, lane holds features 32 s2 + 8 g + i
   bf16x8 xh[4], xl[4], yh[4], yl[4];
-  const float2 st = stats[mc];
+  const float2 st = ld_stats_sys(stats, mc);
   {
     const float* row = Hmid + mc * GHM_D;
     const float* dyr = dHout + mc * GHM_D;
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
   __syncthreads();
   if (active)
-    ln_bwd_acc(dx, Hmid + mc * GHM_D, stats[mc], gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
+    ln_bwd_acc(dx, Hmid + mc * GHM_D, ld_stats_sys(stats, mc), gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
@@ -943,10 +943,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
   } else if (STATS == 1 || STATS == 5) {
     lnst = stats[mc];
   } else if (STATS == 2) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(stats), static_cast<short>(0), 0x7fffffff,
-                                                      0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, static_cast<int>(mc * 8), 0, 1 | 16);  // sc0 sc1
-    lnst = make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+    lnst = ld_stats_sys(stats, mc);
   } else {
     lnst = ld_stats(stats + mc);
   }
@@ -1082,7 +1079,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
     const int nv = __builtin_amdgcn_readfirstlane(S.nvalid > 0 ? S.nvalid : 1);
     if (MODE == 2) {  // one vector load: lane l holds row (l & 15)'s (mean, rstd)
       const int li = lane & 15;
-      S.st = stats[r0 + (li < nv ? li : nv - 1)];
+      S.st = ld_stats_sys(stats, r0 + (li < nv ? li : nv - 1));
     }
     const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * lda * 4));
     const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * ldb * 4));
@@ -1779,6 +1776,7 @@ extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const flo
                               const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln,
                               int64_t M, int D, int F, void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && pack && Dg && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   hipLaunchKernelGGL(k_mlp_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w,
@@ -1800,6 +1798,7 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
                                  const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
                                  float* dH_mid, float* part_ln, int64_t M, int D, int F, void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln, "null pointer");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
   const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
