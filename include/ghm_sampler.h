@@ -30,6 +30,15 @@ typedef struct ghm_sampler ghm_sampler;
  * (batch rows = B*(K+1)).  Returns NULL on bad arguments. */
 ghm_sampler* ghm_sampler_create(const double* t_trans, const double* i_trans, int n_layer,
                                 int n_child, int V, int K);
+/* General form: one [V][V] matrix per edge of each tree, in the reference's
+ * order transition[layer][parent * n_child + child] (layer 0 first; n_child +
+ * n_child^2 + ... + n_child^n_layer edges), so non-translation-invariant
+ * GenTransition trees (data_random_GHM.py:80-85) and text / image trees of
+ * different shapes (ClipSampler n_layers / n_childs, :645-658) draw
+ * bit-exactly.  Leaves: text rows [n_child_t^n_layer_t], image rows
+ * [n_child_i^n_layer_i]. */
+ghm_sampler* ghm_sampler_create_edges(const double* t_edges, int t_layer, int t_child, const double* i_edges,
+                                      int i_layer, int i_child, int V, int K);
 void ghm_sampler_destroy(ghm_sampler* s);
 
 /* Seed like numpy.random.seed(int) (init_genrand). */

@@ -195,10 +195,20 @@ static int pool_threads() {
   return n < 1 ? 1 : (n > 64 ? 64 : n);
 }
 
-struct ghm_sampler {
-  int n_layer, n_child, V, K, T, n_runs;  // n_runs = tree nodes below the root
-  // cdf[tree][layer][child][row][col], cumulative sums in the reference's order
+// One tree shape: n_layer levels of n_child children; its n_runs non-root
+// nodes in BFS order are also its edges (node k >= 1 hangs on edge k - 1, the
+// reference's transition[layer][parent * n_child + child] in order), and
+// cdf[edge][row][col] holds each edge's cumulative rows (translation-invariant
+// trees repeat the per-child-slot templates; non-invariant trees, :80-85, give
+// every edge its own matrix).
+struct Tree {
+  int n_layer = 0, n_child = 0, T = 0, n_runs = 0;
   std::vector<double> cdf;
+};
+
+struct ghm_sampler {
+  int V, K;
+  Tree tree[2];  // text, image
   MT19937 mt;
   int has_gauss = 0;  // numpy legacy Gaussian cache (RandomState state[3], state[4])
   double gauss = 0.0;
@@ -227,36 +237,75 @@ static double legacy_gauss(ghm_sampler* s) {
   return f * x2;
 }
 
-static void build_cdf(const double* trans, int n_layer, int n_child, int V, double* out) {
-  const int nm = n_layer * n_child;
-  for (int m = 0; m < nm; ++m) {
+// Tree shape; false if out of range (T <= 2^20 leaves)
+static bool tree_shape(int n_layer, int n_child, Tree& t) {
+  if (n_layer < 1 || n_child < 1) return false;
+  long T = 1, runs = 0;
+  for (int l = 0; l < n_layer; ++l) {
+    T *= n_child;
+    runs += T;
+    if (T > (1 << 20)) return false;
+  }
+  t.n_layer = n_layer;
+  t.n_child = n_child;
+  t.T = static_cast<int>(T);
+  t.n_runs = static_cast<int>(runs);
+  return true;
+}
+
+// edge matrices [n_runs][V][V] -> cumulative rows (np.cumsum: sequential float64 adds)
+static void build_cdf(const double* edges, int n_edges, int V, double* out) {
+  for (int m = 0; m < n_edges; ++m) {
     for (int r = 0; r < V; ++r) {
-      double acc = 0.0;  // np.cumsum: sequential float64 adds
+      double acc = 0.0;
       for (int c = 0; c < V; ++c) {
-        acc += trans[(static_cast<size_t>(m) * V + r) * V + c];
+        acc += edges[(static_cast<size_t>(m) * V + r) * V + c];
         out[(static_cast<size_t>(m) * V + r) * V + c] = acc;
       }
     }
   }
 }
 
-extern "C" ghm_sampler* ghm_sampler_create(const double* t_trans, const double* i_trans, int n_layer,
-                                           int n_child, int V, int K) {
-  if (!t_trans || !i_trans || n_layer < 1 || n_child < 1 || V < 1 || V > 255 || K < 2) return nullptr;
-  long T = 1;
-  for (int l = 0; l < n_layer; ++l) T *= n_child;
-  if (T > (1 << 20)) return nullptr;
+extern "C" ghm_sampler* ghm_sampler_create_edges(const double* t_edges, int t_layer, int t_child,
+                                                 const double* i_edges, int i_layer, int i_child, int V, int K) {
+  if (!t_edges || !i_edges || V < 1 || V > 255 || K < 2) return nullptr;
   ghm_sampler* s = new ghm_sampler();
-  s->n_layer = n_layer; s->n_child = n_child; s->V = V; s->K = K; s->T = static_cast<int>(T);
-  s->n_runs = static_cast<int>((T * n_child - 1) / (n_child - 1 > 0 ? n_child - 1 : 1)) - 1;
-  if (n_child == 1) s->n_runs = n_layer;
+  if (!tree_shape(t_layer, t_child, s->tree[0]) || !tree_shape(i_layer, i_child, s->tree[1])) {
+    delete s;
+    return nullptr;
+  }
+  s->V = V;
+  s->K = K;
+  const double* src[2] = {t_edges, i_edges};
+  for (int k = 0; k < 2; ++k) {
+    Tree& t = s->tree[k];
+    t.cdf.resize(static_cast<size_t>(t.n_runs) * V * V);
+    build_cdf(src[k], t.n_runs, V, t.cdf.data());
+  }
   s->pool.reset(new Pool(pool_threads()));
-  const size_t per = static_cast<size_t>(n_layer) * n_child * V * V;
-  s->cdf.resize(2 * per);
-  build_cdf(t_trans, n_layer, n_child, V, s->cdf.data());
-  build_cdf(i_trans, n_layer, n_child, V, s->cdf.data() + per);
   s->mt.seed(0);
   return s;
+}
+
+extern "C" ghm_sampler* ghm_sampler_create(const double* t_trans, const double* i_trans, int n_layer,
+                                           int n_child, int V, int K) {
+  if (!t_trans || !i_trans || V < 1 || V > 255) return nullptr;
+  Tree shape;
+  if (!tree_shape(n_layer, n_child, shape)) return nullptr;
+  // expand the per-(layer, child slot) templates to every edge
+  const size_t VV = static_cast<size_t>(V) * V;
+  std::vector<double> te(shape.n_runs * VV), ie(shape.n_runs * VV);
+  size_t e = 0;
+  long width = 1;
+  for (int l = 0; l < n_layer; ++l) {
+    width *= n_child;
+    for (long k = 0; k < width; ++k, ++e) {
+      const size_t m = (static_cast<size_t>(l) * n_child + k % n_child) * VV;
+      std::memcpy(te.data() + e * VV, t_trans + m, VV * sizeof(double));
+      std::memcpy(ie.data() + e * VV, i_trans + m, VV * sizeof(double));
+    }
+  }
+  return ghm_sampler_create_edges(te.data(), n_layer, n_child, ie.data(), n_layer, n_child, V, K);
 }
 
 extern "C" void ghm_sampler_destroy(ghm_sampler* s) { delete s; }
@@ -310,23 +359,23 @@ static inline double to_double(uint32_t a, uint32_t b) {  // numpy legacy random
 // Expand rows [r0, r1) of the rows listed in `sel` (indices into the batch of
 // `rows` trees whose draws start at `draws`): values of every node in a
 // [n_nodes][RB] scratch plane, leaves written row-major to out[i][T].
-static void expand_rows(const ghm_sampler* s, const double* cdf, const uint32_t* draws, int rows,
+static void expand_rows(const ghm_sampler* s, const Tree& tr, const uint32_t* draws, int rows,
                         const uint8_t* root, const int* sel, int r0, int r1, uint8_t* out) {
   constexpr int RB = 32;
-  const int V = s->V, C = s->n_child, T = s->T;
-  const int n_nodes = s->n_runs + 1;
+  const int V = s->V, C = tr.n_child, T = tr.T;
+  const int n_nodes = tr.n_runs + 1;
   std::vector<uint8_t> val(static_cast<size_t>(n_nodes) * RB);
   for (int i0 = r0; i0 < r1; i0 += RB) {
     const int nb = (r1 - i0) < RB ? (r1 - i0) : RB;
     for (int i = 0; i < nb; ++i) val[i] = root[sel[i0 + i]];
     int first = 0, n_par = 1;  // BFS index of the level's first node, its width
-    for (int layer = 0; layer < s->n_layer; ++layer) {
+    for (int layer = 0; layer < tr.n_layer; ++layer) {
       const int child0 = first + n_par;
       for (int p = 0; p < n_par; ++p) {
         const uint8_t* pv = val.data() + static_cast<size_t>(first + p) * RB;
         for (int c = 0; c < C; ++c) {
           const int node = child0 + p * C + c;
-          const double* m = cdf + static_cast<size_t>(layer * C + c) * V * V;
+          const double* m = tr.cdf.data() + static_cast<size_t>(node - 1) * V * V;  // edge node - 1
           const uint32_t* run = draws + static_cast<size_t>(node - 1) * rows * 2;
           uint8_t* o = val.data() + static_cast<size_t>(node) * RB;
           for (int i = 0; i < nb; ++i) {
@@ -355,12 +404,12 @@ static void expand_rows(const ghm_sampler* s, const double* cdf, const uint32_t*
 // the selected rows of both in parallel.
 static void draw_trees(ghm_sampler* s, int rows, const uint8_t* troot, const uint8_t* iroot, const int* sel,
                        int nsel, uint8_t* t_out, uint8_t* i_out) {
-  const size_t per_tree = static_cast<size_t>(s->n_runs) * rows * 2;
-  s->stream.resize(2 * per_tree);
-  pull_stream(s, 2 * per_tree, s->stream.data());
-  const size_t per = static_cast<size_t>(s->n_layer) * s->n_child * s->V * s->V;
+  const size_t t_tree = static_cast<size_t>(s->tree[0].n_runs) * rows * 2;
+  const size_t i_tree = static_cast<size_t>(s->tree[1].n_runs) * rows * 2;
+  s->stream.resize(t_tree + i_tree);
+  pull_stream(s, t_tree + i_tree, s->stream.data());  // the text tree's runs, then the image tree's
   const uint32_t* ts = s->stream.data();
-  const uint32_t* is = ts + per_tree;
+  const uint32_t* is = ts + t_tree;
   const int nw = s->pool->size();
   // 2 trees x row chunks of 32, dealt round-robin over the workers
   const int nch = (nsel + 31) / 32;
@@ -369,9 +418,9 @@ static void draw_trees(ghm_sampler* s, int rows, const uint8_t* troot, const uin
       const int tree = k / nch, ch = k % nch;
       const int r0 = 32 * ch, r1 = (r0 + 32 < nsel) ? r0 + 32 : nsel;
       if (tree == 0)
-        expand_rows(s, s->cdf.data(), ts, rows, troot, sel, r0, r1, t_out);
+        expand_rows(s, s->tree[0], ts, rows, troot, sel, r0, r1, t_out);
       else
-        expand_rows(s, s->cdf.data() + per, is, rows, iroot, sel, r0, r1, i_out);
+        expand_rows(s, s->tree[1], is, rows, iroot, sel, r0, r1, i_out);
     }
   });
 }
@@ -430,7 +479,7 @@ extern "C" int ghm_sampler_randn(ghm_sampler* s, double* out, int64_t n) {
 extern "C" int ghm_sampler_next_cdm(ghm_sampler* s, int B, double sigma, uint8_t* t_leaves,
                                     uint8_t* i_leaves, uint8_t* root, double* z) {
   if (!s || B < 1 || !t_leaves || !i_leaves) return -1;
-  const int V = s->V, T = s->T;
+  const int V = s->V, T = s->tree[1].T;  // z lives on the image leaves
   std::vector<uint8_t> r(B);
   for (int b = 0; b < B; ++b) r[b] = static_cast<uint8_t>(s->mt.bounded(V - 1));
   std::vector<int> sel(B);

@@ -120,6 +120,7 @@ _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i
 
 HOST_SIGNATURES = {
     "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],
+    "ghm_sampler_create_edges": [_p, _i, _i, _p, _i, _i, _i, _i],
     "ghm_sampler_destroy": [_p],
     "ghm_sampler_seed": [_p, _u32],
     "ghm_sampler_set_state": [_p, _p, _i],
@@ -133,7 +134,8 @@ HOST_SIGNATURES = {
     "ghm_sampler_get_gauss": [_p, _p, _p],
     "ghm_sampler_randn": [_p, _p, _i64],
 }
-_HOST_RESTYPE = {"ghm_sampler_create": ctypes.c_void_p, "ghm_sampler_destroy": None}
+_HOST_RESTYPE = {"ghm_sampler_create": ctypes.c_void_p, "ghm_sampler_create_edges": ctypes.c_void_p,
+                 "ghm_sampler_destroy": None}
 
 _hip = None
 _host = None

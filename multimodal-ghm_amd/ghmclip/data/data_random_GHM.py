@@ -52,31 +52,57 @@ def GenTransition(n_layer, n_child, variable_type, p_flip=0.3, flip_scale=1.0,
 
 
 def _templates(transition, n_child):
-    """Distinct per-(layer, child slot) matrices [n_layer, n_child, V, V]."""
+    """Distinct per-(layer, child slot) matrices [n_layer, n_child, V, V] of a
+    translation-invariant tree (what the device BP kernels take), or None when
+    the tree is not translation invariant (GenTransition(translation_invariance=
+    False): a matrix per edge)."""
     out = np.stack([np.stack(layer[:n_child]) for layer in transition])
-    for l, layer in enumerate(transition):  # the native sampler needs translation invariance
+    for l, layer in enumerate(transition):
         for k, mat in enumerate(layer):
             if not np.array_equal(mat, out[l, k % n_child]):
-                raise NotImplementedError("native sampler: translation_invariance=True only")
+                return None
     return np.ascontiguousarray(out)
 
 
-class NativeClipSampler:
-    """Thin owner of a libghm_host sampler handle."""
+def _edge_tables(transition):
+    """Per-layer edge matrices [n_child^(l+1), V, V] (layer l, edge parent*C +
+    child: the reference's transition[l] list as an array)."""
+    return [np.ascontiguousarray(np.stack(layer), dtype=np.float64) for layer in transition]
 
-    def __init__(self, t_templ, i_templ, V, K):
-        if t_templ.shape != i_templ.shape:
-            raise NotImplementedError("native sampler: text and image trees must have the same shape")
-        self.n_layer, self.n_child = t_templ.shape[0], t_templ.shape[1]
+
+def _tables(tr):
+    """BP input as per-layer edge tables: a template array [L, C, V, V] is
+    expanded (node n of layer l uses template n % C), a list of per-layer edge
+    tables passes through."""
+    if isinstance(tr, np.ndarray) and tr.ndim == 4:
+        L, C = tr.shape[0], tr.shape[1]
+        return [np.tile(tr[l], (C ** l, 1, 1)) for l in range(L)]
+    return [np.asarray(t, dtype=np.float64) for t in tr]
+
+
+class NativeClipSampler:
+    """Thin owner of a libghm_host sampler handle.  Built from per-edge
+    transition tables of each tree (any shapes, translation invariant or not),
+    or from two equal-shape template arrays [L, C, V, V]."""
+
+    def __init__(self, t_tr, i_tr, V, K):
+        t_tab, i_tab = _tables(t_tr), _tables(i_tr)
+        self.t_shape = (len(t_tab), t_tab[0].shape[0])
+        self.i_shape = (len(i_tab), i_tab[0].shape[0])
+        if self.t_shape == self.i_shape:
+            self.n_layer, self.n_child = self.t_shape
         self.V, self.K = V, K
-        self.T = self.n_child ** self.n_layer
-        self._t, self._i = t_templ, i_templ  # keep alive
+        self.T_t = self.t_shape[1] ** self.t_shape[0]
+        self.T_i = self.i_shape[1] ** self.i_shape[0]
+        self.T = self.T_t if self.T_t == self.T_i else None  # one T only for equal trees
+        self._t = np.ascontiguousarray(np.concatenate(t_tab))  # [n_edges][V][V], kept alive
+        self._i = np.ascontiguousarray(np.concatenate(i_tab))
         lib = _native.host_lib()
         self._lib = lib
-        self._h = lib.ghm_sampler_create(t_templ.ctypes.data, i_templ.ctypes.data, self.n_layer,
-                                         self.n_child, V, K)
+        self._h = lib.ghm_sampler_create_edges(self._t.ctypes.data, self.t_shape[0], self.t_shape[1],
+                                               self._i.ctypes.data, self.i_shape[0], self.i_shape[1], V, K)
         if not self._h:
-            raise RuntimeError("ghm_sampler_create failed")
+            raise RuntimeError("ghm_sampler_create_edges failed")
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -155,21 +181,24 @@ def _native_check(rc):
 
 def _bp_levels(templ, leaves):
     """BP_CLS messages (data_random_GHM.py:185-208), vectorised over the nodes of a
-    layer (translation invariance makes their matrices equal per child slot).
-    Returns the per-level messages [n_nodes, V, B], depth L-1 first, root last."""
-    n_layer, n_child, V, _ = templ.shape
+    layer with each node's own edge matrices (translation-invariant templates
+    are expanded, _tables).  Returns the per-level messages [n_nodes, V, B],
+    depth L-1 first, root last."""
+    tab = _tables(templ)
+    n_layer = len(tab)
+    C = tab[0].shape[0]
     lv = np.asarray(leaves).astype(np.int64).T
-    n_par = lv.shape[0] // n_child
-    msg = np.zeros((n_par, V, lv.shape[1]))
-    for c in range(n_child):
-        msg += np.log(templ[-1, c][:, lv[c::n_child]].transpose(1, 0, 2))
+    n_par = lv.shape[0] // C
+    msg = np.zeros((n_par, tab[-1].shape[1], lv.shape[1]))
+    for c in range(C):  # leaf edge par*C + c: column leaf value of its matrix
+        msg += np.log(np.take_along_axis(tab[-1][c::C], lv[c::C][:, None, :], axis=2))
     msg -= msg.max(axis=1, keepdims=True)
     levels = [msg]
     for layer in range(n_layer - 2, -1, -1):
-        n_par = msg.shape[0] // n_child
-        new = np.zeros((n_par, V, msg.shape[2]))
-        for c in range(n_child):
-            new += np.log(np.einsum("ij,njb->nib", templ[layer, c], np.exp(msg[c::n_child])))
+        n_par = msg.shape[0] // C
+        new = np.zeros((n_par, msg.shape[1], msg.shape[2]))
+        for c in range(C):
+            new += np.log(np.einsum("nij,njb->nib", tab[layer][c::C], np.exp(msg[c::C])))
         new -= new.max(axis=1, keepdims=True)
         msg = new
         levels.append(msg)
@@ -182,12 +211,12 @@ def guided_targets(templ, leaves, device="cpu"):
     leaf position carrying its ancestor's BP message.  On a HIP device the
     messages come from the ghm_bp_cls kernel (the path ClipTrainer uses);
     otherwise from the host BP above."""
-    templ = np.ascontiguousarray(templ, dtype=np.float64)
-    L, C, V, _ = templ.shape
     leaves = np.asarray(leaves)
     B, T = leaves.shape
     dev = torch.device(device)
-    if dev.type == "cuda":
+    if dev.type == "cuda" and isinstance(templ, np.ndarray) and templ.ndim == 4:
+        templ = np.ascontiguousarray(templ, dtype=np.float64)
+        L, C, V, _ = templ.shape
         n_total = (C ** L - 1) // (C - 1)
         tok = torch.from_numpy(np.ascontiguousarray(leaves, dtype=np.uint8)).to(dev)
         tr = torch.from_numpy(templ).to(dev)
@@ -203,7 +232,7 @@ def guided_targets(templ, leaves, device="cpu"):
     out = []
     for m in _bp_levels(templ, leaves):
         ext = T // m.shape[0]
-        out.append(torch.from_numpy(np.repeat(m.transpose(2, 0, 1), ext, axis=1).astype(np.float32)))
+        out.append(torch.from_numpy(np.repeat(m.transpose(2, 0, 1), ext, axis=1).astype(np.float32)).to(dev))
     return out
 
 
@@ -249,7 +278,24 @@ class DoubleSampler:
                                           translation_invariance=translation_invariance)
         self.i_transition = GenTransition(n_layers[1], n_childs[1], variable_type, p_flips[1], flip_scale,
                                           translation_invariance=translation_invariance)
+        self.translation_invariance = translation_invariance
+        # per-layer edge tables (host BP, the native sampler) and, for translation-
+        # invariant trees, the per-child-slot templates the device BP kernels take
+        self.t_tables, self.i_tables = _edge_tables(self.t_transition), _edge_tables(self.i_transition)
+        self.t_templ = _templates(self.t_transition, n_childs[0])
+        self.i_templ = _templates(self.i_transition, n_childs[1])
         self._zs = None
+
+    def _native_sampler(self, K):
+        return NativeClipSampler(self.t_tables, self.i_tables, self.variable_type, K)
+
+    def device_templates(self, what="this path"):
+        """(text, image) templates for the device BP kernels; raises for
+        non-translation-invariant trees (their BP runs on the host)."""
+        if self.t_templ is None or self.i_templ is None:
+            raise NotImplementedError(f"{what} needs translation-invariant trees: its BP targets / posteriors "
+                                      "run on the device from per-child-slot templates")
+        return self.t_templ, self.i_templ
 
     def get_zeroshot_batch(self, batch_size=128, return_tree=False):
         """:670-683: text and image trees sharing one root per sample (the draw of
@@ -261,13 +307,12 @@ class DoubleSampler:
         if return_tree:
             raise NotImplementedError("return_tree: the trees are drawn natively, no GHMTree objects exist")
         if getattr(self, "_zs", None) is None:
-            t_templ = _templates(self.t_transition, self.n_childs[0])
-            i_templ = _templates(self.i_transition, self.n_childs[1])
-            self._zs = (t_templ, i_templ, NativeClipSampler(t_templ, i_templ, self.variable_type, 2))
-        t_templ, i_templ, nat = self._zs
+            self._zs = self._native_sampler(2)
+        nat = self._zs
+        t_templ, i_templ = self.t_tables, self.i_tables
         B = batch_size
-        tl = np.empty((B, nat.T), np.uint8)
-        il = np.empty((B, nat.T), np.uint8)
+        tl = np.empty((B, nat.T_t), np.uint8)
+        il = np.empty((B, nat.T_i), np.uint8)
         root = np.empty(B, np.uint8)
         nat.pull_numpy_state()
         nat.next_cdm_into(B, 0.0, tl, il, None, root)
@@ -285,16 +330,15 @@ class ClipSampler(DoubleSampler):
         super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
                          translation_invariance, seedtree)
         self.K = K
-        self.t_templ = _templates(self.t_transition, n_childs[0])
-        self.i_templ = _templates(self.i_transition, n_childs[1])
-        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, K)
-        self.T = self.native.T
+        self.native = self._native_sampler(K)
+        self.T, self.T_t, self.T_i = self.native.T, self.native.T_t, self.native.T_i
 
     def draw_numpy(self, batch_size):
-        """One reference-identical draw from numpy's global state (uint8 arrays)."""
+        """One reference-identical draw from numpy's global state (uint8 arrays;
+        text rows T_t wide, image rows T_i wide)."""
         rows = batch_size * (self.K + 1)
-        tl = np.empty((rows, self.T), np.uint8)
-        il = np.empty((rows, self.T), np.uint8)
+        tl = np.empty((rows, self.T_t), np.uint8)
+        il = np.empty((rows, self.T_i), np.uint8)
         tr = np.empty(rows, np.uint8)
         ir = np.empty(rows, np.uint8)
         self.native.pull_numpy_state()
@@ -312,19 +356,19 @@ class ClipSampler(DoubleSampler):
         to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
         tg = ig = tp = ip = None
         if guide:
-            tg = guided_targets(self.t_templ, tl, device)
-            ig = guided_targets(self.i_templ, il, device)
+            tg = guided_targets(self.t_templ if self.t_templ is not None else self.t_tables, tl, device)
+            ig = guided_targets(self.i_templ if self.i_templ is not None else self.i_tables, il, device)
             p_y = np.ones(self.variable_type) / self.variable_type
-            tp = bp_cls_posterior(self.t_templ, tl, p_y)
-            ip = bp_cls_posterior(self.i_templ, il, p_y)
+            tp = bp_cls_posterior(self.t_tables, tl, p_y)
+            ip = bp_cls_posterior(self.i_tables, il, p_y)
         return [to(tl), to(tr), tg, tp], [to(il), to(ir), ig, ip]
 
     def get_Bayes(self, n_eval=10000):
         """:786-817 — exact Bayes CLIP loss from BP posteriors (host, once per run)."""
         tl, _, il, _ = self.draw_numpy(n_eval)
         p_y = np.ones(self.variable_type) / self.variable_type
-        tp = bp_cls_posterior(self.t_templ, tl, p_y).T
-        ip = bp_cls_posterior(self.i_templ, il, p_y).T
+        tp = bp_cls_posterior(self.t_tables, tl, p_y).T
+        ip = bp_cls_posterior(self.i_tables, il, p_y).T
         return PPCLIPLoss(tp, ip, n_eval, self.K, self.variable_type)
 
 
@@ -339,15 +383,13 @@ def bp_dns_posterior(templ, z, sigma, ext):
     layer (translation invariance: node n uses its child-slot matrix n % C).
     z: noisy leaf observations [n_leaves, B] float64; ext: external root message
     [V, B].  Returns the posterior means [n_leaves, B]."""
-    n_layer, C, V, _ = templ.shape
+    tab = _tables(templ)
+    n_layer, C, V = len(tab), tab[0].shape[0], tab[0].shape[1]
     vt = np.linspace(0, V - 1, V).reshape(1, V, 1)
 
-    def up(msg, mats, transpose=False):
-        out = np.empty_like(msg)
-        eq = "ji,njb->nib" if transpose else "ij,njb->nib"
-        for c in range(C):
-            out[c::C] = np.log(np.einsum(eq, mats[c], np.exp(msg[c::C])))
-        return out
+    def up(msg, mats, transpose=False):  # node n of the layer: its edge matrix mats[n]
+        eq = "nji,njb->nib" if transpose else "nij,njb->nib"
+        return np.log(np.einsum(eq, mats, np.exp(msg)))
 
     def children_sum(q):  # sum(child.qd for child in children), children in slot order
         acc = q[0::C].copy()
@@ -356,16 +398,16 @@ def bp_dns_posterior(templ, z, sigma, ext):
         return acc
 
     hd = {n_layer: -0.5 * (np.asarray(z, dtype=np.float64)[:, None, :] - vt) ** 2 / (sigma ** 2)}
-    qd = {n_layer: up(hd[n_layer], templ[-1])}
+    qd = {n_layer: up(hd[n_layer], tab[-1])}
     for layer in range(n_layer - 1, 0, -1):  # leaves -> root (:489-495)
         h = children_sum(qd[layer + 1])
         h -= h.max(axis=1, keepdims=True)
-        hd[layer], qd[layer] = h, up(h, templ[layer - 1])
+        hd[layer], qd[layer] = h, up(h, tab[layer - 1])
     bu = children_sum(qd[1])  # root (:499-504)
     bu -= bu.max(axis=1, keepdims=True)
     bu = bu + np.asarray(ext)[None]
     for layer in range(1, n_layer + 1):  # root -> leaves (:507-512)
-        b = hd[layer] + up(np.repeat(bu, C, axis=0) - qd[layer], templ[layer - 1], transpose=True)
+        b = hd[layer] + up(np.repeat(bu, C, axis=0) - qd[layer], tab[layer - 1], transpose=True)
         bu = b - b.max(axis=1, keepdims=True)
     w = np.exp(bu)
     return ((vt * w).sum(axis=1) / w.sum(axis=1))
@@ -381,9 +423,7 @@ class ConditionalDenoiseSampler(DoubleSampler):
         super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
                          translation_invariance, seedtree)
         self.sigma = sigma
-        self.t_templ = _templates(self.t_transition, n_childs[0])
-        self.i_templ = _templates(self.i_transition, n_childs[1])
-        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, 2)
+        self.native = self._native_sampler(2)
         self.T = self.native.T
 
     def draw_numpy(self, batch_size):
@@ -402,9 +442,9 @@ class ConditionalDenoiseSampler(DoubleSampler):
     def posterior(self, tl, z):
         """(text BP_CLS posteriors [V, B], image BP_DNS posterior means [B, T])."""
         p_y = np.ones(self.variable_type) / self.variable_type
-        t_pp = bp_cls_posterior(self.t_templ, tl, p_y).T
-        ext = bp_cls_root_message(self.t_templ, tl)
-        return t_pp, bp_dns_posterior(self.i_templ, np.asarray(z).T, self.sigma, ext).T
+        t_pp = bp_cls_posterior(self.t_tables, tl, p_y).T
+        ext = bp_cls_root_message(self.t_tables, tl)
+        return t_pp, bp_dns_posterior(self.i_tables, np.asarray(z).T, self.sigma, ext).T
 
     def get_batch(self, batch_size=128, device="cpu", guide=False):
         """:854-884.  Returns (text_leaves int64 [B, T], text_root int64 [B], None,
@@ -441,7 +481,8 @@ def bp_nwp_posterior(templ, leaves, ext, guide=False):
     root's (hd, bu) — one array in the reference (bu_message = hd_message, then
     += in place, :414-421), so both halves hold the final bu; [L+1 .. 2L] the bu
     of the target leaf's path from depth 1 down to the leaf [B, n-1, V] (:449-451)."""
-    n_layer, C, V, _ = templ.shape
+    tab = _tables(templ)
+    n_layer, C, V = len(tab), tab[0].shape[0], tab[0].shape[1]
     lv = np.asarray(leaves).astype(np.int64).T
     n_leaves, B = lv.shape
     qd = [None] + [np.zeros((C ** d, V, B)) for d in range(1, n_layer + 1)]
@@ -452,7 +493,7 @@ def bp_nwp_posterior(templ, leaves, ext, guide=False):
               [np.zeros((B, n_leaves - 1, 2 * V), np.float32) for _ in range(n_layer)] +
               [np.zeros((B, n_leaves - 1, V), np.float32) for _ in range(n_layer)])
     for p in range(n_leaves - 1):
-        q = np.log(templ[-1, p % C][:, lv[p]])  # leaf message :370-371
+        q = np.log(tab[-1][p][:, lv[p]])  # leaf message :370-371 (leaf p's edge)
         qd[n_layer][p] = q - q.max(0)
         if guide:
             gl[0][:, p, :] = qd[n_layer][p].T
@@ -465,7 +506,7 @@ def bp_nwp_posterior(templ, leaves, ext, guide=False):
                     h += qd[layer + 1][par * C + c]
             h -= h.max(0)
             hd[layer][par] = h
-            qq = np.log(templ[layer - 1, par % C] @ np.exp(h))
+            qq = np.log(tab[layer - 1][par] @ np.exp(h))
             qd[layer][par] = qq - qq.max(0)
             if guide:
                 gl[n_layer - layer][:, p, :V] = h.T
@@ -485,7 +526,7 @@ def bp_nwp_posterior(templ, leaves, ext, guide=False):
             gl[n_layer][:, p, V:] = bu.T
         for layer in range(1, n_layer + 1):  # down the target's path :435-452
             k = goal[-layer]
-            mat = templ[layer - 1, k % C].T
+            mat = tab[layer - 1][k].T
             if share[-layer]:
                 b = hd[layer][k] + np.log(mat @ np.exp(bu - qd[layer][k]))
             else:
@@ -531,17 +572,15 @@ class NextWordPredictSampler(DoubleSampler):
                  translation_invariance=True, seedtree=42):
         super().__init__(n_layers, n_childs, p_ys, p_flips, flip_scale, variable_type,
                          translation_invariance, seedtree)
-        self.t_templ = _templates(self.t_transition, n_childs[0])
-        self.i_templ = _templates(self.i_transition, n_childs[1])
-        self.native = NativeClipSampler(self.t_templ, self.i_templ, variable_type, 2)
-        self.T = self.native.T
+        self.native = self._native_sampler(2)
+        self.T, self.T_t, self.T_i = self.native.T, self.native.T_t, self.native.T_i
 
     def draw_numpy(self, batch_size):
         """One reference-identical draw of the paired trees from numpy's global
-        state: (text leaves uint8 [B, T], image leaves uint8 [B, T], roots [B])."""
-        B, T = batch_size, self.T
-        tl = np.empty((B, T), np.uint8)
-        il = np.empty((B, T), np.uint8)
+        state: (text leaves uint8 [B, T_t], image leaves uint8 [B, T_i], roots [B])."""
+        B = batch_size
+        tl = np.empty((B, self.T_t), np.uint8)
+        il = np.empty((B, self.T_i), np.uint8)
         root = np.empty(B, np.uint8)
         self.native.pull_numpy_state()
         self.native.next_cdm_into(B, 0.0, tl, il, None, root)
@@ -554,12 +593,12 @@ class NextWordPredictSampler(DoubleSampler):
         arrays of bp_nwp_posterior), image guide targets (GHMTree.guided_info of the
         image tree: L float32 [B, T, V]))."""
         p_y = np.ones(self.variable_type) / self.variable_type
-        ext = bp_cls_root_message(self.i_templ, il)
-        i_pp = bp_cls_posterior(self.i_templ, il, p_y)
+        ext = bp_cls_root_message(self.i_tables, il)
+        i_pp = bp_cls_posterior(self.i_tables, il, p_y)
         if not guide:
-            return bp_nwp_posterior(self.t_templ, tl, ext), i_pp
-        post, tg = bp_nwp_posterior(self.t_templ, tl, ext, guide=True)
-        ig = [m.numpy() for m in guided_targets(self.i_templ, il)]
+            return bp_nwp_posterior(self.t_tables, tl, ext), i_pp
+        post, tg = bp_nwp_posterior(self.t_tables, tl, ext, guide=True)
+        ig = [m.numpy() for m in guided_targets(self.i_tables, il)]
         return post, i_pp, tg, ig
 
     def get_batch(self, batch_size=128, device="cpu", guide=False):

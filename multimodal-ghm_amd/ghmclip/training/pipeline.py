@@ -65,15 +65,15 @@ class BatchPipeline:
     # -- CLIP batches: text / image leaves [B(K+1), T] uint8 ------------------------
     def _make_slots(self, n_slots):
         rows = self.B * (self.s.K + 1)
-        T = self.s.T
-        self.full_rows, self.T = rows, T
+        Tt, Ti = self.s.T_t, self.s.T_i  # text / image sequence lengths (trees may differ)
+        self.full_rows, self.T = rows, self.s.T
         if self.slice is not None:  # this rank's shard only: (K+1) * B/world rows
             br, rank, world = self.slice
             if br != self.B or br % world:
                 raise ValueError("row_slice must be (batch_size, rank, world) with world | batch_size")
             self.shard_lo, self.shard_n = rank * (br // world), br // world
             rows = (self.s.K + 1) * self.shard_n
-        self.slots = [(_host_buffer((rows, T), torch.uint8), _host_buffer((rows, T), torch.uint8))
+        self.slots = [(_host_buffer((rows, Tt), torch.uint8), _host_buffer((rows, Ti), torch.uint8))
                       for _ in range(n_slots)]
 
     def _fill(self, i):
@@ -141,12 +141,12 @@ class CdmBatchPipeline(BatchPipeline):
         super().__init__(native_sampler, batch_size, n_slots, row_slice)
 
     def _make_slots(self, n_slots):
-        B, T = self.B, self.s.T
-        self.T = T
+        B, Tt, Ti = self.B, self.s.T_t, self.s.T_i
+        self.T = self.s.T
 
         def slot():
-            return (_host_buffer((B, T), torch.uint8), _host_buffer((B, T), torch.uint8),
-                    _host_buffer((B, T), torch.float64))
+            return (_host_buffer((B, Tt), torch.uint8), _host_buffer((B, Ti), torch.uint8),
+                    _host_buffer((B, Ti), torch.float64))
         self.slots = [slot() for _ in range(n_slots)]
         if self.slice is not None:
             self.rows = shard_samples(B, *self.slice)
@@ -178,14 +178,14 @@ class NwpBatchPipeline(BatchPipeline):
         super().__init__(sampler.native, batch_size, n_slots, row_slice)
 
     def _make_slots(self, n_slots):
-        B, T, V = self.B, self.s.T, self.sampler.variable_type
+        B, T, Ti, V = self.B, self.s.T_t, self.s.T_i, self.sampler.variable_type
         self.T = T
         L = self.sampler.n_layers
-        ng = (T - 1) * V * (3 * L[0] + 1) + T * V * L[1] if self.guide else 0
+        ng = (T - 1) * V * (3 * L[0] + 1) + Ti * V * L[1] if self.guide else 0
 
         def slot():
             return (_host_buffer((B, T - 1), torch.uint8), _host_buffer((B, T - 1), torch.uint8),
-                    _host_buffer((B, T - 1, V), torch.float32), _host_buffer((B, T), torch.uint8),
+                    _host_buffer((B, T - 1, V), torch.float32), _host_buffer((B, Ti), torch.uint8),
                     _host_buffer((B, ng), torch.float32) if ng else None)
         self.slots = [slot() for _ in range(n_slots)]
         self.tl = np.empty((B, T), np.uint8)

@@ -122,7 +122,8 @@ def main(argv=None):
 
     sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters)
              for i in range(c.total_iters)]
-    trainer = CdmTrainer(model, None, c.batch_size // ws, sched, sampler.t_templ, sampler.i_templ,
+    trainer = CdmTrainer(model, None, c.batch_size // ws,
+                         sched, *sampler.device_templates("the CDM trainer (BP_DNS on the device)"),
                          sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset,
                          penalty=c.penalty)
     if t_offset:

@@ -139,7 +139,8 @@ def run(c, teardown=True):
     B_local = c.batch_size // ws
     trainer = ClipTrainer(tmodel, imodel, c.K, B_local, sched, max_norm=c.max_norm, device=device, t_offset=start,
                           penalty=c.penalty,
-                          guide_trans=(sampler.t_templ, sampler.i_templ) if c.clip_guide else None)
+                          guide_trans=sampler.device_templates("guided CLIP (--clip_guide=True)") if c.clip_guide
+                          else None)
     if start:
         trainer.load_optimizer_state(optimizer)
 
