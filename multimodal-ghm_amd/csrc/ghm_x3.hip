@@ -619,12 +619,18 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p) {
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
   return v;
 }
-template <int NW>
+// STAMP (bench.py's in-graph timing only, ghm_mlp_bwd_rc_x3_stamped): thread 0
+// of each workgroup writes the 100 MHz constant clock (s_memrealtime) at its
+// start and after its last store to stamps[2 blockIdx.x + {0, 1}]; the launch
+// spans min(start) .. max(end).  Nothing else differs.
+template <int NW, bool STAMP = false>
 __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
     const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
     float* __restrict__ Gout, float* __restrict__ dU, float* __restrict__ dHmid, float* __restrict__ part_ln,
-    int64_t M) {
+    int64_t M, uint64_t* __restrict__ stamps = nullptr) {
+  uint64_t t_start = 0;
+  if (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
   constexpr int NC = GHM_F / 32;
   // [W1 hi|lo][W2^T hi|lo] x 2 buffers (64 KB: two workgroups per CU); the LN
   // partial buffer aliases it after the loop.  The W1 chunk serves both the U
@@ -809,6 +815,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     else
       sum = (rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D]);
     part_ln[static_cast<int64_t>(blockIdx.x) * 2 * GHM_D + q * GHM_D + f] = sum;
+  }
+  if (STAMP) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+      stamps[2 * blockIdx.x] = t_start;
+      stamps[2 * blockIdx.x + 1] = t_end;
+    }
   }
 }
 
@@ -1810,6 +1824,29 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
     hipLaunchKernelGGL(k_mlp_bwd_rc_x3<4>, dim3(nblk), dim3(256), 0, ghm_stream(stream), dH_out, H_mid,
                        reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
                        G, dU, dH_mid, part_ln, M);
+  return ghm_launch_status();
+}
+
+// bench.py's in-graph timing of the dominant kernel: the same launch with
+// per-workgroup clock stamps (2 x ghm_mlp_bwd_rc_x3_blocks(M) uint64).
+extern "C" int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid, const float* stats,
+                                         const float* ln_w, const float* ln_b, const void* pack, const float* b1,
+                                         float* G, float* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
+                                         uint64_t* stamps, void* stream) {
+  GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln && stamps,
+            "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
+  GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
+  const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
+  if (rc_waves(M) == 8)
+    hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, true>), dim3(nblk), dim3(512), 0, ghm_stream(stream), dH_out, H_mid,
+                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                       G, dU, dH_mid, part_ln, M, stamps);
+  else
+    hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, true>), dim3(nblk), dim3(256), 0, ghm_stream(stream), dH_out, H_mid,
+                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                       G, dU, dH_mid, part_ln, M, stamps);
   return ghm_launch_status();
 }
 

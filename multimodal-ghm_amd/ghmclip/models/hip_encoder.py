@@ -401,10 +401,13 @@ class EncoderPlan:
                   _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL,
                   D_HIDDEN, s)
             elif x3:  # recomputes U; writes G (scratch) and dU
-                c("ghm_mlp_bwd_rc_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]),
-                  _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]),
-                  _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M,
-                  D_MODEL, D_HIDDEN, s)
+                args = (_ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                        _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]), _ptr(p[f"_mlps.{l}.0.bias"]),
+                        _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN)
+                if getattr(self, "stamps", None) is not None:  # bench.py's in-graph timing
+                    c("ghm_mlp_bwd_rc_x3_stamped", *args, _ptr(self.stamps[l]), s)
+                else:
+                    c("ghm_mlp_bwd_rc_x3", *args, s)
             else:
                 c("ghm_mlp_bwd", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.2.weight"]), _ptr(self.Dg[l]), _ptr(self.dU),

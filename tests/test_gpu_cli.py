@@ -188,3 +188,19 @@ def test_clip_checkpoint_contract_and_resume(tmp_path, monkeypatch):
     for pid, st in d["optimizer_state_dict"]["state"].items():
         st2 = d2["optimizer_state_dict"]["state"][pid]
         assert st["t"] == st2["t"] and torch.equal(st["m"], st2["m"]) and torch.equal(st["v"], st2["v"])
+
+
+def test_eg_nwp_nontranslation_invariant_cli(tmp_path, monkeypatch):
+    """scripts/examples/eg_nwp.sh (shortened): train_NWP --guide=True
+    --translation_invariance=False --p_*_flip=0.4 --raw=True — the per-edge
+    GHM trees (native sampler + host BP_NWP / guided targets, pinned by
+    tests/test_nonti_host.py) through the guided joint VLM step."""
+    from ghmclip.training import train_NWP
+    monkeypatch.chdir(tmp_path)
+    flags = ["--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4", "--n_ttree_child=3", "--n_itree_child=3",
+             "--p_ttree_flip=0.4", "--p_itree_flip=0.4", "--flip_scale=1", "--batch_size=8", "--variable_type=10",
+             "--d_eb=256", "--n_model_layer=9", "--n_head=4", "--layernorm=True", "--normalize_attn=True",
+             "--lr_max=1e-3", "--lr_min=1e-6", "--guide=True", "--translation_invariance=False", "--total_iters=4",
+             "--penalty=0.001", "--raw=True", "--log_interval=2"]
+    loss, compare = train_NWP.main(flags)
+    assert len(loss) == 4 and np.isfinite(loss).all() and np.isfinite(compare).all()
