@@ -348,6 +348,8 @@ def profiled_kernels():
     agg = {}
     for r in csv.DictReader(open(path)):
         k = _kname(r["Name"])  # instantiation (template arguments kept)
+        if k.startswith("k_mlp_bwd_rc_x3<") and k.endswith(", true>"):  # the stamped twin (in-graph timing)
+            k = k[:-len(", true>")] + ", false>"
         t, n = agg.get(k, (0.0, 0))
         agg[k] = (t + float(r["TotalDurationNs"]), n + int(r["Calls"]))
     return path, {k: (t, n, t / max(1, n)) for k, (t, n) in agg.items()}
@@ -360,10 +362,11 @@ def mfma_busy(kernel):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_util.txt")),
                    key=lambda f: [int(x) for x in __import__("re").findall(r"\d+", os.path.basename(f))[:2]])
     for f in reversed(files):
-        for line in open(f):
-            parts = line.split()
-            if parts and parts[0].split("<")[0] == kernel and len(parts) > 3 and parts[3].endswith("%"):
-                return {"util": float(parts[3][:-1]) / 100.0, "file": os.path.relpath(f, ROOT)}
+        for line in open(f):  # fixed-width: the kernel name in the first 30 columns, then the figures
+            name, rest = line[:30].strip(), line[30:].split()
+            pct = [x for x in rest if x.endswith("%")]
+            if name.split("<")[0] == kernel and pct and ", true>" not in name:
+                return {"util": float(pct[0][:-1]) / 100.0, "kernel": name, "file": os.path.relpath(f, ROOT)}
     return None
 
 
