@@ -356,6 +356,7 @@ class EncoderPlan:
         T, N, L, C = self.T, self.N, self.L, self.C
         cur = self.dH[0]
         jobs = []
+        self.pending = jobs  # flush_pending() reduces what is queued so far (data-parallel buckets)
         c("ghm_readout_bwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(p["_out.weight"]), _ptr(de), _ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro),
           _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, _stream())
@@ -370,6 +371,12 @@ class EncoderPlan:
         c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
         jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
         self._flush(jobs, s)
+
+    def flush_pending(self):
+        """Reduce the parameter-gradient partials queued by the running
+        backward_iter so far (on the current stream): those gradients are final
+        from here on."""
+        self._flush(self.pending, _stream())
 
     def layers_bwd(self, p, g, jobs, s, layer_grad=None):
         """Backward of the n_layer encoder layers from dH[0] (= dL/dH_L, written by

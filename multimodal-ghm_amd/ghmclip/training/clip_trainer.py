@@ -32,6 +32,53 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _layer_of(name):
+    """Encoder layer of a parameter name (_queries.3.weight, _mlps.3.0.bias,
+    _lns_1.3.weight -> 3), None for the embeddings and readout."""
+    parts = name.split(".")
+    if parts[0] in ("_queries", "_keys", "_values", "_mlps", "_lns_1", "_lns_2") and len(parts) > 1:
+        return int(parts[1])
+    return None
+
+
+def flat_layout(models, dp_top):
+    """Offsets of every parameter of the towers in the flat buffers: [text
+    tower][image tower], each in BACKWARD order (layer L-1's parameters first,
+    ..., layer 0's, then the embeddings and the readout), so the gradients that
+    are final once the backward of the top dp_top layers has run form one
+    contiguous range per tower (data-parallel bucket A).  state_dict order is
+    unchanged: the module parameters become views.
+    Returns ([{name: (offset, numel)} per tower], [(start, end) of bucket A per
+    tower], total numel)."""
+    layout, bucket_a, off = [], [], 0
+    for m in models:
+        named = dict(m.named_parameters())
+        order = [n for l in reversed(range(m.n_layer)) for n in named if _layer_of(n) == l]
+        order += [n for n in named if _layer_of(n) is None]
+        slots, start, a_end = {}, off, off
+        for name in order:
+            k = named[name].numel()
+            slots[name] = (off, k)
+            off += k
+            ly = _layer_of(name)
+            if ly is not None and ly >= m.n_layer - dp_top:
+                a_end = off
+        layout.append(slots)
+        bucket_a.append((start, a_end))
+    return layout, bucket_a, off
+
+
+def dp_bucket_ranges(bucket_a, n):
+    """([bucket A ranges], [bucket B ranges]) of a flat gradient of n elements
+    laid out by flat_layout: A = the top layers of each tower, B = the rest of
+    each tower (the image tower starts where the text tower ends).  Together
+    they cover [0, n) exactly once."""
+    (ta, tb), (ia, ib) = bucket_a
+    a = [(ta, tb), (ia, ib)]
+    b = [(tb, ia), (ib, n)]
+    return [r for r in a if r[1] > r[0]], [r for r in b if r[1] > r[0]]
+
+
 class ClipTrainer:
     def __init__(self, tmodel, imodel, K, batch_size, lr_schedule, max_norm=1.0, weight_decay=0.001,
                  betas=(0.9, 0.999), eps=1e-8, device="cuda", t_offset=0, process_group=None,
@@ -60,19 +107,23 @@ class ClipTrainer:
         self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.views = []  # per model: (param dict, grad dict, m dict, v dict)
-        off = 0
+        L0 = tmodel.n_layer
+        self.dp_top = int(os.environ.get("GHM_DP_BUCKET_LAYERS", str(L0 - L0 // 2)))  # layers in bucket A
+        self.dp_top = max(0, min(L0, self.dp_top))
+        layout, self.bucket_a, _ = flat_layout(self.models, self.dp_top)
         with torch.no_grad():
-            for m in self.models:
+            for m, slots in zip(self.models, layout):
+                named = dict(m.named_parameters())
                 pd, gd, md, vd = {}, {}, {}, {}
-                for name, p in m.named_parameters():
-                    k = p.numel()
+                for name in named:  # views keyed in the module's own order (the plans look names up)
+                    off, k = slots[name]
+                    p = named[name]
                     self.pflat[off:off + k].copy_(p.data.reshape(-1))
                     p.data = self.pflat[off:off + k].view(p.shape)
                     p.grad = self.gflat[off:off + k].view(p.shape)
                     pd[name], gd[name] = p.data, p.grad
                     md[name] = self.mflat[off:off + k].view(p.shape)
                     vd[name] = self.vflat[off:off + k].view(p.shape)
-                    off += k
                 self.views.append((pd, gd, md, vd))
         T = tmodel.n_token
         n_seq = batch_size * (K + 1)
@@ -102,6 +153,7 @@ class ClipTrainer:
         self.graphs = None
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
+        self.comm = torch.cuda.Stream(device=self.device)  # data-parallel bucket all-reduces
         self._setup_guide(penalty, guide_trans)
 
     def _setup_guide(self, penalty, guide_trans):
@@ -167,48 +219,57 @@ class ClipTrainer:
 
     # -- the launch sequence -----------------------------------------------------
     @staticmethod
-    def _interleave(jobs):
-        """Advance launch generators [(generator, stream), ...] round-robin, each
-        step issued under its own stream: the two towers' per-layer launches are
-        issued (and, captured, become graph nodes) alternately instead of one
-        tower's whole sequence first."""
-        active = list(jobs)
-        while active:
-            for job in list(active):
-                gen, st = job
-                with torch.cuda.stream(st):
-                    try:
-                        next(gen)
-                    except StopIteration:
-                        active.remove(job)
+    def _advance(jobs, n=None, inter=True):
+        """Advance launch generators [(generator, stream), ...] by n yields each
+        (None: to exhaustion), every step issued under its own stream.  inter:
+        round-robin (the two towers' per-layer launches are issued — and, when
+        captured, become graph nodes — alternately), else one tower after the
+        other.  Exhausted generators are dropped from `jobs`."""
+        def step(job):
+            gen, st = job
+            with torch.cuda.stream(st):
+                try:
+                    next(gen)
+                    return True
+                except StopIteration:
+                    jobs.remove(job)
+                    return False
+        if inter:
+            k = 0
+            while jobs and (n is None or k < n):
+                for job in list(jobs):
+                    step(job)
+                k += 1
+        else:
+            for job in list(jobs):
+                k = 0
+                while (n is None or k < n) and step(job):
+                    k += 1
 
-    def _fwd_bwd(self):
-        """Text tower on the current stream, image tower on a side stream (fork /
-        join through stream waits, which graph capture records as edges), so the
-        two towers' launches overlap and fill each other's tails.  The towers'
-        launches are issued layer by layer alternately ($GHM_TOWER_ORDER =
-        "interleave", default) or one tower after the other ("sequential")."""
+    def _streams(self):
         main = torch.cuda.current_stream()
         side = main if os.environ.get("GHM_SERIAL_TOWERS") == "1" else self.side
-        inter = os.environ.get("GHM_TOWER_ORDER", "interleave") == "interleave"
+        return main, side, os.environ.get("GHM_TOWER_ORDER", "interleave") == "interleave"
+
+    def _fwd_bwd_a(self, flush):
+        """Forward of both towers, the loss, and the backward of the readouts and
+        of the top dp_top layers; flush: reduce their parameter-gradient partials
+        (the data-parallel bucket A is final after this part).  Text tower on the
+        current stream, image tower on a side stream (fork / join through stream
+        waits, which graph capture records as edges), so the two towers' launches
+        overlap and fill each other's tails; the towers' launches are issued
+        layer by layer alternately ($GHM_TOWER_ORDER = "interleave", default) or
+        one tower after the other ("sequential")."""
+        main, side, inter = self._streams()
         pt, pi = self.plans
         (tp, tg, _, _), (ip, ig, _, _) = self.views
         side.wait_stream(main)
         s = ctypes.c_void_p(main.cuda_stream)
-        if inter:
-            self._interleave([(pi.forward_iter(ip), side), (pt.forward_iter(tp), main)])
-            if self.guide:
-                with torch.cuda.stream(side):
-                    self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
-                self._guide_fwd(0, s)
-        else:
+        self._advance([(pi.forward_iter(ip), side), (pt.forward_iter(tp), main)], inter=inter)
+        if self.guide:
             with torch.cuda.stream(side):
-                pi.forward(ip)
-                if self.guide:
-                    self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
-            pt.forward(tp)
-            if self.guide:
-                self._guide_fwd(0, s)
+                self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
+            self._guide_fwd(0, s)
         main.wait_stream(side)
         _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
@@ -216,14 +277,26 @@ class ClipTrainer:
             _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.n_seq, self.penalty,
                          _p(self.loss_out), _p(self.phist), _p(self.step_ctr), s)
         side.wait_stream(main)
-        if inter:
-            self._interleave([(pi.backward_iter(ip, ig, layer_grad=self._guide_hooks(1)), side),
-                              (pt.backward_iter(tp, tg, layer_grad=self._guide_hooks(0)), main)])
-        else:
-            with torch.cuda.stream(side):
-                pi.backward(ip, ig, layer_grad=self._guide_hooks(1))
-            pt.backward(tp, tg, layer_grad=self._guide_hooks(0))
+        self._bwd = [(pi.backward_iter(ip, ig, layer_grad=self._guide_hooks(1)), side),
+                     (pt.backward_iter(tp, tg, layer_grad=self._guide_hooks(0)), main)]
+        self._advance(self._bwd, 1 + self.dp_top, inter=inter)  # readout + the top layers
+        if flush:
+            for plan, st in ((pi, side), (pt, main)):
+                with torch.cuda.stream(st):
+                    plan.flush_pending()
         main.wait_stream(side)
+
+    def _fwd_bwd_b(self):
+        """The rest of the backward (layers below the top dp_top, embeddings, the
+        final partial reductions)."""
+        main, side, inter = self._streams()
+        side.wait_stream(main)
+        self._advance(self._bwd, inter=inter)
+        main.wait_stream(side)
+
+    def _fwd_bwd(self):
+        self._fwd_bwd_a(flush=False)
+        self._fwd_bwd_b()
 
     def _optim(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -233,8 +306,23 @@ class ClipTrainer:
         _native.call("ghm_adamw", _p(self.pflat), _p(self.gflat), _p(self.mflat), _p(self.vflat),
                      self.n_params, _p(self.hyper), b1, omb1, b2, omb2, eps, s)
 
-    def _allreduce(self):
-        distributed.allreduce_mean_(self.gflat, group=self.pg)
+    def dp_buckets(self):
+        """([(start, end) of bucket A per tower], [... bucket B]) of the flat
+        gradient: A = the top dp_top layers' gradients (final after _fwd_bwd_a),
+        B = the rest."""
+        return dp_bucket_ranges(self.bucket_a, self.n_params)
+
+    def _allreduce_ranges(self, ranges):
+        """Mean over ranks of gflat[a:b] for each range, issued on the comm
+        stream after the work already queued on the current stream (so the
+        current stream can run on while the collective is in flight)."""
+        comm = self.comm
+        comm.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(comm):
+            distributed.allreduce_ranges_mean_(self.gflat, ranges, group=self.pg)
+
+    def _dp(self):
+        return self.pg is not None or distributed.is_on()
 
     def set_tokens(self, t_tokens, i_tokens):
         """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
@@ -244,38 +332,55 @@ class ClipTrainer:
         self.plans[1].tokens.copy_(i_tokens, non_blocking=True)
 
     def step(self):
-        """One training step on the staged tokens (async; no host sync)."""
+        """One training step on the staged tokens (async; no host sync).  Data
+        parallel: the all-reduce of bucket A (the top layers' gradients) runs on
+        the comm stream while the rest of the backward runs; bucket B follows."""
         if self.steps_done >= self.n_sched:
             raise RuntimeError("schedule exhausted")
-        if self.graphs is not None:
-            self.graphs[0].replay()
-            if len(self.graphs) > 1:
-                self._allreduce()
-                self.graphs[1].replay()
+        if not self._dp():
+            if self.graphs is not None:
+                self.graphs[0].replay()
+            else:
+                self._fwd_bwd()
+                self._optim()
         else:
-            self._fwd_bwd()
-            if self.pg is not None or distributed.is_on():
-                self._allreduce()
-            self._optim()
+            bucket_a, bucket_b = self.dp_buckets()
+            if self.graphs is not None:
+                self.graphs[0].replay()
+            else:
+                self._fwd_bwd_a(flush=True)
+            self._allreduce_ranges(bucket_a)
+            if self.graphs is not None:
+                self.graphs[1].replay()
+            else:
+                self._fwd_bwd_b()
+            self._allreduce_ranges(bucket_b)
+            torch.cuda.current_stream().wait_stream(self.comm)
+            if self.graphs is not None:
+                self.graphs[2].replay()
+            else:
+                self._optim()
         self.steps_done += 1
 
     def capture(self):
         """Capture the step into HIP graphs (call after >= 1 eager step so all
         lazy initialisation has happened).  Replays reuse the staged tokens.
         One process: fwd/bwd and the optimizer are one graph (one launch, no
-        host gap between them).  Data parallel: two graphs with the gradient
-        all-reduce between them."""
+        host gap between them).  Data parallel: three graphs (forward + top of
+        the backward, rest of the backward, optimizer) with the two bucket
+        all-reduces between them."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        dp = self.pg is not None or distributed.is_on()
         with torch.cuda.stream(s):
-            if dp:
-                g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g1, stream=s):
-                    self._fwd_bwd()
-                with torch.cuda.graph(g2, stream=s):
+            if self._dp():
+                ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, stream=s):
+                    self._fwd_bwd_a(flush=True)
+                with torch.cuda.graph(gb, stream=s):
+                    self._fwd_bwd_b()
+                with torch.cuda.graph(gc, stream=s):
                     self._optim()
-                graphs = (g1, g2)
+                graphs = (ga, gb, gc)
             else:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):

@@ -77,6 +77,19 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+def allreduce_ranges_mean_(flat, ranges, group=None):
+    """allreduce_mean_ of flat[a:b] for each (a, b) of `ranges`, in order: one
+    collective per bucket, issued by every rank with the same ranges (the
+    bucketed gradient all-reduce of ClipTrainer.step).  Each element is still
+    the SUM of the ranks' values times 1/world; at world 2 that sum is one
+    addition, so bucketed == flat bit for bit (tests/test_dp_gloo.py); beyond 2
+    ranks a ring may add an element's terms in an order that depends on its
+    chunk, which can change its last bit (the same on every rank)."""
+    for a, b in ranges:
+        allreduce_mean_(flat[a:b], group=group)
+    return flat
+
+
 def mean_histories(arrays, device):
     """Average equal-length float64 host arrays over ranks (every rank calls
     this at the same iteration).  Returns the averaged arrays; identity with one

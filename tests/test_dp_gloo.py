@@ -143,3 +143,73 @@ def test_cdm_sharded_grads_equal_full_batch():
     g = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None]).numpy()
     assert abs(loss_dp - loss.item()) <= 1e-6 * loss.item()
     np.testing.assert_allclose(g_dp, g, rtol=1e-4, atol=1e-6)
+
+
+def _bucket_worker(rank, world, port, out):
+    """Every rank: the product's flat layout of two 5-layer towers, a rank-seeded
+    gradient, then (a) one flat all-reduce, (b) the two buckets ClipTrainer.step
+    issues (A = top layers, B = the rest), each through distributed.py."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-ghm_amd")]
+    from ghmclip.training import distributed
+    from ghmclip.training.clip_trainer import dp_bucket_ranges, flat_layout
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    tm, im = _towers()
+    _, bucket_a, n = flat_layout([tm, im], 3)
+    g = torch.randn(n, generator=torch.Generator().manual_seed(100 + rank)) * 10.0 ** torch.randint(
+        -6, 3, (n,), generator=torch.Generator().manual_seed(7 + rank))
+    flat = distributed.allreduce_mean_(g.clone())
+    a, b = dp_bucket_ranges(bucket_a, n)
+    bucketed = g.clone()
+    distributed.allreduce_ranges_mean_(bucketed, a)
+    distributed.allreduce_ranges_mean_(bucketed, b)
+    if rank == 0:
+        out.put((flat.numpy(), bucketed.numpy()))
+    dist.destroy_process_group()
+
+
+def _towers():
+    from ghmclip.models.model import EncoderTransformer
+    torch.manual_seed(0)
+    return EncoderTransformer(81, 10, n_embd=128, n_layer=5), EncoderTransformer(27, 10, n_embd=128, n_layer=5)
+
+
+def test_bucketed_allreduce_equals_flat_bit_for_bit():
+    """SURVEY §5 / DP=8 prep: the per-layer-bucket all-reduce (bucket A issued
+    while the lower layers' backward runs) gives exactly the flat all-reduce's
+    gradient at world 2."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    flat, bucketed = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert flat.tobytes() == bucketed.tobytes()
+
+
+def test_flat_layout_buckets_cover_top_layers():
+    """Bucket A of each tower holds exactly its top dp_top layers' parameters
+    and A + B tile [0, n) once."""
+    from ghmclip.training.clip_trainer import _layer_of, dp_bucket_ranges, flat_layout
+    tm, im = _towers()
+    for top in range(0, 6):
+        layout, bucket_a, n = flat_layout([tm, im], top)
+        assert n == sum(p.numel() for m in (tm, im) for p in m.parameters())
+        a, b = dp_bucket_ranges(bucket_a, n)
+        cover = np.zeros(n, dtype=np.int64)
+        for lo, hi in a + b:
+            cover[lo:hi] += 1
+        assert (cover == 1).all()
+        for m, slots, (lo, hi) in zip((tm, im), layout, bucket_a):
+            for name, (off, k) in slots.items():
+                ly = _layer_of(name)
+                in_a = lo <= off and off + k <= hi
+                assert in_a == (ly is not None and ly >= m.n_layer - top), (top, name)
