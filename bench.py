@@ -348,8 +348,8 @@ def profiled_kernels():
     agg = {}
     for r in csv.DictReader(open(path)):
         k = _kname(r["Name"])  # instantiation (template arguments kept)
-        if k.startswith("k_mlp_bwd_rc_x3<") and k.endswith(", true>"):  # the stamped twin (in-graph timing)
-            k = k[:-len(", true>")] + ", false>"
+        if k.startswith("k_mlp_bwd_rc_x3<") and k.endswith(", 2>"):  # the concurrent-step stamped twin
+            k = k[:-len(", 2>")] + ", 0>"
         t, n = agg.get(k, (0.0, 0))
         agg[k] = (t + float(r["TotalDurationNs"]), n + int(r["Calls"]))
     return path, {k: (t, n, t / max(1, n)) for k, (t, n) in agg.items()}
@@ -365,41 +365,51 @@ def mfma_busy(kernel):
         for line in open(f):  # fixed-width: the kernel name in the first 30 columns, then the figures
             name, rest = line[:30].strip(), line[30:].split()
             pct = [x for x in rest if x.endswith("%")]
-            if name.split("<")[0] == kernel and pct and ", true>" not in name:
+            if name.split("<")[0] == kernel and pct and not name.endswith((", true>", ", 1>", ", 2>")):
                 return {"util": float(pct[0][:-1]) / 100.0, "kernel": name, "file": os.path.relpath(f, ROOT)}
     return None
 
 
-def time_mlp_bwd_in_graph(trainer, replays=10):
+def time_mlp_bwd_in_graph(trainer, replays=10, serial=True):
     """Average span (ms) of the MLP backward launches inside GRAPH-REPLAYED
     training steps: the step is captured once more with every layer's
     ghm_mlp_bwd_rc_x3 launch replaced by its stamped twin (the same kernel plus
     a 100 MHz clock stamp per workgroup at its start and end), the graph is
     replayed `replays` times, and a launch spans its first workgroup's start to
-    its last workgroup's end.  The bench's own graphs are restored afterwards.
+    its last workgroup's end.  serial: the two towers' phase graphs are replayed
+    on ONE stream (GHM_SERIAL_TOWERS=1), so the kernel has the GPU to itself and its
+    span is its own duration (twin 1: what the roofline is computed from, and
+    what a rocprofv3 trace of the same command reports for it); else the real
+    concurrent step (twin 2), where the other tower's kernels share the CUs and
+    stretch the span.  The bench's own graphs are left in place.
     Returns (ms, launches averaged)."""
     from ghmclip import _native
     plans = trainer.plans
     nblk = int(_native.hip_lib().ghm_mlp_bwd_rc_x3_blocks(plans[0].M))
     stamps = [torch.zeros(pl.L, 2 * nblk, dtype=torch.int64, device=pl.device) for pl in plans]
     for pl, st in zip(plans, stamps):
-        pl.stamps = st
-    saved = trainer.graphs
+        pl.stamps, pl.stamp_twin = st, 1 if serial else 2
+    env = os.environ.get("GHM_SERIAL_TOWERS")
     try:
-        trainer.capture()
-        graphs = trainer.graphs
+        graphs = trainer._capture_graphs()
     finally:
-        trainer.graphs = saved
         for pl in plans:
             pl.stamps = None
+    if serial:
+        os.environ["GHM_SERIAL_TOWERS"] = "1"
     spans = []
-    for _ in range(replays):
-        for g in graphs:
-            g.replay()
-        torch.cuda.synchronize()
-        for st in stamps:
-            v = st.view(st.shape[0], -1, 2)
-            spans += ((v[:, :, 1].max(1).values - v[:, :, 0].min(1).values).double() * 1e-5).tolist()  # 10-ns ticks
+    try:
+        for _ in range(replays):
+            trainer._run(graphs)
+            torch.cuda.synchronize()
+            for st in stamps:
+                v = st.view(st.shape[0], -1, 2)
+                spans += ((v[:, :, 1].max(1).values - v[:, :, 0].min(1).values).double() * 1e-5).tolist()  # 10 ns
+    finally:
+        if env is None:
+            os.environ.pop("GHM_SERIAL_TOWERS", None)
+        else:
+            os.environ["GHM_SERIAL_TOWERS"] = env
     return sum(spans) / len(spans), len(spans)
 
 
@@ -551,12 +561,15 @@ def main():
     dom_inst = top if top and top.split("<")[0] == dom else None
     if tr.precision != "x3" or not tr.plans[0].mlp_rc:
         dom = "k_ln_mlp_fwd_x3b" if tr.precision == "x3" else None
-    dom_ms, dom_how = None, None
+    dom_ms, dom_how, dom_ms_conc = None, None, None
     if dom:
         if dom == "k_mlp_bwd_rc_x3" and ws == 1 and not a.no_graph:
-            dom_ms, n_l = time_mlp_bwd_in_graph(tr)
-            dom_how = (f"graph replay: every launch's first-workgroup start to last-workgroup end "
-                       f"(s_memrealtime stamps of the kernel's stamped twin), {n_l} launches")
+            dom_ms, n_l = time_mlp_bwd_in_graph(tr, serial=True)
+            dom_ms_conc, n_c = time_mlp_bwd_in_graph(tr, serial=False)
+            dom_how = (f"graph replay with the two towers' launches on one stream (the kernel alone on the GPU): "
+                       f"every launch's first-workgroup start to last-workgroup end (s_memrealtime stamps of the "
+                       f"kernel's stamped twin k_mlp_bwd_rc_x3<8, 1>), {n_l} launches; the rocprofv3 average of "
+                       f"that twin in the same command is profile_avg_ms")
         else:
             dom_ms = time_kernel_in_step(tr, DOMINANT_CANDIDATES[dom]["entry"])
             dom_how = "eager in-step: HIP events around each launch on its stream, both towers live"
@@ -601,9 +614,10 @@ def main():
         dach = dflop / (dom_ms * 1e-3) / 1e3
         ptot = sum(v[0] for v in prof.values()) if prof else 0.0
         dtraffic = pmc_traffic(dom_inst or dom)
-        if dtraffic is None and dom == "k_mlp_bwd_rc_x3":
-            dtraffic = pmc_traffic("k_mlp_bwd_rc_x3<8>")
-        prof_avg_ms = prof[dom_inst][2] / 1e6 if dom_inst in prof else None
+        if dtraffic is None and dom == "k_mlp_bwd_rc_x3":  # names of older profiles
+            dtraffic = pmc_traffic("k_mlp_bwd_rc_x3<8, false>") or pmc_traffic("k_mlp_bwd_rc_x3<8>")
+        twin = (dom_inst or "")[:-len(", 0>")] + ", 1>" if (dom_inst or "").endswith(", 0>") else None
+        prof_avg_ms = prof[twin][2] / 1e6 if twin in prof else None  # the serialized-measurement twin
         roofline = {"bound": "mfma",
                     "kernel": f"{dom} ({d['what']})",
                     "achieved": round(dach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -614,6 +628,9 @@ def main():
                     "design_gflop": round(d["design_gflop"] * scale, 2),
                     "algorithmic_bytes": round(d["bytes"] * scale), "design_bytes": round(d["design_bytes"] * scale),
                     "kernel_ms": round(dom_ms, 4), "timing": dom_how,
+                    "kernel_ms_concurrent": None if dom_ms_conc is None else round(dom_ms_conc, 4),
+                    "concurrent_note": "span of the same launches in the real step (twin k_mlp_bwd_rc_x3<8, 2>), "
+                                       "where the other tower's kernels share the CUs",
                     "dominant_by": (f"{dom_inst}: {100 * prof[dom_inst][0] / ptot:.1f} % of kernel time in "
                                     f"{os.path.relpath(prof_path, ROOT)}" if dom_inst in prof and ptot else
                                     "default (no committed kernel stats)"),

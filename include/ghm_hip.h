@@ -189,11 +189,13 @@ int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stat
                       float* part_ln, int64_t M, int D, int F, void* stream);
 /* The same launch with per-workgroup clock stamps for bench.py's in-graph
  * kernel timing: stamps[2 b], stamps[2 b + 1] = s_memrealtime (100 MHz) at
- * workgroup b's start and end, 2 x ghm_mlp_bwd_rc_x3_blocks(M) uint64. */
+ * workgroup b's start and end, 2 x ghm_mlp_bwd_rc_x3_blocks(M) uint64.  twin
+ * (1 or 2) picks one of two identical kernel instantiations, so a profiler
+ * trace separates two measurements. */
 int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
                               const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
                               float* dH_mid, float* part_ln, int64_t M, int D, int F, uint64_t* stamps,
-                              void* stream);
+                              int twin, void* stream);
 /* As ghm_qkv_bwd (backward of model.py:772-775), with the LN1 statistics
  * recomputed from H exactly as the forward computed them (eps = the LayerNorm
  * eps); stats (the forward's [M][2] buffer) is accepted and not read

@@ -425,7 +425,11 @@ __global__ __launch_bounds__(256) void k_readout_fwd(const float* __restrict__ H
 // K-way symmetric CLIP loss + gradient, one workgroup        (model.py:877-907)
 // Rows are blocks b = 0..K of B rows; row i of block 0 (text) / 1 (image) is
 // scored against its matched partner and row i of blocks 2..K.  exp() is
-// unshifted, exactly as the reference.
+// unshifted, exactly as the reference.  The (K+1) B x C embeddings of both
+// towers are first staged into LDS with coalesced loads (the round-2 kernel
+// read them row by row from HBM in a chain of dependent loads: 25 us per step
+// on one workgroup while the rest of the GPU idled); thread t < B then scores
+// direction 1 of row t, thread B + t direction 2.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float dotc(const float* a, const float* b, int C) {
   float s = 0.f;
@@ -433,65 +437,69 @@ __device__ __forceinline__ float dotc(const float* a, const float* b, int C) {
   return s;
 }
 
-__global__ __launch_bounds__(256) void k_clip_loss(const float* __restrict__ te,
-                                                   const float* __restrict__ ie,
-                                                   float* __restrict__ dte, float* __restrict__ die,
-                                                   float* __restrict__ loss_out,
-                                                   float* __restrict__ hist,
-                                                   const int32_t* __restrict__ step, int B, int K,
-                                                   int C) {
-  __shared__ float red[4];
+// direction of row i: the matched pair (tm, im) scored against the negatives
+// ng(k) = row i of block k (k = 2..K) of the other tower; writes the gradients
+// of tm, im and the negatives; returns -log(Sm / (Sm + Sn))
+__device__ __forceinline__ float clip_dir(const float* tm, const float* im, const float* neg, int B, int K, int C,
+                                          float invB, float* dtm, float* dim, float* dneg, bool neg_is_text) {
+  const float* self = neg_is_text ? im : tm;  // the row the negatives are scored against
+  const float Sm = expf(dotc(tm, im, C));
+  float Sn = 0.f;
+  for (int k = 2; k <= K; ++k) Sn += expf(dotc(neg + static_cast<int64_t>(k) * B * C, self, C));
+  const float den = Sm + Sn;
+  const float ga = -(Sn / den) * invB;
+  float* dself = neg_is_text ? dim : dtm;
+  for (int c = 0; c < C; ++c) { dtm[c] = ga * im[c]; dim[c] = ga * tm[c]; }
+  for (int k = 2; k <= K; ++k) {
+    const float* nk = neg + static_cast<int64_t>(k) * B * C;
+    const float gb = (expf(dotc(nk, self, C)) / den) * invB;
+    float* dnk = dneg + static_cast<int64_t>(k) * B * C;
+    for (int c = 0; c < C; ++c) { dnk[c] = gb * self[c]; dself[c] += gb * nk[c]; }
+  }
+  return -logf(Sm / (Sm + Sn));
+}
+
+template <bool STAGE>
+__global__ __launch_bounds__(1024) void k_clip_loss(const float* __restrict__ te, const float* __restrict__ ie,
+                                                    float* __restrict__ dte, float* __restrict__ die,
+                                                    float* __restrict__ loss_out, float* __restrict__ hist,
+                                                    const int32_t* __restrict__ step, int B, int K, int C) {
+  extern __shared__ float sm[];  // STAGE: [te | ie], (K+1) B C floats each
+  __shared__ float red[16];
+  const int n = (K + 1) * B * C;
+  const float* T = te;
+  const float* I = ie;
+  if (STAGE) {
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      sm[e] = te[e];
+      sm[n + e] = ie[e];
+    }
+    __syncthreads();
+    T = sm;
+    I = sm + n;
+  }
   const float invB = 1.f / static_cast<float>(B);
   float acc = 0.f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) {
-    // direction 1: image i of block 0 vs text i of block 0 and of blocks 2..K
-    {
-      const float* tm = te + static_cast<int64_t>(i) * C;
-      const float* im = ie + static_cast<int64_t>(i) * C;
-      const float Sm = expf(dotc(tm, im, C));
-      float Sn = 0.f;
-      for (int k = 2; k <= K; ++k) Sn += expf(dotc(te + (static_cast<int64_t>(k) * B + i) * C, im, C));
-      acc += -logf(Sm / (Sm + Sn));
-      const float den = Sm + Sn;
-      const float ga = -(Sn / den) * invB;
-      float* dtm = dte + static_cast<int64_t>(i) * C;
-      float* dim = die + static_cast<int64_t>(i) * C;
-      for (int c = 0; c < C; ++c) { dtm[c] = ga * im[c]; dim[c] = ga * tm[c]; }
-      for (int k = 2; k <= K; ++k) {
-        const float* tk = te + (static_cast<int64_t>(k) * B + i) * C;
-        const float gb = (expf(dotc(tk, im, C)) / den) * invB;
-        float* dtk = dte + (static_cast<int64_t>(k) * B + i) * C;
-        for (int c = 0; c < C; ++c) { dtk[c] = gb * im[c]; dim[c] += gb * tk[c]; }
-      }
-    }
-    // direction 2: text i of block 1 vs image i of block 1 and of blocks 2..K
-    {
-      const float* tm = te + (static_cast<int64_t>(B) + i) * C;
-      const float* im = ie + (static_cast<int64_t>(B) + i) * C;
-      const float Sm = expf(dotc(tm, im, C));
-      float Sn = 0.f;
-      for (int k = 2; k <= K; ++k) Sn += expf(dotc(ie + (static_cast<int64_t>(k) * B + i) * C, tm, C));
-      acc += -logf(Sm / (Sm + Sn));
-      const float den = Sm + Sn;
-      const float ga = -(Sn / den) * invB;
-      float* dtm = dte + (static_cast<int64_t>(B) + i) * C;
-      float* dim = die + (static_cast<int64_t>(B) + i) * C;
-      for (int c = 0; c < C; ++c) { dtm[c] = ga * im[c]; dim[c] = ga * tm[c]; }
-      for (int k = 2; k <= K; ++k) {
-        const float* ik = ie + (static_cast<int64_t>(k) * B + i) * C;
-        const float gb = (expf(dotc(ik, tm, C)) / den) * invB;
-        float* dik = die + (static_cast<int64_t>(k) * B + i) * C;
-        for (int c = 0; c < C; ++c) { dik[c] = gb * tm[c]; dtm[c] += gb * ik[c]; }
-      }
+  for (int r = threadIdx.x; r < 2 * B; r += blockDim.x) {
+    const int i = r < B ? r : r - B;
+    if (r < B) {  // direction 1: image i of block 0 vs text i of block 0 and of blocks 2..K
+      const int64_t o = static_cast<int64_t>(i) * C;
+      acc += clip_dir(T + o, I + o, T + o, B, K, C, invB, dte + o, die + o, dte + o, true);
+    } else {      // direction 2: text i of block 1 vs image i of block 1 and of blocks 2..K
+      const int64_t o = (static_cast<int64_t>(B) + i) * C, on = static_cast<int64_t>(i) * C;
+      acc += clip_dir(T + o, I + o, I + on, B, K, C, invB, dte + o, die + o, die + on, false);
     }
   }
   // deterministic block reduction
   acc = sum32(acc);
   acc += __shfl_xor(acc, 32, 64);
+  const int nw = (blockDim.x + 63) / 64;
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float loss = ((red[0] + red[1]) + (red[2] + red[3])) * invB;
+    float tot = 0.f;
+    for (int w = 0; w < nw; ++w) tot += red[w];
+    const float loss = tot * invB;
     loss_out[0] = loss;
     loss_out[1] = loss;
     if (hist) hist[*step] = loss;
@@ -569,7 +577,13 @@ extern "C" int ghm_clip_loss(const float* t_emb, const float* i_emb, float* dt_e
   GHM_CHECK(t_emb && i_emb && dt_emb && di_emb && loss_out, "null pointer");
   GHM_CHECK(!hist || step, "hist needs step");
   GHM_CHECK(B >= 1 && K >= 2 && C >= 1, "shape");
-  hipLaunchKernelGGL(k_clip_loss, dim3(1), dim3(256), 0, ghm_stream(stream), t_emb, i_emb, dt_emb,
-                     di_emb, loss_out, hist, step, B, K, C);
+  const int threads = 2 * B >= 1024 ? 1024 : ((2 * B + 63) / 64) * 64;
+  const size_t lds = 2 * static_cast<size_t>(K + 1) * B * C * sizeof(float);
+  if (lds <= 64 * 1024)
+    hipLaunchKernelGGL(k_clip_loss<true>, dim3(1), dim3(threads), lds, ghm_stream(stream), t_emb, i_emb, dt_emb,
+                       di_emb, loss_out, hist, step, B, K, C);
+  else
+    hipLaunchKernelGGL(k_clip_loss<false>, dim3(1), dim3(threads), 0, ghm_stream(stream), t_emb, i_emb, dt_emb,
+                       di_emb, loss_out, hist, step, B, K, C);
   return ghm_launch_status();
 }

@@ -26,6 +26,10 @@
 #error "GHM_ABL timing ablations give wrong results: only with -DGHM_ABLATION_BUILD (tools/, never the product library)"
 #endif
 
+// waves per workgroup of the split-K weight gradient (k_wgrad_x3)
+#ifndef GHM_WGRAD_WAVES
+#define GHM_WGRAD_WAVES 4
+#endif
 // ---------------------------------------------------------------------------
 // Weight pack (bf16 elements per layer; each region = hi plane then lo plane)
 // ---------------------------------------------------------------------------
@@ -183,50 +187,6 @@ __device__ __forceinline__ void load_split64(const float* __restrict__ p, bool a
   }
 #pragma unroll
   for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
-}
-
-// ---------------------------------------------------------------------------
-// LN1 + Q/K/V projections                                       (model.py:772-775)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
-    const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
-    const __bf16* __restrict__ pack, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
-    float eps) {
-  __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
-  const bool active = m0 < M;
-  const int64_t m = m0 + j;
-  const bool valid = m < M;
-  const int64_t mc = valid ? m : M - 1;
-  bf16x8 xh[8], xl[8];
-  {
-    float mean = 0.f, rstd = 0.f;
-    ln_row_split(H + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
-    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
-  }
-  const __bf16* W = pack + PK_QKV_N;
-  uint4 st[2 * stage_bf_n<32, GHM_D>()];
-  stage_bf_load<32, GHM_D>(st, W, GHM_D, PK_QKV);
-  stage_bf_store<32, GHM_D, PB1>(st, swh[0], swl[0]);
-  __syncthreads();
-#pragma unroll 1
-  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
-    const int cur = b & 1;
-    stage_bf_load<32, GHM_D>(st, W + (b + 1 < 12 ? b + 1 : 11) * 32 * GHM_D, GHM_D, PK_QKV);
-    if (active) {
-      const f32x16 acc = proj_x3(swh[cur] + j * PB1 + 64 * h, swl[cur] + j * PB1 + 64 * h, xh, xl, zero16());
-      if (valid) {
-        float* o = qkv + m * (3 * GHM_D) + 32 * b;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          st4(o + quad_off(q, h), acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
-      }
-    }
-    stage_bf_store<32, GHM_D, PB1>(st, swh[cur ^ 1], swl[cur ^ 1]);
-    __syncthreads();
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -390,6 +350,84 @@ __device__ __forceinline__ void fill_r128_w8(const __bf16* g, int ldg, int lo_of
       glds16(src, ih + 512 * b);
       glds16(src + lo_off, il + 512 * b);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LN1 + Q/K/V projections                                       (model.py:772-775)
+// Wave = 32 tokens (v_mfma_f32_32x32x16_bf16, the LN'd token row split into 8
+// k-steps in registers); workgroup = 4 waves.  The 12 weight tiles (32 rows of
+// [Wq; Wk; Wv] x 128) arrive by LDS-DMA from the pre-split pack into a
+// double-buffered R32 ring (16-B chunk c of row r at c ^ (r & 15): the operand
+// reads, row j and chunk 8h + t per lane, are conflict-free).  Round 2 staged
+// the tiles through registers; the compiler sank those loads below the MFMAs
+// to their LDS stores and waited for them at once (the L2 latency exposed in
+// every tile).  Each tile's outputs are stored one tile later, so the
+// barrier's vmcnt(0) that retires the next fill never waits for fresh stores.
+// ---------------------------------------------------------------------------
+// Y^T tile (32 rows x 32 tokens) = A[32][128] . X^T, A from an R32 image pair
+__device__ __forceinline__ f32x16 proj_x3_r32(const __bf16* ih, const __bf16* il, int row, int h,
+                                              const bf16x8* xh, const bf16x8* xl, f32x16 acc) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int o = r32_off(row, 8 * h + t);
+    acc = mfma_x3(ldsb8(ih + o), ldsb8(il + o), xh[t], xl[t], acc);
+  }
+  return acc;
+}
+
+// One weight tile of a 4-wave token-parallel projection: LDS-DMA fill of the
+// next tile (global rows at g, pitch ldg, lo plane at +PK_QKV) into ring
+// buffer nb, then the product from the current buffer cb.  cb / nb are
+// __restrict__ parameters of one inlined function, so the waitcnt pass knows
+// the DMA target and the operand reads are disjoint (k_mlp_bwd_rc_x3).
+__device__ __forceinline__ f32x16 qkv_tile_x3(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
+                                              const __bf16* g, int ldg, int row, int h, bool active,
+                                              const bf16x8* xh, const bf16x8* xl, f32x16 acc) {
+  fill_r32_w8<4>(g, ldg, PK_QKV, nb, nb + PLANE);
+  if (active) acc = proj_x3_r32(cb, cb + PLANE, row, h, xh, xl, acc);
+  return acc;
+}
+
+__global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
+    const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* pack, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
+    float eps) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PLANE];  // 2 buffers x (hi, lo)
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const bool active = m0 < M;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W = pack + PK_QKV_N;
+  fill_r32_w8<4>(W, GHM_D, PK_QKV, lds, lds + PLANE);  // tile 0, in flight over the LayerNorm
+  bf16x8 xh[8], xl[8];
+  {
+    float mean = 0.f, rstd = 0.f;
+    ln_row_split(H + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
+    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  f32x16 prev = zero16();
+  float* orow = qkv + m * (3 * GHM_D);
+#pragma unroll 1
+  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
+    const int cur = b & 1;
+    if (b > 0 && active && valid) {  // tile b - 1's outputs
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(orow + 32 * (b - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
+    }
+    const int bn = b + 1 < 12 ? b + 1 : 11;  // branch-free: the last tile refills tile 11
+    prev = qkv_tile_x3(lds + 2 * PLANE * cur, lds + 2 * PLANE * (cur ^ 1), W + bn * 32 * GHM_D, GHM_D, j, h,
+                       active, xh, xl, zero16());
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (active && valid) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      st4(orow + 32 * 11 + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
   }
 }
 
@@ -619,11 +657,76 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p) {
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
   return v;
 }
-// STAMP (bench.py's in-graph timing only, ghm_mlp_bwd_rc_x3_stamped): thread 0
+// G (for dW2) and dU (for dW1) of one hidden chunk: 4 stores per wave
+__device__ __forceinline__ void store_g_du(const float* gv, const float* du, float* grow, float* drow) {
+  st4(grow, gv[0], gv[1], gv[2], gv[3]);
+  st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
+  st4(drow, du[0], du[1], du[2], du[3]);
+  st4(drow + 16, du[4], du[5], du[6], du[7]);
+}
+
+// One 32-unit hidden chunk of k_mlp_bwd_rc_x3: LDS-DMA fills of the next chunk
+// into ring buffer `nb`, products from the current buffer `cb`.  Both buffers
+// are __restrict__ parameters of one inlined function, so every access carries
+// alias-scope metadata that tells the waitcnt pass the DMA target and the
+// operand reads are disjoint: without it the compiler waited vmcnt(0) for the
+// just-issued fills before the first transposed read of the W1 image, which
+// exposed the whole L2 -> LDS latency in every chunk.
+template <int NW>
+__device__ __forceinline__ void mlp_bwd_rc_chunk(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
+                                                 const __bf16* W1n, const __bf16* W2Tn, const float4* bb,
+                                                 const bf16x8* xh, const bf16x8* xl, const bf16x8* yh,
+                                                 const bf16x8* yl, f32x4* dx, float* grow, float* drow, int t,
+                                                 int g, int lane) {
+  fill_r32t_w8<NW>(W1n, GHM_D, PK_W, nb, nb + PLANE);
+  fill_r32_w8<NW>(W2Tn, GHM_D, PK_W, nb + 2 * PLANE, nb + 3 * PLANE);
+  const __bf16* w1h = cb;
+  const __bf16* w1l = cb + PLANE;
+  const __bf16* w2h = cb + 2 * PLANE;
+  const __bf16* w2l = cb + 3 * PLANE;
+  f32x4 u[2], dg[2];
+  float gv[8], du[8];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    u[jt] = zero4();
+    dg[jt] = zero4();
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int o1 = r32t_off(16 * jt + t, 4 * s2 + g), o = r32_off(16 * jt + t, 4 * s2 + g);
+      u[jt] = mfma16_x3(ldsb8(w1h + o1), ldsb8(w1l + o1), xh[s2], xl[s2], u[jt]);
+      dg[jt] = mfma16_x3(ldsb8(w2h + o), ldsb8(w2l + o), yh[s2], yl[s2], dg[jt]);
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {  // + b1, GELU, GELU'
+    const float bs[4] = {bb[jt].x, bb[jt].y, bb[jt].z, bb[jt].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float gd;
+      gelu_fast(u[jt][r] + bs[r], gv[4 * jt + r], gd);
+      du[4 * jt + r] = dg[jt][r] * gd;
+    }
+  }
+  store_g_du(gv, du, grow, drow);
+  bf16x8 dh, dl;
+  split8(du, dh, dl);
+  // dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
+  // i.e. rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of the W1 chunk at
+  // column 16 j + t: two transposed reads per plane
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int o = w1t_tr_off(j, lane);
+    dx[j] = mfma16_x3(tr_pair(w1h + o), tr_pair(w1l + o), dh, dl, dx[j]);
+  }
+}
+
+// STAMP (bench.py's in-graph timing only, ghm_mlp_bwd_rc_x3_stamped; 1 and 2 are
+// two identical twins, so that a rocprofv3 trace tells bench.py's two
+// measurements apart): thread 0
 // of each workgroup writes the 100 MHz constant clock (s_memrealtime) at its
 // start and after its last store to stamps[2 blockIdx.x + {0, 1}]; the launch
 // spans min(start) .. max(end).  Nothing else differs.
-template <int NW, bool STAMP = false>
+template <int NW, int STAMP = 0>
 __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
     const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
@@ -691,54 +794,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
     issue_fence();
-    {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
-      const int cn = c + 1 < NC ? c + 1 : NC - 1;
-      fill_r32t_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, sw1h(cur ^ 1), sw1l(cur ^ 1));
-      fill_r32_w8<NW>(W2T + cn * 32 * GHM_D, GHM_D, PK_W, sw2h(cur ^ 1), sw2l(cur ^ 1));
-    }
-    f32x4 u[2], dg[2];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      u[jt] = zero4();
-      dg[jt] = zero4();
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-        const int o1 = r32t_off(16 * jt + t, 4 * s2 + g), o = r32_off(16 * jt + t, 4 * s2 + g);
-        u[jt] = mfma16_x3(ldsb8(sw1h(cur) + o1), ldsb8(sw1l(cur) + o1), xh[s2], xl[s2], u[jt]);
-        dg[jt] = mfma16_x3(ldsb8(sw2h(cur) + o), ldsb8(sw2l(cur) + o), yh[s2], yl[s2], dg[jt]);
-      }
-    }
-    float gv[8], du[8];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {  // + b1, GELU, GELU'
-      const float bs[4] = {bb[jt].x, bb[jt].y, bb[jt].z, bb[jt].w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float gd;
-        gelu_fast(u[jt][r] + bs[r], gv[4 * jt + r], gd);
-        du[4 * jt + r] = dg[jt][r] * gd;
-      }
-    }
-    {  // G (for dW2) and dU (for dW1): 4 stores per wave
-      float* grow = Gout + mc * GHM_F + 32 * c + 4 * g;
-      float* drow = dU + mc * GHM_F + 32 * c + 4 * g;
-      st4(grow, gv[0], gv[1], gv[2], gv[3]);
-      st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
-      st4(drow, du[0], du[1], du[2], du[3]);
-      st4(drow + 16, du[4], du[5], du[6], du[7]);
-    }
-    bf16x8 dh, dl;
-    split8(du, dh, dl);
-    // dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
-    // i.e. rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of the W1 chunk at
-    // column 16 j + t: two transposed reads per plane
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int o = w1t_tr_off(j, lane);
-      dx[j] = mfma16_x3(tr_pair(sw1h(cur) + o), tr_pair(sw1l(cur) + o), dh, dl, dx[j]);
-    }
+    const int cn = c + 1 < NC ? c + 1 : NC - 1;  // branch-free: the last iteration refills chunk NC-1
+    mlp_bwd_rc_chunk<NW>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
+                         W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, Gout + mc * GHM_F + 32 * c + 4 * g,
+                         dU + mc * GHM_F + 32 * c + 4 * g, t, g, lane);
     // retire this iteration's LDS-DMA fills: vmcnt(0), also covering the G / dU
-    // stores issued after them (see k_ln_mlp_fwd_x3b)
+    // stores issued after them (see k_ln_mlp_fwd_x3b).  Storing them one chunk
+    // later instead, so this wait would not cover fresh stores, measured slower
+    // (isolated 119 -> 130 us, profiles/r3_ab2).
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   // LN2 backward: lane holds dX2 of features d = 16 j + 4 g + r
@@ -932,16 +995,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
 template <int STATS>
 __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
     const float* __restrict__ dqkv, const float* __restrict__ H, const float* __restrict__ lnw,
-    const __bf16* __restrict__ pack, const float* __restrict__ dHmid, float* __restrict__ dH,
+    const __bf16* pack, const float* __restrict__ dHmid, float* __restrict__ dH,
     float* __restrict__ part_ln, int64_t M, float eps, const float2* __restrict__ stats,
     float4* __restrict__ dbg) {
-  __shared__ __attribute__((aligned(16))) __bf16 swh[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 swl[2][32 * PB1];
+  // weight tiles of W^T ([128 d][384], 32 d-rows x 128 columns) by LDS-DMA into
+  // a double-buffered R32 ring, as k_ln_qkv_fwd_x3
+  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PLANE];
   __shared__ float red[2 * 4 * GHM_D];
   __shared__ __attribute__((aligned(16))) float gam[GHM_D];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
   const bool active = m0 < M;
+  const __bf16* W = pack + PK_QKV_T;  // [128 d][384]
+  fill_r32_w8<4>(W, 3 * GHM_D, PK_QKV, lds, lds + PLANE);  // tile 0, in flight over the prologue
   for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
   if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
   const int64_t m = m0 + j;
@@ -966,11 +1032,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
   f32x16 dx[4];
 #pragma unroll
   for (int it = 0; it < 4; ++it) dx[it] = zero16();
-  const __bf16* W = pack + PK_QKV_T;  // [128 d][384]
-  uint4 st[2 * stage_bf_n<32, GHM_D>()];
-  stage_bf_load<32, GHM_D>(st, W, 3 * GHM_D, PK_QKV);
-  stage_bf_store<32, GHM_D, PB1>(st, swh[0], swl[0]);
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll 1
   for (int mat = 0; mat < 3; ++mat) {
     bf16x8 gh[8], gl[8];
@@ -978,13 +1040,11 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int b = mat * 4 + it, cur = b & 1;
-      {
-        const int nb = b + 1 < 12 ? b + 1 : 11;  // tile nb: rows 32*(nb&3).., columns 128*(nb>>2)..
-        stage_bf_load<32, GHM_D>(st, W + (nb & 3) * 32 * (3 * GHM_D) + (nb >> 2) * GHM_D, 3 * GHM_D, PK_QKV);
-      }
-      if (active) dx[it] = proj_x3(swh[cur] + j * PB1 + 64 * h, swl[cur] + j * PB1 + 64 * h, gh, gl, dx[it]);
-      stage_bf_store<32, GHM_D, PB1>(st, swh[cur ^ 1], swl[cur ^ 1]);
-      __syncthreads();
+      const int nb = b + 1 < 12 ? b + 1 : 11;  // tile nb: rows 32*(nb&3).., columns 128*(nb>>2)..
+      dx[it] = qkv_tile_x3(lds + 2 * PLANE * cur, lds + 2 * PLANE * (cur ^ 1),
+                           W + (nb & 3) * 32 * (3 * GHM_D) + (nb >> 2) * GHM_D, 3 * GHM_D, j, h, active, gh, gl,
+                           dx[it]);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
   }
   if (STATS == 4 && valid && h == 0) dbg[m] = make_float4(loaded.x, loaded.y, lnst.x, lnst.y);
@@ -1004,7 +1064,9 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 // wave), splits them and writes [column][token] bf16 images (64-B rows, 16-B
 // chunks XOR-swizzled by row so the operand reads are conflict-free), so a
 // lane's 8-token operand fragment is one ds_read_b128.  Workgroup = 128 x 128
-// output tile, 4 waves as 2 x 2 of 64 x 64.
+// output tile, NWV = 4 waves as 2 x 2 of 64 x 64, or NWV = 8 waves as 2 x 4 of
+// 64 x 32 (each thread then stages 8 tokens of its column: two waves per SIMD,
+// so one wave's staging VALU runs beside its partner's MFMAs).
 // ---------------------------------------------------------------------------
 // 16-B chunk ch of image row r at ch ^ s(r), s(r) = bit 2 of r | (bit 1 ^ bit 3) << 1:
 // the operand reads (ds_read_b128, rows 32n + j) stay conflict-free and the
@@ -1014,8 +1076,8 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 __device__ __forceinline__ int wg_swz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
 __device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (ch ^ wg_swz(row)); }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A, int lda,
+template <int MODE, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __restrict__ A, int lda,
                                                      const float* __restrict__ Bs, int ldb,
                                                      const float2* __restrict__ stats,
                                                      const float* __restrict__ lnw,
@@ -1028,8 +1090,12 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   __shared__ __attribute__((aligned(16))) __bf16 sAl[2][IMG];
   __shared__ __attribute__((aligned(16))) __bf16 sBh[2][IMG];
   __shared__ __attribute__((aligned(16))) __bf16 sBl[2][IMG];
+  constexpr int NB = NWV == 8 ? 1 : 2;    // 32-column b blocks per wave
+  constexpr int NBW = 4 / NB;              // waves along b
+  constexpr int TPT = 64 / NWV;            // tokens per thread and step (16 or 8)
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int wa = (wave >> 1) * 64, wb = (wave & 1) * 64;
+  const int wa = (wave / NBW) * 64, wb = (wave % NBW) * 32 * NB;
   // XCD-aware order (linear id w runs on XCD w % 8): each XCD walks a contiguous
   // run of (tile, split) pairs, tiles fastest, so the tiles of one token range
   // read their shared operand through the same L2
@@ -1046,7 +1112,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   int64_t m_end = m_begin + tok_per_split;
   if (m_end > M) m_end = M;
   const int nsteps = static_cast<int>((m_end - m_begin + KT - 1) / KT);
-  // staging role: column c of the tile, tokens 16*th .. 16*th + 15 of the step.
+  // staging role: column c of the tile, tokens TPT*th .. TPT*th + TPT - 1 of the step.
   // th is wave-uniform: readfirstlane makes every row index and row pointer
   // scalar, so a load is one global_load_dword (SGPR row base + the lane's
   // column offset) with no per-lane 64-bit address arithmetic or clamping.
@@ -1069,8 +1135,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
   // each load has two compute phases to land (one phase, ~0.4 us of MFMAs, is
   // well under the loaded HBM latency).
   struct Slot {
-    float va[16], vb[16];
-    float2 st;  // MODE 2: LayerNorm statistics of the slot's row (lane & 15)
+    float va[TPT], vb[TPT];
+    float2 st;  // MODE 2: LayerNorm statistics of the slot's row (lane & (TPT - 1))
     int nvalid;
   };
   Slot S0, S1;
@@ -1085,20 +1151,20 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
                                                      0x7fffffff, 0x00020000);
   const int voa = 4 * ca, vob = 4 * cb;
   auto load = [&](Slot& S, int step) {
-    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + 16 * th;  // uniform
+    const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + TPT * th;  // uniform
     const int64_t left = m_end - mb;
-    S.nvalid = left < 0 ? 0 : (left > 16 ? 16 : static_cast<int>(left));
+    S.nvalid = left < 0 ? 0 : (left > TPT ? TPT : static_cast<int>(left));
     // rows past m_end re-read the last valid row (masked in store())
     const int64_t r0 = S.nvalid ? mb : m_begin;
     const int nv = __builtin_amdgcn_readfirstlane(S.nvalid > 0 ? S.nvalid : 1);
-    if (MODE == 2) {  // one vector load: lane l holds row (l & 15)'s (mean, rstd)
-      const int li = lane & 15;
+    if (MODE == 2) {  // one vector load: lane l holds row (l & (TPT - 1))'s (mean, rstd)
+      const int li = lane & (TPT - 1);
       S.st = ld_stats_sys(stats, r0 + (li < nv ? li : nv - 1));
     }
     const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * lda * 4));
     const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * ldb * 4));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < TPT; ++i) {
       const int ri = i < nv ? i : nv - 1;  // uniform
       S.va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, voa, sa + ri * lda * 4, 0));
       S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob, sb + ri * ldb * 4, 0));
@@ -1109,50 +1175,54 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
     if (MODE == 2) {  // row i's statistics broadcast from lane i (v_readlane)
       const int mx = __float_as_int(S.st.x), rx = __float_as_int(S.st.y);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < TPT; ++i) {
         const float mean = __int_as_float(__builtin_amdgcn_readlane(mx, i));
         const float rstd = __int_as_float(__builtin_amdgcn_readlane(rx, i));
         S.vb[i] = (S.vb[i] - mean) * rstd * gam + bet;
       }
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < TPT; ++i)
       if (i >= S.nvalid) S.va[i] = 0.f;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int half = 0; half < TPT / 8; ++half) {
       bf16x8 ah, al, bh, bl;
       split8(S.va + 8 * half, ah, al);
       split8(S.vb + 8 * half, bh, bl);
-      const int off = wg_img(c, 2 * th + half);
+      const int off = wg_img(c, (TPT / 8) * th + half);
       *reinterpret_cast<bf16x8*>(sAh[buf] + off) = ah;
       *reinterpret_cast<bf16x8*>(sAl[buf] + off) = al;
       *reinterpret_cast<bf16x8*>(sBh[buf] + off) = bh;
       *reinterpret_cast<bf16x8*>(sBl[buf] + off) = bl;
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bsum += S.va[i];
+    for (int i = 0; i < TPT; ++i) bsum += S.va[i];
   };
-  f32x16 acc[2][2];
+  f32x16 acc[2][NB];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) acc[i][k] = zero16();
+    for (int k = 0; k < NB; ++k) acc[i][k] = zero16();
   auto compute = [&](int cur) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 ah[2], al[2], bh[2], bl[2];
+      bf16x8 ah[2], al[2], bh[NB], bl[NB];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int oa = wg_img(wa + 32 * i + j, 2 * s + h), ob = wg_img(wb + 32 * i + j, 2 * s + h);
+        const int oa = wg_img(wa + 32 * i + j, 2 * s + h);
         ah[i] = ldsb8(sAh[cur] + oa);
         al[i] = ldsb8(sAl[cur] + oa);
-        bh[i] = ldsb8(sBh[cur] + ob);
-        bl[i] = ldsb8(sBl[cur] + ob);
+      }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const int ob = wg_img(wb + 32 * k + j, 2 * s + h);
+        bh[k] = ldsb8(sBh[cur] + ob);
+        bl[k] = ldsb8(sBl[cur] + ob);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) acc[i][k] = mfma_x3(ah[i], al[i], bh[k], bl[k], acc[i][k]);
+        for (int k = 0; k < NB; ++k) acc[i][k] = mfma_x3(ah[i], al[i], bh[k], bl[k], acc[i][k]);
     }
   };
   // The loads are unconditional (past the last step they re-read it, L2-hot)
@@ -1184,13 +1254,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x3(const float* __restrict__ A
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int k = 0; k < 2; ++k) pz[(ra + 32 * i) * Bcols + b_base + 32 * k + j] = acc[i][k][r];
+      for (int k = 0; k < NB; ++k) pz[(ra + 32 * i) * Bcols + b_base + 32 * k + j] = acc[i][k][r];
   }
   if (bias_part && tby == 0) {
     float* red = reinterpret_cast<float*>(&sAh[0][0]);  // the ring is idle after the last barrier
     red[th * 128 + c] = bsum;
     __syncthreads();
-    if (th == 0) bias_part[static_cast<int64_t>(tbz) * Acols + a_blk + c] = red[c] + red[128 + c];
+    if (th == 0)
+      bias_part[static_cast<int64_t>(tbz) * Acols + a_blk + c] =
+          NWV == 8 ? (red[c] + red[128 + c]) + (red[256 + c] + red[384 + c]) : red[c] + red[128 + c];
   }
 }
 
@@ -1832,21 +1904,32 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
 extern "C" int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid, const float* stats,
                                          const float* ln_w, const float* ln_b, const void* pack, const float* b1,
                                          float* G, float* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
-                                         uint64_t* stamps, void* stream) {
+                                         uint64_t* stamps, int twin, void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln && stamps,
             "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
+  GHM_CHECK(twin == 1 || twin == 2, "twin must be 1 or 2");
   const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
-  if (rc_waves(M) == 8)
-    hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, true>), dim3(nblk), dim3(512), 0, ghm_stream(stream), dH_out, H_mid,
-                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
-                       G, dU, dH_mid, part_ln, M, stamps);
-  else
-    hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, true>), dim3(nblk), dim3(256), 0, ghm_stream(stream), dH_out, H_mid,
-                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
-                       G, dU, dH_mid, part_ln, M, stamps);
+  const float2* st = reinterpret_cast<const float2*>(stats);
+  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
+  hipStream_t s = ghm_stream(stream);
+  if (rc_waves(M) == 8) {
+    if (twin == 1)
+      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, 1>), dim3(nblk), dim3(512), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
+                         dU, dH_mid, part_ln, M, stamps);
+    else
+      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, 2>), dim3(nblk), dim3(512), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
+                         dU, dH_mid, part_ln, M, stamps);
+  } else {
+    if (twin == 1)
+      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, 1>), dim3(nblk), dim3(256), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
+                         dU, dH_mid, part_ln, M, stamps);
+    else
+      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, 2>), dim3(nblk), dim3(256), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
+                         dU, dH_mid, part_ln, M, stamps);
+  }
   return ghm_launch_status();
 }
 
@@ -1903,12 +1986,20 @@ extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B,
   dim3 grid(A_cols / 128, B_cols / 128, static_cast<unsigned>(nsplit));
   hipStream_t s = ghm_stream(stream);
   const float2* st = reinterpret_cast<const float2*>(stats);
-  if (b_mode == 0)
+  if (GHM_WGRAD_WAVES == 8) {
+    if (b_mode == 0)
+      hipLaunchKernelGGL((k_wgrad_x3<0, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part,
+                         M, tok_per_split, A_cols, B_cols);
+    else
+      hipLaunchKernelGGL((k_wgrad_x3<2, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part,
+                         M, tok_per_split, A_cols, B_cols);
+  } else if (b_mode == 0) {
     hipLaunchKernelGGL(k_wgrad_x3<0>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
                        tok_per_split, A_cols, B_cols);
-  else
+  } else {
     hipLaunchKernelGGL(k_wgrad_x3<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
                        tok_per_split, A_cols, B_cols);
+  }
   return ghm_launch_status();
 }
 

@@ -98,7 +98,7 @@ HIP_SIGNATURES = {
     "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_mlp_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_mlp_bwd_rc_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
-    "ghm_mlp_bwd_rc_x3_stamped": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p, _p],
+    "ghm_mlp_bwd_rc_x3_stamped": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p, _i, _p],
     "ghm_qkv_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_qkv_bwd_x3_probe": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _i, _p],
     "ghm_wgrad_x3": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],

@@ -412,7 +412,7 @@ class EncoderPlan:
                         _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]), _ptr(p[f"_mlps.{l}.0.bias"]),
                         _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN)
                 if getattr(self, "stamps", None) is not None:  # bench.py's in-graph timing
-                    c("ghm_mlp_bwd_rc_x3_stamped", *args, _ptr(self.stamps[l]), s)
+                    c("ghm_mlp_bwd_rc_x3_stamped", *args, _ptr(self.stamps[l]), self.stamp_twin, s)
                 else:
                     c("ghm_mlp_bwd_rc_x3", *args, s)
             else:

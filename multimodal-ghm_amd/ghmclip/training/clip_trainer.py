@@ -8,13 +8,13 @@ Design:
   optimizer are two launches over 1.84 M floats;
 * every per-step scalar (lr_t, lr*wd) comes from a device table indexed by a
   device step counter, so the whole step is a static launch sequence that is
-  captured once into a HIP graph and replayed;
+  captured once (one linear HIP graph per phase and tower) and replayed;
 * the loss of every step is written on device into ``hist`` (no host sync per
   step; the host reads it at log intervals);
 * data parallel (optional): each rank owns a shard of the within-block index i
-  (the loss is a mean over i, model.py:906-907), grads are averaged with one
-  RCCL all-reduce of the flat buffer between the backward graph and the
-  optimizer graph.
+  (the loss is a mean over i, model.py:906-907), grads are averaged by two
+  bucketed RCCL all-reduces of the flat buffer (top layers while the lower
+  layers' backward runs, then the rest) before the optimizer.
 """
 import ctypes
 import os
@@ -154,6 +154,7 @@ class ClipTrainer:
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
         self.comm = torch.cuda.Stream(device=self.device)  # data-parallel bucket all-reduces
+        self._bwd_it = [None, None]  # the towers' running backward launch generators
         self._setup_guide(penalty, guide_trans)
 
     def _setup_guide(self, penalty, guide_trans):
@@ -218,85 +219,110 @@ class ClipTrainer:
         return hooks
 
     # -- the launch sequence -----------------------------------------------------
-    @staticmethod
-    def _advance(jobs, n=None, inter=True):
-        """Advance launch generators [(generator, stream), ...] by n yields each
-        (None: to exhaustion), every step issued under its own stream.  inter:
-        round-robin (the two towers' per-layer launches are issued — and, when
-        captured, become graph nodes — alternately), else one tower after the
-        other.  Exhausted generators are dropped from `jobs`."""
-        def step(job):
-            gen, st = job
-            with torch.cuda.stream(st):
-                try:
-                    next(gen)
-                    return True
-                except StopIteration:
-                    jobs.remove(job)
-                    return False
-        if inter:
-            k = 0
-            while jobs and (n is None or k < n):
-                for job in list(jobs):
-                    step(job)
-                k += 1
-        else:
-            for job in list(jobs):
-                k = 0
-                while (n is None or k < n) and step(job):
-                    k += 1
-
+    # A step is a fixed sequence of phases; the two towers' phases run on two
+    # streams (text: the current stream, image: a side stream), joined by stream
+    # waits:
+    #   fwd(text) || fwd(image) -> loss -> bwd_a(text) || bwd_a(image)
+    #   [-> DP bucket A all-reduce] -> bwd_b(text) || bwd_b(image) [-> bucket B] -> optim
+    # A tower's phase is a generator of pieces (the embedding, each encoder
+    # layer, the readout), and the two towers' pieces are issued alternately.
+    # Captured, every piece is its own small linear graph, replayed in the same
+    # alternation.  Why pieces: a HIP graph launch submits its kernel nodes from
+    # the host one by one (~7.5 us each), so the stream whose graph is launched
+    # second starts that much later: with the whole step in one two-branch graph
+    # (rounds 2-3) or one graph per tower and phase, the second tower started
+    # 120-250 us after the first in the forward and in the backward and ran its
+    # last layers alone (profiles/r3_v6, r3_ab3; tools/timeline.py).
     def _streams(self):
         main = torch.cuda.current_stream()
         side = main if os.environ.get("GHM_SERIAL_TOWERS") == "1" else self.side
-        return main, side, os.environ.get("GHM_TOWER_ORDER", "interleave") == "interleave"
+        return main, side
 
-    def _fwd_bwd_a(self, flush):
-        """Forward of both towers, the loss, and the backward of the readouts and
-        of the top dp_top layers; flush: reduce their parameter-gradient partials
-        (the data-parallel bucket A is final after this part).  Text tower on the
-        current stream, image tower on a side stream (fork / join through stream
-        waits, which graph capture records as edges), so the two towers' launches
-        overlap and fill each other's tails; the towers' launches are issued
-        layer by layer alternately ($GHM_TOWER_ORDER = "interleave", default) or
-        one tower after the other ("sequential")."""
-        main, side, inter = self._streams()
-        pt, pi = self.plans
-        (tp, tg, _, _), (ip, ig, _, _) = self.views
-        side.wait_stream(main)
-        s = ctypes.c_void_p(main.cuda_stream)
-        self._advance([(pi.forward_iter(ip), side), (pt.forward_iter(tp), main)], inter=inter)
+    def _fwd_gen(self, tower):
+        """Forward of one tower (+ its guide targets and penalty partials) as
+        pieces: embedding, each layer, readout (+ guide)."""
+        plan, p = self.plans[tower], self.views[tower][0]
+        for _ in plan.forward_iter(p):
+            yield
         if self.guide:
-            with torch.cuda.stream(side):
-                self._guide_fwd(1, ctypes.c_void_p(side.cuda_stream))
-            self._guide_fwd(0, s)
-        main.wait_stream(side)
+            self._guide_fwd(tower, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+
+    def _loss(self):
+        pt, pi = self.plans
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
         if self.guide:
             _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.n_seq, self.penalty,
                          _p(self.loss_out), _p(self.phist), _p(self.step_ctr), s)
-        side.wait_stream(main)
-        self._bwd = [(pi.backward_iter(ip, ig, layer_grad=self._guide_hooks(1)), side),
-                     (pt.backward_iter(tp, tg, layer_grad=self._guide_hooks(0)), main)]
-        self._advance(self._bwd, 1 + self.dp_top, inter=inter)  # readout + the top layers
+
+    def _bwd_a_gen(self, tower, flush):
+        """Backward of one tower's readout and top dp_top layers as pieces; flush:
+        reduce their parameter-gradient partials at the end (the data-parallel
+        bucket A of this tower is final after it)."""
+        plan = self.plans[tower]
+        p, g = self.views[tower][0], self.views[tower][1]
+        it = plan.backward_iter(p, g, layer_grad=self._guide_hooks(tower))
+        self._bwd_it[tower] = it
+        for k in range(1 + self.dp_top):
+            next(it)
+            if k < self.dp_top:
+                yield  # (the last piece ends with the generator: no empty piece)
         if flush:
-            for plan, st in ((pi, side), (pt, main)):
-                with torch.cuda.stream(st):
-                    plan.flush_pending()
-        main.wait_stream(side)
+            plan.flush_pending()
 
-    def _fwd_bwd_b(self):
-        """The rest of the backward (layers below the top dp_top, embeddings, the
-        final partial reductions)."""
-        main, side, inter = self._streams()
+    def _bwd_b_gen(self, tower):
+        """The rest of one tower's backward as pieces (lower layers; the last
+        piece also runs the embeddings and the final partial reductions)."""
+        for _ in self._bwd_it[tower]:
+            yield
+
+    def _phase(self, genf, graphs=None, key=None):
+        """Run a two-tower phase: the pieces of genf(1) (image, side stream) and
+        genf(0) (text, current stream) alternately, joined back into the current
+        stream; graphs: replay the captured piece graphs[(key, tower)] instead."""
+        main, side = self._streams()
+        st = {1: side, 0: main}
         side.wait_stream(main)
-        self._advance(self._bwd, inter=inter)
+        if graphs is None:
+            live = {1: genf(1), 0: genf(0)}
+            while live:
+                for t in (1, 0):
+                    if t in live:
+                        with torch.cuda.stream(st[t]):
+                            try:
+                                next(live[t])
+                            except StopIteration:
+                                del live[t]
+        else:
+            pieces = {t: graphs[(key, t)] for t in (1, 0)}
+            for i in range(max(len(v) for v in pieces.values())):
+                for t in (1, 0):
+                    if i < len(pieces[t]):
+                        with torch.cuda.stream(st[t]):
+                            pieces[t][i].replay()
         main.wait_stream(side)
 
-    def _fwd_bwd(self):
-        self._fwd_bwd_a(flush=False)
-        self._fwd_bwd_b()
+    def _single(self, fn, graphs=None, key=None):
+        if graphs is None:
+            fn()
+        else:
+            graphs[key].replay()
+
+    def _run(self, graphs=None):
+        """One step (eager, or by replaying `graphs` from _capture_graphs)."""
+        dp = self._dp()
+        self._phase(self._fwd_gen, graphs, "fwd")
+        self._single(self._loss, graphs, "loss")
+        self._phase(lambda t: self._bwd_a_gen(t, flush=dp), graphs, "bwd_a")
+        if dp:
+            bucket_a, bucket_b = self.dp_buckets()
+            self._allreduce_ranges(bucket_a)
+        self._phase(self._bwd_b_gen, graphs, "bwd_b")
+        if dp:
+            self._allreduce_ranges(bucket_b)
+            torch.cuda.current_stream().wait_stream(self.comm)
+        self._single(self._optim, graphs, "optim")
 
     def _optim(self):
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -308,7 +334,7 @@ class ClipTrainer:
 
     def dp_buckets(self):
         """([(start, end) of bucket A per tower], [... bucket B]) of the flat
-        gradient: A = the top dp_top layers' gradients (final after _fwd_bwd_a),
+        gradient: A = the top dp_top layers' gradients (final after the bwd_a phase),
         B = the rest."""
         return dp_bucket_ranges(self.bucket_a, self.n_params)
 
@@ -327,7 +353,7 @@ class ClipTrainer:
     def set_tokens(self, t_tokens, i_tokens):
         """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
         the plans' token buffers, async on the current stream (the side stream
-        is ordered after it by the fork in _fwd_bwd)."""
+        is ordered after it by the fork of each phase)."""
         self.plans[0].tokens.copy_(t_tokens, non_blocking=True)
         self.plans[1].tokens.copy_(i_tokens, non_blocking=True)
 
@@ -337,58 +363,49 @@ class ClipTrainer:
         the comm stream while the rest of the backward runs; bucket B follows."""
         if self.steps_done >= self.n_sched:
             raise RuntimeError("schedule exhausted")
-        if not self._dp():
-            if self.graphs is not None:
-                self.graphs[0].replay()
-            else:
-                self._fwd_bwd()
-                self._optim()
-        else:
-            bucket_a, bucket_b = self.dp_buckets()
-            if self.graphs is not None:
-                self.graphs[0].replay()
-            else:
-                self._fwd_bwd_a(flush=True)
-            self._allreduce_ranges(bucket_a)
-            if self.graphs is not None:
-                self.graphs[1].replay()
-            else:
-                self._fwd_bwd_b()
-            self._allreduce_ranges(bucket_b)
-            torch.cuda.current_stream().wait_stream(self.comm)
-            if self.graphs is not None:
-                self.graphs[2].replay()
-            else:
-                self._optim()
+        self._run(self.graphs)
         self.steps_done += 1
+
+    def _capture_graphs(self):
+        """{(phase, tower): [piece graphs] | phase: graph}: every piece of every
+        phase captured as its own linear graph (see the launch-sequence notes)."""
+        graphs = {}
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        dp = self._dp()
+
+        def one(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                fn()
+            return g
+
+        def pieces(gen):
+            out, done = [], False
+            while not done:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    try:
+                        next(gen)
+                    except StopIteration:
+                        done = True
+                out.append(g)
+            return out
+        for t in (0, 1):
+            graphs[("fwd", t)] = pieces(self._fwd_gen(t))
+        graphs["loss"] = one(self._loss)
+        for t in (0, 1):
+            graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=dp))
+        for t in (0, 1):
+            graphs[("bwd_b", t)] = pieces(self._bwd_b_gen(t))
+        graphs["optim"] = one(self._optim)
+        torch.cuda.current_stream().wait_stream(s)
+        return graphs
 
     def capture(self):
         """Capture the step into HIP graphs (call after >= 1 eager step so all
-        lazy initialisation has happened).  Replays reuse the staged tokens.
-        One process: fwd/bwd and the optimizer are one graph (one launch, no
-        host gap between them).  Data parallel: three graphs (forward + top of
-        the backward, rest of the backward, optimizer) with the two bucket
-        all-reduces between them."""
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            if self._dp():
-                ga, gb, gc = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, stream=s):
-                    self._fwd_bwd_a(flush=True)
-                with torch.cuda.graph(gb, stream=s):
-                    self._fwd_bwd_b()
-                with torch.cuda.graph(gc, stream=s):
-                    self._optim()
-                graphs = (ga, gb, gc)
-            else:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s):
-                    self._fwd_bwd()
-                    self._optim()
-                graphs = (g,)
-        torch.cuda.current_stream().wait_stream(s)
-        self.graphs = graphs
+        lazy initialisation has happened).  Replays reuse the staged tokens."""
+        self.graphs = self._capture_graphs()
 
     # -- host-side views -----------------------------------------------------------
     def loss_history(self, upto=None):

@@ -1,0 +1,19 @@
+# usage: bash tools/gpu_abenv.sh TAG "TESTS" SETTING... : GPU tests (in-tree lib), then alternating 200-step
+#        CLIP benches, one per SETTING ("-" = defaults, else VAR=VAL[,VAR=VAL...])
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=$1; TESTS=$2; shift 2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread $TESTS > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 2; }
+  tail -2 $OUT/tests.log
+fi
+for i in 1 2 3; do
+  for v in "$@"; do
+    if [ "$v" = "-" ]; then E=""; else E=$(echo $v | tr ',' ' '); fi
+    env $E timeout -k 10 200 python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-final-risk > $OUT/b.json 2> $OUT/b.err || { tail -5 $OUT/b.err; exit 3; }
+    echo "$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/b.json)"
+  done
+done | tee $OUT/ab.txt
+echo done
