@@ -557,8 +557,11 @@ def main():
     # here inside graph-replayed steps
     prof_path, prof = profiled_kernels()
     top = max(prof, key=lambda k: prof[k][0]) if prof else None
-    dom = top.split("<")[0] if top and top.split("<")[0] in DOMINANT_CANDIDATES else "k_mlp_bwd_rc_x3"
-    dom_inst = top if top and top.split("<")[0] == dom else None
+    # the largest single call site: k_wgrad_x3<2, .> totals two different GEMMs (dW1 and
+    # dWqkv, one instantiation), so the candidates are the one-call-site kernels
+    cands = [k for k in prof if k.split("<")[0] in DOMINANT_CANDIDATES and not k.endswith(", 1>")]
+    dom_inst = max(cands, key=lambda k: prof[k][0]) if cands else None
+    dom = dom_inst.split("<")[0] if dom_inst else "k_mlp_bwd_rc_x3"
     if tr.precision != "x3" or not tr.plans[0].mlp_rc:
         dom = "k_ln_mlp_fwd_x3b" if tr.precision == "x3" else None
     dom_ms, dom_how, dom_ms_conc = None, None, None
@@ -632,8 +635,10 @@ def main():
                     "concurrent_note": "span of the same launches in the real step (twin k_mlp_bwd_rc_x3<8, 2>), "
                                        "where the other tower's kernels share the CUs",
                     "dominant_by": (f"{dom_inst}: {100 * prof[dom_inst][0] / ptot:.1f} % of kernel time in "
-                                    f"{os.path.relpath(prof_path, ROOT)}" if dom_inst in prof and ptot else
-                                    "default (no committed kernel stats)"),
+                                    f"{os.path.relpath(prof_path, ROOT)}, the largest single call site"
+                                    + (f" ({top}: {100 * prof[top][0] / ptot:.1f} % over two GEMMs)"
+                                       if top != dom_inst and top.startswith("k_wgrad") else "")
+                                    if dom_inst in prof and ptot else "default (no committed kernel stats)"),
                     "profile_avg_ms": None if prof_avg_ms is None else round(prof_avg_ms, 4),
                     "profile_frac": None if prof_avg_ms is None else round(dflop / (prof_avg_ms * 1e-3) / 1e3 / peak, 4),
                     "mfma_busy": mfma_busy(dom),

@@ -665,21 +665,14 @@ __device__ __forceinline__ void store_g_du(const float* gv, const float* du, flo
   st4(drow + 16, du[4], du[5], du[6], du[7]);
 }
 
-// One 32-unit hidden chunk of k_mlp_bwd_rc_x3: LDS-DMA fills of the next chunk
-// into ring buffer `nb`, products from the current buffer `cb`.  Both buffers
-// are __restrict__ parameters of one inlined function, so every access carries
-// alias-scope metadata that tells the waitcnt pass the DMA target and the
-// operand reads are disjoint: without it the compiler waited vmcnt(0) for the
-// just-issued fills before the first transposed read of the W1 image, which
-// exposed the whole L2 -> LDS latency in every chunk.
-template <int NW>
-__device__ __forceinline__ void mlp_bwd_rc_chunk(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
-                                                 const __bf16* W1n, const __bf16* W2Tn, const float4* bb,
-                                                 const bf16x8* xh, const bf16x8* xl, const bf16x8* yh,
-                                                 const bf16x8* yl, f32x4* dx, float* grow, float* drow, int t,
-                                                 int g, int lane) {
-  fill_r32t_w8<NW>(W1n, GHM_D, PK_W, nb, nb + PLANE);
-  fill_r32_w8<NW>(W2Tn, GHM_D, PK_W, nb + 2 * PLANE, nb + 3 * PLANE);
+// Pieces of one 32-unit hidden chunk of k_mlp_bwd_rc_x3 (operands from ring
+// buffer cb = [W1 hi | W1 lo | W2^T hi | W2^T lo]):
+//   rc_ud:  U = W1[c] LN2(Hmid)^T + b1 (recomputed), dG = W2^T[c] dY^T,
+//           G = GELU(U), dU = dG GELU'(U) -> HBM; returns dU split (dh, dl)
+//   rc_dx2: dX2^T += W1^T[:, c] dU^T
+__device__ __forceinline__ void rc_ud(const __bf16* cb, const float4* bb, const bf16x8* xh, const bf16x8* xl,
+                                      const bf16x8* yh, const bf16x8* yl, float* grow, float* drow, int t, int g,
+                                      bf16x8& dh, bf16x8& dl) {
   const __bf16* w1h = cb;
   const __bf16* w1l = cb + PLANE;
   const __bf16* w2h = cb + 2 * PLANE;
@@ -708,16 +701,40 @@ __device__ __forceinline__ void mlp_bwd_rc_chunk(const __bf16* __restrict__ cb, 
     }
   }
   store_g_du(gv, du, grow, drow);
-  bf16x8 dh, dl;
   split8(du, dh, dl);
-  // dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
-  // i.e. rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of the W1 chunk at
-  // column 16 j + t: two transposed reads per plane
+}
+
+// dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
+// i.e. rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of the W1 chunk at
+// column 16 j + t: two transposed reads per plane
+__device__ __forceinline__ void rc_dx2(const __bf16* cb, bf16x8 dh, bf16x8 dl, f32x4* dx, int lane) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int o = w1t_tr_off(j, lane);
-    dx[j] = mfma16_x3(tr_pair(w1h + o), tr_pair(w1l + o), dh, dl, dx[j]);
+    dx[j] = mfma16_x3(tr_pair(cb + o), tr_pair(cb + PLANE + o), dh, dl, dx[j]);
   }
+}
+
+// One chunk iteration: LDS-DMA fills of the next chunk into ring buffer `nb`,
+// then the products of chunk c from `cb`.  The buffers are __restrict__
+// parameters of one inlined function, so every access carries alias-scope
+// metadata that tells the waitcnt pass the DMA target and the operand reads are
+// disjoint (without it the compiler waited vmcnt(0) for the just-issued fills
+// before the first transposed read of the W1 image).  Tried and slower: waves
+// 4-7 one dX2 behind on a 3-buffer ring, so the two waves of a SIMD sit in
+// opposite MFMA / GELU phases (isolated 119 -> 124 us, step +1 %,
+// profiles/r3_ab5).
+template <int NW>
+__device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
+                                                const __bf16* W1n, const __bf16* W2Tn, const float4* bb,
+                                                const bf16x8* xh, const bf16x8* xl, const bf16x8* yh,
+                                                const bf16x8* yl, f32x4* dx, float* grow, float* drow, int t,
+                                                int g, int lane) {
+  fill_r32t_w8<NW>(W1n, GHM_D, PK_W, nb, nb + PLANE);
+  fill_r32_w8<NW>(W2Tn, GHM_D, PK_W, nb + 2 * PLANE, nb + 3 * PLANE);
+  bf16x8 dh, dl;
+  rc_ud(cb, bb, xh, xl, yh, yl, grow, drow, t, g, dh, dl);
+  rc_dx2(cb, dh, dl, dx, lane);
 }
 
 // STAMP (bench.py's in-graph timing only, ghm_mlp_bwd_rc_x3_stamped; 1 and 2 are
@@ -795,9 +812,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
     issue_fence();
     const int cn = c + 1 < NC ? c + 1 : NC - 1;  // branch-free: the last iteration refills chunk NC-1
-    mlp_bwd_rc_chunk<NW>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
-                         W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, Gout + mc * GHM_F + 32 * c + 4 * g,
-                         dU + mc * GHM_F + 32 * c + 4 * g, t, g, lane);
+    mlp_bwd_rc_iter<NW>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
+                        W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, Gout + mc * GHM_F + 32 * c + 4 * g,
+                        dU + mc * GHM_F + 32 * c + 4 * g, t, g, lane);
     // retire this iteration's LDS-DMA fills: vmcnt(0), also covering the G / dU
     // stores issued after them (see k_ln_mlp_fwd_x3b).  Storing them one chunk
     // later instead, so this wait would not cover fresh stores, measured slower
