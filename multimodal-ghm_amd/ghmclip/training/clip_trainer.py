@@ -222,8 +222,9 @@ class ClipTrainer:
     # A step is a fixed sequence of phases; the two towers' phases run on two
     # streams (text: the current stream, image: a side stream), joined by stream
     # waits:
-    #   fwd(text) || fwd(image) -> loss -> bwd_a(text) || bwd_a(image)
-    #   [-> DP bucket A all-reduce] -> bwd_b(text) || bwd_b(image) [-> bucket B] -> optim
+    #   fwd(text) || fwd(image) -> loss -> bwd(text) || bwd(image) -> optim
+    # (data parallel: bwd splits into bwd_a || bwd_a -> bucket A all-reduce on the
+    # comm stream -> bwd_b || bwd_b -> bucket B -> optim)
     # A tower's phase is a generator of pieces (the embedding, each encoder
     # layer, the readout), and the two towers' pieces are issued alternately.
     # Captured, every piece is its own small linear graph, replayed in the same
@@ -309,17 +310,25 @@ class ClipTrainer:
         else:
             graphs[key].replay()
 
+    def _bwd_gen(self, tower):
+        """The whole backward of one tower as pieces (one process: no bucket
+        boundary, so no join of the two towers in the middle of the backward)."""
+        yield from self._bwd_a_gen(tower, flush=False)
+        yield
+        yield from self._bwd_b_gen(tower)
+
     def _run(self, graphs=None):
         """One step (eager, or by replaying `graphs` from _capture_graphs)."""
         dp = self._dp()
         self._phase(self._fwd_gen, graphs, "fwd")
         self._single(self._loss, graphs, "loss")
-        self._phase(lambda t: self._bwd_a_gen(t, flush=dp), graphs, "bwd_a")
-        if dp:
+        if not dp:
+            self._phase(self._bwd_gen, graphs, "bwd")
+        else:
+            self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a")
             bucket_a, bucket_b = self.dp_buckets()
             self._allreduce_ranges(bucket_a)
-        self._phase(self._bwd_b_gen, graphs, "bwd_b")
-        if dp:
+            self._phase(self._bwd_b_gen, graphs, "bwd_b")
             self._allreduce_ranges(bucket_b)
             torch.cuda.current_stream().wait_stream(self.comm)
         self._single(self._optim, graphs, "optim")
@@ -394,10 +403,14 @@ class ClipTrainer:
         for t in (0, 1):
             graphs[("fwd", t)] = pieces(self._fwd_gen(t))
         graphs["loss"] = one(self._loss)
-        for t in (0, 1):
-            graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=dp))
-        for t in (0, 1):
-            graphs[("bwd_b", t)] = pieces(self._bwd_b_gen(t))
+        if not dp:
+            for t in (0, 1):
+                graphs[("bwd", t)] = pieces(self._bwd_gen(t))
+        else:
+            for t in (0, 1):
+                graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=True))
+            for t in (0, 1):
+                graphs[("bwd_b", t)] = pieces(self._bwd_b_gen(t))
         graphs["optim"] = one(self._optim)
         torch.cuda.current_stream().wait_stream(s)
         return graphs
