@@ -234,10 +234,15 @@ class ClipTrainer:
     # (rounds 2-3) or one graph per tower and phase, the second tower started
     # 120-250 us after the first in the forward and in the backward and ran its
     # last layers alone (profiles/r3_v6, r3_ab3; tools/timeline.py).
-    def _streams(self):
+    def _tower_streams(self):
+        """(current stream, text tower's stream, image tower's stream);
+        GHM_SERIAL_TOWERS=1 puts both towers on the current stream.  (Tried and
+        slower: each tower on its own CU-masked stream, hipExtStreamCreateWithCUMask
+        over halves / alternate CUs: 4.2 -> 4.95 / 4.5 ms per step, profiles/r3_ab8.)"""
         main = torch.cuda.current_stream()
-        side = main if os.environ.get("GHM_SERIAL_TOWERS") == "1" else self.side
-        return main, side
+        if os.environ.get("GHM_SERIAL_TOWERS") == "1":
+            return main, main, main
+        return main, main, self.side
 
     def _fwd_gen(self, tower):
         """Forward of one tower (+ its guide targets and penalty partials) as
@@ -282,9 +287,11 @@ class ClipTrainer:
         """Run a two-tower phase: the pieces of genf(1) (image, side stream) and
         genf(0) (text, current stream) alternately, joined back into the current
         stream; graphs: replay the captured piece graphs[(key, tower)] instead."""
-        main, side = self._streams()
-        st = {1: side, 0: main}
-        side.wait_stream(main)
+        main, s0, s1 = self._tower_streams()
+        st = {1: s1, 0: s0}
+        for x in (s0, s1):
+            if x != main:
+                x.wait_stream(main)
         if graphs is None:
             live = {1: genf(1), 0: genf(0)}
             while live:
@@ -302,7 +309,9 @@ class ClipTrainer:
                     if i < len(pieces[t]):
                         with torch.cuda.stream(st[t]):
                             pieces[t][i].replay()
-        main.wait_stream(side)
+        for x in (s0, s1):
+            if x != main:
+                main.wait_stream(x)
 
     def _single(self, fn, graphs=None, key=None):
         if graphs is None:
