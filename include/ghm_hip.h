@@ -219,6 +219,17 @@ int ghm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, in
                     float scale_div, void* stream);
 int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
                     int T, int D, float scale_div, void* stream);
+/* The same attention with the activation of the reference's get_activation
+ * (models/model.py:121-130, applied at :781; train_CLIP --clip_activation):
+ * act 0 softmax (identical to ghm_attn_fwd_x3 / ghm_attn_bwd_x3), 1 relu, 2
+ * gelu (erf form) of the scaled scores, keys past T contributing 0.  P holds
+ * act(s); for gelu the forward also writes GELU'(s) to Pd (same layout,
+ * required) and the backward reads it.  The backward is the fused one-kernel
+ * form (no dS buffer). */
+int ghm_attn_fwd_x3_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq, int T,
+                        int D, float scale_div, int act, void* stream);
+int ghm_attn_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dqkv,
+                        int64_t n_seq, int T, int D, float scale_div, int act, void* stream);
 /* As ghm_wgrad (b_mode 0 plain or 2 layernorm). */
 int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
                  const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,

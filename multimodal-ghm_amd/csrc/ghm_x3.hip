@@ -1388,12 +1388,18 @@ __device__ __forceinline__ void rows_dot_half(const __bf16* ih, const __bf16* il
   }
 }
 
-template <int NKT>
+// Attention activation (model.py:121-130, applied at :781): ACT_SOFTMAX, or the
+// elementwise ACT_RELU / ACT_GELU of the scaled scores (no normalisation; keys
+// past T contribute 0).  The backward needs act'(s): relu' = [P > 0]; for gelu
+// the forward stores GELU'(s) beside P (Pd, same layout).
+constexpr int ACT_SOFTMAX = 0, ACT_RELU = 1, ACT_GELU = 2;
+
+template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __restrict__ qkv,
                                                              const float* __restrict__ H,
                                                              float* __restrict__ Hmid,
                                                              float* __restrict__ P, int T,
-                                                             float scale_div) {
+                                                             float scale_div, float* __restrict__ Pd = nullptr) {
   constexpr int TP = NKT * 32;
   __shared__ __attribute__((aligned(16))) __bf16 sh[TP * AH_PITCH];
   __shared__ __attribute__((aligned(16))) __bf16 sl[TP * AH_PITCH];
@@ -1424,31 +1430,61 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   // argument: two VALU ops per score instead of an IEEE divide and a libm expf
   // (each ~10); both within 2 ulp, far below the split products' 2^-16
   const float inv_scale = 1.f / scale_div, l2e = 1.4426950408889634f;
-  float mx = -INFINITY;
+  float inv = 0.f;
+  if (ACT == ACT_SOFTMAX) {
+    float mx = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = 32 * kt + acc_row(r, h);
-      const float v = key < T ? s[kt][r] * inv_scale : -INFINITY;
-      s[kt][r] = v;
-      mx = fmaxf(mx, v);
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float v = key < T ? s[kt][r] * inv_scale : -INFINITY;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, xhalf(mx));
+    const float mx2 = mx * l2e;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
+        s[kt][r] = e;
+        sum += e;
+      }
+    }
+    sum += xhalf(sum);
+    inv = qv ? 1.f / sum : 0.f;
+  } else {  // elementwise activation of the scaled score; act' for the backward (gelu)
+    inv = qv ? 1.f : 0.f;
+    float* drow = ACT == ACT_GELU ? Pd + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD : nullptr;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      float dv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float x = s[kt][r] * inv_scale;
+        float a, d;
+        if (ACT == ACT_RELU) {
+          a = fmaxf(x, 0.f);
+          d = 0.f;
+        } else {
+          gelu_fast(x, a, d);
+        }
+        const bool ok = key < T && qv;
+        s[kt][r] = ok ? a : 0.f;
+        dv[r] = ok ? d : 0.f;
+      }
+      if (ACT == ACT_GELU) {
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+          st4(drow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+      }
     }
   }
-  mx = fmaxf(mx, xhalf(mx));
-  const float mx2 = mx * l2e;
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
-      s[kt][r] = e;
-      sum += e;
-    }
-  }
-  sum += xhalf(sum);
-  const float inv = qv ? 1.f / sum : 0.f;
   float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_PAD + q) * AT_PAD;
   bf16x8 ph[2 * NKT], pl[2 * NKT];
 #pragma unroll
@@ -1673,12 +1709,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_kv_x3(const float* __r
 // x TP bf16) + one operand-staging region (V half images, then K, then dO / Q
 // column blocks).
 // ---------------------------------------------------------------------------
-template <int NKT>
+template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __restrict__ qkv,
                                                              const float* __restrict__ P,
                                                              const float* __restrict__ dHmid,
                                                              float* __restrict__ dqkv, int T,
-                                                             float scale_div) {
+                                                             float scale_div,
+                                                             const float* __restrict__ Pd = nullptr) {
   constexpr int TP = NKT * 32, KS = TP / 16;
   constexpr int IMG = TP * TP;  // one [query][32] image per key block, NKT blocks: TP * 32 * NKT elements
   constexpr int STG = TP * AH_PITCH > 2 * TP * 32 ? TP * AH_PITCH : 2 * TP * 32;
@@ -1716,27 +1753,37 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
   }
   const float inv_scale = 1.f / scale_div;
   float delta = 0.f;
-  f32x16 p[NKT];
+  f32x16 p[NKT];  // softmax / relu: P; gelu: GELU'(s) (the factor dS needs)
+  const float* arow = ACT == ACT_GELU ? Pd + (prow - P) : prow;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) {
-      const float4 pv = *reinterpret_cast<const float4*>(prow + 32 * kt + quad_off(qd, h));
+      const float4 pv = *reinterpret_cast<const float4*>(arow + 32 * kt + quad_off(qd, h));
       p[kt][4 * qd + 0] = qv ? pv.x : 0.f;
       p[kt][4 * qd + 1] = qv ? pv.y : 0.f;
       p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
       p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
     }
+    if (ACT == ACT_SOFTMAX) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+      for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+    }
   }
-  delta += xhalf(delta);
+  if (ACT == ACT_SOFTMAX) delta += xhalf(delta);
   bf16x8 dh[2 * NKT], dl[2 * NKT];
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     float dv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
+    for (int r = 0; r < 16; ++r) {
+      if (ACT == ACT_SOFTMAX)
+        dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
+      else if (ACT == ACT_RELU)
+        dv[r] = (p[kt][r] > 0.f ? dp[kt][r] : 0.f) * inv_scale;
+      else
+        dv[r] = (p[kt][r] * dp[kt][r]) * inv_scale;
+    }
     // dS of this key block into the [query][32] images (row = this lane's query)
     __bf16* dsh = sim_h + (kt * TP + q) * 32;
     __bf16* dsl = sim_l + (kt * TP + q) * 32;
@@ -2032,6 +2079,63 @@ extern "C" int ghm_attn_fwd_x3(const float* qkv, const float* H, float* H_mid, f
     hipLaunchKernelGGL(k_attn_fwd_x3<2>, dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div);
   else
     hipLaunchKernelGGL(k_attn_fwd_x3<3>, dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div);
+  return ghm_launch_status();
+}
+
+// attention with an elementwise activation (model.py:121-130): act 0 softmax
+// (= ghm_attn_fwd_x3), 1 relu, 2 gelu (Pd: GELU'(s) [n_seq][96][96], required)
+template <int ACT>
+static void attn_fwd_x3_launch(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq,
+                               int T, float scale_div, hipStream_t s) {
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (T <= 32)
+    hipLaunchKernelGGL((k_attn_fwd_x3<1, ACT>), dim3(g), dim3(64), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+  else if (T <= 64)
+    hipLaunchKernelGGL((k_attn_fwd_x3<2, ACT>), dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+  else
+    hipLaunchKernelGGL((k_attn_fwd_x3<3, ACT>), dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+}
+extern "C" int ghm_attn_fwd_x3_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd,
+                                   int64_t n_seq, int T, int D, float scale_div, int act, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  GHM_CHECK(act >= 0 && act <= 2, "act must be 0 (softmax), 1 (relu) or 2 (gelu)");
+  GHM_CHECK(act != 2 || Pd, "gelu attention needs Pd");
+  hipStream_t s = ghm_stream(stream);
+  if (act == 0)
+    attn_fwd_x3_launch<ACT_SOFTMAX>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
+  else if (act == 1)
+    attn_fwd_x3_launch<ACT_RELU>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
+  else
+    attn_fwd_x3_launch<ACT_GELU>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
+  return ghm_launch_status();
+}
+
+template <int ACT>
+static void attn_bwd_x3_launch(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dqkv,
+                               int64_t n_seq, int T, float scale_div, hipStream_t s) {
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (T <= 32)
+    hipLaunchKernelGGL((k_attn_bwd_x3f<1, ACT>), dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dqkv, T, scale_div, Pd);
+  else if (T <= 64)
+    hipLaunchKernelGGL((k_attn_bwd_x3f<2, ACT>), dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dqkv, T, scale_div, Pd);
+  else
+    hipLaunchKernelGGL((k_attn_bwd_x3f<3, ACT>), dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dqkv, T, scale_div, Pd);
+}
+extern "C" int ghm_attn_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid,
+                                   float* dqkv, int64_t n_seq, int T, int D, float scale_div, int act,
+                                   void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dqkv, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  GHM_CHECK(act >= 0 && act <= 2, "act must be 0 (softmax), 1 (relu) or 2 (gelu)");
+  GHM_CHECK(act != 2 || Pd, "gelu attention needs Pd");
+  hipStream_t s = ghm_stream(stream);
+  if (act == 0)
+    attn_bwd_x3_launch<ACT_SOFTMAX>(qkv, P, Pd, dH_mid, dqkv, n_seq, T, scale_div, s);
+  else if (act == 1)
+    attn_bwd_x3_launch<ACT_RELU>(qkv, P, Pd, dH_mid, dqkv, n_seq, T, scale_div, s);
+  else
+    attn_bwd_x3_launch<ACT_GELU>(qkv, P, Pd, dH_mid, dqkv, n_seq, T, scale_div, s);
   return ghm_launch_status();
 }
 

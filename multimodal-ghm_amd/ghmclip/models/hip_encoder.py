@@ -80,7 +80,7 @@ def require_hip(t):
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", wgrad_target_blocks=256, precision=None,
-                 wgrad_min_tokens=None, defer_reduce=False):
+                 wgrad_min_tokens=None, defer_reduce=False, activation="softmax"):
         """defer_reduce: every layer keeps its own parameter-gradient partial
         buffers and backward() reduces all of them at its end in batched launches
         of up to 32 jobs (2 launches per encoder instead of one per layer), as a
@@ -100,6 +100,15 @@ class EncoderPlan:
         # separates the split-bf16 rounding from the curve's chaos)
         self.long_attn = n_token > 96
         pad = 192 if self.long_attn else 96
+        # attention activation (model.py:121-130): softmax, or elementwise relu / gelu
+        # on the split-bf16 one-sequence kernels (ghm_attn_{fwd,bwd}_x3_act)
+        acts = {"softmax": 0, "relu": 1, "gelu": 2}
+        if activation not in acts:
+            raise NotImplementedError(f"attention activation {activation!r}")
+        self.act = acts[activation]
+        if self.act and (self.precision != "x3" or self.long_attn):
+            raise NotImplementedError(f"attention activation {activation!r} runs on the split-bf16 (x3) kernels "
+                                      f"for sequences of <= 96 tokens only")
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -113,6 +122,8 @@ class EncoderPlan:
         self.Hmid = e(L, M, D_MODEL)
         self.qkv = e(L, M, 3 * D_MODEL)
         self.P = torch.zeros(L, N, pad, pad, dtype=f32, device=dev)
+        # gelu attention: GELU'(scores) saved beside P for the backward
+        self.Pd = torch.zeros(L, N, pad, pad, dtype=f32, device=dev) if self.act == 2 else None
         # x3: the MLP forward saves nothing and its backward recomputes U
         # (GHM_MLP_RECOMPUTE=1, default) or the forward saves G and GELU'(U) (=0)
         self.mlp_rc = self.precision == "x3" and os.environ.get("GHM_MLP_RECOMPUTE", "1") != "0"
@@ -236,6 +247,9 @@ class EncoderPlan:
                 elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
                     c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
                       _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+                elif self.act:
+                    c("ghm_attn_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                      None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
                 else:
                     c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                       N, T, D_MODEL, self.scale_div, s)
@@ -436,6 +450,10 @@ class EncoderPlan:
             elif self.long_attn:
                 c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
                   _ptr(self.dqkv), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+            elif self.act:
+                c("ghm_attn_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
+                  None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,
+                  self.scale_div, self.act, s)
             else:
                 c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
                   _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)

@@ -31,11 +31,12 @@ def seed_everything(seed: int):
 
 
 def get_activation(activation="softmax"):
-    """models/model.py:121-130.  Only softmax attention has a HIP kernel."""
-    if activation in ("relu", "gelu"):
-        raise NotImplementedError(f"attention activation '{activation}' has no HIP kernel (softmax only)")
-    if activation == "softmax":
-        return "softmax"
+    """models/model.py:121-130: the attention activation by name ("softmax",
+    "relu", "gelu"; anything else raises NotImplementedError, as the reference).
+    Returned as the name: the HIP attention kernels apply it (relu / gelu on the
+    split-bf16 kernels, sequences of <= 96 tokens)."""
+    if activation in ("softmax", "relu", "gelu"):
+        return activation
     raise NotImplementedError
 
 
@@ -137,13 +138,13 @@ class EncoderTransformer(nn.Module):
         self.precision = None
 
     def _plan(self, n_seq, T, device):
-        key = (n_seq, T, str(device), self.precision)
+        key = (n_seq, T, str(device), self.precision, self.activation)
         if key not in self._plans:
             self._plans.clear()  # keep one workspace set alive per module
             self._plans[key] = EncoderPlan(self.n_layer, T, n_seq, num_class=self.vocab_size,
                                            vocab=self.vocab_size, n_embd=self.n_embd,
                                            normalize_attn=self.normalize_attn, device=device,
-                                           precision=self.precision)
+                                           precision=self.precision, activation=self.activation)
         return self._plans[key]
 
     def _guided_layers(self):

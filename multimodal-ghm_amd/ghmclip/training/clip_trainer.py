@@ -129,7 +129,7 @@ class ClipTrainer:
         n_seq = batch_size * (K + 1)
         self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
                                   n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
-                                  precision=precision,
+                                  precision=precision, activation=getattr(m, "activation", "softmax"),
                                   defer_reduce=os.environ.get("GHM_DEFER_REDUCE", "1") != "0")
                       for m in self.models]
         self.precision = self.plans[0].precision

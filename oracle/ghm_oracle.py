@@ -195,16 +195,20 @@ def clip_bayes(sampler, n_eval=10000):
 
 
 # ----------------------------------------------------------------------------
-# encoder — models/model.py:690-808 (guide=False, softmax, normalize_attn=True)
+# encoder — models/model.py:690-808 (normalize_attn=True; attention activation
+# softmax | relu | gelu as get_activation, models/model.py:121-130)
 # ----------------------------------------------------------------------------
 class OracleEncoder(nn.Module):
     """Same module construction order as the reference so torch.manual_seed gives
     identical initial weights and identical state_dict keys (model.py:725-758)."""
 
     def __init__(self, n_token, num_class, n_embd=128, n_layer=12, n_mlp_multiplier=4,
-                 normalize_attn=True, guide=False, n_guided_layer=4):
+                 normalize_attn=True, guide=False, n_guided_layer=4, activation="softmax"):
         super().__init__()
         self.n_embd, self.normalize_attn = n_embd, normalize_attn
+        if activation not in ("softmax", "relu", "gelu"):
+            raise NotImplementedError(activation)  # :129-130
+        self.activation = activation
         self.vocab_size = num_class
         # guided layer flags, model.py:716-718,751-755
         gap = max(1, n_layer // n_guided_layer)
@@ -240,7 +244,12 @@ class OracleEncoder(nn.Module):
             S = torch.matmul(q(H1), k(H1).transpose(-2, -1))  # :778
             if self.normalize_attn:
                 S = S / np.sqrt(self.n_embd)  # :779-780
-            A = F.softmax(S, dim=-1)  # :781
+            if self.activation == "softmax":  # :781 through get_activation (:121-130)
+                A = F.softmax(S, dim=-1)
+            elif self.activation == "relu":
+                A = F.relu(S)
+            else:
+                A = F.gelu(S)
             H = H + torch.einsum("bij,bjd->bid", A, v(H1))  # :782
             H = H + mlp(ln2(H))  # :784-788
             if flag:  # :790-800 — the slice index never advances (_layer_count stays 0)
@@ -325,19 +334,20 @@ def lr_cosine(t, lr_max, lr_min, warmup_iters, total_iters):
 # ----------------------------------------------------------------------------
 # training loop — training/train_CLIP.py:62-201 (raw=True, guide=False)
 # ----------------------------------------------------------------------------
-def build_encoders(T=81, L=5, d=128, V=10, guide=False):
-    return (OracleEncoder(T, V, d, L, guide=guide), OracleEncoder(T, V, d, L, guide=guide))
+def build_encoders(T=81, L=5, d=128, V=10, guide=False, activation="softmax"):
+    return (OracleEncoder(T, V, d, L, guide=guide, activation=activation),
+            OracleEncoder(T, V, d, L, guide=guide, activation=activation))
 
 
 class OracleTrainer:
     def __init__(self, p=0.2, B=128, L=5, d=128, K=4, lr_max=3e-4, lr_min=3e-7, warmup=0,
                  total_iters=3000, max_norm=1.0, seed=224, seedtree=42, n_layer_tree=4,
-                 n_child=3, guide=False, penalty=1e-3):
+                 n_child=3, guide=False, penalty=1e-3, activation="softmax"):
         self.sampler = ClipSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], K=K,
                                          seedtree=seedtree)
         seed_everything(seed)  # :83
         T = n_child ** n_layer_tree
-        self.tm, self.im = build_encoders(T, L, d, guide=guide)
+        self.tm, self.im = build_encoders(T, L, d, guide=guide, activation=activation)
         self.guide, self.penalty = guide, penalty
         self.last_penalty = 0.0
         self.params = list(self.tm.parameters()) + list(self.im.parameters())

@@ -77,9 +77,9 @@ def sampler_fixture(p, B, nb, name):
     print("wrote", name)
 
 
-def build_models(T, L, d):
+def build_models(T, L, d, activation="softmax"):
     kw = dict(n_token=T, num_class=10, n_embd=d, n_layer=L, n_guided_layer=4, n_head=4,
-              n_mlp_multiplier=4, activation="softmax", mlp=True, normalize_attn=True,
+              n_mlp_multiplier=4, activation=activation, mlp=True, normalize_attn=True,
               layernorm=True, guide=False)
     return EncoderTransformer(**kw), EncoderTransformer(**kw)
 
@@ -88,11 +88,12 @@ def flat_state(model, prefix):
     return {f"{prefix}.{k}": v.detach().clone().numpy() for k, v in model.state_dict().items()}
 
 
-def step_fixture(name, L, d, B, nsteps, p=0.2, total_iters=3000, checksum_only=False):
-    """Mirror of train_CLIP.py:83-167 for a few steps on a small config."""
+def step_fixture(name, L, d, B, nsteps, p=0.2, total_iters=3000, checksum_only=False, activation="softmax"):
+    """Mirror of train_CLIP.py:83-167 for a few steps on a small config
+    (activation: train_CLIP --clip_activation, models/model.py:121-130)."""
     s = make_sampler(p)
     seed_everything(224)
-    tm, im = build_models(81, L, d)
+    tm, im = build_models(81, L, d, activation)
     loss = GuidedClipLoss(4, B, penalty=1e-3, guide=False)
     loss_nop = GuidedClipLoss(4, B, penalty=0, guide=False)
     params = list(tm.parameters()) + list(im.parameters())
@@ -126,6 +127,7 @@ def step_fixture(name, L, d, B, nsteps, p=0.2, total_iters=3000, checksum_only=F
         out.update({f"s{it}.post.{k}": v for k, v in flat_state(im, "i").items()})
     out["meta"] = np.array([L, d, B, nsteps, total_iters], dtype=np.int64)
     out["p"] = np.float64(p)
+    out["activation"] = np.array(activation)
     if checksum_only:
         # keep big configs small on disk: per-tensor (sum, sum of squares, abs-max)
         # for weight/grad tensors; full arrays for leaves, embeddings and scalars.

@@ -34,7 +34,8 @@ def test_sampler_bit_exact(name):
 def _check_steps(g, full):
     L, d, B, nsteps, total = [int(x) for x in g["meta"]]
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    tr = O.OracleTrainer(p=float(g["p"]), B=B, L=L, d=d, total_iters=total)
+    act = str(g["activation"]) if "activation" in g else "softmax"
+    tr = O.OracleTrainer(p=float(g["p"]), B=B, L=L, d=d, total_iters=total, activation=act)
     keys_t = list(tr.tm.state_dict().keys())
     for k in keys_t:  # initial weights identical => same init RNG order & key layout
         for pref, m in (("t", tr.tm), ("i", tr.im)):
@@ -92,6 +93,13 @@ def test_tiny_training_steps():
 
 def test_d128_training_steps():
     _check_steps(_load("clip_d128.npz"), full=False)
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+def test_d128_training_steps_attention_activation(act):
+    """train_CLIP --clip_activation=relu|gelu (model.py:121-130, :781), pinned to
+    the reference's own run (make_golden_act.py)."""
+    _check_steps(_load(f"clip_d128_{act}.npz"), full=False)
 
 
 @pytest.mark.parametrize("p", [0.2, 0.4])
@@ -160,3 +168,13 @@ def test_guided_training_steps():
         for pref, m in (("t", tr.tm), ("i", tr.im)):
             for k, v in m.state_dict().items():
                 np.testing.assert_allclose(v.numpy(), g[f"s{it}.post.{pref}.{k}"], rtol=1e-5, atol=1e-7)
+
+
+def test_get_activation_names():
+    """models/model.py:121-130: softmax, relu and gelu resolve (the HIP kernels
+    apply them); any other name raises NotImplementedError, as the reference."""
+    from ghmclip.models.model import get_activation
+    for a in ("softmax", "relu", "gelu"):
+        assert get_activation(a) == a
+    with pytest.raises(NotImplementedError):
+        get_activation("tanh")
