@@ -434,6 +434,20 @@ int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* 
  * (autograd's sum over batch rows, model.py:291-293, :330-347). */
 int64_t ghm_colsum_part_elems(int64_t M, int64_t N);
 int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, float* part, void* stream);
+/* Weighted column sums: out[c][n] = sum_m w(m, c) X[xrow(m)][n] and (if wsum)
+ * wsum[c] = sum_m w(m, c), c < C <= 64, N/4 dividing 256.  w(m, c) = W[m][c]
+ * (dense [M][C]; the readout weight and bias gradients from dlogits) or
+ * [tok[m] == c] when W is NULL (token ids [M]; the t_embedding / i_embedding
+ * gradients, autograd's embedding backward of model.py:238-241 and :444); xrow(m) = (m / rps) * seq_rows + off + m % rps.  Deterministic two
+ * stages; part scratch of ghm_wcolsum_part_elems(M, N, C) floats. */
+int64_t ghm_wcolsum_part_elems(int64_t M, int64_t N, int C);
+int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const float* X, int64_t rps, int64_t seq_rows, int64_t off,
+                int64_t M, int64_t N, float* out, float* wsum, float* part, void* stream);
+/* The readout Linear for C <= 64 classes, D in {128, 256} (model.py:332 _read_out):
+ * Y[m][c] = b[c] + sum_d X[m][d] W[c][d]; its data gradient
+ * dX[m][d] = sum_c dZ[m][c] W[c][d]. */
+int ghm_rows_linear(const float* X, const float* W, const float* b, float* Y, int64_t M, int D, int C, void* stream);
+int ghm_rows_linear_t(const float* dZ, const float* W, float* dX, int64_t M, int D, int C, void* stream);
 
 /* ---- zero-shot classification (figures/eval-zsc-risk.py:107-118) --------
  * logits[q][r][c] = log( mean_{k < n_list[q]} exp(<i_emb[r], t_emb[proto_idx[c][k]]>) )

@@ -374,8 +374,11 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ X
 // chunk partials summed per column: 64 float4 columns per workgroup (fewer when
 // N/4 < 64), the chunks split over 256 / columns thread groups, groups combined in
 // order through LDS
+// Columns from float4 index split4 on go to out2 (its first n2 floats): the
+// weighted sums' class totals ride in the same partial rows (ghm_wcolsum).
 __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int nchunk, int64_t N,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, float* __restrict__ out2,
+                                                      int64_t split4, int n2) {
   __shared__ float4 red[256];
   const int64_t N4 = N / 4;
   const int CB = N4 < 64 ? static_cast<int>(N4) : 64;
@@ -407,8 +410,166 @@ __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ 
       const float4 v = red[t + q * CB];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
-    reinterpret_cast<float4*>(out)[c4] = a;
+    if (c4 < split4) {
+      reinterpret_cast<float4*>(out)[c4] = a;
+    } else if (out2) {
+      const int j = static_cast<int>(4 * (c4 - split4));
+      const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (j + k < n2) out2[j + k] = v[k];
+    }
   }
+}
+
+// Weighted column sums (the readout and token-embedding weight gradients,
+// reference model.py _read_out / t_embedding through autograd):
+//   out[c][n] = sum_m w(m, c) X[xrow(m)][n],   wsum[c] = sum_m w(m, c)
+// w(m, c) = W[m][c] (dense, e.g. dlogits) or [tok[m] == c] (token ids: the one-hot
+// product without the one-hot matrix); xrow(m) = (m / rps) * seq_rows + off + m % rps
+// picks the text (or prefix) rows of each sequence.  Up to 16 classes per
+// workgroup (blockIdx.y selects the class block); rows split over 256 / (N/4)
+// thread groups combined in group order through LDS, chunk partials
+// [chunk][C*N | wsum] summed in chunk order by k_colsum_final: deterministic.
+template <bool TOK>
+__global__ __launch_bounds__(256) void k_wcolsum_part(const float* __restrict__ W, const uint8_t* __restrict__ tok,
+                                                      int C, const float* __restrict__ X, int64_t rps,
+                                                      int64_t seq_rows, int64_t off, int64_t M, int64_t N, int64_t R,
+                                                      int64_t ldp, float* __restrict__ part) {
+  __shared__ float4 red[256];
+  __shared__ float redw[64][16];  // up to 256 / (N/4) = 64 row groups
+  const int N4 = static_cast<int>(N / 4);
+  const int G = 256 / N4;
+  const int t = threadIdx.x, grp = t / N4, c4 = t % N4;
+  const int cb = static_cast<int>(blockIdx.y) * 16;
+  const int nc = C - cb < 16 ? C - cb : 16;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t r1 = r0 + R < M ? r0 + R : M;
+  float4 acc[16];
+  float ws[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    ws[c] = 0.f;
+  }
+  if (grp < G) {
+    for (int64_t row = r0 + grp; row < r1; row += G) {
+      const int64_t xr = (row / rps) * seq_rows + off + row % rps;
+      const float4 x = *reinterpret_cast<const float4*>(X + xr * N + 4 * c4);
+      if (TOK) {
+        const int k = static_cast<int>(tok[row]) - cb;
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (c == k) {
+            acc[c].x += x.x; acc[c].y += x.y; acc[c].z += x.z; acc[c].w += x.w;
+            ws[c] += 1.f;
+          }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (c < nc) {
+            const float w = W[row * C + cb + c];
+            acc[c].x += w * x.x; acc[c].y += w * x.y; acc[c].z += w * x.z; acc[c].w += w * x.w;
+            ws[c] += w;
+          }
+      }
+    }
+  }
+  float* dst = part + static_cast<int64_t>(blockIdx.x) * ldp;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c < nc) {  // uniform over the workgroup
+      red[t] = acc[c];
+      __syncthreads();
+      if (grp == 0) {
+        float4 a = acc[c];
+        for (int q = 1; q < G; ++q) {
+          const float4 v = red[t + q * N4];
+          a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        reinterpret_cast<float4*>(dst + static_cast<int64_t>(cb + c) * N)[c4] = a;
+      }
+      __syncthreads();
+    }
+  }
+  if (c4 == 0 && grp < G) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) redw[grp][c] = ws[c];
+  }
+  __syncthreads();
+  if (t < nc) {
+    float a = redw[0][t];
+    for (int q = 1; q < G; ++q) a += redw[q][t];
+    dst[static_cast<int64_t>(C) * N + cb + t] = a;
+  }
+}
+
+// Small-C linear rows (the VLM readout, reference model.py _read_out):
+//   Y[m][c] = b[c] + sum_d X[m][d] W[c][d]       (k_rows_linear, forward logits)
+// W [C][D] staged in LDS; 16 lanes per row, lane l holding features 4l + 64j..;
+// each class's 16 lane partials summed by a 4-step xor butterfly, lane c % 16
+// keeps class c.  Fixed order per row: deterministic.
+template <int D>
+__global__ __launch_bounds__(256) void k_rows_linear(const float* __restrict__ X, const float* __restrict__ W,
+                                                     const float* __restrict__ b, float* __restrict__ Y, int64_t M,
+                                                     int C) {
+  extern __shared__ float ws[];
+  constexpr int NJ = D / 64;
+  for (int i = threadIdx.x; i < C * D / 4; i += 256)
+    reinterpret_cast<float4*>(ws)[i] = reinterpret_cast<const float4*>(W)[i];
+  __syncthreads();
+  const int l = threadIdx.x & 15;
+  const int64_t m = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
+  if (m >= M) return;
+  float4 x[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) x[j] = *reinterpret_cast<const float4*>(X + m * D + 64 * j + 4 * l);
+  float out[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cq = 0; cq < 4; ++cq) {
+    for (int ci = 0; ci < 16; ++ci) {
+      const int c = 16 * cq + ci;
+      if (c >= C) break;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float4 w = reinterpret_cast<const float4*>(ws + c * D + 64 * j)[l];
+        s += x[j].x * w.x + x[j].y * w.y + x[j].z * w.z + x[j].w * w.w;
+      }
+      s += __shfl_xor(s, 8, 16);
+      s += __shfl_xor(s, 4, 16);
+      s += __shfl_xor(s, 2, 16);
+      s += __shfl_xor(s, 1, 16);
+      if (l == ci) out[cq] = s;
+    }
+  }
+#pragma unroll
+  for (int cq = 0; cq < 4; ++cq) {
+    const int c = 16 * cq + l;
+    if (c < C) Y[m * C + c] = out[cq] + b[c];
+  }
+}
+
+// dX[m][d] = sum_c dZ[m][c] W[c][d]   (the readout's data gradient): one float4 of
+// a row per thread, W [C][D] in LDS, classes summed in order.
+template <int D>
+__global__ __launch_bounds__(256) void k_rows_linear_t(const float* __restrict__ dZ, const float* __restrict__ W,
+                                                       float* __restrict__ dX, int64_t M, int C) {
+  extern __shared__ float ws[];
+  constexpr int D4 = D / 4, RPB = 256 / D4;
+  for (int i = threadIdx.x; i < C * D4; i += 256)
+    reinterpret_cast<float4*>(ws)[i] = reinterpret_cast<const float4*>(W)[i];
+  __syncthreads();
+  const int q = threadIdx.x % D4;
+  const int64_t m = static_cast<int64_t>(blockIdx.x) * RPB + threadIdx.x / D4;
+  if (m >= M) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < C; ++c) {
+    const float z = dZ[m * C + c];
+    const float4 w = reinterpret_cast<const float4*>(ws + c * D)[q];
+    a.x += z * w.x; a.y += z * w.y; a.z += z * w.z; a.w += z * w.w;
+  }
+  reinterpret_cast<float4*>(dX + m * D)[q] = a;
 }
 
 void colsum_plan(int64_t M, int64_t N, int64_t& colblocks, int64_t& nchunk, int64_t& R) {
@@ -515,6 +676,79 @@ extern "C" int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, floa
                      N, R, part);
   const int64_t CBf = N / 4 < 64 ? N / 4 : 64;
   hipLaunchKernelGGL(k_colsum_final, dim3(static_cast<unsigned>((N / 4 + CBf - 1) / CBf)), dim3(256), 0, s, part,
-                     static_cast<int>(nc), N, out);
+                     static_cast<int>(nc), N, out, nullptr, N / 4, 0);
+  return ghm_launch_status();
+}
+
+namespace {
+// partial row: C*N weighted sums, then the C class totals padded to a float4
+int64_t wcolsum_ldp(int64_t N, int C) { return static_cast<int64_t>(C) * N + 4 * ((C + 3) / 4); }
+
+void wcolsum_plan(int64_t M, int64_t& nchunk, int64_t& R) {
+  const int64_t cap = (M + 7) / 8;
+  nchunk = cap < 256 ? cap : 256;
+  if (nchunk < 1) nchunk = 1;
+  R = (M + nchunk - 1) / nchunk;
+  nchunk = (M + R - 1) / R;
+}
+}  // namespace
+
+extern "C" int64_t ghm_wcolsum_part_elems(int64_t M, int64_t N, int C) {
+  int64_t nc, R;
+  wcolsum_plan(M, nc, R);
+  return nc * wcolsum_ldp(N, C);
+}
+
+extern "C" int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const float* X, int64_t rps, int64_t seq_rows,
+                           int64_t off, int64_t M, int64_t N, float* out, float* wsum, float* part, void* stream) {
+  GHM_CHECK((W || tok) && !(W && tok) && X && out && part, "exactly one of W / tok; X, out, part");
+  GHM_CHECK(C >= 1 && C <= 64 && M >= 1 && rps >= 1 && seq_rows >= rps && off >= 0 && off + rps <= seq_rows,
+            "shape (1 <= C <= 64, row map inside each sequence)");
+  GHM_CHECK(N >= 4 && N <= 1024 && N % 4 == 0 && 256 % (N / 4) == 0, "N / 4 must divide 256");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(part)) &
+             15) == 0, "16-byte aligned X, out, part");
+  int64_t nc, R;
+  wcolsum_plan(M, nc, R);
+  const int64_t ldp = wcolsum_ldp(N, C);
+  hipStream_t s = ghm_stream(stream);
+  const dim3 grid(static_cast<unsigned>(nc), static_cast<unsigned>((C + 15) / 16));
+  if (tok)
+    hipLaunchKernelGGL(k_wcolsum_part<true>, grid, dim3(256), 0, s, W, tok, C, X, rps, seq_rows, off, M, N, R, ldp,
+                       part);
+  else
+    hipLaunchKernelGGL(k_wcolsum_part<false>, grid, dim3(256), 0, s, W, tok, C, X, rps, seq_rows, off, M, N, R, ldp,
+                       part);
+  const int64_t L4 = ldp / 4;
+  const int64_t CBf = L4 < 64 ? L4 : 64;
+  hipLaunchKernelGGL(k_colsum_final, dim3(static_cast<unsigned>((L4 + CBf - 1) / CBf)), dim3(256), 0, s, part,
+                     static_cast<int>(nc), ldp, out, wsum, static_cast<int64_t>(C) * N / 4, C);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_rows_linear(const float* X, const float* W, const float* b, float* Y, int64_t M, int D, int C,
+                               void* stream) {
+  GHM_CHECK(X && W && b && Y && M >= 1 && C >= 1 && C <= 64 && (D == 128 || D == 256) && C * D <= 16384, "shape");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) == 0, "16-byte aligned X, W");
+  const dim3 grid(static_cast<unsigned>((M + 15) / 16));
+  const size_t lds = static_cast<size_t>(C) * D * sizeof(float);
+  hipStream_t s = ghm_stream(stream);
+  if (D == 128)
+    hipLaunchKernelGGL(k_rows_linear<128>, grid, dim3(256), lds, s, X, W, b, Y, M, C);
+  else
+    hipLaunchKernelGGL(k_rows_linear<256>, grid, dim3(256), lds, s, X, W, b, Y, M, C);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_rows_linear_t(const float* dZ, const float* W, float* dX, int64_t M, int D, int C, void* stream) {
+  GHM_CHECK(dZ && W && dX && M >= 1 && C >= 1 && C <= 64 && (D == 128 || D == 256) && C * D <= 16384, "shape");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(dX)) & 15) == 0, "16-byte aligned W, dX");
+  const int64_t rpb = 256 / (D / 4);
+  const dim3 grid(static_cast<unsigned>((M + rpb - 1) / rpb));
+  const size_t lds = static_cast<size_t>(C) * D * sizeof(float);
+  hipStream_t s = ghm_stream(stream);
+  if (D == 128)
+    hipLaunchKernelGGL(k_rows_linear_t<128>, grid, dim3(256), lds, s, dZ, W, dX, M, C);
+  else
+    hipLaunchKernelGGL(k_rows_linear_t<256>, grid, dim3(256), lds, s, dZ, W, dX, M, C);
   return ghm_launch_status();
 }

@@ -89,6 +89,10 @@ HIP_SIGNATURES = {
     "ghm_gemm_reduce": [_p, _i, _i64, _i64, _p, _p, _p, _i64, _p],
     "ghm_colsum_part_elems": [_i64, _i64],
     "ghm_colsum": [_p, _i64, _i64, _p, _p, _p],
+    "ghm_wcolsum_part_elems": [_i64, _i64, _i],
+    "ghm_wcolsum": [_p, _p, _i, _p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p],
+    "ghm_rows_linear": [_p, _p, _p, _p, _i64, _i, _i, _p],
+    "ghm_rows_linear_t": [_p, _p, _p, _i64, _i, _i, _p],
     "ghm_mul": [_p, _p, _p, _i64, _p],
     "ghm_add": [_p, _p, _p, _i64, _p],
     "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
@@ -119,6 +123,7 @@ HIP_SIGNATURES = {
 _RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
             "ghm_mlp_bwd_rc_x3_blocks": _i64,
             "ghm_ln_rows_blocks": _i64, "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
+            "ghm_wcolsum_part_elems": _i64,
             "ghm_ce_kl_out_elems": _i64}
 
 HOST_SIGNATURES = {

@@ -73,8 +73,9 @@ class CdmPlan(EncoderPlan):
         self.joint = joint
         if joint:  # text leaves as tokens through t_embedding (sequential=False)
             self.tok = torch.empty(n_seq, n_token - n_i_token, dtype=torch.uint8, device=self.device)
-            self.onehot = torch.zeros(n_seq * (n_token - n_i_token), num_class, dtype=torch.float32,
-                                      device=self.device)
+            lib = _native.hip_lib()
+            self.wpart = torch.empty(lib.ghm_wcolsum_part_elems(n_seq * (n_token - n_i_token), D_MODEL, num_class),
+                                     dtype=torch.float32, device=self.device)
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         self.pred = e(n_seq, n_i_token)
         self.dpred = e(n_seq, n_i_token)
@@ -116,10 +117,9 @@ class CdmPlan(EncoderPlan):
         jobs.append(J(cur, self.N, [g["position_embeddings.weight"]]))
         self._flush(jobs, s)
         if self.joint:  # d t_embedding[v] = sum of the text rows of dH_0 holding token v
-            self.onehot.zero_()
-            self.onehot.scatter_(1, self.tok.view(-1, 1).long(), 1.0)
-            dtext = cur.view(self.N, self.T, D_MODEL)[:, self.Ti:, :].reshape(-1, D_MODEL)
-            torch.mm(self.onehot.t(), dtext, out=g["t_embedding.weight"])
+            Tt = self.T - self.Ti
+            _native.call("ghm_wcolsum", None, _ptr(self.tok), self.V, _ptr(cur), Tt, self.T, self.Ti, self.N * Tt,
+                         D_MODEL, _ptr(g["t_embedding.weight"]), None, _ptr(self.wpart), s)
         return cur
 
 

@@ -114,7 +114,8 @@ class VlmPlan:
         self.Pm = torch.zeros(L, N, pad, pad, dtype=torch.float32, device=self.device)
         self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
         self.logits, self.dlogits = e(M, num_class), e(M, num_class)
-        self.onehot = e(M, num_class)
+        if self.precision != "x3":  # the x3 path sums dH0 rows by token id (ghm_wcolsum)
+            self.onehot = e(M, num_class)
         self.dH = e(2, M, D)
         self.dX = e(M, D)
         self.dG = e(M, F)
@@ -127,7 +128,8 @@ class VlmPlan:
             self.slab = e(self.nsplit * max(D * F, 3 * D * D))
             lib = _native.hip_lib()
             self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
-                                 lib.ghm_colsum_part_elems(N, n_token * D)))
+                                 lib.ghm_colsum_part_elems(N, n_token * D),
+                                 lib.ghm_wcolsum_part_elems(M, D, num_class)))
         else:
             self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
             self.U, self.Y = e(M, F), e(M, D)
@@ -137,7 +139,8 @@ class VlmPlan:
         self.xt = torch.empty(N, n_token - n_prefix, dtype=torch.uint8, device=self.device)
         if joint:
             self.itok = torch.empty(N, n_prefix, dtype=torch.uint8, device=self.device)
-            self.onehot_i = e(M, num_class)
+            if self.precision != "x3":
+                self.onehot_i = e(M, num_class)
         self._gen = 0
 
     # ------------------------------------------------------------------
@@ -227,10 +230,10 @@ class VlmPlan:
         if self.joint:  # feat unused: self.itok holds the image leaves
             c("ghm_vlm_embed_joint_fwd", _ptr(xt), _ptr(self.itok), _ptr(p["i_embedding.weight"]),
               _ptr(p["t_embedding.weight"]), _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]),
-              _ptr(self.onehot), _ptr(self.onehot_i), N, T, self.P, self.V, D, s)
+              None, None, N, T, self.P, self.V, D, s)
         else:
             c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
-              _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
+              _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), None, N, T, self.P, self.V, D, s)
         for l in range(self.L):
             c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
@@ -244,7 +247,9 @@ class VlmPlan:
                   C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
             _gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
                   bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
-        torch.addmm(p["_read_out.bias"], self.H[self.L], p["_read_out.weight"].t(), out=self.logits)
+        c("ghm_rows_linear", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
+          _ptr(self.logits), M, D, self.V, s)  # model.py:332
+        self._xt_fwd = xt
         self._gen += 1
         return self.logits
 
@@ -261,9 +266,9 @@ class VlmPlan:
         M, D, F = self.M, self.D, self.F
         dz = self.dlogits if dlogits is None else dlogits
         cur, nxt = self.dH[0], self.dH[1]
-        torch.mm(dz, p["_read_out.weight"], out=cur)
-        torch.mm(dz.t(), self.H[self.L], out=g["_read_out.weight"])
-        torch.sum(dz, 0, out=g["_read_out.bias"])
+        c("ghm_rows_linear_t", _ptr(dz), _ptr(p["_read_out.weight"]), _ptr(cur), M, D, self.V, s)
+        c("ghm_wcolsum", _ptr(dz), None, self.V, _ptr(self.H[self.L]), M, M, 0, M, D, _ptr(g["_read_out.weight"]),
+          _ptr(g["_read_out.bias"]), _ptr(self.colpart), s)
         for l in reversed(range(self.L)):
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
@@ -288,9 +293,14 @@ class VlmPlan:
               _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 1, l, s)
         self._colsum(cur, self.N, self.T * D, g["position_embeddings.weight"], s)  # sum over sequences
-        torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
+        # token-embedding gradients: rows of dH0 summed per token value (text rows
+        # t >= P; the joint model's prefix rows through i_embedding)
+        T, P, N = self.T, self.P, self.N
+        c("ghm_wcolsum", None, _ptr(self._xt_fwd), self.V, _ptr(cur), T - P, T, P, N * (T - P), D,
+          _ptr(g["t_embedding.weight"]), None, _ptr(self.colpart), s)
         if self.joint:
-            torch.mm(self.onehot_i.t(), cur, out=g["i_embedding.weight"])
+            c("ghm_wcolsum", None, _ptr(self.itok), self.V, _ptr(cur), P, T, 0, N * P, D,
+              _ptr(g["i_embedding.weight"]), None, _ptr(self.colpart), s)
         return cur
 
     def _colsum(self, X, rows, cols, out, s):

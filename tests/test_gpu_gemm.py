@@ -209,6 +209,73 @@ def test_colsum(M, N):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("C,D,tok,rowmap", [(10, 256, False, None), (10, 128, True, (35, 41, 6)),
+                                             (33, 128, False, None), (64, 256, True, (9, 17, 8)),
+                                             (3, 16, True, (5, 5, 0))])
+def test_wcolsum(C, D, tok, rowmap):
+    """ghm_wcolsum (readout weight / bias and token-embedding gradients): dense
+    weights or token ids, text-row maps inside each sequence, several class blocks;
+    fp32 against the float64 product, bit-identical on repeat."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(C * D)
+    n_seq = 300
+    rps, seq_rows, off = rowmap if rowmap else (1, 1, 0)
+    Mrows = n_seq * seq_rows if rowmap else 10_368
+    M = n_seq * rps if rowmap else Mrows
+    X = torch.randn(Mrows, D, generator=g)
+    rows = torch.arange(M)
+    xrow = (rows // rps) * seq_rows + off + rows % rps
+    if tok:
+        ids = torch.randint(0, C, (M,), generator=g, dtype=torch.uint8)
+        Wm = torch.nn.functional.one_hot(ids.long(), C).double()
+    else:
+        Wm = torch.randn(M, C, generator=g).double()
+    want = Wm.t() @ X[xrow].double()
+    want_w = Wm.sum(0)
+    Xd = X.to(DEV)
+    if tok:
+        idd = ids.to(DEV)
+        src = (None, _ptr(idd))
+    else:
+        wd = Wm.float().to(DEV)
+        src = (_ptr(wd), None)
+    part = torch.empty(_native.hip_lib().ghm_wcolsum_part_elems(M, D, C), device=DEV)
+    outs = []
+    for _ in range(2):
+        out, ws = torch.full((C, D), float("nan"), device=DEV), torch.full((C,), float("nan"), device=DEV)
+        _native.call("ghm_wcolsum", src[0], src[1], C, _ptr(Xd), rps, seq_rows, off, M, D, _ptr(out), _ptr(ws),
+                     _ptr(part), ctypes_stream())
+        torch.cuda.synchronize()
+        outs.append((out.cpu(), ws.cpu()))
+    bound = 1e-6 * (Wm.abs().t() @ X[xrow].double().abs()) + 1e-6
+    assert ((outs[0][0].double() - want).abs() <= bound).all()
+    assert ((outs[0][1].double() - want_w).abs() <= 1e-6 * Wm.abs().sum(0) + 1e-6).all()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("C,D,M", [(10, 256, 10_368), (10, 128, 1000), (64, 256, 333), (17, 128, 77)])
+def test_rows_linear(C, D, M):
+    """ghm_rows_linear / _t (the VLM readout, model.py:332): logits = X W^T + b and
+    dX = dZ W against the float64 products."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(C + D + M)
+    X, W, b = torch.randn(M, D, generator=g), torch.randn(C, D, generator=g) * 0.1, torch.randn(C, generator=g)
+    dZ = torch.randn(M, C, generator=g)
+    Xd, Wd, bd, dZd = X.to(DEV), W.to(DEV), b.to(DEV), dZ.to(DEV)
+    Y, dX = torch.empty(M, C, device=DEV), torch.empty(M, D, device=DEV)
+    _native.call("ghm_rows_linear", _ptr(Xd), _ptr(Wd), _ptr(bd), _ptr(Y), M, D, C, ctypes_stream())
+    _native.call("ghm_rows_linear_t", _ptr(dZd), _ptr(Wd), _ptr(dX), M, D, C, ctypes_stream())
+    torch.cuda.synchronize()
+    want_y = X.double() @ W.double().t() + b.double()
+    want_dx = dZ.double() @ W.double()
+    by = 1e-6 * (X.double().abs() @ W.double().abs().t() + b.double().abs()) + 1e-6
+    bx = 1e-6 * (dZ.double().abs() @ W.double().abs()) + 1e-6
+    assert ((Y.cpu().double() - want_y).abs() <= by).all()
+    assert ((dX.cpu().double() - want_dx).abs() <= bx).all()
+
+
 @pytest.mark.parametrize("T,npre,dbl", [(162, 162, 0.0), (130, 1, 1 / 128), (81, 81, 0.0), (100, 100, 0.0)])
 def test_attention_ext_long_sequences(T, npre, dbl):
     """ghm_attn_ext_*_x3 at D = 128: sequences past 96 tokens (the joint CDM's 162,
