@@ -103,11 +103,8 @@ int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, int ldb, int 
               int b_mode, const float* stats, const float* ln_w, const float* ln_b, float* part,
               float* bias_part, int64_t M, int tok_per_split, void* stream);
 
-/* Token-embedding backward partials part_tok [n_seq][V][D] (reduce over n_seq
- * with ghm_reduce_partials); the position-embedding gradient is
- * ghm_reduce_partials(dH0, n_seq, T*D, ...)  —  backward of model.py:764-765. */
-int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok, int64_t n_seq, int T,
-                  int V, int D, void* stream);
+/* (The embedding gradients of model.py:764-765 are ghm_wcolsum by token id and
+ * ghm_colsum over the sequences, declared with the VLM GEMM entry points.) */
 
 /* out[i] = sum_{s<n_split} part[s*n + i] in fixed order (deterministic).  The
  * n outputs are written to up to 4 destination segments: segment k takes
@@ -435,7 +432,7 @@ int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* 
 int64_t ghm_colsum_part_elems(int64_t M, int64_t N);
 int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, float* part, void* stream);
 /* Weighted column sums: out[c][n] = sum_m w(m, c) X[xrow(m)][n] and (if wsum)
- * wsum[c] = sum_m w(m, c), c < C <= 64, N/4 dividing 256.  w(m, c) = W[m][c]
+ * wsum[c] = sum_m w(m, c) (dense W only), c < C <= 64, N/4 dividing 256.  w(m, c) = W[m][c]
  * (dense [M][C]; the readout weight and bias gradients from dlogits) or
  * [tok[m] == c] when W is NULL (token ids [M]; the t_embedding / i_embedding
  * gradients, autograd's embedding backward of model.py:238-241 and :444); xrow(m) = (m / rps) * seq_rows + off + m % rps.  Deterministic two

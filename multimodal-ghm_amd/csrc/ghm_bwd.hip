@@ -548,32 +548,6 @@ __global__ __launch_bounds__(256) void k_readout_bwd(
 }
 
 // ---------------------------------------------------------------------------
-// Token-embedding backward partials: one workgroup per sequence, thread = feature
-// d; part_tok[n][v][d] = sum_{t : tok[n,t] = v} dH0[n,t,d].  (The position
-// embedding gradient is a plain reduction of dH0 over sequences: ghm_reduce.)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void k_embed_bwd(const float* __restrict__ dH0,
-                                                   const uint8_t* __restrict__ tok,
-                                                   float* __restrict__ part_tok, int T, int V) {
-  const int d = threadIdx.x;
-  const int64_t n = blockIdx.x;
-  float at[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) at[c] = 0.f;
-#pragma unroll 9
-  for (int t = 0; t < T; ++t) {
-    const int64_t m = n * T + t;
-    const float v = dH0[m * GHM_D + d];
-    const int tv = tok[m];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) at[c] += (tv == c) ? v : 0.f;
-  }
-#pragma unroll
-  for (int c = 0; c < 16; ++c)
-    if (c < V) part_tok[(n * V + c) * GHM_D + d] = at[c];
-}
-
-// ---------------------------------------------------------------------------
 // Deterministic partial reductions, several jobs per launch.  Wide, shallow jobs
 // (the weight-gradient partials): thread = one output, its splits summed in 8
 // interleaved partial sums and a balanced tree, 256 outputs per block.  The others (LayerNorm / readout /
@@ -728,15 +702,6 @@ extern "C" int ghm_wgrad(const float* A, int lda, int A_cols, const float* B, in
   else
     hipLaunchKernelGGL(k_wgrad<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
                        tok_per_split, A_cols, B_cols);
-  return ghm_launch_status();
-}
-
-extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, float* part_tok,
-                             int64_t n_seq, int T, int V, int D, void* stream) {
-  GHM_CHECK(dH0 && tokens && part_tok, "null pointer");
-  GHM_CHECK(D == GHM_D && T >= 1 && V >= 1 && V <= 16 && n_seq >= 1, "shape");
-  hipLaunchKernelGGL(k_embed_bwd, dim3(static_cast<unsigned>(n_seq)), dim3(128), 0, ghm_stream(stream), dH0,
-                     tokens, part_tok, T, V);
   return ghm_launch_status();
 }
 

@@ -355,9 +355,17 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ X
   const int64_t r1 = r0 + R < M ? r0 + R : M;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (grp < G && c4 < N4) {
-    for (int64_t row = r0 + grp; row < r1; row += G) {
-      const float4 v = *reinterpret_cast<const float4*>(X + row * N + 4 * c4);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    for (int64_t row0 = r0 + grp; row0 < r1; row0 += 4 * G) {  // 4 loads in flight, summed in row order
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t row = row0 + u * G;
+        v[u] = row < r1 ? *reinterpret_cast<const float4*>(X + row * N + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
     }
   }
   red[t] = a;
@@ -378,10 +386,10 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* __restrict__ X
 // weighted sums' class totals ride in the same partial rows (ghm_wcolsum).
 __global__ __launch_bounds__(256) void k_colsum_final(const float* __restrict__ part, int nchunk, int64_t N,
                                                       float* __restrict__ out, float* __restrict__ out2,
-                                                      int64_t split4, int n2) {
+                                                      int64_t split4, int n2, int cbw) {
   __shared__ float4 red[256];
   const int64_t N4 = N / 4;
-  const int CB = N4 < 64 ? static_cast<int>(N4) : 64;
+  const int CB = N4 < cbw ? static_cast<int>(N4) : cbw;
   const int G = 256 / CB;
   const int t = threadIdx.x, grp = t / CB;
   const int64_t c4 = static_cast<int64_t>(blockIdx.x) * CB + t % CB;
@@ -453,25 +461,63 @@ __global__ __launch_bounds__(256) void k_wcolsum_part(const float* __restrict__ 
     ws[c] = 0.f;
   }
   if (grp < G) {
-    for (int64_t row = r0 + grp; row < r1; row += G) {
-      const int64_t xr = (row / rps) * seq_rows + off + row % rps;
-      const float4 x = *reinterpret_cast<const float4*>(X + xr * N + 4 * c4);
+    // U rows' loads in flight per round, accumulated in row order; the row map in
+    // 32-bit arithmetic (rows < 2^31), skipped when it is the identity
+    const bool ident = rps == seq_rows && off == 0;
+    const uint32_t rps32 = static_cast<uint32_t>(rps), sr32 = static_cast<uint32_t>(seq_rows),
+                   off32 = static_cast<uint32_t>(off);
+    constexpr int U = TOK ? 8 : 4;  // rows in flight per round
+    for (int64_t row0 = r0 + grp; row0 < r1; row0 += U * G) {
+      // branch-free body: rows past the chunk re-read row0 with weight 0
+      float4 x[U];
+      int k[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = row0 + u * G;
+        ok[u] = row < r1;
+        const int64_t rr = ok[u] ? row : row0;
+        const uint32_t r = static_cast<uint32_t>(rr);
+        const int64_t xr = ident ? rr : static_cast<int64_t>((r / rps32) * sr32 + off32 + r % rps32);
+        x[u] = *reinterpret_cast<const float4*>(X + xr * N + 4 * c4);
+        if (TOK) {
+          const int tv = static_cast<int>(tok[rr]);  // unconditional: a guarded load serialises the round
+          k[u] = ok[u] ? tv - cb : -1;
+        }
+      }
       if (TOK) {
-        const int k = static_cast<int>(tok[row]) - cb;
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c == k) {
-            acc[c].x += x.x; acc[c].y += x.y; acc[c].z += x.z; acc[c].w += x.w;
-            ws[c] += 1.f;
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            if (c < nc) {  // uniform
+              const bool hit = c == k[u];
+              acc[c].x += hit ? x[u].x : 0.f;
+              acc[c].y += hit ? x[u].y : 0.f;
+              acc[c].z += hit ? x[u].z : 0.f;
+              acc[c].w += hit ? x[u].w : 0.f;
+            }
           }
+        }
       } else {
+        // every weight load issued before the first use (clamped columns, zeroed)
+        float wv[U][16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c < nc) {
-            const float w = W[row * C + cb + c];
-            acc[c].x += w * x.x; acc[c].y += w * x.y; acc[c].z += w * x.z; acc[c].w += w * x.w;
-            ws[c] += w;
-          }
+        for (int u = 0; u < U; ++u) {
+          const int64_t rr = ok[u] ? row0 + u * G : row0;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) wv[u][c] = W[rr * C + (cb + c < C ? cb + c : C - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c)
+            if (c < nc) {  // uniform
+              const float w = ok[u] ? wv[u][c] : 0.f;
+              acc[c].x += w * x[u].x; acc[c].y += w * x[u].y; acc[c].z += w * x[u].z; acc[c].w += w * x[u].w;
+              ws[c] += w;
+            }
+        }
       }
     }
   }
@@ -676,7 +722,7 @@ extern "C" int ghm_colsum(const float* X, int64_t M, int64_t N, float* out, floa
                      N, R, part);
   const int64_t CBf = N / 4 < 64 ? N / 4 : 64;
   hipLaunchKernelGGL(k_colsum_final, dim3(static_cast<unsigned>((N / 4 + CBf - 1) / CBf)), dim3(256), 0, s, part,
-                     static_cast<int>(nc), N, out, nullptr, N / 4, 0);
+                     static_cast<int>(nc), N, out, nullptr, N / 4, 0, 64);
   return ghm_launch_status();
 }
 
@@ -686,7 +732,7 @@ int64_t wcolsum_ldp(int64_t N, int C) { return static_cast<int64_t>(C) * N + 4 *
 
 void wcolsum_plan(int64_t M, int64_t& nchunk, int64_t& R) {
   const int64_t cap = (M + 7) / 8;
-  nchunk = cap < 256 ? cap : 256;
+  nchunk = cap < 512 ? cap : 512;
   if (nchunk < 1) nchunk = 1;
   R = (M + nchunk - 1) / nchunk;
   nchunk = (M + R - 1) / R;
@@ -702,6 +748,8 @@ extern "C" int64_t ghm_wcolsum_part_elems(int64_t M, int64_t N, int C) {
 extern "C" int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const float* X, int64_t rps, int64_t seq_rows,
                            int64_t off, int64_t M, int64_t N, float* out, float* wsum, float* part, void* stream) {
   GHM_CHECK((W || tok) && !(W && tok) && X && out && part, "exactly one of W / tok; X, out, part");
+  GHM_CHECK(!(tok && wsum), "class totals (wsum) only with dense weights");
+  GHM_CHECK(M < (int64_t(1) << 31) && ((M + rps - 1) / rps) * seq_rows < (int64_t(1) << 31), "rows < 2^31");
   GHM_CHECK(C >= 1 && C <= 64 && M >= 1 && rps >= 1 && seq_rows >= rps && off >= 0 && off + rps <= seq_rows,
             "shape (1 <= C <= 64, row map inside each sequence)");
   GHM_CHECK(N >= 4 && N <= 1024 && N % 4 == 0 && 256 % (N / 4) == 0, "N / 4 must divide 256");
@@ -718,10 +766,12 @@ extern "C" int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const floa
   else
     hipLaunchKernelGGL(k_wcolsum_part<false>, grid, dim3(256), 0, s, W, tok, C, X, rps, seq_rows, off, M, N, R, ldp,
                        part);
+  // 16 float4 columns x 16 chunk groups per workgroup: the partial rows are short
+  // and many (64 columns per workgroup left ~6 workgroups on a latency chain)
   const int64_t L4 = ldp / 4;
-  const int64_t CBf = L4 < 64 ? L4 : 64;
+  const int64_t CBf = L4 < 16 ? L4 : 16;
   hipLaunchKernelGGL(k_colsum_final, dim3(static_cast<unsigned>((L4 + CBf - 1) / CBf)), dim3(256), 0, s, part,
-                     static_cast<int>(nc), ldp, out, wsum, static_cast<int64_t>(C) * N / 4, C);
+                     static_cast<int>(nc), ldp, out, wsum, static_cast<int64_t>(C) * N / 4, C, 16);
   return ghm_launch_status();
 }
 

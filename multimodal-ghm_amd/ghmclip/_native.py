@@ -52,7 +52,6 @@ HIP_SIGNATURES = {
     "ghm_attn_bwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_qkv_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_wgrad": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
-    "ghm_embed_bwd": [_p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_reduce_partials": [_p, _i, _i64, _i, _p, _p, _p],
     "ghm_reduce_batch": [_p, _i, _p],
     "ghm_clip_prepare": [_p, _i64, _f, _p, _i, _p, _p, _p, _p],

@@ -185,7 +185,11 @@ class EncoderPlan:
         self.part_bro = e(N * num_class)
         self.part_wout = e(N * T)
         self.part_bout = e(N)
-        self.part_tok = e(N * vocab * D_MODEL)
+        lib = _native.hip_lib()
+        # embedding backward scratch: token sums by id (ghm_wcolsum), then the
+        # position gradient's sum over sequences (ghm_colsum), one after the other
+        self.part_emb = e(max(lib.ghm_wcolsum_part_elems(M, D_MODEL, vocab),
+                              lib.ghm_colsum_part_elems(N, T * D_MODEL)))
         self.d_emb = e(N, num_class)
         self.pack = None
         if self.precision == "x3":
@@ -382,9 +386,12 @@ class EncoderPlan:
             cur, nxt = self._layer_bwd(p, g, l, cur, nxt, jobs, _stream(), layer_grad)
             yield
         s = _stream()
-        c("ghm_embed_bwd", _ptr(cur), _ptr(tok), _ptr(self.part_tok), N, T, self.V, D_MODEL, s)
-        jobs += [J(self.part_tok, N, [g["token_embeddings.weight"]]), J(cur, N, [g["position_embeddings.weight"]])]
         self._flush(jobs, s)
+        # embeddings (model.py:765 via autograd): dH0 rows summed by token id,
+        # and over the sequences for the positions
+        c("ghm_wcolsum", None, _ptr(tok), self.V, _ptr(cur), self.M, self.M, 0, self.M, D_MODEL,
+          _ptr(g["token_embeddings.weight"]), None, _ptr(self.part_emb), s)
+        c("ghm_colsum", _ptr(cur), N, T * D_MODEL, _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)
 
     def flush_pending(self):
         """Reduce the parameter-gradient partials queued by the running

@@ -117,8 +117,10 @@ def main():
         "readout_bwd": (lambda: c("ghm_readout_bwd", P(plan.H[5]), P(p["_read_out.weight"]), P(p["_read_out.bias"]),
                                   P(p["_out.weight"]), P(plan.d_emb), P(plan.dH[0]), P(plan.part_ro),
                                   P(plan.part_bro), P(plan.part_wout), P(plan.part_bout), N, T, 128, 10, sp), None),
-        "embed_bwd": (lambda: c("ghm_embed_bwd", P(plan.dH[0]), P(plan.tokens), P(plan.part_tok), N, T, 10, 128, sp),
-                      None),
+        "embed_bwd_tok": (lambda: c("ghm_wcolsum", None, P(plan.tokens), 10, P(plan.dH[0]), M, M, 0, M, 128,
+                                    P(g["token_embeddings.weight"]), None, P(plan.part_emb), sp), None),
+        "embed_bwd_pos": (lambda: c("ghm_colsum", P(plan.dH[0]), N, T * 128, P(g["position_embeddings.weight"]),
+                                    P(plan.part_emb), sp), None),
     })
     only = set(a.only.split(",")) if a.only else None
     res = {}
