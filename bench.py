@@ -334,7 +334,7 @@ def _kname(raw):
     m = re.match(r"_Z(\d+)(\w+)", raw)
     if m:
         return m.group(2)[:int(m.group(1))]
-    name = raw.split("(")[0]
+    name = raw.replace("(anonymous namespace)::", "").split("(")[0]
     return name[5:] if name.startswith("void ") else name
 
 

@@ -87,7 +87,11 @@ def test_clip_cli_dp2_equals_single_rank(tmp_path):
     two = _run(2, tmp_path / "two")
     assert len(one) == 9 and np.isfinite(one).all()
     np.testing.assert_array_equal(two[0], two[1])
-    np.testing.assert_allclose(two[0], one, rtol=0, atol=1e-6)
+    # the two ranks' gradients are summed over half batches and then across the
+    # ranks, the single rank's over the whole batch: a different fp32 summation
+    # order, a few ulps of the loss (ulp 2.4e-7 at 2.5) after 8 AdamW steps
+    # (measured 1.2e-6 worst, profiles/r3_v8_gpu_tests.log)
+    np.testing.assert_allclose(two[0], one, rtol=0, atol=3e-6)
     ck = glob.glob(str(tmp_path / "two/logs/CLIP/*/*/*/checkpoint.pth"))
     assert len(ck) == 1, ck  # rank 0 saves, rank 1 is raw
     d = load_checkpoint(ck[0], "cpu")

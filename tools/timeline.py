@@ -49,7 +49,7 @@ def main():
           f"idle gaps >2us: {[(round(a / 1e3, 1), round(b / 1e3, 1)) for a, b in gaps]}")
     agg = {}
     for r in step:
-        k = r["Kernel_Name"].split("(")[0][:48]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:48]
         a = agg.setdefault(k, [0, 0.0])
         a[0] += 1
         a[1] += (r["e"] - r["s"]) / 1e3
