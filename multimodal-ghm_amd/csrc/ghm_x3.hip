@@ -1401,11 +1401,6 @@ __device__ __forceinline__ void rows_dot_half(const __bf16* ih, const __bf16* il
 // past T contribute 0).  The backward needs act'(s): relu' = [P > 0]; for gelu
 // the forward stores GELU'(s) beside P (Pd, same layout).
 constexpr int ACT_SOFTMAX = 0, ACT_RELU = 1, ACT_GELU = 2;
-#ifdef GHM_ATT_IGLP
-#define ATT_HINT() __builtin_amdgcn_iglp_opt(GHM_ATT_IGLP)
-#else
-#define ATT_HINT() ((void)0)
-#endif
 
 template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __restrict__ qkv,
@@ -1431,13 +1426,13 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
   half_store<NKT>(kst, sh, sl);
   half_load<NKT>(seq, T, 1, GHM_D, kst);  // K half 1 in flight across the first half's MFMAs
-  __syncthreads(); ATT_HINT();
+  __syncthreads();
   rows_dot_half<NKT>(sh, sl, qh, ql, 0, j, h, s);
-  __syncthreads(); ATT_HINT();
+  __syncthreads();
   half_store<NKT>(kst, sh, sl);
   float4 vst[COLS_NIT];
   cols_load<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D, vst);  // V column block 0 in flight across softmax
-  __syncthreads(); ATT_HINT();
+  __syncthreads();
   rows_dot_half<NKT>(sh, sl, qh, ql, 1, j, h, s);
   // scores scaled by one reciprocal and exponentiated as exp2 of a base-2
   // argument: two VALU ops per score instead of an IEEE divide and a libm expf
@@ -1517,14 +1512,14 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __rest
   // A fragment of k-step (kt, s) = keys 32kt + 16s + 4h + 0..3 and + 8
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    __syncthreads(); ATT_HINT();  // the previous phase's LDS reads are done
+    __syncthreads();  // the previous phase's LDS reads are done
     cols_store<NKT>(vst, sh, sl);
     if (dt < 3) cols_load<NKT>(seq, 3 * GHM_D, T, 2 * GHM_D + 32 * (dt + 1), vst);
     const int64_t row = (base + qc) * GHM_D + 32 * dt;
     float4 hv[4];
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -1756,12 +1751,12 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
     for (int kt = 0; kt < NKT; ++kt) dp[kt] = zero16();
     half_store<NKT>(vst, sh, sl);
     half_load<NKT>(seq, T, 1, 2 * GHM_D, vst);
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     rows_dot_half<NKT>(sh, sl, oh, ol, 0, j, h, dp);
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     half_store<NKT>(vst, sh, sl);
     cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D, kc);  // K column block 0 in flight across dS
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     rows_dot_half<NKT>(sh, sl, oh, ol, 1, j, h, dp);
   }
   const float inv_scale = 1.f / scale_div;
@@ -1825,10 +1820,10 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
   // ---- phase B: dQ^T[d][q] = sum_key K[key][d] dS[q][key] ----
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    __syncthreads(); ATT_HINT();  // the previous phase's LDS reads are done
+    __syncthreads();  // the previous phase's LDS reads are done
     cols_store<NKT>(kc, sh, sl);
     if (dt < 3) cols_load<NKT>(seq, 3 * GHM_D, T, GHM_D + 32 * (dt + 1), kc);
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     f32x16 acc = zero16();
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
@@ -1855,7 +1850,7 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
   float4 ost[COLS_NIT], qst[COLS_NIT];
   cols_load<NKT>(dO, GHM_D, T, 0, ost);
   cols_load<NKT>(seq, 3 * GHM_D, T, 0, qst);
-  __syncthreads(); ATT_HINT();  // the P / dS images are complete; phase B's staging reads are done
+  __syncthreads();  // the P / dS images are complete; phase B's staging reads are done
   bf16x8 pbh[KS], pbl[KS], sbh[KS], sbl[KS];
   {
     const __bf16* sih = sim_h + w * TP * 32;
@@ -1870,14 +1865,14 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
   }
 #pragma unroll 1
   for (int dt = 0; dt < 4; ++dt) {
-    if (dt) __syncthreads(); ATT_HINT();  // the previous block's LDS reads are done
+    if (dt) __syncthreads();  // the previous block's LDS reads are done
     cols_store<NKT>(ost, soh, sol);
     cols_store<NKT>(qst, sqh, sql);
     if (dt < 3) {
       cols_load<NKT>(dO, GHM_D, T, 32 * (dt + 1), ost);
       cols_load<NKT>(seq, 3 * GHM_D, T, 32 * (dt + 1), qst);
     }
-    __syncthreads(); ATT_HINT();
+    __syncthreads();
     f32x16 aV = zero16(), aK = zero16();
 #pragma unroll
     for (int st = 0; st < KS; ++st) {
