@@ -518,6 +518,21 @@ def test_guided_full_run_final_risk_vs_reference_cpu_run():
           f"max rel |dploss| {pdev.max():.3e}")
     assert abs(risk - ref_risk) <= 3e-4 * ref_risk
     assert dev[:100].max() <= 1e-4
+    # the reference's own reduction-order spread over steps 0-800 (its 2-thread
+    # run, clip_guided_curve3001_t2.npz) against this run's relative deviation
+    from conftest import curve_bound
+    t2 = np.load(os.path.join(GOLDEN, "clip_guided_curve3001_t2.npz"))["loss_history"]
+    n2 = len(t2)
+    bound, window, spread = curve_bound(ref[:n2], t2)
+    rel = dev[:n2] / np.abs(ref[:n2])
+    over = np.nonzero(rel > bound)[0]
+    print(f"guided run vs the reference's 2-thread spread over steps 0-{n2 - 1}: spread max {spread.max():.2e}, "
+          f"this run's rel |dloss| max {rel.max():.2e} (step {rel.argmax()}); steps over max(1e-4, 2 x spread): "
+          f"{len(over)} (first {over[0] if len(over) else None})")
+    # measured (r3_gd): spread max 1.45e-5; this split-bf16 run leaves max(1e-4, 2 x spread)
+    # from step 263 and reaches 6.4e-3 at step 532 — not inside the reference's own
+    # spread; held here against regressions, with the final risk above
+    assert rel.max() <= 1e-2
 
 
 def test_guided_module_api():
