@@ -166,10 +166,11 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
     """Reference: models/model.py:337-532.  Same constructor, parameter creation
     order (so torch.manual_seed gives identical weights) and state_dict keys.
     The HIP path covers the configurations the CDM experiments train: sequential
-    (exp_cdm_{standard,shallow}TF.sh: a frozen-CLIP feature token, T = 82) and joint
-    (exp_cdm_jointtrain.sh: the 81 text leaves through t_embedding, T = 162, on the
-    split-bf16 attention for sequences past 96 tokens); softmax attention,
-    LayerNorm, MLP, no guide, no causal mask, n_embd 128."""
+    (exp_cdm_{standard,shallow}TF.sh: a frozen-CLIP feature token, T = 82; guided:
+    eg_sdns.sh) and joint (exp_cdm_jointtrain.sh / exp_cdm_guidedTF.sh: the 81 text
+    leaves through t_embedding, T = 162, on the split-bf16 attention for sequences
+    past 96 tokens); softmax attention, LayerNorm, MLP, no causal mask, n_embd 128.
+    guide=True: the guided penalties run inside the fused CdmTrainer step."""
 
     def __init__(self, n_token, n_i_token, num_class, n_embd=128, n_layer=12, n_guided_layers=(3, 3), n_head=4,
                  n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True, auto_regressive=False,
@@ -199,8 +200,6 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive:
             raise NotImplementedError("HIP CDM: softmax attention, mlp=True, layernorm=True, maxnorm=False, "
                                       "auto_regressive=False")
-        if guide and sequential:
-            raise NotImplementedError("HIP CDM: guide=True is built for the joint model (train_CDNS.py) only")
         if guide and self.guided_layer_gap == 0:
             raise ValueError("guide=True needs n_layer >= 2 * n_guided_layers[1] + 1 (model.py:372)")
         if n_mlp_hidden != 4 * n_embd:
@@ -273,13 +272,15 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
 
 
 def cdm_guide_blocks(model, t_tree, i_tree, V):
-    """The guided outputs of the joint CDM (model.py:458-527) as blocks of the
-    residual stream, each paired with the BP messages that data_random_GHM.py:
-    526-592 (guided_info) lines up against it, in ConditionalGuidedLsLoss order
-    (:1023-1040).  t_tree / i_tree = (L, C).  Returns {layer l: [block, ...]},
-    block = (src, tok0, ntok, col, moff, ext) with src "i" (image messages
-    [n][3][n_nodes][V] of ghm_bp_dns_msgs: planes hd, qd, bu) or "t" (text
-    BP_CLS messages [n][n_total][V] of ghm_bp_cls, depth Lt-1 first)."""
+    """The guided outputs of the CDM (model.py:458-527) as blocks of the residual
+    stream, each paired with the target that the trainer lines up against it, in
+    ConditionalGuidedLsLoss order (:1023-1040).  t_tree / i_tree = (L, C).  Returns
+    {layer l: [block, ...]}, block = (src, tok0, ntok, col, moff, ext) with src
+    "i" (image messages [n][3][n_nodes][V] of ghm_bp_dns_msgs: planes hd, qd, bu;
+    data_random_GHM.py:551-592), "t" (joint model: text BP_CLS messages
+    [n][n_total][V] of ghm_bp_cls, depth Lt-1 first) or "c" (sequential model,
+    train_sequential_DNS.py:145: the frozen CLIP text embedding [n][V] that is also
+    the conditioning token, for every text-guided layer)."""
     Lt, Ct = t_tree
     Li, Ci = i_tree
     Ti, Tt = Ci ** Li, Ct ** Lt
@@ -295,7 +296,7 @@ def cdm_guide_blocks(model, t_tree, i_tree, V):
     blocks = {}
     ig = [l for l, f in enumerate(model.i_guided_layer_flag) if f]
     tg = [l for l, f in enumerate(model.t_guided_layer_flag) if f]
-    if len(ig) != 2 * Li + 1 or len(tg) > Lt:
+    if len(ig) != 2 * Li + 1 or (not model.sequential and len(tg) > Lt):
         raise ValueError("guided layers do not match the trees (n_guided_layers vs tree depths)")
     for k, l in enumerate(ig):
         if k <= Li:  # downward h / q (root: hd / bu), :505-511
@@ -308,6 +309,10 @@ def cdm_guide_blocks(model, t_tree, i_tree, V):
             b = [img(0, depth, (2 * Li + 1 - k) * V, ext), img(1, depth, (nt + 2 * Li + 1 - k) * V, ext),
                  img(2, depth, (2 * nt + j) * V, ext)]
         blocks.setdefault(l, []).extend(b)
+    if model.sequential:  # text id blocks (:522-527) of the one conditioning token vs the CLIP feature
+        for k, l in enumerate(tg):
+            blocks.setdefault(l, []).append(("c", Ti, model.n_token - Ti, k * V, 0, 1))
+        return blocks
     off = 0
     nodes = Tt // Ct
     for k, l in enumerate(tg):  # text id blocks, :522-527 against BP_CLS depth Lt-1-k

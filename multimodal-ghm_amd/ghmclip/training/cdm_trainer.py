@@ -4,6 +4,9 @@ CLIP text encoder, denoiser forward, ConditionalGuidedLsLoss / LsLoss / Compare,
 backward, clip_grad_norm_, cosine LR, AdamW).
 
 Per step, on the device (one captured graph + one optimizer graph):
+  (guide=True: the BP messages of the image tree on the side stream, the guided
+  penalty blocks after the loss, their gradients added into the residual stream
+  before each guided layer's backward)
   side stream: ghm_bp_dns — exact BP posterior means from the staged text leaves
                and the f64 noisy observations (the "Compare" target), and the f32
                model input z (the reference computes both on the host, :145,
@@ -132,22 +135,34 @@ class CdmTrainer:
         self._setup_guide(penalty)
 
     def _setup_guide(self, penalty):
-        """Guided joint CDM (train_CDNS.py --guide=True): BP message buffers (image
-        hd/qd/bu planes, text BP_CLS levels), one penalty partial row per guided
-        block, and the penalised loss history (ploss_history)."""
+        """Guided CDM (train_CDNS.py / train_sequential_DNS.py --guide=True): BP
+        message buffers (image hd/qd/bu planes; the joint model's text BP_CLS
+        levels), one penalty partial row per guided block, and the penalised loss
+        history (ploss_history).  The sequential model's text blocks target the
+        frozen CLIP text embedding (train_sequential_DNS.py:145)."""
         self.guide = bool(getattr(self.model, "guide", False))
         self.phist = None
         if not self.guide:
             return
-        if not self.joint:
-            raise NotImplementedError("guided CDM is built for the joint model only")
         Lt, Ct, Li, Ci, V = self.tree
         self.penalty = float(penalty)
         self.gblocks = cdm_guide_blocks(self.model, (Lt, Ct), (Li, Ci), V)
         self.n_inodes = sum(Ci ** d for d in range(1, Li + 1)) + 1
         n_tnodes = sum(Ct ** d for d in range(Lt))
         self.imsgs = torch.zeros(self.B, 3, self.n_inodes, V, dtype=torch.float32, device=self.device)
-        self.tmsgs = torch.zeros(self.B, n_tnodes, V, dtype=torch.float32, device=self.device)
+        self.tmsgs = torch.zeros(self.B, n_tnodes, V, dtype=torch.float32, device=self.device) if self.joint else None
+        # ConditionalGuidedLsLoss's diagnostic groups (model.py:1023-1040): loss2 = the
+        # first Li image-guided layers, loss4 = the middle (root) one, loss5 = the
+        # last Li, loss3 = the text blocks; one group id per penalty partial row
+        ig = [l for l, f in enumerate(self.model.i_guided_layer_flag) if f]
+        self.gpart_group = []
+        for l, blks in sorted(self.gblocks.items()):
+            for b in blks:
+                if b[0] != "i":
+                    self.gpart_group.append(3)
+                else:
+                    k = ig.index(l)
+                    self.gpart_group.append(0 if k < Li else (1 if k == Li else 2))
         self.n_gparts = sum(len(b) for b in self.gblocks.values())
         self.gpart = torch.zeros(self.n_gparts, self.B, dtype=torch.float32, device=self.device)
         self.gloss = torch.zeros(3, dtype=torch.float32, device=self.device)
@@ -156,7 +171,7 @@ class CdmTrainer:
 
     def _blk_args(self, blk):
         src, tok0, ntok, col, moff, ext = blk
-        msgs = self.imsgs if src == "i" else self.tmsgs
+        msgs = {"i": self.imsgs, "t": self.tmsgs, "c": None if self.joint else self.clip_plan.emb}[src]
         return tok0, ntok, col, _p(msgs), msgs[0].numel(), moff, ext, self.tree[4]
 
     def _blk_list(self, items):
@@ -216,7 +231,9 @@ class CdmTrainer:
             if self.guide:
                 _native.call("ghm_bp_dns_msgs", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
                              self.sigma, _p(self.post), _p(self.z32), _p(self.imsgs), self.B, Lt, Ct, Li, Ci, V, ss)
-                _native.call("ghm_bp_cls", _p(self.t_trans), _p(self.t_tok), _p(self.tmsgs), self.B, Lt, Ct, V, ss)
+                if self.joint:  # (the sequential model's text blocks target the CLIP feature)
+                    _native.call("ghm_bp_cls", _p(self.t_trans), _p(self.t_tok), _p(self.tmsgs), self.B, Lt, Ct, V,
+                                 ss)
             else:
                 _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
                              self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V, ss)
@@ -306,6 +323,18 @@ class CdmTrainer:
             return self.loss_history(upto)
         n = self.steps_done if upto is None else upto
         return self.phist[:n].double().cpu().numpy()
+
+    def penalty_groups(self):
+        """The last step's ConditionalGuidedLsLoss diagnostics (loss2, loss4, loss5,
+        loss3): penalty x the batch mean of each group's squared Frobenius norms
+        (model.py:1023-1040; train_sequential_DNS.py logs them).  Host sync."""
+        if not self.guide:
+            return np.zeros(4)
+        part = self.gpart.double().cpu().numpy()
+        out = np.zeros(4)
+        for row, grp in enumerate(self.gpart_group):
+            out[grp] += part[row].mean()
+        return self.penalty * out
 
     def compare_history(self, upto=None):
         """Squared error against the BP posterior means per step (compare_history)."""

@@ -24,7 +24,7 @@ import torch
 
 from .. import _native
 from . import distributed
-from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.hip_encoder import EncoderPlan, default_precision, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
 
@@ -52,6 +52,7 @@ def flat_layout(models, dp_top):
     tower], total numel)."""
     layout, bucket_a, off = [], [], 0
     for m in models:
+        top = min(dp_top, m.n_layer)  # a tower may have fewer layers than the text tower
         named = dict(m.named_parameters())
         order = [n for l in reversed(range(m.n_layer)) for n in named if _layer_of(n) == l]
         order += [n for n in named if _layer_of(n) is None]
@@ -61,7 +62,7 @@ def flat_layout(models, dp_top):
             slots[name] = (off, k)
             off += k
             ly = _layer_of(name)
-            if ly is not None and ly >= m.n_layer - dp_top:
+            if ly is not None and ly >= m.n_layer - top:
                 a_end = off
         layout.append(slots)
         bucket_a.append((start, a_end))
@@ -86,7 +87,10 @@ class ClipTrainer:
         """lr_schedule: sequence of python-float learning rates, one per step
         (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
         precision: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA); None ->
-        $GHM_PRECISION or "x3".
+        $GHM_PRECISION, else "x3" (unguided) / "f32" (guided: the guided run
+        amplifies the split products' 2^-17 rounding 20x past an f32 path's, which
+        sits at the level of any one-ulp perturbation of the reference's own
+        arithmetic).
         Guided CLIP (train_CLIP.py --clip_guide=True) is on when the encoders were
         built with guide=True: guide_trans = (text, image) transition templates
         [L][C][V][V] (ClipSampler.t_templ / i_templ) for the on-device BP guide
@@ -107,8 +111,9 @@ class ClipTrainer:
         self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.views = []  # per model: (param dict, grad dict, m dict, v dict)
-        L0 = tmodel.n_layer
-        self.dp_top = int(os.environ.get("GHM_DP_BUCKET_LAYERS", str(L0 - L0 // 2)))  # layers in bucket A
+        L0 = max(m.n_layer for m in self.models)
+        # layers in bucket A (clamped per tower in flat_layout / _bwd_a_gen)
+        self.dp_top = int(os.environ.get("GHM_DP_BUCKET_LAYERS", str(L0 - L0 // 2)))
         self.dp_top = max(0, min(L0, self.dp_top))
         layout, self.bucket_a, _ = flat_layout(self.models, self.dp_top)
         with torch.no_grad():
@@ -127,6 +132,8 @@ class ClipTrainer:
                 self.views.append((pd, gd, md, vd))
         T = tmodel.n_token
         n_seq = batch_size * (K + 1)
+        if precision is None:
+            precision = default_precision("f32" if all(getattr(m, "guide", False) for m in self.models) else "x3")
         self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
                                   n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
                                   precision=precision, activation=getattr(m, "activation", "softmax"),
@@ -270,9 +277,10 @@ class ClipTrainer:
         p, g = self.views[tower][0], self.views[tower][1]
         it = plan.backward_iter(p, g, layer_grad=self._guide_hooks(tower))
         self._bwd_it[tower] = it
-        for k in range(1 + self.dp_top):
+        top = min(self.dp_top, plan.L)  # the towers' layer counts may differ (clip_{t,i}model_nlayer)
+        for k in range(1 + top):
             next(it)
-            if k < self.dp_top:
+            if k < top:
                 yield  # (the last piece ends with the generator: no empty piece)
         if flush:
             plan.flush_pending()

@@ -8,7 +8,10 @@ checkpoint.pth keys as the reference (src/ghmclip/training/train_sequential_DNS.
 step: frozen CLIP text encoder, denoiser forward/backward, loss, Compare against
 the exact BP posterior (computed on the device), clip and AdamW; the native
 sampler runs in a producer thread.  Differences, by design:
-  * --device must be a HIP device; guide=True is not built (NotImplementedError);
+  * --device must be a HIP device;
+  * --guide=True (scripts/examples/eg_sdns.sh) computes the image tree's BP guide
+    targets on the device and adds the guided penalties (text blocks against the
+    frozen CLIP feature, :145) inside the fused step;
   * the CLIP checkpoint is read with the weights-only unpickler;
   * wandb/s3fs are optional (skipped with a warning when not installed);
   * with torchrun (WORLD_SIZE > 1) each rank takes a contiguous 1/world of the
@@ -81,8 +84,6 @@ def find_clip_checkpoint(tree_folder, clip_feature, root="logs"):
 
 def main(argv=None):
     c = parse(argv)
-    if c.guide:
-        raise NotImplementedError("guided CDM (guide=True) is not built on the HIP path yet")
     ws, rank, device = distributed.setup()
     if ws == 1:
         print(f"Using GPU: {torch.cuda.get_device_name(0)}")
@@ -150,7 +151,8 @@ def main(argv=None):
              for i in range(c.total_iters)]
     trainer = CdmTrainer(model, clip_text_model, c.batch_size // ws,
                          sched, *sampler.device_templates("the CDM trainer (BP_DNS on the device)"),
-                         sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset)
+                         sigma=c.sigma, max_norm=c.max_norm, device=device, t_offset=t_offset,
+                         penalty=c.penalty)
     if t_offset:
         trainer.load_optimizer_state(optimizer)
     sampler.native.pull_numpy_state()  # the producer owns numpy's MT stream from here on
@@ -158,10 +160,10 @@ def main(argv=None):
                             row_slice=(rank, ws) if ws > 1 else None)
 
     def sync_hist(upto):
-        h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
-        h, ch = distributed.mean_histories([h, ch], device)  # every rank
+        h, ph, ch = trainer.loss_history(upto), trainer.ploss_history(upto), trainer.compare_history(upto)
+        h, ph, ch = distributed.mean_histories([h, ph, ch], device)  # every rank
         loss_history[:upto] = h
-        ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
+        ploss_history[:upto] = ph  # equals the loss without guidance
         compare_history[:upto] = ch
 
     def save(iter_num):
@@ -181,10 +183,11 @@ def main(argv=None):
             lr = sched[iter_num]
             if iter_num > 0 and iter_num % c.log_interval == 0:
                 sync_hist(iter_num + 1)
+                pen = distributed.mean_histories([trainer.penalty_groups()], device)[0]  # (loss2, 4, 5, 3)
                 finish_time = time.time()
                 h = iter_num // 2
                 logger.info(f'Iter: {iter_num},Penalty train loss: {np.mean(ploss_history[h:iter_num]):.4f}, '
-                            f'Penalty: [{0:.2f},{0:.2f},{0:.2f},{0:.2f}],  '
+                            f'Penalty: [{pen[0]:.2f},{pen[1]:.2f},{pen[2]:.2f},{pen[3]:.2f}],  '
                             f'Train loss: {np.mean(loss_history[h:iter_num]):.4f}, '
                             f'Compare: {np.mean(compare_history[h:iter_num]):.4f},  Bayes:{Bayes_loss:.4f}, '
                             f'LR: {lr:.6f}, Time: {(finish_time - curr_time):.2f}s')

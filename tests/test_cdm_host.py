@@ -169,8 +169,13 @@ def test_cdm_module_api_matches_reference_construction():
         assert torch.equal(a, b), k
     with pytest.raises(ValueError):  # guided-layer gap 3 // 7 == 0 (the reference divides by it)
         ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 3, sequential=False, guide=True)
-    with pytest.raises(NotImplementedError):  # guidance is built for the joint model
-        ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 9, [4, 4], sequential=True, guide=True)
+    # guided sequential model (eg_sdns.sh): same construction (RNG order) as unguided
+    torch.manual_seed(3)
+    ms = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 9, [1, 4], 4, 512, sequential=True, guide=True)
+    torch.manual_seed(3)
+    os_ = CO.OracleCdm(82, 81, 10, 128, 9, 512)
+    for (k, a), (_, b) in zip(ms.state_dict().items(), os_.state_dict().items()):
+        assert torch.equal(a, b), k
     # guided joint model (exp_cdm_guidedTF.sh): flags and guide blocks as model.py:392-416, 458-527
     from ghmclip.models.cdm import cdm_guide_blocks
     torch.manual_seed(3)
@@ -300,3 +305,26 @@ def test_oracle_guided_targets_match_reference():
             want = f[f"i_guide{k}_{j}"]
             assert g.shape == want.shape, (j, g.shape, want.shape)
             assert np.abs(g.numpy() - want).max() <= 1e-5 * np.abs(want).max() + 1e-6, ("image", k, j)
+
+
+def test_sguided_flags_and_blocks_match_reference_layout():
+    """Guided sequential CDM (eg_sdns.sh, model.py:372, :407-416, :448-527 with
+    n_guided_layers [1, 4], L = 9): every layer image-guided; text-guided at
+    counter 0 and n_i - 1 = 3, their blocks (index_i = 0, 10) on the conditioning
+    token (index 81) against the CLIP feature ("c"); index_q starts at n_t V = 10
+    and index_u at 2 n_t V = 20 (model.py:455-457)."""
+    from ghmclip import ConditionalDenoiseEncoderTransformer
+    from ghmclip.models.cdm import cdm_guide_blocks
+    m = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 9, [1, 4], 4, 512, sequential=True, guide=True)
+    assert m.i_guided_layer_flag == [True] * 9
+    assert m.t_guided_layer_flag == [True, False, False, True] + [False] * 5
+    blocks = cdm_guide_blocks(m, (4, 3), (4, 3), 10)
+    assert [b for b in blocks[0] if b[0] == "c"] == [("c", 81, 1, 0, 0, 1)]
+    assert [b for b in blocks[3] if b[0] == "c"] == [("c", 81, 1, 10, 0, 1)]
+    assert sum(b[0] == "c" for v in blocks.values() for b in v) == 2
+    # downward layers k = 0..4: h at k V, q at (n_t + k) V (the root's q plane is bu)
+    assert [[b[3] for b in blocks[k] if b[0] == "i"] for k in range(5)] == [[0, 10], [10, 20], [20, 30],
+                                                                            [30, 40], [40, 50]]
+    # upward layers: h, q one block back, u from 2 n_t V = 20 upwards
+    assert [[b[3] for b in blocks[k] if b[0] == "i"] for k in range(5, 9)] == [[40, 50, 20], [30, 40, 30],
+                                                                               [20, 30, 40], [10, 20, 50]]

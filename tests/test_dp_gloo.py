@@ -213,3 +213,25 @@ def test_flat_layout_buckets_cover_top_layers():
                 ly = _layer_of(name)
                 in_a = lo <= off and off + k <= hi
                 assert in_a == (ly is not None and ly >= m.n_layer - top), (top, name)
+
+
+def test_flat_layout_unequal_towers():
+    """--clip_tmodel_nlayer=4 --clip_imodel_nlayer=1 (the reference takes separate
+    layer counts, utils/config.py): the bucket depth is clamped per tower, so the
+    1-layer tower's bucket A is its one layer and A + B still tile [0, n) once."""
+    from ghmclip.models.model import EncoderTransformer
+    from ghmclip.training.clip_trainer import _layer_of, dp_bucket_ranges, flat_layout
+    torch.manual_seed(0)
+    tm, im = EncoderTransformer(81, 10, n_embd=128, n_layer=4), EncoderTransformer(81, 10, n_embd=128, n_layer=1)
+    for top in range(0, 5):
+        layout, bucket_a, n = flat_layout([tm, im], top)
+        a, b = dp_bucket_ranges(bucket_a, n)
+        cover = np.zeros(n, dtype=np.int64)
+        for lo, hi in a + b:
+            cover[lo:hi] += 1
+        assert (cover == 1).all()
+        for m, slots, (lo, hi) in zip((tm, im), layout, bucket_a):
+            for name, (off, k) in slots.items():
+                ly = _layer_of(name)
+                in_a = lo <= off and off + k <= hi
+                assert in_a == (ly is not None and ly >= m.n_layer - min(top, m.n_layer)), (top, name)

@@ -204,3 +204,37 @@ def test_eg_nwp_nontranslation_invariant_cli(tmp_path, monkeypatch):
              "--penalty=0.001", "--raw=True", "--log_interval=2"]
     loss, compare = train_NWP.main(flags)
     assert len(loss) == 4 and np.isfinite(loss).all() and np.isfinite(compare).all()
+
+
+def test_guided_sequential_cdm_cli(tmp_path, monkeypatch, capsys):
+    """scripts/examples/eg_sdns.sh (shortened: batch 8, 5 iterations, log every 2):
+    train_sequential_DNS --guide=True with the default --clip_feature=GT finds a
+    guided CLIP run (train_CLIP --clip_guide=True writes GT_L5...) as its frozen text
+    encoder (train_sequential_DNS.py:99-111), trains the guided denoiser and writes
+    logs/Sequential_CDNS/<tree>/GT_L9H4D128/ with the penalised loss in
+    ploss_history and the four penalty groups in the log line (:160)."""
+    from ghmclip.training import train_CLIP, train_sequential_DNS
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    clip_flags = [f for f in CLIP_FLAGS if not f.startswith(("--p_ttree_flip", "--p_itree_flip", "--clip_guide",
+                                                              "--lr_max", "--lr_min"))]
+    clip_flags += ["--p_ttree_flip=0.04", "--p_itree_flip=0.04", "--clip_guide=True", "--lr_max=1e-3",
+                   "--lr_min=1e-6"]
+    train_CLIP.main(clip_flags)
+    assert len(glob.glob("logs/CLIP/K4_L4C3p4_L4C3p4sc10/GT_L5H4D128_L5H4D128/*/checkpoint.pth")) == 1
+    flags = ["--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4", "--n_ttree_child=3", "--n_itree_child=3",
+             "--p_ttree_flip=0.04", "--p_itree_flip=0.04", "--flip_scale=1", "--sigma=1", "--batch_size=8",
+             "--variable_type=10", "--d_eb=128", "--n_model_layer=9", "--n_head=4", "--layernorm=True",
+             "--normalize_attn=True", "--lr_max=3e-4", "--lr_min=3e-7", "--guide=True", "--total_iters=5",
+             "--penalty=0.1", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+    loss, compare = train_sequential_DNS.main(flags)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/Sequential_CDNS/K4_L4C3p4_L4C3p4sc10/GT_L9H4D128/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert d["iter"] == 5
+    np.testing.assert_allclose(d["loss_history"], loss)
+    assert (d["ploss_history"] > d["loss_history"]).all()
+    with open(os.path.join(os.path.dirname(ck[0]), "training.log")) as f:
+        lines = [ln for ln in f if "Penalty: [" in ln]
+    assert lines and "Penalty: [0.00,0.00,0.00,0.00]" not in lines[-1], lines[-1:]

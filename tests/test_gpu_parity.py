@@ -240,11 +240,12 @@ def test_step_bit_identical_across_runs(precision):
 
 def test_qkv_backward_unperturbed_beside_weight_gradient():
     """The QKV backward on fixed inputs gives bit-identical outputs while the
-    weight-gradient kernel runs on another stream.  Its LN statistics come from
-    the forward's buffer through an agent-scope load (ld_stats); the round-2
-    plain load of the same buffer returned wrong 128-B lines (16 tokens) in 2 of
-    14 repetitions under this aggressor (tools/race_probe.py qkv_load wgrad0,
-    profiles/r3_probe.txt; DESIGN.md section 4 "Determinism")."""
+    weight-gradient kernel runs on another stream.  k_qkv_bwd_x3 recomputes its LN
+    statistics from H (the stats pointer is accepted and unused): the round-2
+    plain load of the forward's statistics buffer returned wrong 128-B lines (16
+    tokens) in 2 of 14 repetitions under this aggressor, and an agent-scope load
+    in 32 of 39 (tools/race_probe.py qkv_load wgrad0, profiles/r3_probe.txt;
+    DESIGN.md section 4 "Determinism")."""
     import ctypes
     from ghmclip import _native
     sampler, tr = _trainer(5, 128, 0.2, precision="x3")
@@ -567,3 +568,55 @@ def test_guided_module_api():
     assert abs(pen - rpen_v) <= 1e-5 * abs(rpen_v)
     for (k, a), (_, b) in zip(tp.named_parameters(), tr_.named_parameters()):
         assert _rel(a.grad, b.grad) < 1e-4, k
+
+
+@pytest.mark.parametrize("layers", [(4, 1), (1, 3)])
+def test_unequal_tower_depths_eager_graph_and_oracle(layers):
+    """--clip_tmodel_nlayer != --clip_imodel_nlayer (train_CLIP.py:99-125 builds the
+    towers separately): two steps against the oracle with the same towers, and
+    graph replay == eager (the backward's bucket depth is clamped per tower)."""
+    from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
+    from ghmclip.training.clip_trainer import ClipTrainer
+    Lt, Li = layers
+
+    def build():
+        p_y = np.ones(10) / 10
+        sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [0.2, 0.2], K=4, seedtree=42)
+        seed_everything(224)
+        tm = EncoderTransformer(81, 10, 128, Lt).to(DEV)
+        im = EncoderTransformer(81, 10, 128, Li).to(DEV)
+        sched = [get_lr_cosine_schedule(s, 3e-4, 3e-7, 0, 3000) for s in range(3001)]
+        return sampler, ClipTrainer(tm, im, 4, 8, sched, device=DEV, precision="f32")
+    s1, t1 = build()
+    h1 = _run(s1, t1, 8, 5)
+    s2, t2 = build()
+    h2 = _run(s2, t2, 8, 5, graph_after=2)
+    np.testing.assert_array_equal(h1, h2)
+    # the oracle with the same towers (same seeded construction) and draws
+    s3, t3 = build()
+    O.seed_everything(224)
+    otm, oim = O.OracleEncoder(81, 10, 128, Lt), O.OracleEncoder(81, 10, 128, Li)
+    for a, b in zip(list(otm.parameters()) + list(oim.parameters()), list(t3.tm.parameters()) + list(t3.im.parameters())):
+        assert torch.equal(a, b.detach().cpu())
+    params = list(otm.parameters()) + list(oim.parameters())
+    opt = O.OracleAdamW(params)
+    for it in range(2):
+        tl, _, il, _ = s3.draw_numpy(8)
+        t3.set_tokens(torch.from_numpy(tl), torch.from_numpy(il))
+        t3.step()
+        for p in params:
+            p.grad = None
+        loss = O.clip_loss(otm(torch.from_numpy(tl.astype(np.int64)))[0], oim(torch.from_numpy(il.astype(np.int64)))[0],
+                           4, 8)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.set_lr(O.lr_cosine(it, 3e-4, 3e-7, 0, 3000))
+        opt.step()
+        torch.cuda.synchronize()
+        assert abs(t3.loss_history()[it] - loss.item()) < 1e-5
+        coef = t3.hyper[1].item()  # the trainer keeps raw gradients, the clip coefficient in hyper[1]
+        for a, b in zip(params, list(t3.tm.parameters()) + list(t3.im.parameters())):
+            assert _rel(b.grad * coef, a.grad) < GRAD_TOL["f32"]
+    # (AdamW's first steps move near-zero-gradient entries by +-lr whatever their size)
+    for a, b in zip(params, list(t3.tm.parameters()) + list(t3.im.parameters())):
+        assert _rel(b, a) < 1e-3
