@@ -222,7 +222,6 @@ def dominant_kernel(trainer):
         def launch():
             _native.call("ghm_ln_mlp_fwd_x3b", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                          ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]),
-                         None if plan.mlp_rc else ptr(plan.G[0]), None if plan.mlp_rc else ptr(plan.Dg[0]),
                          ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
         return "k_ln_mlp_fwd_x3b", launch
 
@@ -415,8 +414,12 @@ def time_mlp_bwd_in_graph(trainer, replays=10, serial=True):
 
 def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     from oracle import ghm_oracle as O
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    host_cpus = os.cpu_count() or 1
+    threads = min(host_cpus, int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
+    cores = {"cores": threads, "host_cpus": host_cpus,
+             "cores_note": "threads used = the GPU job's CPU share on the box ($OMP_NUM_THREADS, 16 per GPU); "
+                           "host_cpus = os.cpu_count() of the whole machine"}
     if workload in ("cdm", "cdm_joint", "cdm_guided"):
         from oracle import cdm_oracle as CO
         joint = workload != "cdm"
@@ -428,7 +431,7 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
         dt = (time.time() - t0) / steps
         note = (" (unguided: the oracle has no guided step; guidance adds BP messages and 26 small penalty "
                 "blocks)" if workload == "cdm_guided" else "")
-        return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+        return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
                 "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if joint else 'sequential'} "
                           f"CDM config{note}, "
                           f"B={B}, L={L}, fp32 PyTorch-CPU restatement of the reference "
@@ -442,7 +445,7 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
         for _ in range(steps):
             tr.step()
         dt = (time.time() - t0) / steps
-        return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+        return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
                 "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if jt else 'sequential'} "
                           f"{'(unguided: the oracle has no guided VLM step) ' if workload == 'vlm_guided' else ''}"
                           f"VLM config, B={B}, L={L}, d=256, fp32 PyTorch-CPU restatement of the reference "
@@ -454,7 +457,7 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     for _ in range(steps):
         tr.step()
     dt = (time.time() - t0) / steps
-    return {"value": round(B / dt, 3), "unit": "samples/s", "cores": threads, "kind": "port",
+    return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
             "sample": f"{steps} steps (after 1 warm-up) of the {'guided' if guide else 'default'} CLIP config, B={B}, fp32 "
                       f"PyTorch-CPU restatement of the reference (oracle/ghm_oracle.py); "
                       f"{dt:.3f} s/step"}
@@ -531,16 +534,25 @@ def main():
                          "(exp_cdm_guidedTF.sh); vlm: sequential VLM next-word prediction "
                          "(BASELINE config 5); vlm_joint: joint VLM (train_NWP.py, T = 161); vlm_guided: the same "
                          "with --guide=True (exp_vlm_guidedTF.sh)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the global batch of 128 rows split over the ranks (128 / N rows per rank; "
+                         "default: weak scaling, --batch rows per rank)")
     ap.add_argument("--precision", default=None, choices=["f32", "x3"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
+    if a.strong:
+        if a.batch % ws:
+            raise SystemExit(f"--strong: the global batch {a.batch} must divide over {ws} ranks")
+        a.global_batch, a.batch = a.batch, a.batch // ws
+    else:
+        a.global_batch = a.batch * ws
     if a.workload in ("cdm", "cdm_joint", "cdm_guided"):
         return main_cdm(a, ws, rank)
     if a.workload in ("vlm", "vlm_joint", "vlm_guided"):
         return main_vlm(a, ws, rank)
-    total_iters = max(3000, a.steps + a.warmup + 1)
+    total_iters = max(3000, a.steps + a.warmup + 6)
     sampler, tr = build(rank, a.batch, a.layers, 0.2, total_iters, a.precision, a.guide)
     ring = make_ring(sampler, a.batch, a.ring)
     host_sampler = time_sampler(sampler, a.batch)
@@ -550,6 +562,20 @@ def main():
         tr.step()
 
     elapsed = timed_steps(a, ws, tr, one)
+    comm = None
+    if ws > 1:  # the data-parallel exchange, measured on extra replayed steps (every rank)
+        import torch.distributed as dist
+        tr.comm_timing = []
+        for k in range(5):
+            one(a.warmup + a.steps + k)
+        comm = tr.comm_stats()
+        tr.comm_timing = None
+        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), **(comm or {}),
+                "bytes_per_step": 4 * tr.n_params,
+                "what": "two bucketed all-reduces of the flat fp32 gradient per step on the comm stream (bucket A "
+                        "= the top layers, overlapped with the lower layers' backward; bucket B = the rest); "
+                        "exposed = the main stream's wait for them after its backward (events on both streams, "
+                        "5 graph-replayed steps after the timed ones)"}
     losses = tr.loss_history()
     finite = bool(np.isfinite(losses).all())
     # the dominant kernel: the largest share of kernel time in the committed rocprofv3
@@ -562,8 +588,8 @@ def main():
     cands = [k for k in prof if k.split("<")[0] in DOMINANT_CANDIDATES and not k.endswith(", 1>")]
     dom_inst = max(cands, key=lambda k: prof[k][0]) if cands else None
     dom = dom_inst.split("<")[0] if dom_inst else "k_mlp_bwd_rc_x3"
-    if tr.precision != "x3" or not tr.plans[0].mlp_rc:
-        dom = "k_ln_mlp_fwd_x3b" if tr.precision == "x3" else None
+    if tr.precision != "x3":
+        dom = None
     dom_ms, dom_how, dom_ms_conc = None, None, None
     if dom:
         if dom == "k_mlp_bwd_rc_x3" and ws == 1 and not a.no_graph:
@@ -580,7 +606,7 @@ def main():
     kern_ms = time_kernel(klaunch)
     kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
     risk = None if a.no_final_risk else final_risk(a, ws)
-    rc = tr.precision == "x3" and tr.plans[0].mlp_rc
+    rc = tr.precision == "x3"
     del ring, tr
     if rank != 0:
         teardown()
@@ -588,7 +614,7 @@ def main():
 
     ms = 1000.0 * elapsed / a.steps
     steps_per_s = a.steps / elapsed
-    samples = a.batch * ws * a.steps
+    samples = a.global_batch * a.steps
     step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
     scale = a.batch / 128
     traffic = pmc_traffic(kname)
@@ -659,7 +685,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
@@ -667,11 +693,12 @@ def main():
                    + "2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW"
                    + (" + on-device BP guide targets and penalty on 4 layers" if a.guide else ""),
                    "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,
-                   "global_batch_rows": a.batch * ws, "n_layer": a.layers, "parallelism": f"dp{ws}",
+                   "global_batch_rows": a.global_batch, "n_layer": a.layers, "parallelism": f"dp{ws}",
                    "hip_graph": not a.no_graph},
         "roofline": roofline,
         "steps_per_s": round(steps_per_s, 3),
         "sequences_per_s": round(samples * 10 / elapsed, 1),
+        "dist": comm,
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
         "step_mfma_frac": round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
         "step_mfma_basis": f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s",
@@ -749,7 +776,8 @@ def main_cdm(a, ws, rank):
                   f"CDM config)",
         "value": round(a.batch * ws * a.steps / elapsed, 2),
         "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True,
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native ConditionalDenoiseSampler, p=0.2, sigma=1), ring of {a.ring} "
@@ -831,7 +859,8 @@ def main_vlm(a, ws, rank):
                   f"VLM config)",
         "value": round(a.batch * ws * a.steps / elapsed, 2),
         "unit": "samples/s", "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True,
+        "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if tr.plan.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
         "data": f"synthetic GHM draws (native NextWordPredictSampler, p=0.2, host BP posteriors), ring of {a.ring} "

@@ -60,6 +60,8 @@ int ghm_readout_fwd(const float* H, const float* W_ro, const float* b_ro, const 
 /* K-way symmetric CLIP loss (GuidedClipLoss, guide=False) and its gradient
  * d(loss)/d(emb) for both towers; loss_out[0] = loss_out[1] = loss.  If hist is
  * non-NULL, hist[*step] = loss (step read on device, for graph replay).
+ * dt_emb = di_emb = NULL: the loss value only (ghm_readout_bwd_clip computes the
+ * gradient rows)
  * —  models/model.py:877-907; train_CLIP.py:153-161. */
 int ghm_clip_loss(const float* t_emb, const float* i_emb, float* dt_emb, float* di_emb,
                   float* loss_out, float* hist, const int32_t* step, int B, int K, int C,
@@ -73,6 +75,16 @@ int ghm_readout_bwd(const float* H, const float* W_ro, const float* b_ro, const 
                     const float* d_emb, float* dH, float* part_wro, float* part_bro,
                     float* part_wout, float* part_bout, int64_t n_seq, int T, int D, int C,
                     void* stream);
+
+/* ghm_readout_bwd of one CLIP tower (0 text, 1 image) with the K-way loss
+ * gradient of each row recomputed from both towers' embeddings (t_emb, i_emb;
+ * n_seq = (K + 1) B rows) instead of read: d_emb is written, equal to
+ * ghm_clip_loss's; the towers' backwards then need no loss kernel between the
+ * forward and the backward  —  backward of model.py:877-907 and :802-805. */
+int ghm_readout_bwd_clip(const float* H, const float* W_ro, const float* b_ro, const float* w_out,
+                         const float* t_emb, const float* i_emb, int tower, int B, int K, float* d_emb,
+                         float* dH, float* part_wro, float* part_bro, float* part_wout, float* part_bout,
+                         int64_t n_seq, int T, int D, int C, void* stream);
 
 /* MLP + LN2 backward for one layer (Dg = GELU'(U) from ghm_ln_mlp_fwd, passed as U):
  * writes dU [M][F] and dH_mid = dH_out + dLN2;
@@ -161,21 +173,13 @@ int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream);
 /* As ghm_ln_qkv_fwd (model.py:772-775). */
 int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, const void* pack, float* qkv,
                       float* stats, int64_t M, int D, float eps, void* stream);
-/* As ghm_ln_mlp_fwd (model.py:741-747,784-788); b1 [512], b2 [128] stay f32. */
-int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
-                      const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
-                      int64_t M, int D, int F, float eps, void* stream);
-/* Same contract and results as ghm_ln_mlp_fwd_x3 (model.py:741-747,784-788), 16 tokens per
-   wave on v_mfma_f32_16x16x32_bf16 (the variant the trainer launches).  G == Dg == NULL:
-   nothing but H_out and the LN2 stats leaves the chip (the backward is then
-   ghm_mlp_bwd_rc_x3, which recomputes U). */
+/* LN2 + MLP + residual forward of one layer (as ghm_ln_mlp_fwd, model.py:741-747,
+ * 784-788) on split-bf16 products, 16 tokens per wave (v_mfma_f32_16x16x32_bf16);
+ * b1 [512], b2 [128] stay f32.  Only H_out and the LN2 stats leave the chip: the
+ * backward, ghm_mlp_bwd_rc_x3, recomputes U. */
 int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
-                       const float* b1, const float* b2, float* H_out, float* G, float* Dg, float* stats,
-                       int64_t M, int D, int F, float eps, void* stream);
-/* As ghm_mlp_bwd (backward of model.py:784-788); Dg = GELU'(U) from the forward. */
-int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
-                   const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln, int64_t M,
-                   int D, int F, void* stream);
+                       const float* b1, const float* b2, float* H_out, float* stats, int64_t M, int D, int F,
+                       float eps, void* stream);
 /* MLP + LN2 backward with the up-projection recomputed from H_mid and the LN2
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),

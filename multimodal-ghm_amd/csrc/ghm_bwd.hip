@@ -469,18 +469,85 @@ __device__ __forceinline__ float wave_sum64(float v) {
   return v;
 }
 
+// d(CLIP loss)/d(emb) of row n of one tower, recomputed from the loss terms that
+// touch it (model.py:877-907): rows are blocks b = 0..K of B rows, and row n =
+// b B + i belongs to group i only.  Text rows of blocks 0 and >= 2 and image row
+// i of block 0 get their gradient from direction 1 (image i of block 0 scored
+// against text i of blocks 0, 2..K), the others from direction 2 (text i of block
+// 1 against image i of blocks 1, 2..K).  Same arithmetic, in the same order, as
+// clip_dir (ghm_fwd.hip), so the values equal k_clip_loss's bit for bit.
+template <int NC>
+__device__ __forceinline__ void clip_row_grad(const float* __restrict__ te, const float* __restrict__ ie, int tower,
+                                              int n, int B, int K, float* de) {
+  const int b = n / B, i = n - b * B;
+  const bool dir1 = tower == 0 ? b != 1 : b == 0;
+  // direction 1: tm = text i of block 0, im = image i of block 0, negatives = text
+  // rows, self = im; direction 2: tm / im of block 1, negatives = image rows, self = tm
+  const int64_t om = static_cast<int64_t>(dir1 ? i : B + i) * NC;
+  const float* tm = te + om;
+  const float* im = ie + om;
+  const float* neg = dir1 ? te : ie;
+  const float* self = dir1 ? im : tm;
+  auto dot = [&](const float* a, const float* c) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s += a[k] * c[k];
+    return s;
+  };
+  const float invB = 1.f / static_cast<float>(B);
+  const float Sm = expf(dot(tm, im));
+  float Sn = 0.f;
+  for (int k = 2; k <= K; ++k) Sn += expf(dot(neg + (static_cast<int64_t>(k) * B + i) * NC, self));
+  const float den = Sm + Sn;
+  const float ga = -(Sn / den) * invB;
+  if (b >= 2) {  // a negative row: gb_b * self
+    const float gb = (expf(dot(neg + (static_cast<int64_t>(b) * B + i) * NC, self)) / den) * invB;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) de[c] = gb * self[c];
+    return;
+  }
+  // a matched row: ga * (the other tower's matched row), plus (for the row the
+  // negatives were scored against) sum_k gb_k * negative k, k ascending
+  const float* other = tower == 0 ? im : tm;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) de[c] = ga * other[c];
+  const bool is_self = (tower == 0) != dir1;  // text row of block 1 (dir 2) / image row of block 0 (dir 1)
+  if (is_self) {
+    for (int k = 2; k <= K; ++k) {
+      const float* nk = neg + (static_cast<int64_t>(k) * B + i) * NC;
+      const float gb = (expf(dot(nk, self)) / den) * invB;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) de[c] += gb * nk[c];
+    }
+  }
+}
+
+// CLIP: te / ie non-null -> the row's loss gradient is recomputed here (and
+// written to demb) instead of read from a separate loss kernel's output, so the
+// backward of each tower starts as soon as both towers' embeddings exist
 template <int NC>
 __global__ __launch_bounds__(256) void k_readout_bwd(
     const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
-    const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
+    const float* __restrict__ wout, float* __restrict__ demb, float* __restrict__ dH,
     float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
-    float* __restrict__ part_bout, int T) {
+    float* __restrict__ part_bout, int T, const float* __restrict__ te = nullptr,
+    const float* __restrict__ ie = nullptr, int tower = 0, int B = 0, int K = 0) {
   __shared__ float2 red[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, n = blockIdx.x;
   const int64_t base = static_cast<int64_t>(n) * T;
   float de[NC];
+  if (te) {
+    clip_row_grad<NC>(te, ie, tower, n, B, K, de);
+    if (threadIdx.x < NC) {
+      float v = 0.f;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
+      for (int c = 0; c < NC; ++c) v = threadIdx.x == c ? de[c] : v;
+      demb[static_cast<int64_t>(n) * NC + threadIdx.x] = v;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
+  }
   float2 u = make_float2(0.f, 0.f);
   float bdot = 0.f;
   {
@@ -590,6 +657,16 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceJobs J) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) a[u] = 0.f;
     int k = 0;
+    // 32 loads in flight per round trip (the launch is latency-bound: 8 per trip
+    // took 64-85 splits / 8 serial trips); the sums keep their order (split k
+    // into a[k % 8], k ascending), so the result is unchanged bit for bit
+    for (; k + 32 <= jb.n_split; k += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = p[static_cast<int64_t>(k + u) * n];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) a[u & 7] += v[u];
+    }
     for (; k + 8 <= jb.n_split; k += 8) {
       float v[8];
 #pragma unroll
@@ -605,7 +682,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceJobs J) {
   const int64_t i = blk * 16 + e;
   float s = 0.f;
   if (i < n) {
-#pragma unroll 4
+#pragma unroll 8
     for (int k = g; k < jb.n_split; k += 16) s += jb.part[static_cast<int64_t>(k) * n + i];
   }
   red[g][e] = s;
@@ -630,7 +707,24 @@ extern "C" int ghm_readout_bwd(const float* H, const float* W_ro, const float* b
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
   GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
   hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
-                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T);
+                     H, W_ro, b_ro, w_out, const_cast<float*>(d_emb), dH, part_wro, part_bro, part_wout, part_bout,
+                     T);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_readout_bwd_clip(const float* H, const float* W_ro, const float* b_ro, const float* w_out,
+                                    const float* t_emb, const float* i_emb, int tower, int B, int K, float* d_emb,
+                                    float* dH, float* part_wro, float* part_bro, float* part_wout, float* part_bout,
+                                    int64_t n_seq, int T, int D, int C, void* stream) {
+  GHM_CHECK(H && W_ro && b_ro && w_out && t_emb && i_emb && d_emb && dH && part_wro && part_bro && part_wout &&
+                part_bout, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
+  GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
+  GHM_CHECK(tower == 0 || tower == 1, "tower 0 (text) or 1 (image)");
+  GHM_CHECK(B >= 1 && K >= 2 && n_seq == static_cast<int64_t>(K + 1) * B, "n_seq must be (K + 1) B");
+  hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
+                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T, t_emb, i_emb,
+                     tower, B, K);
   return ghm_launch_status();
 }
 

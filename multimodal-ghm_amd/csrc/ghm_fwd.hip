@@ -459,7 +459,19 @@ __device__ __forceinline__ float clip_dir(const float* tm, const float* im, cons
   return -logf(Sm / (Sm + Sn));
 }
 
-template <bool STAGE>
+// the loss term of a direction only (clip_dir without the gradient writes)
+__device__ __forceinline__ float clip_dir_value(const float* tm, const float* im, const float* neg, int B, int K,
+                                                int C, bool neg_is_text) {
+  const float* self = neg_is_text ? im : tm;
+  const float Sm = expf(dotc(tm, im, C));
+  float Sn = 0.f;
+  for (int k = 2; k <= K; ++k) Sn += expf(dotc(neg + static_cast<int64_t>(k) * B * C, self, C));
+  return -logf(Sm / (Sm + Sn));
+}
+
+// GRAD = false: the loss value only (the trainer's readout backward recomputes
+// each row's gradient itself: ghm_readout_bwd_clip)
+template <bool STAGE, bool GRAD = true>
 __global__ __launch_bounds__(1024) void k_clip_loss(const float* __restrict__ te, const float* __restrict__ ie,
                                                     float* __restrict__ dte, float* __restrict__ die,
                                                     float* __restrict__ loss_out, float* __restrict__ hist,
@@ -484,10 +496,12 @@ __global__ __launch_bounds__(1024) void k_clip_loss(const float* __restrict__ te
     const int i = r < B ? r : r - B;
     if (r < B) {  // direction 1: image i of block 0 vs text i of block 0 and of blocks 2..K
       const int64_t o = static_cast<int64_t>(i) * C;
-      acc += clip_dir(T + o, I + o, T + o, B, K, C, invB, dte + o, die + o, dte + o, true);
+      acc += GRAD ? clip_dir(T + o, I + o, T + o, B, K, C, invB, dte + o, die + o, dte + o, true)
+                  : clip_dir_value(T + o, I + o, T + o, B, K, C, true);
     } else {      // direction 2: text i of block 1 vs image i of block 1 and of blocks 2..K
       const int64_t o = (static_cast<int64_t>(B) + i) * C, on = static_cast<int64_t>(i) * C;
-      acc += clip_dir(T + o, I + o, I + on, B, K, C, invB, dte + o, die + o, die + on, false);
+      acc += GRAD ? clip_dir(T + o, I + o, I + on, B, K, C, invB, dte + o, die + o, die + on, false)
+                  : clip_dir_value(T + o, I + o, I + on, B, K, C, false);
     }
   }
   // deterministic block reduction
@@ -574,16 +588,21 @@ extern "C" int ghm_readout_fwd(const float* H, const float* W_ro, const float* b
 extern "C" int ghm_clip_loss(const float* t_emb, const float* i_emb, float* dt_emb, float* di_emb,
                              float* loss_out, float* hist, const int32_t* step, int B, int K, int C,
                              void* stream) {
-  GHM_CHECK(t_emb && i_emb && dt_emb && di_emb && loss_out, "null pointer");
+  GHM_CHECK(t_emb && i_emb && loss_out, "null pointer");
+  GHM_CHECK((dt_emb == nullptr) == (di_emb == nullptr), "both gradients or neither (value only)");
   GHM_CHECK(!hist || step, "hist needs step");
   GHM_CHECK(B >= 1 && K >= 2 && C >= 1, "shape");
   const int threads = 2 * B >= 1024 ? 1024 : ((2 * B + 63) / 64) * 64;
   const size_t lds = 2 * static_cast<size_t>(K + 1) * B * C * sizeof(float);
-  if (lds <= 64 * 1024)
-    hipLaunchKernelGGL(k_clip_loss<true>, dim3(1), dim3(threads), lds, ghm_stream(stream), t_emb, i_emb, dt_emb,
-                       di_emb, loss_out, hist, step, B, K, C);
+  hipStream_t s = ghm_stream(stream);
+  if (!dt_emb)
+    hipLaunchKernelGGL((k_clip_loss<false, false>), dim3(1), dim3(threads), 0, s, t_emb, i_emb, dt_emb, di_emb,
+                       loss_out, hist, step, B, K, C);
+  else if (lds <= 64 * 1024)
+    hipLaunchKernelGGL(k_clip_loss<true>, dim3(1), dim3(threads), lds, s, t_emb, i_emb, dt_emb, di_emb, loss_out,
+                       hist, step, B, K, C);
   else
-    hipLaunchKernelGGL(k_clip_loss<false>, dim3(1), dim3(threads), 0, ghm_stream(stream), t_emb, i_emb, dt_emb,
-                       di_emb, loss_out, hist, step, B, K, C);
+    hipLaunchKernelGGL(k_clip_loss<false>, dim3(1), dim3(threads), 0, s, t_emb, i_emb, dt_emb, di_emb, loss_out,
+                       hist, step, B, K, C);
   return ghm_launch_status();
 }

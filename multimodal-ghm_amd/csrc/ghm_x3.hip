@@ -117,50 +117,6 @@ __global__ __launch_bounds__(256) void k_split_weights(SplitJobs J) {
   stb4(pk + base + n + idx, lo);
 }
 
-// ---------------------------------------------------------------------------
-// bf16 tile staging: R x C elements (global row pitch ldg) -> LDS pitch P,
-// 16 bytes per thread-load, 256 threads; both planes (lo plane at +plane).
-// ---------------------------------------------------------------------------
-template <int R, int C>
-__device__ __forceinline__ constexpr int stage_bf_n() { return R * (C / 8) / 256; }
-
-template <int R, int C>
-__device__ __forceinline__ void stage_bf_load(uint4* v, const __bf16* __restrict__ g, int ldg, int plane) {
-  constexpr int C8 = C / 8, N = R * C8 / 256;
-  static_assert(R * C8 % 256 == 0, "tile must be a multiple of 256 x 16 B");
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    const int idx = threadIdx.x + 256 * k;
-    const __bf16* p = g + static_cast<size_t>(idx / C8) * ldg + 8 * (idx % C8);
-    v[k] = *reinterpret_cast<const uint4*>(p);
-    v[N + k] = *reinterpret_cast<const uint4*>(p + plane);
-  }
-}
-
-template <int R, int C, int P>
-__device__ __forceinline__ void stage_bf_store(const uint4* v, __bf16* hi, __bf16* lo) {
-  constexpr int C8 = C / 8, N = R * C8 / 256;
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    const int idx = threadIdx.x + 256 * k;
-    const int off = (idx / C8) * P + 8 * (idx % C8);
-    *reinterpret_cast<uint4*>(hi + off) = v[k];
-    *reinterpret_cast<uint4*>(lo + off) = v[N + k];
-  }
-}
-
-constexpr int PB1 = GHM_D + 8;  // [32][128] tile row pitch (bf16): 272 B
-constexpr int PB2 = 32 + 8;     // [128][32] tile row pitch (bf16): 80 B
-
-// Y^T tile (32 rows x 32 tokens) = A[32][128] . X^T with A rows in LDS
-// (pitch PB1) and X a row-layout token split into 8 k-steps (k = 64h + 8t + i)
-__device__ __forceinline__ f32x16 proj_x3(const __bf16* ah, const __bf16* al, const bf16x8* xh,
-                                          const bf16x8* xl, f32x16 acc) {
-#pragma unroll
-  for (int t = 0; t < 8; ++t) acc = mfma_x3(ldsb8(ah + 8 * t), ldsb8(al + 8 * t), xh[t], xl[t], acc);
-  return acc;
-}
-
 // LN a token row (row layout) and split it into the 8 k-step fragments
 __device__ __forceinline__ void ln_row_split(const float* __restrict__ row, const float* __restrict__ lnw,
                                              const float* __restrict__ lnb, int h, float eps, bool active,
@@ -187,109 +143,6 @@ __device__ __forceinline__ void load_split64(const float* __restrict__ p, bool a
   }
 #pragma unroll
   for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
-}
-
-// ---------------------------------------------------------------------------
-// LN2 + MLP (128 -> 512 -> GELU -> 128) + residual             (model.py:784-788)
-// Per 32-unit chunk: W1 rows [32][128] and W2 columns [128][32] (k-permuted)
-// through a double-buffered LDS ring; the hidden chunk stays in registers.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd_x3(
-    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
-    const __bf16* __restrict__ pack, const float* __restrict__ b1, const float* __restrict__ b2,
-    float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
-    int64_t M, float eps) {
-  __shared__ __attribute__((aligned(16))) __bf16 s1h[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 s1l[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 s2h[2][GHM_D * PB2];
-  __shared__ __attribute__((aligned(16))) __bf16 s2l[2][GHM_D * PB2];
-  __shared__ __attribute__((aligned(16))) float sb1[GHM_F];
-  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
-  const bool active = m0 < M;
-  const int64_t m = m0 + j;
-  const bool valid = m < M;
-  const int64_t mc = valid ? m : M - 1;
-  for (int i = threadIdx.x; i < GHM_F; i += 256) sb1[i] = b1[i];
-  bf16x8 xh[8], xl[8];
-  {
-    float mean = 0.f, rstd = 0.f;
-    ln_row_split(Hmid + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
-    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
-  }
-  f32x16 y[4];
-#pragma unroll
-  for (int ot = 0; ot < 4; ++ot) y[ot] = zero16();
-  const __bf16* W1 = pack + PK_W1_N;
-  const __bf16* W2 = pack + PK_W2_P;
-  uint4 st1[2 * stage_bf_n<32, GHM_D>()], st2[2 * stage_bf_n<GHM_D, 32>()];
-  stage_bf_load<32, GHM_D>(st1, W1, GHM_D, PK_W);
-  stage_bf_load<GHM_D, 32>(st2, W2, GHM_F, PK_W);
-  stage_bf_store<32, GHM_D, PB1>(st1, s1h[0], s1l[0]);
-  stage_bf_store<GHM_D, 32, PB2>(st2, s2h[0], s2l[0]);
-  __syncthreads();
-#pragma unroll 1
-  for (int c = 0; c < GHM_F / 32; ++c) {
-    const int cur = c & 1;
-    {
-      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
-      stage_bf_load<32, GHM_D>(st1, W1 + nc * 32 * GHM_D, GHM_D, PK_W);
-      stage_bf_load<GHM_D, 32>(st2, W2 + nc * 32, GHM_F, PK_W);
-    }
-    if (active) {
-      const f32x16 u = proj_x3(s1h[cur] + j * PB1 + 64 * h, s1l[cur] + j * PB1 + 64 * h, xh, xl, zero16());
-      float g[16], dg[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 bb = lds4(sb1 + 32 * c + quad_off(q, h));
-        g[4 * q + 0] = u[4 * q + 0] + bb.x;
-        g[4 * q + 1] = u[4 * q + 1] + bb.y;
-        g[4 * q + 2] = u[4 * q + 2] + bb.z;
-        g[4 * q + 3] = u[4 * q + 3] + bb.w;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) gelu_fast(g[r], g[r], dg[r]);
-      if (valid) {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward
-        float* grow = G + m * GHM_F + 32 * c;
-        float* drow = Dg + m * GHM_F + 32 * c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          st4(grow + quad_off(q, h), g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
-          st4(drow + quad_off(q, h), dg[4 * q], dg[4 * q + 1], dg[4 * q + 2], dg[4 * q + 3]);
-        }
-      }
-      bf16x8 gh[2], gl[2];
-      split_acc(g, 0, gh[0], gl[0]);
-      split_acc(g, 1, gh[1], gl[1]);
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        const __bf16* w2h = s2h[cur] + (32 * ot + j) * PB2 + 8 * h;
-        const __bf16* w2l = s2l[cur] + (32 * ot + j) * PB2 + 8 * h;
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          y[ot] = mfma_x3(ldsb8(w2h + 16 * s), ldsb8(w2l + 16 * s), gh[s], gl[s], y[ot]);
-      }
-    }
-    stage_bf_store<32, GHM_D, PB1>(st1, s1h[cur ^ 1], s1l[cur ^ 1]);
-    stage_bf_store<GHM_D, 32, PB2>(st2, s2h[cur ^ 1], s2l[cur ^ 1]);
-    __syncthreads();
-  }
-  if (active && valid) {
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      float4 hv[4], bv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        hv[q] = *reinterpret_cast<const float4*>(Hmid + m * GHM_D + 32 * ot + quad_off(q, h));
-        bv[q] = *reinterpret_cast<const float4*>(b2 + 32 * ot + quad_off(q, h));
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        st4(Hout + m * GHM_D + 32 * ot + quad_off(q, h), hv[q].x + (y[ot][4 * q] + bv[q].x),
-            hv[q].y + (y[ot][4 * q + 1] + bv[q].y), hv[q].z + (y[ot][4 * q + 2] + bv[q].z),
-            hv[q].w + (y[ot][4 * q + 3] + bv[q].w));
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -440,15 +293,14 @@ __device__ __forceinline__ float pick16(const float4* b4, int g, int r) {
 // NW = waves per workgroup (8: 128 tokens; 4: 64 tokens, for token counts too
 // small to fill 256 CUs with 128-token workgroups).  Measured: a 7-wave /
 // 112-token variant (463 workgroups instead of 405) runs 96.6 us vs 79.1 us at
-// the CLIP's 51,840 tokens.  SAVE = false: only H_out leaves the chip (the
-// backward recomputes U, k_mlp_bwd_rc_x3): 2 x [M,128] of HBM traffic instead of
-// 2 x [M,128] + 2 x [M,512].
-template <int NW, bool SAVE>
+// the CLIP's 51,840 tokens.  Only H_out (and the LN statistics) leave the chip:
+// the backward recomputes U (k_mlp_bwd_rc_x3), 2 x [M,128] of HBM traffic
+// instead of 2 x [M,128] + 2 x [M,512] with G and GELU'(U) saved.
+template <int NW>
 __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
-    float* __restrict__ Hout, float* __restrict__ G, float* __restrict__ Dg, float2* __restrict__ stats,
-    int64_t M, float eps) {
+    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
   // ONE __shared__ object: [W1 hi|lo][W2 hi|lo] x 2 buffers, then b1 (f32).  The
   // chunk's b1 values are read at the top of the iteration, before its LDS-DMA
   // fills: any LDS read issued after them gets an s_waitcnt vmcnt(0) on the new
@@ -509,9 +361,25 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       split8(x + 8 * s2, xh[s2], xl[s2]);
     }
   }
+  // the residual and b2 seed the accumulators (H = Hmid + b2 + sum_c W2[:, c] G_c):
+  // the rows were just read (L1 / L2-hot), so the epilogue needs no second read of
+  // Hmid, which the 16 chunks' traffic had evicted from the L2 (an extra 26 MB
+  // per launch, profiles/r3_v10_traffic.txt)
   f32x4 y[8];
+  __builtin_amdgcn_sched_barrier(0);  // (after the LN block: its 32 row values are dead by now)
+  {
+    const float* hr = Hmid + mc * GHM_D;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) y[j] = zero4();
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
+      y[j][0] = hv.x + bv.x;
+      y[j][1] = hv.y + bv.y;
+      y[j][2] = hv.z + bv.z;
+      y[j][3] = hv.w + bv.w;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
@@ -547,14 +415,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     }
 #pragma unroll
     for (int r = 0; r < 8 * (GHM_ABL != 2); ++r) gelu_fast(gv[r], gv[r], dg[r]);
-    if (SAVE) {  // G = GELU(U) for dW2, Dg = GELU'(U) for the backward: 4 stores per wave
-      float* grow = G + mc * GHM_F + 32 * c + 4 * g;
-      float* drow = Dg + mc * GHM_F + 32 * c + 4 * g;
-      st4(grow, gv[0], gv[1], gv[2], gv[3]);
-      st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
-      st4(drow, dg[0], dg[1], dg[2], dg[3]);
-      st4(drow + 16, dg[4], dg[5], dg[6], dg[7]);
-    }
     bf16x8 gh, gl;
     split8(gv, gh, gl);
 #pragma unroll
@@ -573,16 +433,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if (valid) {
-    const float* hr = Hmid + m * GHM_D;
     float* orow = Hout + m * GHM_D;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = 16 * j + 4 * g;
-      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
-      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
-      st4(orow + f, hv.x + (y[j][0] + bv.x), hv.y + (y[j][1] + bv.y), hv.z + (y[j][2] + bv.z),
-          hv.w + (y[j][3] + bv.w));
-    }
+    for (int j = 0; j < 8; ++j) st4(orow + 16 * j + 4 * g, y[j][0], y[j][1], y[j][2], y[j][3]);
   }
 }
 
@@ -915,96 +768,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
 }
 
 // ---------------------------------------------------------------------------
-// MLP + LN2 backward                                          (model.py:784-788)
-//   dG^T = W2^T dY^T (per chunk), dU = dG * GELU'(U) (stored),
-//   dX2^T += W1^T dU^T (registers), then LN2 backward + residual.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_mlp_bwd_x3(
-    const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
-    const float* __restrict__ lnw, const __bf16* __restrict__ pack, const float* __restrict__ Dg,
-    float* __restrict__ dU, float* __restrict__ dHmid, float* __restrict__ part_ln, int64_t M) {
-  // the LN partial buffer `red` aliases the first ring buffer after the loop
-  __shared__ __attribute__((aligned(16))) __bf16 sah[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 sal[2][32 * PB1];
-  __shared__ __attribute__((aligned(16))) __bf16 sbh[2][GHM_D * PB2];
-  __shared__ __attribute__((aligned(16))) __bf16 sbl[2][GHM_D * PB2];
-  __shared__ __attribute__((aligned(16))) float gam[GHM_D];
-  static_assert(sizeof(sah) >= 2 * 4 * GHM_D * sizeof(float), "red alias");
-  float* red = reinterpret_cast<float*>(&sah[0][0]);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 32;
-  const bool active = m0 < M;
-  if (threadIdx.x < GHM_D) gam[threadIdx.x] = lnw[threadIdx.x];
-  const int64_t m = m0 + j;
-  const bool valid = active && m < M;
-  const int64_t mc = m < M ? m : M - 1;
-  f32x16 dx[4];
-#pragma unroll
-  for (int it = 0; it < 4; ++it) dx[it] = zero16();
-  bf16x8 yh[8], yl[8];
-  load_split64(dHout + mc * GHM_D + 64 * h, active, yh, yl);  // dY[token][o = 64h + 8t + i]
-  const __bf16* WA = pack + PK_W2_T;  // rows = hidden unit, cols = o
-  const __bf16* WB = pack + PK_W1_T;  // rows = d, cols = hidden (permuted)
-  uint4 sta[2 * stage_bf_n<32, GHM_D>()], stb[2 * stage_bf_n<GHM_D, 32>()];
-  stage_bf_load<32, GHM_D>(sta, WA, GHM_D, PK_W);
-  stage_bf_load<GHM_D, 32>(stb, WB, GHM_F, PK_W);
-  float4 un[4];
-  const float* urow = Dg + mc * GHM_F;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + quad_off(q, h));
-  stage_bf_store<32, GHM_D, PB1>(sta, sah[0], sal[0]);
-  stage_bf_store<GHM_D, 32, PB2>(stb, sbh[0], sbl[0]);
-  __syncthreads();
-#pragma unroll 1
-  for (int c = 0; c < GHM_F / 32; ++c) {
-    const int cur = c & 1;
-    float uc[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uc[4 * q] = un[q].x; uc[4 * q + 1] = un[q].y; uc[4 * q + 2] = un[q].z; uc[4 * q + 3] = un[q].w;
-    }
-    {
-      const int nc = c + 1 < GHM_F / 32 ? c + 1 : c;
-      stage_bf_load<32, GHM_D>(sta, WA + nc * 32 * GHM_D, GHM_D, PK_W);
-      stage_bf_load<GHM_D, 32>(stb, WB + nc * 32, GHM_F, PK_W);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) un[q] = *reinterpret_cast<const float4*>(urow + 32 * nc + quad_off(q, h));
-    }
-    if (active) {
-      const f32x16 g = proj_x3(sah[cur] + j * PB1 + 64 * h, sal[cur] + j * PB1 + 64 * h, yh, yl, zero16());
-      float du[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) du[r] = g[r] * uc[r];
-      if (valid) {
-        float* drow = dU + m * GHM_F + 32 * c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) st4(drow + quad_off(q, h), du[4 * q], du[4 * q + 1], du[4 * q + 2], du[4 * q + 3]);
-      }
-      bf16x8 dh[2], dl[2];
-      split_acc(du, 0, dh[0], dl[0]);
-      split_acc(du, 1, dh[1], dl[1]);
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const __bf16* wh = sbh[cur] + (32 * it + j) * PB2 + 8 * h;
-        const __bf16* wl = sbl[cur] + (32 * it + j) * PB2 + 8 * h;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) dx[it] = mfma_x3(ldsb8(wh + 16 * s), ldsb8(wl + 16 * s), dh[s], dl[s], dx[it]);
-      }
-    }
-    stage_bf_store<32, GHM_D, PB1>(sta, sah[cur ^ 1], sal[cur ^ 1]);
-    stage_bf_store<GHM_D, 32, PB2>(stb, sbh[cur ^ 1], sbl[cur ^ 1]);
-    __syncthreads();
-  }
-  for (int i = threadIdx.x; i < 2 * 4 * GHM_D; i += 256) red[i] = 0.f;
-  __syncthreads();
-  if (active)
-    ln_bwd_acc(dx, Hmid + mc * GHM_D, ld_stats_sys(stats, mc), gam, dHout + mc * GHM_D, dHmid + mc * GHM_D, valid, h, j,
-               red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
-  __syncthreads();
-  ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
-}
-
-// ---------------------------------------------------------------------------
 // QKV + LN1 backward                                          (model.py:772-775)
 //   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.
 // ---------------------------------------------------------------------------
@@ -1313,6 +1076,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const __bf16* img, int r0, int r1, int
   const int col = 16 * (g & 1) + 4 * p;
   const bf16x4 a = ldtr(img + (r0 + q) * 32 + col);
   const bf16x4 b = ldtr(img + (r1 + q) * 32 + col);
+  bf16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return v;
+}
+
+// The fused backward's dS images ([query][32] per key block, 64-B rows) are
+// written by ds_write_b64 with one query row per lane: 16 consecutive rows at the
+// same column all land on banks {0, 1} or {16, 17} of the 32 a store spreads over
+// (8-way: 1.29 M SQ_LDS_BANK_CONFLICT cycles per launch).  The 8-B chunk c of row
+// r sits at c ^ ((r >> 1) & 7): 16 consecutive rows then cover all 32 banks once,
+// and a transposed read (4 whole rows per 32-lane half) still covers 256
+// contiguous bytes.
+__device__ __forceinline__ int ds_img_off(int row, int chunk) { return row * 32 + 4 * (chunk ^ ((row >> 1) & 7)); }
+__device__ __forceinline__ bf16x8 tr_frag_ds(const __bf16* img, int r0, int r1, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = 4 * (g & 1) + p;
+  const bf16x4 a = ldtr(img + ds_img_off(r0 + q, c));
+  const bf16x4 b = ldtr(img + ds_img_off(r1 + q, c));
   bf16x8 v;
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
   v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
@@ -1792,15 +1574,16 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
       else
         dv[r] = (p[kt][r] * dp[kt][r]) * inv_scale;
     }
-    // dS of this key block into the [query][32] images (row = this lane's query)
-    __bf16* dsh = sim_h + (kt * TP + q) * 32;
-    __bf16* dsl = sim_l + (kt * TP + q) * 32;
+    // dS of this key block into the [query][32] images (row = this lane's query;
+    // 8-B chunk quad_off / 4 = 2 qd + h, swizzled: ds_img_off)
+    __bf16* dsh = sim_h + kt * TP * 32;
+    __bf16* dsl = sim_l + kt * TP * 32;
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) {
       bf16x4 a, b;
       split4(make_float4(dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]), a, b);
-      stb4(dsh + quad_off(qd, h), a);
-      stb4(dsl + quad_off(qd, h), b);
+      stb4(dsh + ds_img_off(q, 2 * qd + h), a);
+      stb4(dsl + ds_img_off(q, 2 * qd + h), b);
     }
     split_acc(dv, 0, dh[2 * kt], dl[2 * kt]);
     split_acc(dv, 1, dh[2 * kt + 1], dl[2 * kt + 1]);
@@ -1859,8 +1642,8 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_x3f(const float* __res
     for (int st = 0; st < KS; ++st) {  // B fragment: rows (queries) 16 st + 8 h .. + 7, column = the lane's key
       const int r0 = 16 * st + 8 * h;
       split8(pcol[st], pbh[st], pbl[st]);
-      sbh[st] = tr_frag(sih, r0, r0 + 4, lane);
-      sbl[st] = tr_frag(sil, r0, r0 + 4, lane);
+      sbh[st] = tr_frag_ds(sih, r0, r0 + 4, lane);
+      sbl[st] = tr_frag_ds(sil, r0, r0 + 4, lane);
     }
   }
 #pragma unroll 1
@@ -1919,33 +1702,6 @@ extern "C" int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float*
   return ghm_launch_status();
 }
 
-extern "C" int ghm_ln_mlp_fwd_x3(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
-                                 const float* b1, const float* b2, float* H_out, float* G, float* Dg,
-                                 float* stats, int64_t M, int D, int F, float eps, void* stream) {
-  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && G && Dg && stats, "null pointer");
-  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  hipLaunchKernelGGL(k_ln_mlp_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1, b2,
-                     H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
-  return ghm_launch_status();
-}
-
-extern "C" int ghm_mlp_bwd_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
-                              const void* pack, const float* Dg, float* dU, float* dH_mid, float* part_ln,
-                              int64_t M, int D, int F, void* stream) {
-  GHM_CHECK(dH_out && H_mid && stats && ln_w && pack && Dg && dU && dH_mid && part_ln, "null pointer");
-  GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
-  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  hipLaunchKernelGGL(k_mlp_bwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w,
-                     reinterpret_cast<const __bf16*>(pack), Dg, dU, dH_mid, part_ln, M);
-  return ghm_launch_status();
-}
-
-// waves per workgroup of k_mlp_bwd_rc_x3 (16 tokens each): 8 when M gives every
-// CU a 128-token workgroup (the CLIP's 51,840 tokens: measured 4.42 ms/step vs
-// 4.43-4.48 for 4 waves), else 4 (the CDM's 10,496 tokens: 164 workgroups
-// instead of 82), the rule of ghm_ln_mlp_fwd_x3b
 static int rc_waves(int64_t M) { return (M + 127) / 128 >= 256 ? 8 : 4; }
 extern "C" int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M) {
   const int64_t tok = 16 * rc_waves(M);
@@ -2186,30 +1942,18 @@ extern "C" int ghm_attn_bwd_x3(const float* qkv, const float* P, const float* dH
 }
 
 extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
-                                  const float* b1, const float* b2, float* H_out, float* G, float* Dg,
-                                  float* stats, int64_t M, int D, int F, float eps, void* stream) {
+                                  const float* b1, const float* b2, float* H_out, float* stats, int64_t M, int D,
+                                  int F, float eps, void* stream) {
   GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && stats, "null pointer");
-  GHM_CHECK((G == nullptr) == (Dg == nullptr), "G and Dg: both or neither");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
   float2* st = reinterpret_cast<float2*>(stats);
   hipStream_t s = ghm_stream(stream);
   const bool big = (M + 127) / 128 >= 256;  // enough 128-token workgroups to give every CU one
   const dim3 g8(static_cast<unsigned>((M + 127) / 128)), g4(static_cast<unsigned>((M + 63) / 64));
-  if (G) {
-    if (big)
-      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<8, true>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, G,
-                         Dg, st, M, eps);
-    else
-      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<4, true>), g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, G,
-                         Dg, st, M, eps);
-  } else {
-    if (big)
-      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<8, false>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out,
-                         G, Dg, st, M, eps);
-    else
-      hipLaunchKernelGGL((k_ln_mlp_fwd_x3b<4, false>), g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out,
-                         G, Dg, st, M, eps);
-  }
+  if (big)
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+  else
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
   return ghm_launch_status();
 }

@@ -48,6 +48,7 @@ HIP_SIGNATURES = {
     "ghm_readout_fwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_clip_loss": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p],
     "ghm_readout_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_readout_bwd_clip": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_mlp_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_attn_bwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_qkv_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
@@ -97,9 +98,7 @@ HIP_SIGNATURES = {
     "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_ce_kl_out_elems": [_i64, _i, _i],
     "ghm_ln_qkv_fwd_x3": [_p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
-    "ghm_ln_mlp_fwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
-    "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
-    "ghm_mlp_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
+    "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_mlp_bwd_rc_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_mlp_bwd_rc_x3_stamped": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p, _i, _p],
     "ghm_qkv_bwd_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],

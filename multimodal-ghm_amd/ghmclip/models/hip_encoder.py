@@ -125,8 +125,7 @@ class EncoderPlan:
         # gelu attention: GELU'(scores) saved beside P for the backward
         self.Pd = torch.zeros(L, N, pad, pad, dtype=f32, device=dev) if self.act == 2 else None
         # x3: the MLP forward saves nothing and its backward recomputes U
-        # (GHM_MLP_RECOMPUTE=1, default) or the forward saves G and GELU'(U) (=0)
-        self.mlp_rc = self.precision == "x3" and os.environ.get("GHM_MLP_RECOMPUTE", "1") != "0"
+        self.mlp_rc = self.precision == "x3"
         # past 96 tokens the f32 plan runs the attention core on the split-bf16
         # ghm_attn_ext kernels (the joint CDM's curves stay inside the reference's
         # own thread-count spread with them: DESIGN.md §2); GHM_LONG_ATTN=f32
@@ -259,8 +258,7 @@ class EncoderPlan:
                       N, T, D_MODEL, self.scale_div, s)
                 c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
-                  _ptr(self.H[l + 1]), None if self.mlp_rc else _ptr(self.G[l]),
-                  None if self.mlp_rc else _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+                  _ptr(self.H[l + 1]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
                 return
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
@@ -364,9 +362,12 @@ class EncoderPlan:
         for _ in self.backward_iter(p, g, d_emb, tokens, layer_grad):
             pass
 
-    def backward_iter(self, p, g, d_emb=None, tokens=None, layer_grad=None):
+    def backward_iter(self, p, g, d_emb=None, tokens=None, layer_grad=None, clip=None):
         """backward() as a generator yielding after the readout backward and after
-        each layer (launches on the stream current when each is issued)."""
+        each layer (launches on the stream current when each is issued).
+        clip = (t_emb, i_emb, tower, B, K): the CLIP trainer's readout backward,
+        which recomputes this tower's rows of d(loss)/d(emb) from both towers'
+        embeddings (ghm_readout_bwd_clip) instead of reading d_emb."""
         tok = self.tokens if tokens is None else tokens
         de = self.d_emb if d_emb is None else d_emb
         c = _native.call
@@ -375,9 +376,14 @@ class EncoderPlan:
         cur = self.dH[0]
         jobs = []
         self.pending = jobs  # flush_pending() reduces what is queued so far (data-parallel buckets)
-        c("ghm_readout_bwd", _ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
-          _ptr(p["_out.weight"]), _ptr(de), _ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro),
-          _ptr(self.part_wout), _ptr(self.part_bout), N, T, D_MODEL, C, _stream())
+        ro = (_ptr(self.H[L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]), _ptr(p["_out.weight"]))
+        parts = (_ptr(cur), _ptr(self.part_ro), _ptr(self.part_bro), _ptr(self.part_wout), _ptr(self.part_bout))
+        if clip is None:
+            c("ghm_readout_bwd", *ro, _ptr(de), *parts, N, T, D_MODEL, C, _stream())
+        else:
+            te, ie, tower, B, K = clip
+            c("ghm_readout_bwd_clip", *ro, _ptr(te), _ptr(ie), tower, B, K, _ptr(de), *parts, N, T, D_MODEL, C,
+              _stream())
         jobs += [J(self.part_ro, N, [g["_read_out.weight"]]), J(self.part_bro, N, [g["_read_out.bias"]]),
                  J(self.part_wout, N, [g["_out.weight"]]), J(self.part_bout, N, [g["_out.bias"]])]
         yield
@@ -424,11 +430,7 @@ class EncoderPlan:
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
             # MLP + LN2: cur = dH_{l+1} -> nxt = dHmid_l
-            if x3 and not self.mlp_rc:
-                c("ghm_mlp_bwd_x3", _ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-                  _ptr(self.pack[l]), _ptr(self.Dg[l]), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL,
-                  D_HIDDEN, s)
-            elif x3:  # recomputes U; writes G (scratch) and dU
+            if x3:  # recomputes U; writes G (scratch) and dU
                 args = (_ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                         _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]), _ptr(p[f"_mlps.{l}.0.bias"]),
                         _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN)

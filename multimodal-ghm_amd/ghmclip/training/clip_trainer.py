@@ -161,6 +161,9 @@ class ClipTrainer:
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
         self.comm = torch.cuda.Stream(device=self.device)  # data-parallel bucket all-reduces
+        # data-parallel timing (bench.py): None, or a list that each step appends
+        # (bucket A ms, bucket B ms, exposed ms) event triples to
+        self.comm_timing = None
         self._bwd_it = [None, None]  # the towers' running backward launch generators
         self._setup_guide(penalty, guide_trans)
 
@@ -229,9 +232,11 @@ class ClipTrainer:
     # A step is a fixed sequence of phases; the two towers' phases run on two
     # streams (text: the current stream, image: a side stream), joined by stream
     # waits:
-    #   fwd(text) || fwd(image) -> loss -> bwd(text) || bwd(image) -> optim
-    # (data parallel: bwd splits into bwd_a || bwd_a -> bucket A all-reduce on the
-    # comm stream -> bwd_b || bwd_b -> bucket B -> optim)
+    #   fwd(text) || fwd(image) -> bwd(text) || bwd(image) -> loss value + optim
+    # (each tower's readout backward recomputes its rows of the loss gradient from
+    # both towers' embeddings, so no loss kernel sits between the phases; data
+    # parallel: bwd splits into bwd_a || bwd_a -> bucket A all-reduce on the comm
+    # stream -> bwd_b || bwd_b -> bucket B -> optim)
     # A tower's phase is a generator of pieces (the embedding, each encoder
     # layer, the readout), and the two towers' pieces are issued alternately.
     # Captured, every piece is its own small linear graph, replayed in the same
@@ -261,9 +266,14 @@ class ClipTrainer:
             self._guide_fwd(tower, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
 
     def _loss(self):
+        """The loss value of the step (and the penalised one) into the histories.
+        Runs at the start of the optimizer phase, off the forward -> backward
+        path: each tower's readout backward recomputes its rows of the loss
+        gradient from both towers' embeddings (ghm_readout_bwd_clip), which stay
+        untouched until the next forward."""
         pt, pi = self.plans
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), _p(pt.d_emb), _p(pi.d_emb), _p(self.loss_out),
+        _native.call("ghm_clip_loss", _p(pt.emb), _p(pi.emb), None, None, _p(self.loss_out),
                      _p(self.hist), _p(self.step_ctr), self.B, self.K, self.C, s)
         if self.guide:
             _native.call("ghm_guide_total", _p(self.gpart), self.n_gparts, self.n_seq, self.penalty,
@@ -275,7 +285,8 @@ class ClipTrainer:
         bucket A of this tower is final after it)."""
         plan = self.plans[tower]
         p, g = self.views[tower][0], self.views[tower][1]
-        it = plan.backward_iter(p, g, layer_grad=self._guide_hooks(tower))
+        clip = (self.plans[0].emb, self.plans[1].emb, tower, self.B, self.K)
+        it = plan.backward_iter(p, g, layer_grad=self._guide_hooks(tower), clip=clip)
         self._bwd_it[tower] = it
         top = min(self.dp_top, plan.L)  # the towers' layer counts may differ (clip_{t,i}model_nlayer)
         for k in range(1 + top):
@@ -338,19 +349,28 @@ class ClipTrainer:
         """One step (eager, or by replaying `graphs` from _capture_graphs)."""
         dp = self._dp()
         self._phase(self._fwd_gen, graphs, "fwd")
-        self._single(self._loss, graphs, "loss")
         if not dp:
             self._phase(self._bwd_gen, graphs, "bwd")
         else:
+            ev = [] if self.comm_timing is not None else None
             self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a")
             bucket_a, bucket_b = self.dp_buckets()
-            self._allreduce_ranges(bucket_a)
+            self._allreduce_ranges(bucket_a, ev)
             self._phase(self._bwd_b_gen, graphs, "bwd_b")
-            self._allreduce_ranges(bucket_b)
-            torch.cuda.current_stream().wait_stream(self.comm)
+            self._allreduce_ranges(bucket_b, ev)
+            main = torch.cuda.current_stream()
+            if ev is not None:  # exposed: the main stream's wait for the collectives after its backward
+                ev.append(torch.cuda.Event(enable_timing=True))
+                ev[-1].record(main)
+            main.wait_stream(self.comm)
+            if ev is not None:
+                ev.append(torch.cuda.Event(enable_timing=True))
+                ev[-1].record(main)
+                self.comm_timing.append(ev)
         self._single(self._optim, graphs, "optim")
 
     def _optim(self):
+        self._loss()
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         b1, omb1, b2, omb2, eps = self.consts
         _native.call("ghm_clip_prepare", _p(self.gflat), self.n_params, self.max_norm, _p(self.sched),
@@ -364,14 +384,35 @@ class ClipTrainer:
         B = the rest."""
         return dp_bucket_ranges(self.bucket_a, self.n_params)
 
-    def _allreduce_ranges(self, ranges):
+    def _allreduce_ranges(self, ranges, ev=None):
         """Mean over ranks of gflat[a:b] for each range, issued on the comm
         stream after the work already queued on the current stream (so the
-        current stream can run on while the collective is in flight)."""
+        current stream can run on while the collective is in flight).  ev: a
+        list to append the collective's start / end events (comm stream) to."""
         comm = self.comm
         comm.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(comm):
+            if ev is not None:
+                ev.append(torch.cuda.Event(enable_timing=True))
+                ev[-1].record(comm)
             distributed.allreduce_ranges_mean_(self.gflat, ranges, group=self.pg)
+            if ev is not None:
+                ev.append(torch.cuda.Event(enable_timing=True))
+                ev[-1].record(comm)
+
+    def comm_stats(self):
+        """Per-step averages (ms) of the recorded data-parallel timing: bucket A
+        and bucket B all-reduce durations on the comm stream, and the exposed
+        part (the main stream waiting for the collectives once its backward is
+        done).  Host sync."""
+        torch.cuda.synchronize()
+        rows = [(a0.elapsed_time(a1), b0.elapsed_time(b1), w0.elapsed_time(w1))
+                for a0, a1, b0, b1, w0, w1 in self.comm_timing]
+        if not rows:
+            return None
+        a, b, w = (sum(r[k] for r in rows) / len(rows) for k in range(3))
+        return {"bucket_a_ms": round(a, 4), "bucket_b_ms": round(b, 4), "exposed_ms": round(w, 4),
+                "steps": len(rows)}
 
     def _dp(self):
         return self.pg is not None or distributed.is_on()
@@ -419,7 +460,6 @@ class ClipTrainer:
             return out
         for t in (0, 1):
             graphs[("fwd", t)] = pieces(self._fwd_gen(t))
-        graphs["loss"] = one(self._loss)
         if not dp:
             for t in (0, 1):
                 graphs[("bwd", t)] = pieces(self._bwd_gen(t))

@@ -23,14 +23,18 @@ def pytest_configure(config):
 
 def curve_bound(ref, ref_t2, floor=1e-4, factor=2.0):
     """Per-step relative tolerance of a curve against the reference's PyTorch-CPU
-    run `ref` (8 threads): floor, or `factor` x the largest relative disagreement
-    between that run and the reference's own 2-thread run `ref_t2` up to that
-    step (the reference's reduction-order spread, committed as *_t2.npz
-    fixtures).  Also returns the self-consistent window: the leading steps whose
-    spread stays under `floor`."""
+    run `ref`: floor, or `factor` x the largest relative disagreement up to that
+    step between that run and the reference's own reruns `ref_t2` (one curve or a
+    list: another thread count, *_t2.npz; another CPU dispatch of the same code,
+    *_avx2.npz) -- the spread of the reference's own arithmetic.  `ref` is cut to
+    the reruns' length.  Also returns the self-consistent window: the leading
+    steps whose spread stays under `floor`."""
     import numpy as np
-    ref, ref_t2 = np.asarray(ref, np.float64), np.asarray(ref_t2, np.float64)
-    spread = np.maximum.accumulate(np.abs(ref - ref_t2) / np.abs(ref))
+    alts = [ref_t2] if np.ndim(ref_t2[0] if len(ref_t2) else 0) == 0 else list(ref_t2)
+    n = min(len(a) for a in alts)
+    ref = np.asarray(ref, np.float64)[:n]
+    dev = np.max([np.abs(ref - np.asarray(a, np.float64)[:n]) / np.abs(ref) for a in alts], axis=0)
+    spread = np.maximum.accumulate(dev)
     bound = np.maximum(floor, factor * spread)
     window = int(np.argmax(spread > floor)) if (spread > floor).any() else len(spread)
     return bound, window, spread

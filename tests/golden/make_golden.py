@@ -29,6 +29,16 @@ guide_tiny.npz      guided CLIP (clip_guide=True, exp_clip_guidedTF.sh: lr 1e-3 
                     raw grads, weights after each step.
 guide_curve.npz     the guided default config (L=5, d=128, B=128) ploss/loss history
                     for the first --guide-steps steps.
+
+The long reference runs (hours on this container's CPU) were made with:
+  clip_default_curve3001.npz   --only curve --curve-steps 3001 --curve-out clip_default_curve3001.npz --threads 6
+  clip_shallow_curve3001.npz   --only curve --curve-steps 3001 --curve-layers 1 --curve-out ... --threads 3
+  clip_guided_curve3001.npz    --only guide_curve --guide-steps 3001 --guide-out ... --threads 5
+  clip_guided_curve3001_t2.npz --only guide_curve --guide-steps 1101 --guide-out ... --threads 2
+  clip_guided_curve3001_avx2.npz  ATEN_CPU_CAPABILITY=avx2 MKL_CBWR=AVX2 (the same command,
+                    --guide-steps 1101 --threads 5): the reference's own code on the kernels a
+                    host without AVX-512 runs -- with the 2-thread run, the spread of the
+                    reference's own fp32 arithmetic (tests/conftest.py curve_bound).
 """
 import argparse
 import json

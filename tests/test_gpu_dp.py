@@ -111,3 +111,20 @@ def test_bench_dp2_weak_scaling_line(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["value"] > 0
     assert out["config"]["global_batch_rows"] == 256
+    d = out["dist"]  # self-describing data-parallel line: backend, ranks, collective and exposed time
+    assert d["backend"] == "gloo" and d["world_size"] == 2 and d["steps"] == 5
+    assert d["bucket_a_ms"] >= 0 and d["bucket_b_ms"] >= 0 and d["exposed_ms"] >= 0
+
+
+def test_bench_dp2_strong_scaling_line(tmp_path):
+    """--strong: the global batch of 128 rows split over the ranks (BASELINE.md
+    section 3.4 asks for weak and strong scaling)."""
+    env = dict(os.environ, GHM_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup",
+           "3", "--no-cpu-baseline", "--no-final-risk", "--strong"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["scaling"] == "strong" and out["config"]["global_batch_rows"] == 128
+    assert out["config"]["batch_rows_per_rank"] == 64

@@ -1,6 +1,7 @@
 # usage: bash tools/gpu_abenv.sh TAG "TESTS" SETTING... : GPU tests (in-tree lib), kbench (in-tree lib and every
 #        GHM_HIP_LIB= setting), then alternating 200-step CLIP benches, one per SETTING ("-" = defaults, else
-#        VAR=VAL[,VAR=VAL...]; GHM_HIP_LIB=<relative path> selects a variant library)
+#        VAR=VAL[,VAR=VAL...]; GHM_HIP_LIB=<relative path> selects a variant library; DIR=<dir> runs
+#        <dir>/bench.py, a checkout made by tools/make_abbase.sh)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=$1; TESTS=$2; shift 2
@@ -16,8 +17,9 @@ for v in "$@"; do
 done
 for i in 1 2 3; do
   for v in "$@"; do
-    if [ "$v" = "-" ]; then E=""; else E=$(echo $v | tr ',' ' '); fi
-    env $E timeout -k 10 200 python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-final-risk > $OUT/b.json 2> $OUT/b.err || { tail -5 $OUT/b.err; exit 3; }
+    B=bench.py
+    case "$v" in DIR=*) B=${v#DIR=}/bench.py; E="";; -) E="";; *) E=$(echo $v | tr ',' ' ');; esac
+    env $E timeout -k 10 200 python $B --steps 200 --warmup 10 --no-cpu-baseline --no-final-risk > $OUT/b.json 2> $OUT/b.err || { tail -5 $OUT/b.err; exit 3; }
     echo "$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/b.json)"
   done
 done | tee $OUT/ab.txt

@@ -82,19 +82,12 @@ def main():
                                       N, T, 128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
             "ln_mlp_fwd_x3b": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                          P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
-                                         P(xo["H"]), None, None, P(xo["st"]), M, 128, 512, plan.eps, sp),
+                                         P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp),
                                gf(4 * M * 128 * 512)),
-            "ln_mlp_fwd_x3b_save": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
-                                              P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
-                                              P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["G"]), P(xo["Dg"]),
-                                              P(xo["st"]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
             "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
                                         P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512, sp),
                               gf(6 * M * 128 * 512)),
-            "mlp_bwd_x3": (lambda: c("ghm_mlp_bwd_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
-                                     P(p["_lns_2.0.weight"]), pk, P(xo["Dg"]), P(plan.dU), P(xo["dHm"]),
-                                     P(plan.part_ln), M, 128, 512, sp), gf(4 * M * 128 * 512)),
             "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]), pk,
                                      P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, plan.eps, sp),
                            gf(2 * M * 128 * 384)),

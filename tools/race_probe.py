@@ -90,7 +90,7 @@ def main():
               M, 128, 512, B)
         elif aggr == "fwd_mlp":
             c("ghm_ln_mlp_fwd_x3b", P(p1.Hmid[l]), P(w1[f"_lns_2.{l}.weight"]), P(w1[f"_lns_2.{l}.bias"]),
-              P(p1.pack[l]), P(w1[f"_mlps.{l}.0.bias"]), P(w1[f"_mlps.{l}.2.bias"]), P(xH), None, None,
+              P(p1.pack[l]), P(w1[f"_mlps.{l}.0.bias"]), P(w1[f"_mlps.{l}.2.bias"]), P(xH),
               P(p1.st2[l + 1 if l + 1 < p1.L else l]), M, 128, 512, p1.eps, B)
         elif aggr == "wgrad0":
             tps, ns = p1.wg["w2"]
