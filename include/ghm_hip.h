@@ -86,6 +86,15 @@ int ghm_readout_bwd_clip(const float* H, const float* W_ro, const float* b_ro, c
                          float* dH, float* part_wro, float* part_bro, float* part_wout, float* part_bout,
                          int64_t n_seq, int T, int D, int C, void* stream);
 
+/* Token- and position-embedding gradients of one encoder in one pass over dH0
+ * [n_seq][T][D] (D = 128, V = 10): tok_grad [V][D] = sums of dH0 rows by token id,
+ * pos_grad [T][D] = sums over the sequences; part: ghm_embed_bwd_part_elems(T, V)
+ * floats of scratch.  Deterministic (fixed summation order)  —  backward of
+ * models/model.py:764-765 (token_embeddings(x) + position_embeddings(positions)). */
+int64_t ghm_embed_bwd_part_elems(int T, int V);
+int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D,
+                  float* tok_grad, float* pos_grad, float* part, void* stream);
+
 /* MLP + LN2 backward for one layer (Dg = GELU'(U) from ghm_ln_mlp_fwd, passed as U):
  * writes dU [M][F] and dH_mid = dH_out + dLN2;
  * part_ln [n_blocks][2][D] = partial (dgamma, dbeta) of LN2 where

@@ -615,6 +615,91 @@ __global__ __launch_bounds__(256) void k_readout_bwd(
 }
 
 // ---------------------------------------------------------------------------
+// Embedding gradients in one pass over dH_0 [n_seq][T][128]   (model.py:764-765)
+//   tok_grad[v] = sum over (n, t) with token v of dH_0[n][t],
+//   pos_grad[t] = sum over n of dH_0[n][t].
+// Workgroup (t, s): position t of the sequences of split s, 32 lanes (float4)
+// per row, 8 rows at a time; every thread sums its rows in sequence order into
+// the position sum and, through a 0/1 fused multiply-add (exact), into the sum
+// of the row's token; the 8 row slots combine in order through LDS.  Partials
+// [s][t][V + 1][128] (tokens, then the position) are summed in a fixed order by
+// k_embed_grad_final: deterministic.  Replaces two column-sum passes over dH_0
+// (token ids, then positions: 4 launches, ~50 us of the step's serial tail).
+// ---------------------------------------------------------------------------
+constexpr int EMB_SPLIT = 4;
+template <int V>
+__global__ __launch_bounds__(256) void k_embed_grad_part(const float* __restrict__ dH, const uint8_t* __restrict__ tok,
+                                                         int n_seq, int T, float* __restrict__ part) {
+  __shared__ float4 red[8][V + 1][32];
+  const int t = blockIdx.x, sp = blockIdx.y, slot = threadIdx.x >> 5, c4 = threadIdx.x & 31;
+  const int n0 = static_cast<int>((static_cast<int64_t>(n_seq) * sp) / EMB_SPLIT);
+  const int n1 = static_cast<int>((static_cast<int64_t>(n_seq) * (sp + 1)) / EMB_SPLIT);
+  float4 pos = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int n = n0 + slot; n < n1; n += 8) {
+    const int64_t row = static_cast<int64_t>(n) * T + t;
+    const float4 x = reinterpret_cast<const float4*>(dH + row * GHM_D)[c4];
+    const int tv = tok[row];
+    pos.x += x.x; pos.y += x.y; pos.z += x.z; pos.w += x.w;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float w = tv == v ? 1.f : 0.f;  // acc + 1 * x = acc + x, acc + 0 * x = acc: exact
+      acc[v].x = fmaf(x.x, w, acc[v].x);
+      acc[v].y = fmaf(x.y, w, acc[v].y);
+      acc[v].z = fmaf(x.z, w, acc[v].z);
+      acc[v].w = fmaf(x.w, w, acc[v].w);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[slot][v][c4] = acc[v];
+  red[slot][V][c4] = pos;
+  __syncthreads();
+  // thread (k, c4), k < V + 1 (the 8 row slots in order) -> part[sp][t][k][4 c4 ..]
+  for (int e = threadIdx.x; e < (V + 1) * 32; e += 256) {
+    const int k = e >> 5, c = e & 31;
+    float4 a = red[0][k][c];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+      const float4 b = red[q][k][c];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    reinterpret_cast<float4*>(part + ((static_cast<int64_t>(sp) * T + t) * (V + 1) + k) * GHM_D)[c] = a;
+  }
+}
+
+// tok_grad[v][d] = sum over (s, t) of part[s][t][v][d] (s, then t ascending);
+// pos_grad[t][d] = sum over s of part[s][t][V][d].  One thread per output.
+__global__ __launch_bounds__(256) void k_embed_grad_final(const float* __restrict__ part, int T, int V,
+                                                          float* __restrict__ tok_grad, float* __restrict__ pos_grad) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t ntok = static_cast<int64_t>(V) * GHM_D;
+  const int64_t stride_s = static_cast<int64_t>(T) * (V + 1) * GHM_D;
+  if (i < ntok) {
+    const int v = static_cast<int>(i / GHM_D), d = static_cast<int>(i % GHM_D);
+    const float* p = part + static_cast<int64_t>(v) * GHM_D + d;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};  // the four splits' sums, each over t in order
+    for (int t = 0; t < T; ++t) {
+      float x[EMB_SPLIT];
+#pragma unroll
+      for (int s = 0; s < EMB_SPLIT; ++s) x[s] = p[s * stride_s + static_cast<int64_t>(t) * (V + 1) * GHM_D];
+#pragma unroll
+      for (int s = 0; s < EMB_SPLIT; ++s) a[s] += x[s];
+    }
+    tok_grad[i] = (a[0] + a[1]) + (a[2] + a[3]);
+  } else if (i < ntok + static_cast<int64_t>(T) * GHM_D) {
+    const int64_t j = i - ntok;
+    const int t = static_cast<int>(j / GHM_D), d = static_cast<int>(j % GHM_D);
+    const float* p = part + (static_cast<int64_t>(t) * (V + 1) + V) * GHM_D + d;
+    float a = 0.f;
+#pragma unroll
+    for (int s = 0; s < EMB_SPLIT; ++s) a += p[s * stride_s];
+    pos_grad[j] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Deterministic partial reductions, several jobs per launch.  Wide, shallow jobs
 // (the weight-gradient partials): thread = one output, its splits summed in 8
 // interleaved partial sums and a balanced tree, 256 outputs per block.  The others (LayerNorm / readout /
@@ -725,6 +810,25 @@ extern "C" int ghm_readout_bwd_clip(const float* H, const float* W_ro, const flo
   hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
                      H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T, t_emb, i_emb,
                      tower, B, K);
+  return ghm_launch_status();
+}
+
+extern "C" int64_t ghm_embed_bwd_part_elems(int T, int V) {
+  return static_cast<int64_t>(EMB_SPLIT) * T * (V + 1) * GHM_D;
+}
+
+extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D,
+                             float* tok_grad, float* pos_grad, float* part, void* stream) {
+  GHM_CHECK(dH0 && tokens && tok_grad && pos_grad && part, "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && n_seq >= 1 && n_seq < (int64_t(1) << 30), "shape (D == 128)");
+  GHM_CHECK(V == 10, "token embedding gradients are built for the 10-value GHM vocabulary");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(dH0) | reinterpret_cast<uintptr_t>(part)) & 15) == 0, "16-byte aligned");
+  hipStream_t s = ghm_stream(stream);
+  hipLaunchKernelGGL(k_embed_grad_part<10>, dim3(static_cast<unsigned>(T), EMB_SPLIT), dim3(256), 0, s, dH0, tokens,
+                     static_cast<int>(n_seq), T, part);
+  const int64_t nout = static_cast<int64_t>(V + T) * GHM_D;
+  hipLaunchKernelGGL(k_embed_grad_final, dim3(static_cast<unsigned>((nout + 255) / 256)), dim3(256), 0, s, part, T,
+                     V, tok_grad, pos_grad);
   return ghm_launch_status();
 }
 

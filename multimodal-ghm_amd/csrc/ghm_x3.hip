@@ -62,59 +62,72 @@ struct SplitJobs {
   ghm_split_job job[GHM_SPLIT_MAX_JOBS];
 };
 
+// inverse of perm32: the k-slot holding unit f
+__device__ __forceinline__ constexpr int inv_perm32(int f) {
+  return (f & ~31) + ((f >> 3) & 1) * 16 + ((f >> 2) & 1) * 8 + ((f >> 4) & 1) * 4 + (f & 3);
+}
+
+// One workgroup per (layer, 64 x 64 tile of one weight matrix): the tile is read
+// once, coalesced, into LDS, and written (split) into every pack region that
+// holds it, 8 consecutive output columns (16 B per plane) per thread-store.
+// Tiles 0-11: Wq / Wk / Wv (2 x 2 each), 12-27: W1 [512][128] (8 x 2), 28-43: W2
+// [128][512] (2 x 8).  (The round-1 kernel gathered the transposed layouts with
+// one 4-B load per element, 512 B apart: 11 us per tower, latency-bound.)
+constexpr int SPLIT_TILES = 44;
 __global__ __launch_bounds__(256) void k_split_weights(SplitJobs J) {
+  __shared__ float tile[64][65];
   const ghm_split_job& jb = J.job[blockIdx.y];
-  const int e = 4 * (static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x));
-  if (e >= PK_ELEMS / 2) return;
-  float v[4];
-  int base, n, idx;
-  if (e < PK_QKV) {
-    idx = e; base = PK_QKV_N; n = PK_QKV;
-    const int row = e >> 7, col = e & 127;
-    const float* W = row < 128 ? jb.Wq : (row < 256 ? jb.Wk : jb.Wv);
-    const float4 f = *reinterpret_cast<const float4*>(W + (row & 127) * GHM_D + col);
-    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-  } else if (e < 2 * PK_QKV) {
-    idx = e - PK_QKV; base = PK_QKV_T; n = PK_QKV;
-    const int d = idx / 384, c = idx % 384, mat = c >> 7, o = c & 127;
-    const float* W = mat == 0 ? jb.Wq : (mat == 1 ? jb.Wk : jb.Wv);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = W[(o + t) * GHM_D + d];
-  } else if (e < 2 * PK_QKV + PK_W) {
-    idx = e - 2 * PK_QKV; base = PK_W1_N; n = PK_W;
-    const float4 f = *reinterpret_cast<const float4*>(jb.W1 + idx);
-    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-  } else if (e < 2 * PK_QKV + 2 * PK_W) {
-    idx = e - 2 * PK_QKV - PK_W; base = PK_W1_T; n = PK_W;
-    const int d = idx >> 9, q = idx & 511;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = jb.W1[perm_col(q + t) * GHM_D + d];
-  } else if (e < 2 * PK_QKV + 3 * PK_W) {
-    idx = e - 2 * PK_QKV - 2 * PK_W; base = PK_W2_P; n = PK_W;
-    const int o = idx >> 9, q = idx & 511;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = jb.W2[o * GHM_F + perm_col(q + t)];
-  } else if (e < 2 * PK_QKV + 4 * PK_W) {
-    idx = e - 2 * PK_QKV - 3 * PK_W; base = PK_W2_T; n = PK_W;
-    const int f = idx >> 7, o = idx & 127;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = jb.W2[(o + t) * GHM_F + f];
-  } else if (e < 2 * PK_QKV + 5 * PK_W) {
-    idx = e - 2 * PK_QKV - 4 * PK_W; base = PK_W1_T32; n = PK_W;
-    const int d = idx >> 9, q = idx & 511;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = jb.W1[perm32(q + t) * GHM_D + d];
+  const int tix = blockIdx.x, t = threadIdx.x;
+  int kind, m = 0, r0, c0, ld;  // kind 0: Q/K/V (m), 1: W1, 2: W2
+  const float* W;
+  if (tix < 12) {
+    kind = 0; m = tix >> 2; r0 = 64 * ((tix & 3) >> 1); c0 = 64 * (tix & 1); ld = GHM_D;
+    W = m == 0 ? jb.Wq : (m == 1 ? jb.Wk : jb.Wv);
+  } else if (tix < 28) {
+    kind = 1; r0 = 64 * ((tix - 12) >> 1); c0 = 64 * ((tix - 12) & 1); ld = GHM_D; W = jb.W1;
   } else {
-    idx = e - 2 * PK_QKV - 5 * PK_W; base = PK_W2_P32; n = PK_W;
-    const int o = idx >> 9, q = idx & 511;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = jb.W2[o * GHM_F + perm32(q + t)];
+    kind = 2; r0 = 64 * ((tix - 28) >> 3); c0 = 64 * ((tix - 28) & 7); ld = GHM_F; W = jb.W2;
   }
-  bf16x4 hi, lo;
-  split4(make_float4(v[0], v[1], v[2], v[3]), hi, lo);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i4 = t + 256 * k, row = i4 >> 4, col = 4 * (i4 & 15);
+    const float4 v = *reinterpret_cast<const float4*>(W + static_cast<int64_t>(r0 + row) * ld + c0 + col);
+    tile[row][col] = v.x; tile[row][col + 1] = v.y; tile[row][col + 2] = v.z; tile[row][col + 3] = v.w;
+  }
+  __syncthreads();
   __bf16* pk = reinterpret_cast<__bf16*>(jb.pack);
-  stb4(pk + base + idx, hi);
-  stb4(pk + base + n + idx, lo);
+  // out(r, q) of a 64 x 64 output block: transposed layouts read tile[src][r],
+  // the others tile[r][src], src = the permuted index of q inside the tile
+  auto emit = [&](int base, int n, int ld_out, int orow0, int ocol0, bool trans, int perm) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int g = t + 256 * k, r = g >> 3, q0 = 8 * (g & 7);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = q0 + e;
+        const int src = perm == 1 ? perm_col(q) : (perm == 2 ? perm32(q) : q);
+        v[e] = trans ? tile[src][r] : tile[r][src];
+      }
+      bf16x8 hi, lo;
+      split8(v, hi, lo);
+      const int64_t o = base + static_cast<int64_t>(orow0 + r) * ld_out + ocol0 + q0;
+      *reinterpret_cast<bf16x8*>(pk + o) = hi;
+      *reinterpret_cast<bf16x8*>(pk + o + n) = lo;
+    }
+  };
+  if (kind == 0) {  // [384][128] row 128 m + o, col d; [128][384] row d, col 128 m + o
+    emit(PK_QKV_N, PK_QKV, GHM_D, 128 * m + r0, c0, false, 0);
+    emit(PK_QKV_T, PK_QKV, 3 * GHM_D, c0, 128 * m + r0, true, 0);
+  } else if (kind == 1) {  // W1[f][d]: N; T / T32: row d, col q = W1[perm(q)][d]
+    emit(PK_W1_N, PK_W, GHM_D, r0, c0, false, 0);
+    emit(PK_W1_T, PK_W, GHM_F, c0, r0, true, 1);
+    emit(PK_W1_T32, PK_W, GHM_F, c0, r0, true, 2);
+  } else {  // W2[o][f]: P / P32: row o, col q = W2[o][perm(q)]; T: row f, col o
+    emit(PK_W2_P, PK_W, GHM_F, r0, c0, false, 1);
+    emit(PK_W2_T, PK_W, GHM_D, c0, r0, true, 0);
+    emit(PK_W2_P32, PK_W, GHM_F, r0, c0, false, 2);
+  }
 }
 
 // LN a token row (row layout) and split it into the 8 k-step fragments
@@ -1684,10 +1697,12 @@ extern "C" int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* st
     const ghm_split_job& jb = jobs[i];
     GHM_CHECK(jb.Wq && jb.Wk && jb.Wv && jb.W1 && jb.W2 && jb.pack, "null pointer in job");
     GHM_CHECK((reinterpret_cast<uintptr_t>(jb.pack) & 15) == 0, "pack must be 16-byte aligned");
+    GHM_CHECK(((reinterpret_cast<uintptr_t>(jb.Wq) | reinterpret_cast<uintptr_t>(jb.Wk) |
+                reinterpret_cast<uintptr_t>(jb.Wv) | reinterpret_cast<uintptr_t>(jb.W1) |
+                reinterpret_cast<uintptr_t>(jb.W2)) & 15) == 0, "weights must be 16-byte aligned");
     J.job[i] = jb;
   }
-  const unsigned nblk = (PK_ELEMS / 2 / 4 + 255) / 256;
-  hipLaunchKernelGGL(k_split_weights, dim3(nblk, static_cast<unsigned>(n_jobs)), dim3(256), 0,
+  hipLaunchKernelGGL(k_split_weights, dim3(SPLIT_TILES, static_cast<unsigned>(n_jobs)), dim3(256), 0,
                      ghm_stream(stream), J);
   return ghm_launch_status();
 }

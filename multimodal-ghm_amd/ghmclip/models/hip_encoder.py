@@ -188,7 +188,8 @@ class EncoderPlan:
         # embedding backward scratch: token sums by id (ghm_wcolsum), then the
         # position gradient's sum over sequences (ghm_colsum), one after the other
         self.part_emb = e(max(lib.ghm_wcolsum_part_elems(M, D_MODEL, vocab),
-                              lib.ghm_colsum_part_elems(N, T * D_MODEL)))
+                              lib.ghm_colsum_part_elems(N, T * D_MODEL),
+                              lib.ghm_embed_bwd_part_elems(T, vocab)))
         self.d_emb = e(N, num_class)
         self.pack = None
         if self.precision == "x3":
@@ -395,9 +396,13 @@ class EncoderPlan:
         self._flush(jobs, s)
         # embeddings (model.py:765 via autograd): dH0 rows summed by token id,
         # and over the sequences for the positions
-        c("ghm_wcolsum", None, _ptr(tok), self.V, _ptr(cur), self.M, self.M, 0, self.M, D_MODEL,
-          _ptr(g["token_embeddings.weight"]), None, _ptr(self.part_emb), s)
-        c("ghm_colsum", _ptr(cur), N, T * D_MODEL, _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)
+        if self.V == 10:  # one pass over dH0 for both
+            c("ghm_embed_bwd", _ptr(cur), _ptr(tok), N, T, self.V, D_MODEL, _ptr(g["token_embeddings.weight"]),
+              _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)
+        else:
+            c("ghm_wcolsum", None, _ptr(tok), self.V, _ptr(cur), self.M, self.M, 0, self.M, D_MODEL,
+              _ptr(g["token_embeddings.weight"]), None, _ptr(self.part_emb), s)
+            c("ghm_colsum", _ptr(cur), N, T * D_MODEL, _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)
 
     def flush_pending(self):
         """Reduce the parameter-gradient partials queued by the running

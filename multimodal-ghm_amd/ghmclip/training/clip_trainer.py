@@ -302,14 +302,15 @@ class ClipTrainer:
         for _ in self._bwd_it[tower]:
             yield
 
-    def _phase(self, genf, graphs=None, key=None):
+    def _phase(self, genf, graphs=None, key=None, fork=True, join=True):
         """Run a two-tower phase: the pieces of genf(1) (image, side stream) and
         genf(0) (text, current stream) alternately, joined back into the current
-        stream; graphs: replay the captured piece graphs[(key, tower)] instead."""
+        stream; graphs: replay the captured piece graphs[(key, tower)] instead.
+        fork / join = False: the caller orders the streams itself (_cross_wait)."""
         main, s0, s1 = self._tower_streams()
         st = {1: s1, 0: s0}
         for x in (s0, s1):
-            if x != main:
+            if x != main and fork:
                 x.wait_stream(main)
         if graphs is None:
             live = {1: genf(1), 0: genf(0)}
@@ -329,8 +330,21 @@ class ClipTrainer:
                         with torch.cuda.stream(st[t]):
                             pieces[t][i].replay()
         for x in (s0, s1):
-            if x != main:
+            if x != main and join:
                 main.wait_stream(x)
+
+    def _cross_wait(self):
+        """Each tower's stream waits for the other's work so far (one hop each way,
+        concurrently) -- between the forward and the backward, where each tower's
+        readout backward needs both towers' embeddings; a join into the current
+        stream and a fork back out would put two hops in series on the side stream."""
+        _, s0, s1 = self._tower_streams()
+        if s0 != s1:
+            e0, e1 = torch.cuda.Event(), torch.cuda.Event()
+            e0.record(s0)
+            e1.record(s1)
+            s0.wait_event(e1)
+            s1.wait_event(e0)
 
     def _single(self, fn, graphs=None, key=None):
         if graphs is None:
@@ -348,15 +362,16 @@ class ClipTrainer:
     def _run(self, graphs=None):
         """One step (eager, or by replaying `graphs` from _capture_graphs)."""
         dp = self._dp()
-        self._phase(self._fwd_gen, graphs, "fwd")
+        self._phase(self._fwd_gen, graphs, "fwd", join=False)
+        self._cross_wait()
         if not dp:
-            self._phase(self._bwd_gen, graphs, "bwd")
+            self._phase(self._bwd_gen, graphs, "bwd", fork=False)
         else:
             ev = [] if self.comm_timing is not None else None
-            self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a")
+            self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a", fork=False, join=False)
             bucket_a, bucket_b = self.dp_buckets()
-            self._allreduce_ranges(bucket_a, ev)
-            self._phase(self._bwd_b_gen, graphs, "bwd_b")
+            self._allreduce_ranges(bucket_a, ev, both=True)
+            self._phase(self._bwd_b_gen, graphs, "bwd_b", fork=False)
             self._allreduce_ranges(bucket_b, ev)
             main = torch.cuda.current_stream()
             if ev is not None:  # exposed: the main stream's wait for the collectives after its backward
@@ -384,13 +399,16 @@ class ClipTrainer:
         B = the rest."""
         return dp_bucket_ranges(self.bucket_a, self.n_params)
 
-    def _allreduce_ranges(self, ranges, ev=None):
+    def _allreduce_ranges(self, ranges, ev=None, both=False):
         """Mean over ranks of gflat[a:b] for each range, issued on the comm
-        stream after the work already queued on the current stream (so the
-        current stream can run on while the collective is in flight).  ev: a
-        list to append the collective's start / end events (comm stream) to."""
+        stream after the work already queued on the current stream (both: and on
+        the side tower's stream), so the towers' streams run on while the
+        collective is in flight.  ev: a list to append the collective's start /
+        end events (comm stream) to."""
         comm = self.comm
         comm.wait_stream(torch.cuda.current_stream())
+        if both:
+            comm.wait_stream(self._tower_streams()[2])
         with torch.cuda.stream(comm):
             if ev is not None:
                 ev.append(torch.cuda.Event(enable_timing=True))
