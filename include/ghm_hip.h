@@ -24,6 +24,16 @@ extern "C" {
 const char* ghm_last_error_string(void);
 /* 1 when the library was built for gfx950 and a device is visible, else 0. */
 int ghm_device_ok(void);
+/* Cross-stream ordering (the two-tower step's fork / join / cross waits,
+ * replacing torch Stream.wait_stream in train_CLIP's step, which has no
+ * reference counterpart: the reference runs the towers one after the other).
+ * ghm_event_create(1): an event recorded with a device-scope release and no
+ * system-scope fence; (0) a default one.  ghm_event_record / ghm_stream_wait:
+ * hipEventRecord / hipStreamWaitEvent (streams: hipStream_t or NULL). */
+void* ghm_event_create(int device_scope);
+int ghm_event_destroy(void* ev);
+int ghm_event_record(void* ev, void* stream);
+int ghm_stream_wait(void* stream, void* ev);
 
 /* ---- forward ---------------------------------------------------------- */
 
@@ -86,14 +96,17 @@ int ghm_readout_bwd_clip(const float* H, const float* W_ro, const float* b_ro, c
                          float* dH, float* part_wro, float* part_bro, float* part_wout, float* part_bout,
                          int64_t n_seq, int T, int D, int C, void* stream);
 
-/* Token- and position-embedding gradients of one encoder in one pass over dH0
- * [n_seq][T][D] (D = 128, V = 10): tok_grad [V][D] = sums of dH0 rows by token id,
- * pos_grad [T][D] = sums over the sequences; part: ghm_embed_bwd_part_elems(T, V)
- * floats of scratch.  Deterministic (fixed summation order)  —  backward of
- * models/model.py:764-765 (token_embeddings(x) + position_embeddings(positions)). */
+/* Token- and position-embedding gradient PARTIALS of one encoder in one pass over
+ * dH0 [n_seq][T][D] (D = 128, V = 10): part = [S T][V][D] token sums (rows of
+ * dH0 by token id, per (split, position)), then [S][T][D] position sums (over
+ * the split's sequences), S = ghm_embed_bwd_splits(), ghm_embed_bwd_part_elems(T, V)
+ * floats.  Reduce them with ghm_reduce_batch: tok_grad = the sum over S T of the
+ * first region, pos_grad = the sum over S of the second.  Deterministic  —
+ * backward of models/model.py:764-765 (token_embeddings(x) + position_embeddings). */
+int ghm_embed_bwd_splits(void);
 int64_t ghm_embed_bwd_part_elems(int T, int V);
-int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D,
-                  float* tok_grad, float* pos_grad, float* part, void* stream);
+int ghm_embed_bwd_part(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D, float* part,
+                       void* stream);
 
 /* MLP + LN2 backward for one layer (Dg = GELU'(U) from ghm_ln_mlp_fwd, passed as U):
  * writes dU [M][F] and dH_mid = dH_out + dLN2;
@@ -434,6 +447,12 @@ int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit);
 int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
                 const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2, const float* bias,
                 const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit, void* stream);
+/* The same product with exact f32 MFMA (v_mfma_f32_32x32x2f32, no split) and the
+ * erf GELU in epilogue 1: the VLM's precision "f32" mode (replaces the torch.mm /
+ * addmm library calls of rounds 1-3).  Arguments and limits as ghm_gemm_x3. */
+int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
+                 const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2, const float* bias,
+                 const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit, void* stream);
 /* D[m][n] = sum_z slab[z][m][n] (z in order: deterministic); rows stacked into
  * D0, D1, D2 by chunk (0: D0 only). */
 int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,

@@ -522,32 +522,33 @@ __device__ __forceinline__ void clip_row_grad(const float* __restrict__ te, cons
   }
 }
 
-// CLIP: te / ie non-null -> the row's loss gradient is recomputed here (and
-// written to demb) instead of read from a separate loss kernel's output, so the
-// backward of each tower starts as soon as both towers' embeddings exist
+// One tower's rows of the loss gradient, one thread per row (a few-microsecond
+// kernel ahead of that tower's readout backward: computing the row inside each
+// readout-backward workgroup put its latency chain in front of every round of
+// the 640 workgroups, 14 -> 28 us)
+template <int NC>
+__global__ __launch_bounds__(64) void k_clip_grad_rows(const float* __restrict__ te, const float* __restrict__ ie,
+                                                       int tower, int B, int K, float* __restrict__ demb) {
+  const int n = blockIdx.x * 64 + threadIdx.x;
+  if (n >= (K + 1) * B) return;
+  float de[NC];
+  clip_row_grad<NC>(te, ie, tower, n, B, K, de);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) demb[static_cast<int64_t>(n) * NC + c] = de[c];
+}
+
 template <int NC>
 __global__ __launch_bounds__(256) void k_readout_bwd(
     const float* __restrict__ H, const float* __restrict__ Wro, const float* __restrict__ bro,
-    const float* __restrict__ wout, float* __restrict__ demb, float* __restrict__ dH,
+    const float* __restrict__ wout, const float* __restrict__ demb, float* __restrict__ dH,
     float* __restrict__ part_wro, float* __restrict__ part_bro, float* __restrict__ part_wout,
-    float* __restrict__ part_bout, int T, const float* __restrict__ te = nullptr,
-    const float* __restrict__ ie = nullptr, int tower = 0, int B = 0, int K = 0) {
+    float* __restrict__ part_bout, int T) {
   __shared__ float2 red[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, n = blockIdx.x;
   const int64_t base = static_cast<int64_t>(n) * T;
   float de[NC];
-  if (te) {
-    clip_row_grad<NC>(te, ie, tower, n, B, K, de);
-    if (threadIdx.x < NC) {
-      float v = 0.f;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) v = threadIdx.x == c ? de[c] : v;
-      demb[static_cast<int64_t>(n) * NC + threadIdx.x] = v;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
-  }
+  for (int c = 0; c < NC; ++c) de[c] = demb[static_cast<int64_t>(n) * NC + c];
   float2 u = make_float2(0.f, 0.f);
   float bdot = 0.f;
   {
@@ -619,12 +620,15 @@ __global__ __launch_bounds__(256) void k_readout_bwd(
 //   tok_grad[v] = sum over (n, t) with token v of dH_0[n][t],
 //   pos_grad[t] = sum over n of dH_0[n][t].
 // Workgroup (t, s): position t of the sequences of split s, 32 lanes (float4)
-// per row, 8 rows at a time; every thread sums its rows in sequence order into
-// the position sum and, through a 0/1 fused multiply-add (exact), into the sum
-// of the row's token; the 8 row slots combine in order through LDS.  Partials
-// [s][t][V + 1][128] (tokens, then the position) are summed in a fixed order by
-// k_embed_grad_final: deterministic.  Replaces two column-sum passes over dH_0
-// (token ids, then positions: 4 launches, ~50 us of the step's serial tail).
+// per row, 8 rows at a time (4 in flight per thread); every thread sums its rows
+// in sequence order into the position sum and, through a 0/1 fused multiply-add
+// (exact), into the sum of the row's token; the 8 row slots combine in order
+// through LDS.  Partials: tokens [s T + t][V][128] then positions [s][T][128];
+// the caller reduces them over their leading index (ghm_reduce_batch jobs of
+// S T and S splits: the trainer's final partial-reduction launch), so the
+// gradients cost one pass over dH_0 and no launch of their own.  Replaces two
+// column-sum passes over dH_0 (token ids, then positions: 4 launches, ~50 us of
+// the step's serial tail).
 // ---------------------------------------------------------------------------
 constexpr int EMB_SPLIT = 4;
 template <int V>
@@ -638,25 +642,40 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* __restrict
   float4 acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int n = n0 + slot; n < n1; n += 8) {
-    const int64_t row = static_cast<int64_t>(n) * T + t;
-    const float4 x = reinterpret_cast<const float4*>(dH + row * GHM_D)[c4];
-    const int tv = tok[row];
-    pos.x += x.x; pos.y += x.y; pos.z += x.z; pos.w += x.w;
+  for (int nb = n0 + slot; nb < n1; nb += 32) {  // 4 rows in flight, summed in sequence order
+    float4 x[4];
+    int tv[4];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const float w = tv == v ? 1.f : 0.f;  // acc + 1 * x = acc + x, acc + 0 * x = acc: exact
-      acc[v].x = fmaf(x.x, w, acc[v].x);
-      acc[v].y = fmaf(x.y, w, acc[v].y);
-      acc[v].z = fmaf(x.z, w, acc[v].z);
-      acc[v].w = fmaf(x.w, w, acc[v].w);
+    for (int u = 0; u < 4; ++u) {
+      const int n = nb + 8 * u;
+      const int nc = n < n1 ? n : nb;  // rows past the split re-read row nb with token -1 (no class)
+      const int64_t row = static_cast<int64_t>(nc) * T + t;
+      x[u] = reinterpret_cast<const float4*>(dH + row * GHM_D)[c4];
+      tv[u] = n < n1 ? static_cast<int>(tok[row]) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pw = tv[u] >= 0 ? 1.f : 0.f;
+      pos.x = fmaf(x[u].x, pw, pos.x); pos.y = fmaf(x[u].y, pw, pos.y);
+      pos.z = fmaf(x[u].z, pw, pos.z); pos.w = fmaf(x[u].w, pw, pos.w);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float w = tv[u] == v ? 1.f : 0.f;  // acc + 1 * x = acc + x, acc + 0 * x = acc: exact
+        acc[v].x = fmaf(x[u].x, w, acc[v].x);
+        acc[v].y = fmaf(x[u].y, w, acc[v].y);
+        acc[v].z = fmaf(x[u].z, w, acc[v].z);
+        acc[v].w = fmaf(x[u].w, w, acc[v].w);
+      }
     }
   }
 #pragma unroll
   for (int v = 0; v < V; ++v) red[slot][v][c4] = acc[v];
   red[slot][V][c4] = pos;
   __syncthreads();
-  // thread (k, c4), k < V + 1 (the 8 row slots in order) -> part[sp][t][k][4 c4 ..]
+  // thread (k, c4), k < V + 1 (the 8 row slots in order): token rows, then the position row
+  float4* ptok = reinterpret_cast<float4*>(part) + (static_cast<int64_t>(sp) * T + t) * V * 32;
+  float4* ppos = reinterpret_cast<float4*>(part) + static_cast<int64_t>(EMB_SPLIT) * T * V * 32 +
+                 (static_cast<int64_t>(sp) * T + t) * 32;
   for (int e = threadIdx.x; e < (V + 1) * 32; e += 256) {
     const int k = e >> 5, c = e & 31;
     float4 a = red[0][k][c];
@@ -665,37 +684,7 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* __restrict
       const float4 b = red[q][k][c];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
-    reinterpret_cast<float4*>(part + ((static_cast<int64_t>(sp) * T + t) * (V + 1) + k) * GHM_D)[c] = a;
-  }
-}
-
-// tok_grad[v][d] = sum over (s, t) of part[s][t][v][d] (s, then t ascending);
-// pos_grad[t][d] = sum over s of part[s][t][V][d].  One thread per output.
-__global__ __launch_bounds__(256) void k_embed_grad_final(const float* __restrict__ part, int T, int V,
-                                                          float* __restrict__ tok_grad, float* __restrict__ pos_grad) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  const int64_t ntok = static_cast<int64_t>(V) * GHM_D;
-  const int64_t stride_s = static_cast<int64_t>(T) * (V + 1) * GHM_D;
-  if (i < ntok) {
-    const int v = static_cast<int>(i / GHM_D), d = static_cast<int>(i % GHM_D);
-    const float* p = part + static_cast<int64_t>(v) * GHM_D + d;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};  // the four splits' sums, each over t in order
-    for (int t = 0; t < T; ++t) {
-      float x[EMB_SPLIT];
-#pragma unroll
-      for (int s = 0; s < EMB_SPLIT; ++s) x[s] = p[s * stride_s + static_cast<int64_t>(t) * (V + 1) * GHM_D];
-#pragma unroll
-      for (int s = 0; s < EMB_SPLIT; ++s) a[s] += x[s];
-    }
-    tok_grad[i] = (a[0] + a[1]) + (a[2] + a[3]);
-  } else if (i < ntok + static_cast<int64_t>(T) * GHM_D) {
-    const int64_t j = i - ntok;
-    const int t = static_cast<int>(j / GHM_D), d = static_cast<int>(j % GHM_D);
-    const float* p = part + (static_cast<int64_t>(t) * (V + 1) + V) * GHM_D + d;
-    float a = 0.f;
-#pragma unroll
-    for (int s = 0; s < EMB_SPLIT; ++s) a += p[s * stride_s];
-    pos_grad[j] = a;
+    (k < V ? ptok[k * 32 + c] : ppos[c]) = a;
   }
 }
 
@@ -792,8 +781,7 @@ extern "C" int ghm_readout_bwd(const float* H, const float* W_ro, const float* b
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96)");
   GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
   hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
-                     H, W_ro, b_ro, w_out, const_cast<float*>(d_emb), dH, part_wro, part_bro, part_wout, part_bout,
-                     T);
+                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T);
   return ghm_launch_status();
 }
 
@@ -807,28 +795,28 @@ extern "C" int ghm_readout_bwd_clip(const float* H, const float* W_ro, const flo
   GHM_CHECK(C == 10, "readout kernels are built for num_class == 10 (the GHM vocabulary)");
   GHM_CHECK(tower == 0 || tower == 1, "tower 0 (text) or 1 (image)");
   GHM_CHECK(B >= 1 && K >= 2 && n_seq == static_cast<int64_t>(K + 1) * B, "n_seq must be (K + 1) B");
-  hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, ghm_stream(stream),
-                     H, W_ro, b_ro, w_out, d_emb, dH, part_wro, part_bro, part_wout, part_bout, T, t_emb, i_emb,
-                     tower, B, K);
+  hipStream_t s = ghm_stream(stream);
+  hipLaunchKernelGGL(k_clip_grad_rows<10>, dim3(static_cast<unsigned>((n_seq + 63) / 64)), dim3(64), 0, s, t_emb,
+                     i_emb, tower, B, K, d_emb);
+  hipLaunchKernelGGL(k_readout_bwd<10>, dim3(static_cast<unsigned>(n_seq)), dim3(256), 0, s, H, W_ro, b_ro, w_out,
+                     d_emb, dH, part_wro, part_bro, part_wout, part_bout, T);
   return ghm_launch_status();
 }
+
+extern "C" int ghm_embed_bwd_splits(void) { return EMB_SPLIT; }
 
 extern "C" int64_t ghm_embed_bwd_part_elems(int T, int V) {
   return static_cast<int64_t>(EMB_SPLIT) * T * (V + 1) * GHM_D;
 }
 
-extern "C" int ghm_embed_bwd(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D,
-                             float* tok_grad, float* pos_grad, float* part, void* stream) {
-  GHM_CHECK(dH0 && tokens && tok_grad && pos_grad && part, "null pointer");
+extern "C" int ghm_embed_bwd_part(const float* dH0, const uint8_t* tokens, int64_t n_seq, int T, int V, int D,
+                                  float* part, void* stream) {
+  GHM_CHECK(dH0 && tokens && part, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && n_seq >= 1 && n_seq < (int64_t(1) << 30), "shape (D == 128)");
   GHM_CHECK(V == 10, "token embedding gradients are built for the 10-value GHM vocabulary");
   GHM_CHECK(((reinterpret_cast<uintptr_t>(dH0) | reinterpret_cast<uintptr_t>(part)) & 15) == 0, "16-byte aligned");
-  hipStream_t s = ghm_stream(stream);
-  hipLaunchKernelGGL(k_embed_grad_part<10>, dim3(static_cast<unsigned>(T), EMB_SPLIT), dim3(256), 0, s, dH0, tokens,
-                     static_cast<int>(n_seq), T, part);
-  const int64_t nout = static_cast<int64_t>(V + T) * GHM_D;
-  hipLaunchKernelGGL(k_embed_grad_final, dim3(static_cast<unsigned>((nout + 255) / 256)), dim3(256), 0, s, part, T,
-                     V, tok_grad, pos_grad);
+  hipLaunchKernelGGL(k_embed_grad_part<10>, dim3(static_cast<unsigned>(T), EMB_SPLIT), dim3(256), 0,
+                     ghm_stream(stream), dH0, tokens, static_cast<int>(n_seq), T, part);
   return ghm_launch_status();
 }
 

@@ -136,13 +136,53 @@ __device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo
   }
 }
 
-template <bool TA, bool TB, int EPI, int TM>
+// exact-f32 variant (F32): [row][k] f32 images with a 36-float pitch, staged
+// without a split; lane (r, h) of a v_mfma_f32_32x32x2f32 takes k = 16 h + kk at
+// step kk (both operands alike), so a lane's 16 operands are four 16-byte reads.
+constexpr int GPF = 36;
+template <int ROWS>
+__device__ __forceinline__ void store_kc_f32(const float4* v, float* img) {
+  constexpr int N = ROWS * 8 / 256;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    *reinterpret_cast<float4*>(img + (idx >> 3) * GPF + 4 * (idx & 7)) = v[i];
+  }
+}
+template <int COLS, bool ZERO>
+__device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_t k0, int64_t kend) {
+  constexpr int C4 = COLS / 4, RPT = COLS / 32;
+  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float x[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      x[i] = c == 0 ? v[i].x : (c == 1 ? v[i].y : (c == 2 ? v[i].z : v[i].w));
+      if constexpr (ZERO) x[i] = (k0 + RPT * kg + i < kend) ? x[i] : 0.f;
+    }
+    float* dst = img + (4 * c4 + c) * GPF + RPT * kg;
+    if constexpr (RPT == 4) *reinterpret_cast<float4*>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+    else *reinterpret_cast<float2*>(dst) = make_float2(x[0], x[1]);
+  }
+}
+
+// F32 = true: the exact-f32 product (the VLM's precision "f32" mode) on the same
+// tiling, prefetch schedule and epilogues; GELU then uses the erf form.
+template <bool TA, bool TB, int EPI, int TM, bool F32>
 __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   constexpr int BM = 64 * TM;
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
   constexpr int NB = TB ? GB_N * 8 / 256 : GB_N / 32;
-  // double-buffered split images: [buf][row][k]
-  __shared__ __attribute__((aligned(16))) __bf16 ah[2][BM * GP], al[2][BM * GP], bh[2][GB_N * GP], bl[2][GB_N * GP];
+  // double-buffered images: [buf][row][k], split (hi, lo) bf16 or (F32) f32
+  constexpr int SM_X3 = 2 * 2 * (BM + GB_N) * GP * 2, SM_F32 = 2 * (BM + GB_N) * GPF * 4;
+  __shared__ __attribute__((aligned(16))) char smem[F32 ? SM_F32 : SM_X3];
+  __bf16(*ah)[BM * GP] = reinterpret_cast<__bf16(*)[BM * GP]>(smem);
+  __bf16(*al)[BM * GP] = ah + 2;
+  __bf16(*bh)[GB_N * GP] = reinterpret_cast<__bf16(*)[GB_N * GP]>(smem + 2 * 2 * BM * GP * 2);
+  __bf16(*bl)[GB_N * GP] = bh + 2;
+  float(*af)[BM * GPF] = reinterpret_cast<float(*)[BM * GPF]>(smem);
+  float(*bf)[GB_N * GPF] = reinterpret_cast<float(*)[GB_N * GPF]>(smem + 2 * BM * GPF * 4);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
@@ -190,6 +230,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   };
   // k0: the K tile being stored (zeroes A's token tail in split-k)
   auto store = [&](const float4* va, const float4* vb, int buf, int64_t k0) {
+    if constexpr (F32) {
+      if constexpr (TA) store_oc_f32<BM, true>(va, af[buf], k0, ke);
+      else store_kc_f32<BM>(va, af[buf]);
+      if constexpr (TB) store_kc_f32<GB_N>(vb, bf[buf]);
+      else store_oc_f32<GB_N, false>(vb, bf[buf], k0, ke);
+      return;
+    }
     if constexpr (TA) store_oc<BM, true>(va, ah[buf], al[buf], k0, ke);
     else store_kc<BM>(va, ah[buf], al[buf]);
     if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
@@ -203,6 +250,30 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = zero16();
 
   auto compute = [&](int buf) {
+    if constexpr (F32) {
+      float xa[TM][16], yb[2][16];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(af[buf] + (32 * (TM * wm + i) + r) * GPF + 16 * h + 4 * q);
+          xa[i][4 * q] = v.x; xa[i][4 * q + 1] = v.y; xa[i][4 * q + 2] = v.z; xa[i][4 * q + 3] = v.w;
+        }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(bf[buf] + (32 * (2 * wn + j) + r) * GPF + 16 * h + 4 * q);
+          yb[j][4 * q] = v.x; yb[j][4 * q + 1] = v.y; yb[j][4 * q + 2] = v.z; yb[j][4 * q + 3] = v.w;
+        }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(yb[j][kk], xa[i][kk], acc[i][j]);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 xh[TM], xl[TM], yh[2], yl[2];
@@ -300,7 +371,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
           const float bb[4] = {bv[qd].x, bv[qd].y, bv[qd].z, bv[qd].w};
           float gg[4], dd[4];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) gelu_fast(x[t] + bb[t], gg[t], dd[t]);
+          for (int t = 0; t < 4; ++t) {
+            if constexpr (F32) gelu_and_grad(x[t] + bb[t], gg[t], dd[t]);
+            else gelu_fast(x[t] + bb[t], gg[t], dd[t]);
+          }
           st4(g.C + m * g.ldc + n, gg[0], gg[1], gg[2], gg[3]);
           st4(g.C2 + m * g.ldc + n, dd[0], dd[1], dd[2], dd[3]);
         } else if constexpr (EPI == EPI_RESID) {
@@ -630,16 +704,16 @@ void colsum_plan(int64_t M, int64_t N, int64_t& colblocks, int64_t& nchunk, int6
   nchunk = (M + R - 1) / R;
 }
 
-template <bool TA, bool TB, int EPI>
+template <bool TA, bool TB, int EPI, bool F32>
 void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   // measured (VLM shapes, M = 10,368): 128 x 128 tiles with one K tile in flight
   // are faster for N >= 768; 64 x 128 tiles with two K tiles in flight for N = 256
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
   if (g.N >= 768)
-    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2>), dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit),
+    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit),
                        dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1>), dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit),
+    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit),
                        dim3(256), 0, s, g);
 }
 
@@ -647,10 +721,10 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
 
 extern "C" int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit) { return M * N * nsplit; }
 
-extern "C" int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
-                           const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2,
-                           const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit,
-                           void* stream) {
+static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_t lda, const float* B0,
+                       const float* B1, const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc,
+                       float* C2, const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K,
+                       int nsplit, void* stream) {
   GHM_CHECK(A && B0 && C, "null pointer");
   GHM_CHECK(M >= 1 && N >= GB_N && N % GB_N == 0 && K >= 1 && nsplit >= 1 && nsplit <= 256, "shape (N % 128 == 0)");
   GHM_CHECK(!(ta && tb), "TA and TB together are not a VLM shape");
@@ -680,17 +754,38 @@ extern "C" int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda,
   g.M = M; g.N = N; g.K = K;
   g.k_per_split = ((K + nsplit - 1) / nsplit + GB_K - 1) / GB_K * GB_K;
   hipStream_t s = ghm_stream(stream);
-#define GHM_GEMM_CASE(TA_, TB_, E_) \
-  if (ta == TA_ && tb == TB_ && epi == E_) { launch_tm<TA_, TB_, E_>(g, nsplit, s); return ghm_launch_status(); }
+#define GHM_GEMM_CASE(TA_, TB_, E_)                                    \
+  if (ta == TA_ && tb == TB_ && epi == E_) {                           \
+    if (f32) launch_tm<TA_, TB_, E_, true>(g, nsplit, s);              \
+    else launch_tm<TA_, TB_, E_, false>(g, nsplit, s);                 \
+    return ghm_launch_status();                                        \
+  }
   GHM_GEMM_CASE(0, 1, EPI_STORE)
   GHM_GEMM_CASE(0, 1, EPI_GELU)
   GHM_GEMM_CASE(0, 1, EPI_RESID)
   GHM_GEMM_CASE(0, 0, EPI_STORE)
   GHM_GEMM_CASE(0, 0, EPI_MUL)
+  GHM_GEMM_CASE(0, 0, EPI_RESID)  // the f32 VLM's dX += dk Wk, dv Wv
   GHM_GEMM_CASE(1, 0, EPI_SLAB)
   GHM_GEMM_CASE(1, 0, EPI_STORE)
 #undef GHM_GEMM_CASE
   GHM_CHECK(false, "unsupported (ta, tb, epilogue) combination");
+}
+
+extern "C" int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
+                           const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2,
+                           const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit,
+                           void* stream) {
+  return gemm_launch(false, ta, tb, epi, A, lda, B0, B1, B2, ldb, b_chunk, C, ldc, C2, bias, R, ldr, M, N, K, nsplit,
+                     stream);
+}
+
+extern "C" int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
+                            const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2,
+                            const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K,
+                            int nsplit, void* stream) {
+  return gemm_launch(true, ta, tb, epi, A, lda, B0, B1, B2, ldb, b_chunk, C, ldc, C2, bias, R, ldr, M, N, K, nsplit,
+                     stream);
 }
 
 extern "C" int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,

@@ -37,6 +37,44 @@ extern "C" int ghm_device_ok(void) {
   return strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
+// Cross-stream ordering for the two-tower step (clip_trainer.py _phase /
+// _cross_wait): events recorded with a device-scope release and no system-scope
+// fence (hipEventReleaseToDevice | hipEventDisableSystemFence | DisableTiming) --
+// the waits order work on one device, no host or peer reads the data.
+extern "C" void* ghm_event_create(int device_scope) {
+  hipEvent_t e = nullptr;
+  const unsigned flags = hipEventDisableTiming |
+                         (device_scope ? (hipEventDisableSystemFence | hipEventReleaseToDevice) : 0u);
+  if (hipEventCreateWithFlags(&e, flags) != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "hipEventCreateWithFlags failed");
+    return nullptr;
+  }
+  return e;
+}
+
+extern "C" int ghm_event_destroy(void* ev) {
+  GHM_CHECK(ev, "null event");
+  return hipEventDestroy(static_cast<hipEvent_t>(ev)) == hipSuccess ? GHM_OK : -1;
+}
+
+extern "C" int ghm_event_record(void* ev, void* stream) {
+  GHM_CHECK(ev, "null event");
+  if (hipEventRecord(static_cast<hipEvent_t>(ev), ghm_stream(stream)) != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "hipEventRecord failed");
+    return -1;
+  }
+  return GHM_OK;
+}
+
+extern "C" int ghm_stream_wait(void* stream, void* ev) {
+  GHM_CHECK(ev, "null event");
+  if (hipStreamWaitEvent(ghm_stream(stream), static_cast<hipEvent_t>(ev), 0) != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "hipStreamWaitEvent failed");
+    return -1;
+  }
+  return GHM_OK;
+}
+
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_sumsq(const float* __restrict__ g, int64_t n,
                                                float* __restrict__ part) {

@@ -27,6 +27,9 @@
 #endif
 
 // waves per workgroup of the split-K weight gradient (k_wgrad_x3)
+#ifndef GHM_WGRAD_FAST
+#define GHM_WGRAD_FAST 0  // 1: the stride-specialised weight gradients (k_wgrad_x3 LDA / LDB)
+#endif
 #ifndef GHM_WGRAD_WAVES
 #define GHM_WGRAD_WAVES 4
 #endif
@@ -792,7 +795,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
 // scope as a global load (ld_stats, sc1), 4 the plain load AND the recompute:
 // the product uses the recomputed pair and every lane with h == 0 writes
 // (loaded mean, loaded rstd, recomputed mean, recomputed rstd) to dbg[m];
-// 5 as 1 (the plain load, used) and dbg[m] = (used mean, used rstd, 0, 0).
+// 5 as 1 (the plain load, used) and dbg[m] = (used mean, used rstd, 0, 0);
+// 6 as 1 with no per-token store: thread 0 writes the workgroup's placement
+// (XCC_ID, HW_ID register bits, blockIdx) to dbg[blockIdx.x] after the product,
+// so the host can place every wrong row group on an XCD and infer the pair the
+// row used from the output itself (tools/race_probe.py qkv_xcc).  Mode 4 writes
+// the same placement record to dbg[M + blockIdx.x].
 template <int STATS>
 __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
     const float* __restrict__ dqkv, const float* __restrict__ H, const float* __restrict__ lnw,
@@ -821,7 +829,7 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
     float x[64];
     load64(H + mc * GHM_D + 64 * h, x);
     ln_stats64(x, eps, lnst.x, lnst.y);
-  } else if (STATS == 1 || STATS == 5) {
+  } else if (STATS == 1 || STATS == 5 || STATS == 6) {
     lnst = stats[mc];
   } else if (STATS == 2) {
     lnst = ld_stats_sys(stats, mc);
@@ -855,6 +863,13 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
                red + wave * GHM_D, red + 4 * GHM_D + wave * GHM_D);
   __syncthreads();
   ln_partial_store(red, part_ln + static_cast<int64_t>(blockIdx.x) * 2 * GHM_D);
+  if ((STATS == 4 || STATS == 6) && threadIdx.x == 0) {
+    // s_getreg immediates: id | offset << 6 | (size - 1) << 11; HW_REG_XCC_ID = 20
+    // (bits 3:0 the XCD), HW_REG_HW_ID = 4 (wave, SIMD, CU, SE fields)
+    const int xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11));
+    const int hwid = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    dbg[(STATS == 4 ? M : 0) + blockIdx.x] = make_float4(__int_as_float(xcc), __int_as_float(hwid), __int_as_float(static_cast<int>(blockIdx.x)), 0.f);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -877,7 +892,11 @@ __global__ __launch_bounds__(256, 2) void k_qkv_bwd_x3(
 __device__ __forceinline__ int wg_swz(int row) { return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1); }
 __device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (ch ^ wg_swz(row)); }
 
-template <int MODE, int NWV = 4>
+// LDA / LDB: the operands' row strides when known at compile time (the encoder's
+// three products), 0 = the run-time lda / ldb.  A step whose 32 tokens are all
+// valid (every step but a split's last) then loads with constant row offsets
+// (folded into the loads' immediate offsets) and skips the token clamps and mask.
+template <int MODE, int NWV = 4, int LDA = 0, int LDB = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __restrict__ A, int lda,
                                                      const float* __restrict__ Bs, int ldb,
                                                      const float2* __restrict__ stats,
@@ -955,6 +974,18 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
     const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + TPT * th;  // uniform
     const int64_t left = m_end - mb;
     S.nvalid = left < 0 ? 0 : (left > TPT ? TPT : static_cast<int>(left));
+    if (LDA > 0 && LDB > 0 && __builtin_amdgcn_readfirstlane(S.nvalid) == TPT) {
+      if (MODE == 2) S.st = ld_stats_sys(stats, mb + (lane & (TPT - 1)));
+      const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(mb * LDA * 4));
+      const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(mb * LDB * 4));
+#pragma unroll
+      for (int i = 0; i < TPT; ++i) {
+        S.va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, voa + i * LDA * 4, sa, 0));
+        S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob + i * LDB * 4, sb, 0));
+      }
+      issue_fence();
+      return;
+    }
     // rows past m_end re-read the last valid row (masked in store())
     const int64_t r0 = S.nvalid ? mb : m_begin;
     const int nv = __builtin_amdgcn_readfirstlane(S.nvalid > 0 ? S.nvalid : 1);
@@ -982,9 +1013,11 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
         S.vb[i] = (S.vb[i] - mean) * rstd * gam + bet;
       }
     }
+    if (LDA == 0 || LDB == 0 || __builtin_amdgcn_readfirstlane(S.nvalid) < TPT) {
 #pragma unroll
-    for (int i = 0; i < TPT; ++i)
-      if (i >= S.nvalid) S.va[i] = 0.f;
+      for (int i = 0; i < TPT; ++i)
+        if (i >= S.nvalid) S.va[i] = 0.f;
+    }
 #pragma unroll
     for (int half = 0; half < TPT / 8; ++half) {
       bf16x8 ah, al, bh, bl;
@@ -1792,8 +1825,8 @@ extern "C" int ghm_qkv_bwd_x3_probe(const float* dqkv, const float* H, const flo
                                     const void* pack, const float* dH_mid, float* dH, float* part_ln, float* dbg,
                                     int64_t M, int D, float eps, int mode, void* stream) {
   GHM_CHECK(dqkv && H && stats && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
-  GHM_CHECK(D == GHM_D && M >= 1 && mode >= 1 && mode <= 5, "shape / mode (1..5)");
-  GHM_CHECK(mode < 4 || dbg, "modes 4 and 5 need dbg [M][4]");
+  GHM_CHECK(D == GHM_D && M >= 1 && mode >= 1 && mode <= 6, "shape / mode (1..6)");
+  GHM_CHECK(mode < 4 || dbg, "modes 4 to 6 need dbg [M + blocks][4]");
   GHM_CHECK(M * 8 < (int64_t(1) << 31), "stats must fit a 31-bit byte range");
   const dim3 g(static_cast<unsigned>(ghm_token_blocks(M)));
   const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
@@ -1808,8 +1841,10 @@ extern "C" int ghm_qkv_bwd_x3_probe(const float* dqkv, const float* H, const flo
     hipLaunchKernelGGL(k_qkv_bwd_x3<3>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
   else if (mode == 4)
     hipLaunchKernelGGL(k_qkv_bwd_x3<4>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
-  else
+  else if (mode == 5)
     hipLaunchKernelGGL(k_qkv_bwd_x3<5>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
+  else
+    hipLaunchKernelGGL(k_qkv_bwd_x3<6>, g, dim3(256), 0, s, dqkv, H, ln_w, pk, dH_mid, dH, part_ln, M, eps, st, d4);
   return ghm_launch_status();
 }
 
@@ -1836,6 +1871,15 @@ extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B,
     else
       hipLaunchKernelGGL((k_wgrad_x3<2, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part,
                          M, tok_per_split, A_cols, B_cols);
+  } else if (GHM_WGRAD_FAST && b_mode == 0 && lda == GHM_D && ldb == GHM_F) {  // dW2
+    hipLaunchKernelGGL((k_wgrad_x3<0, 4, GHM_D, GHM_F>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
+                       bias_part, M, tok_per_split, A_cols, B_cols);
+  } else if (GHM_WGRAD_FAST && b_mode == 2 && lda == GHM_F && ldb == GHM_D) {  // dW1
+    hipLaunchKernelGGL((k_wgrad_x3<2, 4, GHM_F, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
+                       bias_part, M, tok_per_split, A_cols, B_cols);
+  } else if (GHM_WGRAD_FAST && b_mode == 2 && lda == 3 * GHM_D && ldb == GHM_D) {  // dWq|k|v
+    hipLaunchKernelGGL((k_wgrad_x3<2, 4, 3 * GHM_D, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b,
+                       part, bias_part, M, tok_per_split, A_cols, B_cols);
   } else if (b_mode == 0) {
     hipLaunchKernelGGL(k_wgrad_x3<0>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
                        tok_per_split, A_cols, B_cols);

@@ -49,8 +49,9 @@ HIP_SIGNATURES = {
     "ghm_clip_loss": [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p],
     "ghm_readout_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_readout_bwd_clip": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_embed_bwd_splits": [],
     "ghm_embed_bwd_part_elems": [_i, _i],
-    "ghm_embed_bwd": [_p, _p, _i64, _i, _i, _i, _p, _p, _p, _p],
+    "ghm_embed_bwd_part": [_p, _p, _i64, _i, _i, _i, _p, _p],
     "ghm_mlp_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_attn_bwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_qkv_bwd": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _p],
@@ -88,6 +89,12 @@ HIP_SIGNATURES = {
     "ghm_attn_ext_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _f, _p],
     "ghm_gemm_x3": [_i, _i, _i, _p, _i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64,
                     _i, _p],
+    "ghm_event_create": [_i],
+    "ghm_event_destroy": [_p],
+    "ghm_event_record": [_p, _p],
+    "ghm_stream_wait": [_p, _p],
+    "ghm_gemm_f32": [_i, _i, _i, _p, _i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64,
+                     _i, _p],
     "ghm_gemm_reduce": [_p, _i, _i64, _i64, _p, _p, _p, _i64, _p],
     "ghm_colsum_part_elems": [_i64, _i64],
     "ghm_colsum": [_p, _i64, _i64, _p, _p, _p],
@@ -120,7 +127,7 @@ HIP_SIGNATURES = {
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
     "ghm_zsc_logits": [_p, _i64, _p, _i, _p, _i, _i, _p, _i, _p, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_embed_bwd_part_elems": _i64, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_event_create": ctypes.c_void_p, "ghm_embed_bwd_part_elems": _i64, "ghm_embed_bwd_splits": _i, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
             "ghm_mlp_bwd_rc_x3_blocks": _i64,
             "ghm_ln_rows_blocks": _i64, "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
             "ghm_wcolsum_part_elems": _i64,

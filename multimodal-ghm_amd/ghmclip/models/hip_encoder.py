@@ -393,13 +393,17 @@ class EncoderPlan:
             cur, nxt = self._layer_bwd(p, g, l, cur, nxt, jobs, _stream(), layer_grad)
             yield
         s = _stream()
-        self._flush(jobs, s)
         # embeddings (model.py:765 via autograd): dH0 rows summed by token id,
         # and over the sequences for the positions
-        if self.V == 10:  # one pass over dH0 for both
-            c("ghm_embed_bwd", _ptr(cur), _ptr(tok), N, T, self.V, D_MODEL, _ptr(g["token_embeddings.weight"]),
-              _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)
+        if self.V == 10:  # one pass over dH0 for both; their partials join the final reduction
+            c("ghm_embed_bwd_part", _ptr(cur), _ptr(tok), N, T, self.V, D_MODEL, _ptr(self.part_emb), s)
+            S = int(_native.hip_lib().ghm_embed_bwd_splits())
+            ntok = S * T * self.V * D_MODEL
+            jobs += [J(self.part_emb, S * T, [g["token_embeddings.weight"]]),
+                     J(self.part_emb[ntok:], S, [g["position_embeddings.weight"]])]
+            self._flush(jobs, s)
         else:
+            self._flush(jobs, s)
             c("ghm_wcolsum", None, _ptr(tok), self.V, _ptr(cur), self.M, self.M, 0, self.M, D_MODEL,
               _ptr(g["token_embeddings.weight"]), None, _ptr(self.part_emb), s)
             c("ghm_colsum", _ptr(cur), N, T * D_MODEL, _ptr(g["position_embeddings.weight"]), _ptr(self.part_emb), s)

@@ -12,17 +12,20 @@ matrix-product modes:
        GELU / GELU', bias + residual and the GELU' product fused into its epilogues,
        Q/K/V fused into one [M][3D] product), attention on the split-bf16 MFMA
        kernels of csrc/ghm_vlm_x3.hip;
-  "f32": exact fp32 library GEMMs (torch.mm / addmm on rocBLAS / hipBLASLt) and the
-       fp32 attention kernels of csrc/ghm_vlm.hip.
-Both use the hand-written embedding, row LayerNorm forward/backward and cross-entropy
-+ KL kernels (csrc/ghm_vlm.hip); the 10-wide readout and the bias / embedding
-gradient sums stay torch ops.  All buffers are allocated once; a step is a fixed
-launch sequence (graph-capturable).
+  "f32": the same GEMM template with exact f32 products (ghm_gemm_f32:
+       v_mfma_f32_32x32x2f32 on f32 LDS images, erf GELU in the epilogue; Q, K
+       and V as three products into separate buffers) and the fp32 attention
+       kernels of csrc/ghm_vlm.hip.
+Both use the hand-written embedding, row LayerNorm forward/backward, readout
+(ghm_rows_linear), bias / embedding gradient sums (ghm_colsum / ghm_wcolsum) and
+cross-entropy + KL kernels; no library GEMM runs in either mode.  All buffers are
+allocated once; a step is a fixed launch sequence (graph-capturable).
 
 HBM layout (M = n_seq * T tokens, D = n_embd, F = 4 D, fp32 row-major):
   H [L+1][M][D], Hmid / X1 (LN1 out) / X2 (LN2 out) / q / k / v [L][M][D],
   G, Dg (GELU(U), GELU'(U)) [L][M][F], P [L][n_seq][96][96], st1 / st2 [L][M][2];
-  backward scratch dH [2][M][D], dX, dq, dk, dv [M][D], dG [M][F].
+  backward scratch dH [2][M][D], dX, dq, dk, dv [M][D], dG [M][F].  (x3 keeps
+  q | k | v as one [L][M][3D] buffer and dq | dk | dv as [M][3D].)
 """
 import ctypes
 import math
@@ -71,11 +74,11 @@ def _stream():
 
 
 def _gemm(ta, tb, epi, A, lda, Bs, ldb, b_chunk, C, ldc, M, N, K, C2=None, bias=None, R=None, ldr=0, nsplit=1,
-          s=None):
-    """ghm_gemm_x3 (include/ghm_hip.h): C = A(m,k) B(k,n) with the epilogue epi."""
+          s=None, f32=False):
+    """ghm_gemm_x3 / ghm_gemm_f32 (include/ghm_hip.h): C = A(m,k) B(k,n) with the epilogue epi."""
     Bs = list(Bs) + [None] * (3 - len(Bs))
     pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
-    _native.call("ghm_gemm_x3", ta, tb, epi, _ptr(A), lda, pp(Bs[0]), pp(Bs[1]), pp(Bs[2]), ldb, b_chunk, _ptr(C),
+    _native.call("ghm_gemm_f32" if f32 else "ghm_gemm_x3", ta, tb, epi, _ptr(A), lda, pp(Bs[0]), pp(Bs[1]), pp(Bs[2]), ldb, b_chunk, _ptr(C),
                  ldc, pp(C2), pp(bias), pp(R), ldr, M, N, K, nsplit, _stream() if s is None else s)
 
 
@@ -114,63 +117,39 @@ class VlmPlan:
         self.Pm = torch.zeros(L, N, pad, pad, dtype=torch.float32, device=self.device)
         self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
         self.logits, self.dlogits = e(M, num_class), e(M, num_class)
-        if self.precision != "x3":  # the x3 path sums dH0 rows by token id (ghm_wcolsum)
-            self.onehot = e(M, num_class)
         self.dH = e(2, M, D)
         self.dX = e(M, D)
         self.dG = e(M, F)
-        if self.precision == "x3":
-            # fused projections: q | k | v columns of one [M][3D] buffer; split-k wgrad slabs
+        self.f32 = self.precision != "x3"
+        if self.f32:  # separate q / k / v (the fp32 attention kernels' layout)
+            self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
+            self.dq, self.dk, self.dv = e(M, D), e(M, D), e(M, D)
+            self.zero_b = torch.zeros(D, dtype=torch.float32, device=self.device)
+        else:
+            # fused projections: q | k | v columns of one [M][3D] buffer
             self.qkv = e(L, M, 3 * D)
             self.dqkv = e(M, 3 * D)
             self.dS = torch.zeros(N, pad, pad, dtype=torch.float32, device=self.device)
-            self.nsplit = max(1, min(32, M // 256))
-            self.slab = e(self.nsplit * max(D * F, 3 * D * D))
-            lib = _native.hip_lib()
-            self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
-                                 lib.ghm_colsum_part_elems(N, n_token * D),
-                                 lib.ghm_wcolsum_part_elems(M, D, num_class)))
-        else:
-            self.q, self.k, self.v = e(L, M, D), e(L, M, D), e(L, M, D)
-            self.U, self.Y = e(M, F), e(M, D)
-            self.dq, self.dk, self.dv = e(M, D), e(M, D), e(M, D)
+        # split-k weight-gradient slabs, column-sum partials
+        self.nsplit = max(1, min(32, M // 256))
+        self.slab = e(self.nsplit * max(D * F, 3 * D * D))
+        lib = _native.hip_lib()
+        self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
+                             lib.ghm_colsum_part_elems(N, n_token * D),
+                             lib.ghm_wcolsum_part_elems(M, D, num_class)))
         self.nblk = int(_native.hip_lib().ghm_ln_rows_blocks(M))
         self.part_ln = e(self.nblk, 2, D)
         self.xt = torch.empty(N, n_token - n_prefix, dtype=torch.uint8, device=self.device)
         if joint:
             self.itok = torch.empty(N, n_prefix, dtype=torch.uint8, device=self.device)
-            if self.precision != "x3":
-                self.onehot_i = e(M, num_class)
         self._gen = 0
 
     # ------------------------------------------------------------------
     def forward(self, p, xt, feat):
         """p: name -> fp32 device tensor; xt uint8 [N, T - P] text tokens; feat
-        f32 [N, P, V] prefix features.  Returns self.logits [M, V] (all rows)."""
-        if self.precision == "x3":
-            return self._forward_x3(p, xt, feat)
-        s = _stream()
-        c = _native.call
-        M, D, T, N = self.M, self.D, self.T, self.N
-        c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
-          _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), _ptr(self.onehot), N, T, self.P, self.V, D, s)
-        for l in range(self.L):
-            c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-              _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
-            torch.mm(self.X1[l], p[f"_queries.{l}.weight"].t(), out=self.q[l])
-            torch.mm(self.X1[l], p[f"_keys.{l}.weight"].t(), out=self.k[l])
-            torch.mm(self.X1[l], p[f"_values.{l}.weight"].t(), out=self.v[l])
-            c("ghm_vlm_attn_fwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.H[l]),
-              _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, s)
-            c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
-              _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
-            torch.addmm(p[f"_mlps.{l}.0.bias"], self.X2[l], p[f"_mlps.{l}.0.weight"].t(), out=self.U)
-            c("ghm_gelu_fwd", _ptr(self.U), _ptr(self.G[l]), _ptr(self.Dg[l]), M * self.F, s)
-            torch.addmm(p[f"_mlps.{l}.2.bias"], self.G[l], p[f"_mlps.{l}.2.weight"].t(), out=self.Y)
-            c("ghm_add", _ptr(self.Hmid[l]), _ptr(self.Y), _ptr(self.H[l + 1]), M * D, s)  # :344-347
-        torch.addmm(p["_read_out.bias"], self.H[self.L], p["_read_out.weight"].t(), out=self.logits)
-        self._gen += 1
-        return self.logits
+        f32 [N, P, V] prefix features (unused by the joint model: self.itok holds
+        the image leaves).  Returns self.logits [M, V] (all rows)."""
+        return self._forward_hip(p, xt, feat)
 
     def backward(self, p, g, dlogits=None, layer_grad=None):
         """Writes d(loss)/d(param) into g[name] for every trained parameter (not
@@ -178,52 +157,17 @@ class VlmPlan:
         dL/dH_0 [M, D] (its prefix rows give the gradient of the features).
         layer_grad: optional {layer l: fn(dH, stream)} adding a loss term's gradient
         w.r.t. H[l+1] (the guided layers, model.py:303-331) before layer l's
-        backward (split-bf16 path)."""
-        if self.precision == "x3":
-            return self._backward_x3(p, g, dlogits, layer_grad)
-        if layer_grad:
-            raise NotImplementedError("guided VLM layers run on the split-bf16 (x3) path")
-        s = _stream()
-        c = _native.call
-        M, D = self.M, self.D
-        dz = self.dlogits if dlogits is None else dlogits
-        cur, nxt = self.dH[0], self.dH[1]
-        torch.mm(dz, p["_read_out.weight"], out=cur)
-        torch.mm(dz.t(), self.H[self.L], out=g["_read_out.weight"])
-        torch.sum(dz, 0, out=g["_read_out.bias"])
-        for l in reversed(range(self.L)):
-            # MLP: H_{l+1} = Hmid + W2 GELU(W1 LN2(Hmid) + b1) + b2
-            torch.mm(cur.t(), self.G[l], out=g[f"_mlps.{l}.2.weight"])
-            torch.sum(cur, 0, out=g[f"_mlps.{l}.2.bias"])
-            torch.mm(cur, p[f"_mlps.{l}.2.weight"], out=self.dG)
-            c("ghm_mul", _ptr(self.dG), _ptr(self.Dg[l]), _ptr(self.dG), M * self.F, s)  # dU
-            torch.mm(self.dG.t(), self.X2[l], out=g[f"_mlps.{l}.0.weight"])
-            torch.sum(self.dG, 0, out=g[f"_mlps.{l}.0.bias"])
-            torch.mm(self.dG, p[f"_mlps.{l}.0.weight"], out=self.dX)
-            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-              _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
-            self._reduce_ln(g, 2, l, s)
-            # attention (nxt = dHmid)
-            c("ghm_vlm_attn_bwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.Pm[l]), _ptr(nxt),
-              _ptr(self.dq), _ptr(self.dk), _ptr(self.dv), self.N, self.T, D, self.scale_div, s)
-            torch.mm(self.dq.t(), self.X1[l], out=g[f"_queries.{l}.weight"])
-            torch.mm(self.dk.t(), self.X1[l], out=g[f"_keys.{l}.weight"])
-            torch.mm(self.dv.t(), self.X1[l], out=g[f"_values.{l}.weight"])
-            torch.mm(self.dq, p[f"_queries.{l}.weight"], out=self.dX)
-            self.dX.addmm_(self.dk, p[f"_keys.{l}.weight"])
-            self.dX.addmm_(self.dv, p[f"_values.{l}.weight"])
-            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-              _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
-            self._reduce_ln(g, 1, l, s)
-        # embedding: positions summed over sequences, token rows through the one-hot
-        torch.sum(cur.view(self.N, self.T, D), 0, out=g["position_embeddings.weight"])
-        torch.mm(self.onehot.t(), cur, out=g["t_embedding.weight"])
-        return cur
+        backward."""
+        return self._backward_hip(p, g, dlogits, layer_grad)
 
     # ------------------------------------------------------------------
-    # split-bf16 path: every projection on ghm_gemm_x3 (GELU, bias, residual and
-    # GELU' products fused into the GEMM epilogues), attention on ghm_vlm_attn_*_x3
-    def _forward_x3(self, p, xt, feat):
+    # every projection on the hand-written GEMM (ghm_gemm_x3, or ghm_gemm_f32 in the
+    # f32 mode; GELU, bias, residual and GELU' products fused into its epilogues),
+    # attention on ghm_attn_ext_*_x3 (x3) or ghm_vlm_attn_* (f32)
+    def _gemm(self, *a, **k):
+        _gemm(*a, f32=self.f32, **k)
+
+    def _forward_hip(self, p, xt, feat):
         s = _stream()
         c = _native.call
         M, D, F, T, N = self.M, self.D, self.F, self.T, self.N
@@ -238,14 +182,20 @@ class VlmPlan:
             c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
-            _gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
-            c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T,
-              D, self.P, self.scale_div, 1.0 / D, s)
+            if self.f32:
+                for w, out in zip(wqkv, (self.q[l], self.k[l], self.v[l])):
+                    self._gemm(0, 1, EPI_STORE, self.X1[l], D, (w,), D, 0, out, D, M, D, D, s=s)
+                c("ghm_vlm_attn_fwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.H[l]),
+                  _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, s)
+            else:
+                self._gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
+                c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]),
+                  N, T, D, self.P, self.scale_div, 1.0 / D, s)
             c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
-            _gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
+            self._gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
                   C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
-            _gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
+            self._gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
                   bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
         c("ghm_rows_linear", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(self.logits), M, D, self.V, s)  # model.py:332
@@ -255,12 +205,12 @@ class VlmPlan:
 
     def _wgrad(self, A, lda, m, B, ldb, n, dst, chunk, s):
         """dst (rows stacked by chunk) = A^T B over the M tokens: split-k slabs + fixed-order reduce."""
-        _gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.M, nsplit=self.nsplit, s=s)
+        self._gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.M, nsplit=self.nsplit, s=s)
         d = list(dst) + [None] * (3 - len(dst))
         pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
         _native.call("ghm_gemm_reduce", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk, s)
 
-    def _backward_x3(self, p, g, dlogits=None, layer_grad=None):
+    def _backward_hip(self, p, g, dlogits=None, layer_grad=None):
         s = _stream()
         c = _native.call
         M, D, F = self.M, self.D, self.F
@@ -275,20 +225,32 @@ class VlmPlan:
             w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
             self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s)
             self._colsum(cur, M, D, g[f"_mlps.{l}.2.bias"], s)
-            _gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
+            self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
             self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s)
             self._colsum(self.dG, M, F, g[f"_mlps.{l}.0.bias"], s)
-            _gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
+            self._gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
               _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 2, l, s)
             # attention (nxt = dHmid) -> dq | dk | dv
-            c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS), _ptr(self.dqkv),
-              self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
-            self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D,
-                        (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"]), D, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
-            _gemm(0, 0, EPI_STORE, self.dqkv, 3 * D, wqkv, D, D, self.dX, D, M, D, 3 * D, s=s)
+            gqkv = (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"])
+            if self.f32:
+                c("ghm_vlm_attn_bwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.Pm[l]), _ptr(nxt),
+                  _ptr(self.dq), _ptr(self.dk), _ptr(self.dv), self.N, self.T, D, self.scale_div, s)
+                dqkv = (self.dq, self.dk, self.dv)
+                for d, gw in zip(dqkv, gqkv):
+                    self._wgrad(d, D, D, self.X1[l], D, D, (gw,), 0, s)
+                # dX = dq Wq, then (dk Wk + 0) + dX and (dv Wv + 0) + dX in place
+                self._gemm(0, 0, EPI_STORE, self.dq, D, (wqkv[0],), D, 0, self.dX, D, M, D, D, s=s)
+                for d, w in zip(dqkv[1:], wqkv[1:]):
+                    self._gemm(0, 0, EPI_RESID, d, D, (w,), D, 0, self.dX, D, M, D, D, bias=self.zero_b, R=self.dX,
+                               ldr=D, s=s)
+            else:
+                c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS),
+                  _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
+                self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D, gqkv, D, s)
+                self._gemm(0, 0, EPI_STORE, self.dqkv, 3 * D, wqkv, D, D, self.dX, D, M, D, 3 * D, s=s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
               _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 1, l, s)

@@ -161,6 +161,14 @@ class ClipTrainer:
         self.steps_done = 0
         self.side = torch.cuda.Stream(device=self.device)
         self.comm = torch.cuda.Stream(device=self.device)  # data-parallel bucket all-reduces
+        # one process: reduce the top dp_top layers' partials on the (otherwise idle)
+        # comm stream while the towers run their lower layers, instead of all of
+        # them in the serial tail after the last layer (GHM_EARLY_REDUCE=0: tail only)
+        self.early_reduce = os.environ.get("GHM_EARLY_REDUCE", "0") == "1"
+        # cross-stream waits on native device-scope events (no system-scope fence)
+        # instead of torch's Stream.wait_stream (GHM_FAST_EVENTS=1)
+        self.fast_events = os.environ.get("GHM_FAST_EVENTS", "0") == "1"
+        self._evs = {}
         # data-parallel timing (bench.py): None, or a list that each step appends
         # (bucket A ms, bucket B ms, exposed ms) event triples to
         self.comm_timing = None
@@ -311,7 +319,7 @@ class ClipTrainer:
         st = {1: s1, 0: s0}
         for x in (s0, s1):
             if x != main and fork:
-                x.wait_stream(main)
+                self._order(main, x, "fork")
         if graphs is None:
             live = {1: genf(1), 0: genf(0)}
             while live:
@@ -331,7 +339,27 @@ class ClipTrainer:
                             pieces[t][i].replay()
         for x in (s0, s1):
             if x != main and join:
-                main.wait_stream(x)
+                self._order(x, main, "join")
+
+    def _event(self, key):
+        ev = self._evs.get(key)
+        if ev is None:
+            ev = _native.hip_lib().ghm_event_create(1)
+            if not ev:
+                _native.check(-1, "ghm_event_create")
+            self._evs[key] = ev = ctypes.c_void_p(ev)
+        return ev
+
+    def _order(self, producer, consumer, key):
+        """consumer waits for the work enqueued on producer so far."""
+        if producer == consumer:
+            return
+        if not self.fast_events:
+            consumer.wait_stream(producer)
+            return
+        ev = self._event(key)
+        _native.call("ghm_event_record", ev, ctypes.c_void_p(producer.cuda_stream))
+        _native.call("ghm_stream_wait", ctypes.c_void_p(consumer.cuda_stream), ev)
 
     def _cross_wait(self):
         """Each tower's stream waits for the other's work so far (one hop each way,
@@ -339,18 +367,31 @@ class ClipTrainer:
         readout backward needs both towers' embeddings; a join into the current
         stream and a fork back out would put two hops in series on the side stream."""
         _, s0, s1 = self._tower_streams()
-        if s0 != s1:
-            e0, e1 = torch.cuda.Event(), torch.cuda.Event()
-            e0.record(s0)
-            e1.record(s1)
-            s0.wait_event(e1)
-            s1.wait_event(e0)
+        if s0 == s1:
+            return
+        if self.fast_events:
+            e0, e1 = self._event("cross0"), self._event("cross1")
+            _native.call("ghm_event_record", e0, ctypes.c_void_p(s0.cuda_stream))
+            _native.call("ghm_event_record", e1, ctypes.c_void_p(s1.cuda_stream))
+            _native.call("ghm_stream_wait", ctypes.c_void_p(s0.cuda_stream), e1)
+            _native.call("ghm_stream_wait", ctypes.c_void_p(s1.cuda_stream), e0)
+            return
+        e0, e1 = torch.cuda.Event(), torch.cuda.Event()
+        e0.record(s0)
+        e1.record(s1)
+        s0.wait_event(e1)
+        s1.wait_event(e0)
 
     def _single(self, fn, graphs=None, key=None):
         if graphs is None:
             fn()
         else:
             graphs[key].replay()
+
+    def _early(self):
+        """Early reduce of the upper layers' partials (one process, two streams)."""
+        _, s0, s1 = self._tower_streams()
+        return self.early_reduce and s0 != s1 and self.dp_top > 0
 
     def _bwd_gen(self, tower):
         """The whole backward of one tower as pieces (one process: no bucket
@@ -364,7 +405,16 @@ class ClipTrainer:
         dp = self._dp()
         self._phase(self._fwd_gen, graphs, "fwd", join=False)
         self._cross_wait()
-        if not dp:
+        if not dp and self._early():
+            self._phase(lambda t: self._bwd_a_gen(t, flush=False), graphs, "bwd_a", fork=False, join=False)
+            _, s0, s1 = self._tower_streams()
+            for t, st in ((1, s1), (0, s0)):  # each tower's upper partials, after its bwd_a, on the comm stream
+                self._order(st, self.comm, ("early", t))
+                with torch.cuda.stream(self.comm):
+                    self._single(self.plans[t].flush_pending, graphs, ("flush", t))
+            self._phase(self._bwd_b_gen, graphs, "bwd_b", fork=False)
+            self._order(self.comm, torch.cuda.current_stream(), "early_join")
+        elif not dp:
             self._phase(self._bwd_gen, graphs, "bwd", fork=False)
         else:
             ev = [] if self.comm_timing is not None else None
@@ -478,7 +528,13 @@ class ClipTrainer:
             return out
         for t in (0, 1):
             graphs[("fwd", t)] = pieces(self._fwd_gen(t))
-        if not dp:
+        if not dp and self._early():
+            for t in (0, 1):
+                graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=False))
+                graphs[("flush", t)] = one(self.plans[t].flush_pending)
+            for t in (0, 1):
+                graphs[("bwd_b", t)] = pieces(self._bwd_b_gen(t))
+        elif not dp:
             for t in (0, 1):
                 graphs[("bwd", t)] = pieces(self._bwd_gen(t))
         else:

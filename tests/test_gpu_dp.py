@@ -8,6 +8,12 @@ identical otherwise: SUM + 1/world scale, every collective on every rank).
   checkpoint loss_history equals the single-rank run's within 1e-6 (the
   objective is the same: model.py:906-907 is a mean over the within-block index i).
 * bench.py --gpus 2 under torch.distributed.run: the weak-scaling bench line.
+
+Limitation: gloo's all_reduce of a device tensor blocks the issuing host thread
+until the sum is back, so these runs issue the lower layers' backward only after
+bucket A is reduced: they check the bucketed schedule's RESULTS, not the overlap
+of bucket A with the backward that RCCL gives (that needs one GPU per rank: the
+driver's multi-GPU runs; the bench line's `dist` field reports the exposed time).
 """
 import glob
 import json

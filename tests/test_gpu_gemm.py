@@ -1,10 +1,12 @@
-"""Split-bf16 (x3) GEMM (csrc/ghm_gemm.hip) and the VLM's split-bf16 attention
+"""Split-bf16 (x3) GEMM (csrc/ghm_gemm.hip), its exact-f32 variant (ghm_gemm_f32:
+the VLM's precision "f32" mode) and the VLM's split-bf16 attention
 (csrc/ghm_vlm_x3.hip) against float64 torch references of the same ops.
 
 Tolerance of a split-bf16 product: every bf16 x bf16 partial product is exact in
 f32; the dropped lo*lo term and the bf16 rounding of lo bound the error at about
 2^-16 of sum_k |a||b| per element (tests/test_split_numerics.py pins that bound on
-the CPU), so each element is checked against 4e-5 * (|A| |B|)[m][n]."""
+the CPU), so each element is checked against 4e-5 * (|A| |B|)[m][n]; the f32
+variant (f32 products, f32 accumulation over K <= 1024) against 4e-6."""
 import math
 
 import pytest
@@ -15,6 +17,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
 REL = 4e-5
+RELS = {False: 4e-5, True: 4e-6}  # f32=False: split-bf16; True: exact-f32 products
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -44,10 +47,12 @@ def _check(got, want, bound, what):
     assert not bad.any(), f"{what}: max err {err.max().item():.3e}, worst ratio {(err / bound).max().item():.2f}"
 
 
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("M", [405, 1280])
 @pytest.mark.parametrize("K,N", [(256, 256), (256, 1024), (128, 512), (1024, 256)])
-def test_forward_shapes(M, K, N):
+def test_forward_shapes(M, K, N, f32):
     """Y = X W^T (ta=0, tb=1) with the store, GELU and bias+residual epilogues."""
+    REL = RELS[f32]
     g = torch.Generator().manual_seed(M + K + N)
     X = torch.randn(M, K, generator=g)
     W = torch.randn(N, K, generator=g) / math.sqrt(K)
@@ -57,24 +62,26 @@ def test_forward_shapes(M, K, N):
     acc = X.double() @ W.double().t()
     bound = REL * (X.double().abs() @ W.double().abs().t()) + 1e-6
     C = torch.empty(M, N, device=DEV)
-    _gemm(0, 1, EPI_STORE, Xd, K, (Wd,), K, 0, C, N, M, N, K)
+    _gemm(0, 1, EPI_STORE, Xd, K, (Wd,), K, 0, C, N, M, N, K, f32=f32)
     torch.cuda.synchronize()
     _check(C, acc, bound, "store")
     C2 = torch.empty(M, N, device=DEV)
-    _gemm(0, 1, EPI_GELU, Xd, K, (Wd,), K, 0, C, N, M, N, K, C2=C2, bias=bd)
+    _gemm(0, 1, EPI_GELU, Xd, K, (Wd,), K, 0, C, N, M, N, K, C2=C2, bias=bd, f32=f32)
     torch.cuda.synchronize()
     u = acc + b.double()
     _check(C, _gelu64(u), 1.2 * bound + 1e-6, "gelu")
     _check(C2, _dgelu64(u), 0.5 * bound + 1e-6, "gelu'")
-    _gemm(0, 1, EPI_RESID, Xd, K, (Wd,), K, 0, C, N, M, N, K, bias=bd, R=Rd, ldr=N)
+    _gemm(0, 1, EPI_RESID, Xd, K, (Wd,), K, 0, C, N, M, N, K, bias=bd, R=Rd, ldr=N, f32=f32)
     torch.cuda.synchronize()
     _check(C, acc + b.double() + R.double(), bound + 1e-6, "resid")
 
 
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("D", [128, 256])
-def test_stacked_qkv_forward_and_data_grad(D):
+def test_stacked_qkv_forward_and_data_grad(D, f32):
     """The fused QKV product over three separate weights, and its data gradient
     dX = [dq|dk|dv] [Wq; Wk; Wv] (B stacked along k)."""
+    REL = RELS[f32]
     M = 3 * 81
     g = torch.Generator().manual_seed(D)
     X = torch.randn(M, D, generator=g)
@@ -82,35 +89,39 @@ def test_stacked_qkv_forward_and_data_grad(D):
     Wd = [w.to(DEV) for w in Ws]
     Wcat = torch.cat(Ws, 0).double()
     C = torch.empty(M, 3 * D, device=DEV)
-    _gemm(0, 1, EPI_STORE, X.to(DEV), D, Wd, D, D, C, 3 * D, M, 3 * D, D)
+    _gemm(0, 1, EPI_STORE, X.to(DEV), D, Wd, D, D, C, 3 * D, M, 3 * D, D, f32=f32)
     torch.cuda.synchronize()
     _check(C, X.double() @ Wcat.t(), REL * (X.double().abs() @ Wcat.abs().t()) + 1e-6, "qkv")
     dY = torch.randn(M, 3 * D, generator=g)
     dX = torch.empty(M, D, device=DEV)
-    _gemm(0, 0, EPI_STORE, dY.to(DEV), 3 * D, Wd, D, D, dX, D, M, D, 3 * D)
+    _gemm(0, 0, EPI_STORE, dY.to(DEV), 3 * D, Wd, D, D, dX, D, M, D, 3 * D, f32=f32)
     torch.cuda.synchronize()
     _check(dX, dY.double() @ Wcat, REL * (dY.double().abs() @ Wcat.abs()) + 1e-6, "dX")
 
 
-def test_data_grad_product_epilogue():
+@pytest.mark.parametrize("f32", [False, True])
+def test_data_grad_product_epilogue(f32):
     """dU = (dY W2) * GELU'(U) (ta=0, tb=0, product epilogue)."""
+    REL = RELS[f32]
     M, D, F = 700, 256, 1024
     g = torch.Generator().manual_seed(5)
     dY = torch.randn(M, D, generator=g)
     W2 = torch.randn(D, F, generator=g) / 16
     R = torch.rand(M, F, generator=g)
     C = torch.empty(M, F, device=DEV)
-    _gemm(0, 0, EPI_MUL, dY.to(DEV), D, (W2.to(DEV),), F, 0, C, F, M, F, D, R=R.to(DEV), ldr=F)
+    _gemm(0, 0, EPI_MUL, dY.to(DEV), D, (W2.to(DEV),), F, 0, C, F, M, F, D, R=R.to(DEV), ldr=F, f32=f32)
     torch.cuda.synchronize()
     want = (dY.double() @ W2.double()) * R.double()
     bound = REL * (dY.double().abs() @ W2.double().abs()) * R.double() + 1e-6
     _check(C, want, bound, "mul")
 
 
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("M_tok,nsplit", [(405, 1), (2000, 7), (10368, 32), (10368 + 5, 32)])
-def test_wgrad_split_k(M_tok, nsplit):
+def test_wgrad_split_k(M_tok, nsplit, f32):
     """dW = dY^T X over tokens (ta=1, tb=0) in split-k slabs and the fixed-order
     reduce into three stacked destinations; bit-identical when repeated."""
+    REL = RELS[f32]
     D = 256
     g = torch.Generator().manual_seed(M_tok)
     dY = torch.randn(M_tok, 3 * D, generator=g)
@@ -129,7 +140,7 @@ def test_wgrad_split_k(M_tok, nsplit):
     X_big[:M_tok] = X.to(DEV)
     res = []
     for _ in range(2):
-        _gemm(1, 0, EPI_SLAB, dY_big, 3 * D, (X_big,), D, 0, slab, D, 3 * D, D, M_tok, nsplit=nsplit)
+        _gemm(1, 0, EPI_SLAB, dY_big, 3 * D, (X_big,), D, 0, slab, D, 3 * D, D, M_tok, nsplit=nsplit, f32=f32)
         _native.call("ghm_gemm_reduce", _ptr(slab), nsplit, 3 * D, D, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]), D,
                      ctypes_stream())
         torch.cuda.synchronize()

@@ -356,6 +356,25 @@ def test_graph_replay_matches_eager(precision):
         assert torch.equal(a, b)
 
 
+def test_early_reduce_bit_identical(monkeypatch):
+    """The step's stream schedule does not change its arithmetic:
+    GHM_EARLY_REDUCE=1 (the top layers' partials reduced on the comm stream while
+    the lower layers run; the same reduction jobs) and GHM_FAST_EVENTS=1 (the
+    cross-stream waits on native device-scope events) give loss histories and
+    parameters bit-identical to the default schedule, eager and replayed."""
+    out = []
+    for env in ({}, {"GHM_EARLY_REDUCE": "1"}, {"GHM_FAST_EVENTS": "1"}, {"GHM_EARLY_REDUCE": "1", "GHM_FAST_EVENTS": "1"}):
+        for k in ("GHM_EARLY_REDUCE", "GHM_FAST_EVENTS"):
+            monkeypatch.setenv(k, env.get(k, "0"))
+        s, t = _trainer(5, 8, 0.2, precision="x3")
+        assert t._early() == ("GHM_EARLY_REDUCE" in env) and t.fast_events == ("GHM_FAST_EVENTS" in env)
+        out.append((_run(s, t, 8, 6, graph_after=2), [p.detach().clone() for p in t.tm.parameters()]))
+    for h, ps in out[1:]:
+        np.testing.assert_array_equal(out[0][0], h)
+        for a, b in zip(out[0][1], ps):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_default_config_curve_vs_reference(precision):
     """North-star parity: the default CLIP config (p=0.2, L=5, d=128, B=128)

@@ -1,4 +1,4 @@
-# usage: bash tools/gpu_r3_probe2.sh TAG : LN-statistics load characterisation (DESIGN.md §4 "Determinism")
+# usage: bash tools/gpu_stats_probe.sh TAG : LN-statistics load characterisation (DESIGN.md §4 "Determinism")
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/$1

@@ -10,6 +10,7 @@ rc=$?
 echo "prof rc=$rc" >> gpurun_out/tl_$TAG/bench.err
 [ $rc -eq 0 ] || exit $rc
 f=$(find gpurun_out/tl_$TAG -name '*kernel_trace.csv' | head -1)
-python tools/timeline.py "$f" k_adamw -8 -v > gpurun_out/tl_$TAG/timeline.txt
+# step -26: a timed step (bench.py then replays 10 serial + 10 concurrent stamped-twin steps and 3 eager ones)
+python tools/timeline.py "$f" k_adamw -26 -v > gpurun_out/tl_$TAG/timeline.txt
 s=$(find gpurun_out/tl_$TAG -name '*kernel_stats.csv' | head -1)
 python tools/kstats.py "$s" 26 30 > gpurun_out/tl_$TAG/kstats.txt

@@ -3,7 +3,20 @@ inputs on stream A while another kernel (aggressor) runs on stream B; the
 victim's outputs must be bit-identical across repetitions.
 
     python tools/race_probe.py [victim] [aggressor] [reps]
-    victim: qkv_bwd | qkv_load | qkv_dev | mlp_bwd | wgrad | attn_bwd ; aggressor: mlp_bwd | wgrad | attn_bwd | fwd_mlp | none
+    victim: qkv_bwd | qkv_load | qkv_dev | qkv_sc1 | qkv_dbg | qkv_dbgu | qkv_xcc | mlp_bwd | wgrad | attn_bwd
+    aggressor: mlp_bwd | wgrad | wgrad0 | wgrad_nb | attn_bwd | fwd_mlp | mm | copy | none
+
+qkv_xcc (probe mode 6): the plain statistics load, used, with no per-token debug
+store; each workgroup records its XCC_ID / HW_ID.  The reference output is the
+same kernel run alone (checked deterministic).  Rows that differ beside the
+aggressor come in 16-token groups = one 128-byte line of the [M][2] statistics
+buffer; for each wrong group the line it used is searched among every 16-pair
+line of every statistics buffer of both towers, as this step's forward left
+them and as the previous step's did (snapshot): a float64 restatement of the LN
+backward (ghm_ln.h ln_bwd_acc) scores each line, and the best line is confirmed
+by rerunning the kernel alone with that line substituted (bit-exact rows = the
+line it read).  A stale cross-XCD L2 line is the previous step's line at the
+same index.
 """
 import ctypes
 import hashlib
@@ -26,7 +39,41 @@ def digest(t):
     return hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest()[:10]
 
 
-QKV_MODES = {"qkv_load": 1, "qkv_dev": 2, "qkv_sc1": 3, "qkv_dbg": 4, "qkv_dbgu": 5}
+QKV_MODES = {"qkv_load": 1, "qkv_dev": 2, "qkv_sc1": 3, "qkv_dbg": 4, "qkv_dbgu": 5, "qkv_xcc": 6}
+
+
+def stats_candidates(plans, prev):
+    """(label, [L*M, 2] f32 pairs) for every statistics buffer, current and previous step."""
+    out = []
+    for i, pl in enumerate(plans):
+        for name in ("st1", "st2"):
+            out.append((f"p{i}.{name}", getattr(pl, name).reshape(-1, 2)))
+            out.append((f"p{i}.{name}@prev", prev[f"p{i}.{name}"].reshape(-1, 2)))
+    return out
+
+
+def ln_bwd64(X, G, R, mu, rs):
+    """float64 LN backward of 16 rows for candidate lines: X, G (= dx * gamma), R
+    (residual) [16, 128]; mu, rs [K, 16] -> dH [K, 16, 128] (ln_bwd_acc)."""
+    xh = (X[None] - mu[..., None]) * rs[..., None]
+    gm = G.mean(-1)[None, :, None]
+    c2 = (G[None] * xh).mean(-1, keepdim=True)
+    return R[None] + rs[..., None] * (G[None] - gm - xh * c2)
+
+
+def search_line(X, G, R, W, cands):
+    """The 16-pair line of the candidate buffers whose pairs best reproduce the
+    16 wrong rows W: (worst-row error, label, first flat index, pairs)."""
+    best = (float("inf"), None, None, None)
+    for label, c in cands:
+        lines = c.double().view(-1, 16, 2)
+        for k0 in range(0, lines.shape[0], 1024):
+            blk = lines[k0:k0 + 1024]
+            err = (ln_bwd64(X, G, R, blk[..., 0], blk[..., 1]) - W[None]).abs().amax(-1).amax(-1)
+            v, k = torch.min(err, 0)
+            if v.item() < best[0]:
+                best = (v.item(), label, 16 * (k0 + int(k)), c.view(-1, 16, 2)[k0 + int(k)].clone())
+    return best
 
 
 def main():
@@ -38,25 +85,33 @@ def main():
     tr.set_tokens(ring[0, 0], ring[0, 1])
     tr.step()
     torch.cuda.synchronize()
+    p0, p1 = tr.plans
+    # the statistics as the previous step left them, then a step on another batch
+    prev = {f"p{i}.{n}": getattr(pl, n).clone() for i, pl in enumerate((p0, p1)) for n in ("st1", "st2")}
+    tr.set_tokens(ring[1, 0], ring[1, 1])
+    tr.step()
+    torch.cuda.synchronize()
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     c = _native.call
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
     A = ctypes.c_void_p(sa.cuda_stream)
     B = ctypes.c_void_p(sb.cuda_stream)
     l = 2
-    p0, p1 = tr.plans
     w0, w1 = tr.views[0][0], tr.views[1][0]
     M = p0.M
     # victim inputs: plan 0 buffers as left by the step; outputs into fresh tensors
     dHmid = torch.randn(M, 128, device="cuda") * 1e-3
     dqkv = torch.randn(M, 384, device="cuda") * 1e-3
     outH = torch.empty(M, 128, device="cuda")
+    outH2 = torch.empty(M, 128, device="cuda")  # the probe's reference reruns (qkv_xcc)
     outP = torch.empty_like(p0.part_ln2)
+    outP2 = torch.empty_like(p0.part_ln2)
     outG, outU = torch.empty(M, 512, device="cuda"), torch.randn(M, 512, device="cuda") * 1e-3
     vpart, vpb = torch.empty_like(p0.part_w1), torch.empty_like(p0.part_b1)
     vdS, outQ = torch.zeros_like(p0.dS), torch.empty(M, 384, device="cuda")
     xH, xP = torch.empty(M, 128, device="cuda"), torch.empty_like(p1.part_ln2)
-    dbg = torch.zeros(M, 4, device="cuda")
+    nblk = int(_native.hip_lib().ghm_token_blocks(M))
+    dbg = torch.zeros(M + nblk, 4, device="cuda")  # modes 4 / 5: per token; 4 / 6: per-workgroup placement
     n_dbg = 0
     xa, xb, xc = (torch.randn(4096, 4096, device="cuda") for _ in range(3))
 
@@ -82,6 +137,18 @@ def main():
           P(w0[f"_lns_2.{l}.bias"]), P(p0.pack[l]), P(w0[f"_mlps.{l}.0.bias"]), P(outG), P(outU), P(outH), P(outP),
           M, 128, 512, A)
         return [outG, outU, outH, outP]
+
+    def run_recompute():
+        c("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]), P(p0.pack[l]),
+          P(dHmid), P(outH2), P(outP2), M, 128, p0.eps, A)
+        torch.cuda.synchronize()
+        return outH2.clone()
+
+    def run_with_stats(st):  # mode 6 alone on a given statistics buffer
+        c("ghm_qkv_bwd_x3_probe", P(dqkv), P(p0.H[l]), P(st), P(w0[f"_lns_1.{l}.weight"]),
+          P(p0.pack[l]), P(dHmid), P(outH2), P(outP2), P(dbg), M, 128, p0.eps, 6, A)
+        torch.cuda.synchronize()
+        return outH2.clone()
 
     def run_aggr():
         if aggr == "mlp_bwd":
@@ -116,6 +183,20 @@ def main():
             c("ghm_attn_bwd_x3", P(p1.qkv[l]), P(p1.P[l]), P(p1.H[l + 1]), P(p1.dS), P(p1.dqkv), p1.N, p1.T, 128,
               p1.scale_div, B)
 
+    if victim == "qkv_xcc":  # the reference output: the same kernel alone, twice (deterministic)
+        alone = []
+        for _ in range(2):
+            run_victim()
+            torch.cuda.synchronize()
+            alone.append(outH.clone())
+        truthH = alone[0]
+        print(f"mode 6 alone: repeat bit-identical {torch.equal(alone[0], alone[1])}; vs the recomputing kernel: "
+              f"max |d| {(truthH - run_recompute()).abs().max().item():.2e}")
+        Wqkv = torch.cat([w0[f"_queries.{l}.weight"], w0[f"_keys.{l}.weight"], w0[f"_values.{l}.weight"]], 0).double()
+        gam64 = w0[f"_lns_1.{l}.weight"].double()
+        cands = stats_candidates((p0, p1), prev)
+        n_xcc, wrong_xcc, found, n_checked = 0, {}, {}, 0
+        all_xcc = None
     ref = [digest(t) for t in run_victim()]
     torch.cuda.synchronize()
     ref = None
@@ -146,14 +227,55 @@ def main():
             if aggr != "none":
                 run_aggr()
         torch.cuda.synchronize()
+        if victim == "qkv_xcc":
+            xcc = dbg[:nblk, 0].contiguous().view(torch.int32).cpu()
+            if all_xcc is None:
+                all_xcc = torch.bincount(xcc & 15, minlength=8).tolist()
+            got = outH.clone()
+            rows = torch.nonzero((got != truthH).any(1)).flatten().cpu()
+            if len(rows):
+                n_xcc += 1
+                groups = sorted(set((rows // 16 * 16).tolist()))
+                wgs = sorted(set(g // 128 for g in groups))
+                for wg in wgs:
+                    k = int(xcc[wg]) & 15
+                    wrong_xcc[k] = wrong_xcc.get(k, 0) + 1
+                print(f"  rep {r}: {len(rows)} wrong rows in 16-token groups {groups[:8]} (max |d| "
+                      f"{(got - truthH).abs().max().item():.2e}); workgroups {wgs[:8]} on XCC "
+                      f"{[int(xcc[w]) & 15 for w in wgs[:8]]}")
+                for m0 in groups:
+                    if n_checked >= 8:
+                        break
+                    n_checked += 1
+                    sl = slice(m0, m0 + 16)
+                    X, R = p0.H[l][sl].double(), dHmid[sl].double()
+                    G = (dqkv[sl].double() @ Wqkv) * gam64[None]
+                    W = got[sl].double()
+                    true_err = (ln_bwd64(X, G, R, p0.st1[l][sl, 0].double()[None], p0.st1[l][sl, 1].double()[None])
+                                - W[None]).abs().max().item()
+                    err, label, idx, pairs = search_line(X, G, R, W, cands)
+                    st = p0.st1[l].clone()
+                    st[sl] = pairs
+                    exact = int((run_with_stats(st)[sl] == got[sl]).all(1).sum())
+                    lay, tok = idx // M, idx % M
+                    same = label == "p0.st1@prev" and lay == l and tok == m0
+                    key = f"{label}{' same index' if same else ''}{' (exact)' if exact == 16 else ''}"
+                    found[key] = found.get(key, 0) + 1
+                    print(f"    group {m0} (XCC {int(xcc[m0 // 128]) & 15}): best line {label}[layer {lay}, tokens "
+                          f"{tok}..{tok + 15}] fit {err:.2e} (its own line {true_err:.2e}); rerun with that line "
+                          f"substituted: {exact}/16 rows bit-identical to the wrong rows")
         if victim in ("qkv_dbg", "qkv_dbgu"):  # loaded (and used) vs the buffer's statistics, per token
-            bad_rows = torch.nonzero((dbg[:, :2] != p0.st1[l]).any(1)).flatten()
+            if victim == "qkv_dbg" and r == 0:
+                xq = dbg[M:M + nblk, 0].contiguous().view(torch.int32).cpu() & 15
+                print(f"  workgroups per XCC (mode 4 placement record): {torch.bincount(xq, minlength=8).tolist()}")
+            bad_rows = torch.nonzero((dbg[:M, :2] != p0.st1[l]).any(1)).flatten()
             if len(bad_rows):
                 n_dbg += 1
                 rows = bad_rows.tolist()
                 print(f"  rep {r}: loaded stats differ from the buffer's for {len(rows)} tokens "
                       f"(first {rows[:4]}, last {rows[-1]}; 16-aligned groups "
-                      f"{sorted(set(x // 16 * 16 for x in rows))[:8]})")
+                      f"{sorted(set(x // 16 * 16 for x in rows))[:8]}; their workgroups' XCC "
+                      f"{sorted(set(int(dbg[M + x // 128, 0].view(torch.int32)) & 15 for x in rows))})")
                 st_all = {"p0.st1": p0.st1, "p0.st2": p0.st2, "p1.st1": p1.st1, "p1.st2": p1.st2}
                 for m in rows[:3]:
                     v = dbg[m, :2]
@@ -192,6 +314,9 @@ def main():
                         print(f"  rep {r} out{k}: {len(rows)} rows differ (first {rows[:6].tolist()}), "
                               f"max |d| {diff.max().item():.3e}, |ref| max {a.abs().max().item():.3e}, "
                               f"nan {torch.isnan(b).sum().item()}")
+    if victim == "qkv_xcc":
+        print(f"workgroups per XCC (all {nblk}): {all_xcc}; repetitions with wrong rows {n_xcc}/{reps}; "
+              f"wrong workgroups per XCC {dict(sorted(wrong_xcc.items()))}; lines the wrong groups read: {found}")
     print(f"victim {victim} aggressor {aggr}: {bad}/{reps - 1} repetitions differ"
           + (f"; loaded statistics != the buffer's in {n_dbg}/{reps} repetitions" if victim.startswith("qkv_dbg")
              else ""))
