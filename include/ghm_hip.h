@@ -27,10 +27,11 @@ int ghm_device_ok(void);
 /* Cross-stream ordering (the two-tower step's fork / join / cross waits,
  * replacing torch Stream.wait_stream in train_CLIP's step, which has no
  * reference counterpart: the reference runs the towers one after the other).
- * ghm_event_create(1): an event recorded with a device-scope release and no
- * system-scope fence; (0) a default one.  ghm_event_record / ghm_stream_wait:
+ * ghm_event_create(mode): 1 an event recorded with a device-scope release
+ * (hipEventReleaseToDevice), 2 with hipEventDisableSystemFence, 0 a default one
+ * (all without timing).  ghm_event_record / ghm_stream_wait:
  * hipEventRecord / hipStreamWaitEvent (streams: hipStream_t or NULL). */
-void* ghm_event_create(int device_scope);
+void* ghm_event_create(int mode);
 int ghm_event_destroy(void* ev);
 int ghm_event_record(void* ev, void* stream);
 int ghm_stream_wait(void* stream, void* ev);

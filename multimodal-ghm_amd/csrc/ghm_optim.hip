@@ -38,15 +38,17 @@ extern "C" int ghm_device_ok(void) {
 }
 
 // Cross-stream ordering for the two-tower step (clip_trainer.py _phase /
-// _cross_wait): events recorded with a device-scope release and no system-scope
-// fence (hipEventReleaseToDevice | hipEventDisableSystemFence | DisableTiming) --
-// the waits order work on one device, no host or peer reads the data.
-extern "C" void* ghm_event_create(int device_scope) {
+// _cross_wait): events recorded with a device-scope release instead of the
+// default system-scope one (mode 1: hipEventReleaseToDevice; 2:
+// hipEventDisableSystemFence; HIP takes one release flag) -- the waits order work
+// on one device, no host or peer reads the data.
+extern "C" void* ghm_event_create(int mode) {
   hipEvent_t e = nullptr;
-  const unsigned flags = hipEventDisableTiming |
-                         (device_scope ? (hipEventDisableSystemFence | hipEventReleaseToDevice) : 0u);
-  if (hipEventCreateWithFlags(&e, flags) != hipSuccess) {
-    snprintf(g_err, sizeof(g_err), "hipEventCreateWithFlags failed");
+  const unsigned flags = hipEventDisableTiming | (mode == 1 ? hipEventReleaseToDevice
+                                                  : mode == 2 ? hipEventDisableSystemFence : 0u);
+  const hipError_t rc = hipEventCreateWithFlags(&e, flags);
+  if (rc != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "hipEventCreateWithFlags(0x%x): %s", flags, hipGetErrorString(rc));
     return nullptr;
   }
   return e;

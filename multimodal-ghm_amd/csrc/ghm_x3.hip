@@ -28,7 +28,7 @@
 
 // waves per workgroup of the split-K weight gradient (k_wgrad_x3)
 #ifndef GHM_WGRAD_FAST
-#define GHM_WGRAD_FAST 0  // 1: the stride-specialised weight gradients (k_wgrad_x3 LDA / LDB)
+#define GHM_WGRAD_FAST 1  // 0: the run-time-stride weight gradients only (k_wgrad_x3 LDA / LDB = 0)
 #endif
 #ifndef GHM_WGRAD_WAVES
 #define GHM_WGRAD_WAVES 4

@@ -163,11 +163,12 @@ class ClipTrainer:
         self.comm = torch.cuda.Stream(device=self.device)  # data-parallel bucket all-reduces
         # one process: reduce the top dp_top layers' partials on the (otherwise idle)
         # comm stream while the towers run their lower layers, instead of all of
-        # them in the serial tail after the last layer (GHM_EARLY_REDUCE=0: tail only)
-        self.early_reduce = os.environ.get("GHM_EARLY_REDUCE", "0") == "1"
+        # them in the serial tail after the last layer (GHM_EARLY_REDUCE=0: tail
+        # only).  Tail 163 -> 116 us (tl_r4ab6 / tl_r4ab7e), step unchanged (r4_ab7).
+        self.early_reduce = os.environ.get("GHM_EARLY_REDUCE", "1") == "1"
         # cross-stream waits on native device-scope events (no system-scope fence)
         # instead of torch's Stream.wait_stream (GHM_FAST_EVENTS=1)
-        self.fast_events = os.environ.get("GHM_FAST_EVENTS", "0") == "1"
+        self.fast_events = int(os.environ.get("GHM_FAST_EVENTS", "0"))  # ghm_event_create mode (1, 2)
         self._evs = {}
         # data-parallel timing (bench.py): None, or a list that each step appends
         # (bucket A ms, bucket B ms, exposed ms) event triples to
@@ -275,8 +276,8 @@ class ClipTrainer:
 
     def _loss(self):
         """The loss value of the step (and the penalised one) into the histories.
-        Runs at the start of the optimizer phase, off the forward -> backward
-        path: each tower's readout backward recomputes its rows of the loss
+        Runs on the comm stream once both forwards are done, off the towers'
+        paths: each tower's readout backward recomputes its rows of the loss
         gradient from both towers' embeddings (ghm_readout_bwd_clip), which stay
         untouched until the next forward."""
         pt, pi = self.plans
@@ -344,7 +345,7 @@ class ClipTrainer:
     def _event(self, key):
         ev = self._evs.get(key)
         if ev is None:
-            ev = _native.hip_lib().ghm_event_create(1)
+            ev = _native.hip_lib().ghm_event_create(self.fast_events)
             if not ev:
                 _native.check(-1, "ghm_event_create")
             self._evs[key] = ev = ctypes.c_void_p(ev)
@@ -405,7 +406,16 @@ class ClipTrainer:
         dp = self._dp()
         self._phase(self._fwd_gen, graphs, "fwd", join=False)
         self._cross_wait()
-        if not dp and self._early():
+        # the loss value on the comm stream, off both towers' backward paths (the
+        # embeddings stay untouched until the next forward)
+        main, s0, _ = self._tower_streams()
+        self._order(s0, self.comm, "loss")
+        with torch.cuda.stream(self.comm):
+            self._single(self._loss, graphs, "loss")
+        # the schedule the graphs were captured with (bench.py replays them with the
+        # towers on one stream, where _early() would say no)
+        early = self._early() if graphs is None else ("flush", 0) in graphs
+        if not dp and early:
             self._phase(lambda t: self._bwd_a_gen(t, flush=False), graphs, "bwd_a", fork=False, join=False)
             _, s0, s1 = self._tower_streams()
             for t, st in ((1, s1), (0, s0)):  # each tower's upper partials, after its bwd_a, on the comm stream
@@ -416,6 +426,7 @@ class ClipTrainer:
             self._order(self.comm, torch.cuda.current_stream(), "early_join")
         elif not dp:
             self._phase(self._bwd_gen, graphs, "bwd", fork=False)
+            self._order(self.comm, main, "loss_join")
         else:
             ev = [] if self.comm_timing is not None else None
             self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a", fork=False, join=False)
@@ -435,7 +446,6 @@ class ClipTrainer:
         self._single(self._optim, graphs, "optim")
 
     def _optim(self):
-        self._loss()
         s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         b1, omb1, b2, omb2, eps = self.consts
         _native.call("ghm_clip_prepare", _p(self.gflat), self.n_params, self.max_norm, _p(self.sched),
@@ -528,6 +538,7 @@ class ClipTrainer:
             return out
         for t in (0, 1):
             graphs[("fwd", t)] = pieces(self._fwd_gen(t))
+        graphs["loss"] = one(self._loss)
         if not dp and self._early():
             for t in (0, 1):
                 graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=False))

@@ -39,6 +39,10 @@ The long reference runs (hours on this container's CPU) were made with:
                     --guide-steps 1101 --threads 5): the reference's own code on the kernels a
                     host without AVX-512 runs -- with the 2-thread run, the spread of the
                     reference's own fp32 arithmetic (tests/conftest.py curve_bound).
+  clip_guided_curve3001_scalar.npz  ATEN_CPU_CAPABILITY=default (--guide-steps 1101 --threads 4,
+                    69 min): the same code on ATen's scalar (non-SIMD) kernels -- LayerNorm,
+                    softmax, GELU and the reductions summed in another order, the GEMMs
+                    unchanged (MKL).
 """
 import argparse
 import json

@@ -23,6 +23,7 @@ import hashlib
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -195,6 +196,9 @@ def main():
         Wqkv = torch.cat([w0[f"_queries.{l}.weight"], w0[f"_keys.{l}.weight"], w0[f"_values.{l}.weight"]], 0).double()
         gam64 = w0[f"_lns_1.{l}.weight"].double()
         cands = stats_candidates((p0, p1), prev)
+        float_tensors = [(f"p{i}.{k}", v) for i, pl in enumerate((p0, p1)) for k, v in vars(pl).items()
+                         if isinstance(v, torch.Tensor) and v.is_cuda and v.dtype == torch.float32]
+        float_tensors += [(k, v) for k, v in prev.items()] + [("pflat", tr.pflat), ("gflat", tr.gflat)]
         n_xcc, wrong_xcc, found, n_checked = 0, {}, {}, 0
         all_xcc = None
     ref = [digest(t) for t in run_victim()]
@@ -264,6 +268,37 @@ def main():
                     print(f"    group {m0} (XCC {int(xcc[m0 // 128]) & 15}): best line {label}[layer {lay}, tokens "
                           f"{tok}..{tok + 15}] fit {err:.2e} (its own line {true_err:.2e}); rerun with that line "
                           f"substituted: {exact}/16 rows bit-identical to the wrong rows")
+                    # does ANY (mean, rstd) explain a wrong row?  continuous fit per row vs the
+                    # model's own noise (the reference rows fitted with their true pair)
+                    from scipy.optimize import least_squares
+                    Tr = truthH[sl].double()
+                    for rr in range(2):
+                        xs, gs, rs_, ws = (v[rr].cpu().numpy() for v in (X, G, R, W))
+                        tp = p0.st1[l][m0 + rr].double().cpu().numpy()
+
+                        def res(q, xs=xs, gs=gs, rs_=rs_, ws=ws):
+                            xh = (xs - q[0]) * q[1]
+                            return rs_ + q[1] * (gs - gs.mean() - xh * (gs * xh).mean()) - ws
+                        fit = least_squares(res, tp, x_scale=[1e-2, 1e-2], xtol=1e-15, ftol=1e-15, gtol=1e-15)
+                        noise = np.abs(res(tp, ws=Tr[rr].cpu().numpy())).max()
+                        print(f"      row {m0 + rr}: best-fit pair {fit.x.tolist()} (true {tp.tolist()}) leaves "
+                              f"{np.abs(fit.fun).max():.2e}; the true pair leaves {np.abs(res(tp)).max():.2e} on the "
+                              f"wrong row and {noise:.2e} on the correct row (model noise)")
+                        if np.abs(fit.fun).max() < 3 * noise:  # a (mean, rstd) pair explains the row: find it
+                            tgt = torch.tensor(fit.x, dtype=torch.float32, device="cuda")
+                            best = (float("inf"), None)
+                            for name, t in float_tensors:
+                                flat = t.reshape(-1)
+                                for off in (0, 1):
+                                    n2 = (flat.numel() - off) // 2
+                                    if n2 < 1:
+                                        continue
+                                    pr = flat[off:off + 2 * n2].view(n2, 2)
+                                    d = ((pr - tgt).abs() / tgt.abs().clamp_min(1e-12)).amax(1)
+                                    v, k = torch.min(d, 0)
+                                    if v.item() < best[0]:
+                                        best = (v.item(), f"{name}[float {off + 2 * int(k)}]")
+                            print(f"        nearest float pair anywhere: {best[1]} (relative {best[0]:.1e})")
         if victim in ("qkv_dbg", "qkv_dbgu"):  # loaded (and used) vs the buffer's statistics, per token
             if victim == "qkv_dbg" and r == 0:
                 xq = dbg[M:M + nblk, 0].contiguous().view(torch.int32).cpu() & 15
