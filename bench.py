@@ -292,10 +292,10 @@ def pmc_traffic(kernel):
     with open(path) as f:
         t = json.load(f)
     ks = t.get("kernels", {})
-    k = ks.get(kernel)
-    if k is None:  # template instantiation the step launches (x3b: NW = 8, nothing saved)
-        k = ks.get(kernel + "<8, false>")
-    return None if k is None else k["hbm_bytes"]
+    for suffix in ("", "<8>", "<8, 0>", "<8, false>"):  # the instantiation the step launches (NW = 8)
+        if kernel + suffix in ks:
+            return ks[kernel + suffix]["hbm_bytes"]
+    return None
 
 
 def step_hbm_bytes():

@@ -26,10 +26,13 @@
 #error "GHM_ABL timing ablations give wrong results: only with -DGHM_ABLATION_BUILD (tools/, never the product library)"
 #endif
 
-// waves per workgroup of the split-K weight gradient (k_wgrad_x3)
+#ifndef GHM_QKV_STATS_LOAD
+#define GHM_QKV_STATS_LOAD 1  // 0: k_qkv_bwd_x3 recomputes the LN1 statistics from H (one more read of H)
+#endif
 #ifndef GHM_WGRAD_FAST
 #define GHM_WGRAD_FAST 1  // 0: the run-time-stride weight gradients only (k_wgrad_x3 LDA / LDB = 0)
 #endif
+// waves per workgroup of the split-K weight gradient (k_wgrad_x3)
 #ifndef GHM_WGRAD_WAVES
 #define GHM_WGRAD_WAVES 4
 #endif
@@ -410,7 +413,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
       fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
     }
-#endif
     f32x4 u[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -448,6 +450,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     if (GHM_ABL != 5)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
+#endif
   if (valid) {
     float* orow = Hout + m * GHM_D;
 #pragma unroll
@@ -1814,10 +1817,20 @@ extern "C" int ghm_qkv_bwd_x3(const float* dqkv, const float* H, const float* st
                               float eps, void* stream) {
   GHM_CHECK(dqkv && H && ln_w && pack && dH_mid && dH && part_ln, "null pointer");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
+#if GHM_QKV_STATS_LOAD
+  // the forward's statistics by a system-scope load, as every other reader of
+  // cross-kernel statistics (DESIGN.md §4 "Determinism"): one read of H fewer,
+  // 47.6 -> 44.7 us isolated, step 4.155 -> 4.120 ms (r4_ab8)
+  GHM_CHECK(stats && M * 8 < (int64_t(1) << 31), "stats");
+  hipLaunchKernelGGL(k_qkv_bwd_x3<2>, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), dqkv, H, ln_w, reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln,
+                     M, eps, reinterpret_cast<const float2*>(stats), nullptr);
+#else
   (void)stats;  // the statistics are recomputed (DESIGN.md §4 "Determinism")
   hipLaunchKernelGGL(k_qkv_bwd_x3<0>, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), dqkv, H, ln_w, reinterpret_cast<const __bf16*>(pack), dH_mid, dH, part_ln,
                      M, eps, nullptr, nullptr);
+#endif
   return ghm_launch_status();
 }
 

@@ -191,7 +191,7 @@ def main():
             torch.cuda.synchronize()
             alone.append(outH.clone())
         truthH = alone[0]
-        print(f"mode 6 alone: repeat bit-identical {torch.equal(alone[0], alone[1])}; vs the recomputing kernel: "
+        print(f"mode 6 alone: repeat bit-identical {torch.equal(alone[0], alone[1])}; vs the product kernel: "
               f"max |d| {(truthH - run_recompute()).abs().max().item():.2e}")
         Wqkv = torch.cat([w0[f"_queries.{l}.weight"], w0[f"_keys.{l}.weight"], w0[f"_values.{l}.weight"]], 0).double()
         gam64 = w0[f"_lns_1.{l}.weight"].double()
