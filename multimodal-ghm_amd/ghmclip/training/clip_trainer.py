@@ -166,9 +166,11 @@ class ClipTrainer:
         # them in the serial tail after the last layer (GHM_EARLY_REDUCE=0: tail
         # only).  Tail 163 -> 116 us (tl_r4ab6 / tl_r4ab7e), step unchanged (r4_ab7).
         self.early_reduce = os.environ.get("GHM_EARLY_REDUCE", "1") == "1"
-        # cross-stream waits on native device-scope events (no system-scope fence)
-        # instead of torch's Stream.wait_stream (GHM_FAST_EVENTS=1)
-        self.fast_events = int(os.environ.get("GHM_FAST_EVENTS", "0"))  # ghm_event_create mode (1, 2)
+        # cross-stream waits on native events without the system-scope fence
+        # (ghm_event_create mode 2; 1 = device-scope release, 0 = torch's
+        # Stream.wait_stream): a just-in-time wait costs 10.8 instead of 12.7 us of
+        # idle queue, a satisfied one 5.7 (tools/xq_latency.py, profiles/r4_xq_report.txt)
+        self.fast_events = int(os.environ.get("GHM_FAST_EVENTS", "2"))
         self._evs = {}
         # data-parallel timing (bench.py): None, or a list that each step appends
         # (bucket A ms, bucket B ms, exposed ms) event triples to

@@ -391,19 +391,19 @@ def test_graph_replay_matches_eager(precision):
 
 def test_early_reduce_bit_identical(monkeypatch):
     """The step's stream schedule does not change its arithmetic: the default
-    early reduce (the top layers' partials reduced on the comm stream while the
-    lower layers run; the same reduction jobs) against GHM_EARLY_REDUCE=0 (all
-    in the tail), and GHM_FAST_EVENTS=1 / 2 (the
-    cross-stream waits on native device-scope events) give loss histories and
-    parameters bit-identical to the default schedule, eager and replayed."""
+    (early reduce of the top layers' partials on the comm stream while the lower
+    layers run, cross-stream waits on native events without the system-scope
+    fence) against GHM_EARLY_REDUCE=0 (all reductions in the tail) and
+    GHM_FAST_EVENTS=0 / 1 (torch's events / device-scope release): loss
+    histories and parameters bit-identical, eager and replayed."""
     out = []
-    for env in ({"GHM_EARLY_REDUCE": "0"}, {}, {"GHM_FAST_EVENTS": "1"}, {"GHM_FAST_EVENTS": "2"},
-                {"GHM_EARLY_REDUCE": "0", "GHM_FAST_EVENTS": "1"}):
+    for env in ({"GHM_EARLY_REDUCE": "0", "GHM_FAST_EVENTS": "0"}, {}, {"GHM_FAST_EVENTS": "0"},
+                {"GHM_FAST_EVENTS": "1"}, {"GHM_EARLY_REDUCE": "0"}):
         monkeypatch.setenv("GHM_EARLY_REDUCE", env.get("GHM_EARLY_REDUCE", "1"))
-        monkeypatch.setenv("GHM_FAST_EVENTS", env.get("GHM_FAST_EVENTS", "0"))
+        monkeypatch.setenv("GHM_FAST_EVENTS", env.get("GHM_FAST_EVENTS", "2"))
         s, t = _trainer(5, 8, 0.2, precision="x3")
         assert t._early() == (env.get("GHM_EARLY_REDUCE", "1") == "1")
-        assert t.fast_events == int(env.get("GHM_FAST_EVENTS", 0))
+        assert t.fast_events == int(env.get("GHM_FAST_EVENTS", 2))
         out.append((_run(s, t, 8, 6, graph_after=2), [p.detach().clone() for p in t.tm.parameters()]))
     for h, ps in out[1:]:
         np.testing.assert_array_equal(out[0][0], h)
