@@ -432,6 +432,16 @@ int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P
                         int n_prefix, float scale_div, float dbl, void* stream);
 int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv, int64_t n_seq,
                         int T, int D, int n_prefix, float scale_div, float dbl, void* stream);
+/* The same with the attention activation of model.py:121-130 (get_activation,
+ * applied at :485 for the CDM): act 1 relu, 2 gelu of the scaled score,
+ * elementwise (no row normalisation; masked entries 0); gelu writes GELU'(score)
+ * to Pd (same shape as P) for the backward, which takes dS = act'(score) dA /
+ * scale_div.  D == 128 (the joint CDM at T = 162 under train_CDNS.py --activation). */
+int ghm_attn_ext_fwd_x3_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq,
+                            int T, int D, int n_prefix, float scale_div, float dbl, int act, void* stream);
+int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dS,
+                            float* dqkv, int64_t n_seq, int T, int D, int n_prefix, float scale_div, float dbl,
+                            int act, void* stream);
 
 /* ---- split-bf16 (x3) GEMM for the VLM projections (csrc/ghm_gemm.hip) -------
  * Replaces the nn.Linear products of AutoRegressiveTransformer (models/model.py:

@@ -167,11 +167,17 @@ __device__ __forceinline__ int vx_key_tiles(int q1, int T, int npre) {
   return (kmax < T ? kmax : T - 1) / 32 + 1;
 }
 
-template <int NKT, int DD, int NW>
+// attention activation (model.py:121-130 get_activation): softmax, or relu / gelu
+// of the scaled score elementwise (no row normalisation; masked entries 0); gelu
+// also stores GELU'(score) in Pd for the backward
+constexpr int VACT_SOFTMAX = 0, VACT_RELU = 1, VACT_GELU = 2;
+
+template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX>
 __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __restrict__ qkv,
                                                                  const float* __restrict__ H,
                                                                  float* __restrict__ Hmid, float* __restrict__ P,
-                                                                 int T, int npre, float scale_div, float dbl) {
+                                                                 int T, int npre, float scale_div, float dbl,
+                                                                 float* __restrict__ Pd = nullptr) {
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
@@ -189,31 +195,63 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
   vx_scores<NKT, DD, NW>(seq, LD, DD, seq + qc * LD, T, j, h, nk, sh, sl, s);
   // one reciprocal and a base-2 exponent per score (as k_attn_fwd_x3)
   const float inv_scale = 1.f / scale_div, l2e = 1.4426950408889634f;
-  float mx = -INFINITY;
+  float inv;
+  if constexpr (ACT == VACT_SOFTMAX) {
+    float mx = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = 32 * kt + acc_row(r, h);
-      const float v = (key < T && vx_allowed(qc, key, npre)) ? s[kt][r] * inv_scale : -INFINITY;
-      s[kt][r] = v;
-      mx = fmaxf(mx, v);
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float v = (key < T && vx_allowed(qc, key, npre)) ? s[kt][r] * inv_scale : -INFINITY;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, xhalf(mx));
+    const float mx2 = mx * l2e;
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
+        s[kt][r] = e;
+        sum += e;
+      }
+    }
+    sum += xhalf(sum);
+    inv = qv ? 1.f / sum : 0.f;
+  } else {
+    inv = qv ? 1.f : 0.f;
+    float* drow = ACT == VACT_GELU ? Pd + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD : nullptr;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      float dv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float x = s[kt][r] * inv_scale;
+        float a, d;
+        if constexpr (ACT == VACT_RELU) {
+          a = fmaxf(x, 0.f);
+          d = 0.f;
+        } else {
+          gelu_fast(x, a, d);
+        }
+        const bool ok = qv && key < T && vx_allowed(qc, key, npre);
+        s[kt][r] = ok ? a : 0.f;
+        dv[r] = ok ? d : 0.f;
+      }
+      if constexpr (ACT == VACT_GELU) {
+        if (qv) {
+#pragma unroll
+          for (int qd = 0; qd < 4; ++qd)
+            st4(drow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+        }
+      }
     }
   }
-  mx = fmaxf(mx, xhalf(mx));
-  const float mx2 = mx * l2e;
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = __builtin_amdgcn_exp2f(fmaf(s[kt][r], l2e, -mx2));
-      s[kt][r] = e;
-      sum += e;
-    }
-  }
-  sum += xhalf(sum);
-  const float inv = qv ? 1.f / sum : 0.f;
   float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
   bf16x8 ph[2 * NKT], pl[2 * NKT];
 #pragma unroll
@@ -263,13 +301,14 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
 
 // dA^T = (V dO^T)(1 + 1/D), dS = P (dA - rowsum(P dA)) / scale_div (stored dense),
 // dQ^T = K^T dS^T
-template <int NKT, int DD, int NW>
+template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX>
 __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* __restrict__ qkv,
                                                                    const float* __restrict__ P,
                                                                    const float* __restrict__ dHmid,
                                                                    float* __restrict__ dS_out,
                                                                    float* __restrict__ dqkv, int T, float scale_div,
-                                                                   int npre, float dbl) {
+                                                                   int npre, float dbl,
+                                                                   const float* __restrict__ Pd = nullptr) {
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
@@ -284,7 +323,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
   const int nk = vx_key_tiles(NW * (static_cast<int>(blockIdx.y) + 1), T, npre);
   f32x16 dp[NKT];
   vx_scores<NKT, DD, NW>(seq, LD, 2 * DD, dHmid + (base + qc) * DD, T, j, h, nk, sh, sl, dp);
-  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
+  // gelu: dS = GELU'(score) dA / scale_div, so the saved derivative replaces P here
+  const float* prow = (ACT == VACT_GELU ? Pd : P) + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
   const float inv_scale = 1.f / scale_div;
   float delta = 0.f;
   f32x16 p[NKT];
@@ -301,17 +341,24 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       dp[kt][r] = dp[kt][r] + dp[kt][r] * dbl;
-      delta += p[kt][r] * dp[kt][r];
+      if (ACT == VACT_SOFTMAX) delta += p[kt][r] * dp[kt][r];
     }
   }
-  delta += xhalf(delta);
+  if (ACT == VACT_SOFTMAX) delta += xhalf(delta);
   float* srow = dS_out + (static_cast<int64_t>(blockIdx.x) * VX_PAD + q) * VX_PAD;
   bf16x8 dh[2 * NKT], dl[2 * NKT];
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
     float dv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (ACT == VACT_SOFTMAX)
+        dv[r] = (p[kt][r] * (dp[kt][r] - delta)) * inv_scale;
+      else if constexpr (ACT == VACT_RELU)
+        dv[r] = (p[kt][r] > 0.f ? dp[kt][r] : 0.f) * inv_scale;
+      else
+        dv[r] = (p[kt][r] * dp[kt][r]) * inv_scale;
+    }
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
@@ -457,12 +504,23 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
 template <int NKT>
 constexpr int vx_nw() { return NKT == 6 ? 3 : (NKT == 4 ? 2 : (NKT == 5 ? 5 : 1)); }
 
-template <int NKT, int DD>
+template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_fwd_n(unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int T, int npre,
-                  float sd, float dbl) {
+                  float sd, float dbl, float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, H, Hm, P, T, npre,
-                     sd, dbl);
+  hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, H, Hm, P, T,
+                     npre, sd, dbl, Pd);
+}
+
+template <int ACT>
+void launch_fwd_act(int T, unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P,
+                    float* Pd, int npre, float sd, float dbl) {
+  if (T <= 32) launch_fwd_n<1, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 64) launch_fwd_n<2, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 96) launch_fwd_n<3, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 128) launch_fwd_n<4, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 160) launch_fwd_n<5, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else launch_fwd_n<6, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
 }
 
 template <int DD>
@@ -476,14 +534,25 @@ void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float*
   else launch_fwd_n<6, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);  // D = 256: spills 5-12 VGPRs (correct, slower)
 }
 
-template <int NKT, int DD>
+template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
-                  float* dqkv, int T, int npre, float sd, float dbl) {
+                  float* dqkv, int T, int npre, float sd, float dbl, const float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dHm, dS,
-                     dqkv, T, sd, npre, dbl);
+  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dHm,
+                     dS, dqkv, T, sd, npre, dbl, Pd);
   hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dS, dHm,
                      dqkv, T, npre, dbl);
+}
+
+template <int ACT>
+void launch_bwd_act(int T, unsigned g, hipStream_t s, const float* qkv, const float* P, const float* Pd,
+                    const float* dHm, float* dS, float* dqkv, int npre, float sd, float dbl) {
+  if (T <= 32) launch_bwd_n<1, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 64) launch_bwd_n<2, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 96) launch_bwd_n<3, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 128) launch_bwd_n<4, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 160) launch_bwd_n<5, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else launch_bwd_n<6, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
 }
 
 template <int DD>
@@ -536,5 +605,33 @@ extern "C" int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float
   const unsigned g = static_cast<unsigned>(n_seq);
   if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
   else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_ext_fwd_x3_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd,
+                                       int64_t n_seq, int T, int D, int n_prefix, float scale_div, float dbl, int act,
+                                       void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P, "null pointer");
+  GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
+  GHM_CHECK(D == 128 && T >= 1 && T <= 192, "shape (D == 128, T <= 192)");
+  GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (act == VACT_RELU) launch_fwd_act<VACT_RELU>(T, g, ghm_stream(stream), qkv, H, H_mid, P, Pd, n_prefix, scale_div, dbl);
+  else launch_fwd_act<VACT_GELU>(T, g, ghm_stream(stream), qkv, H, H_mid, P, Pd, n_prefix, scale_div, dbl);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid,
+                                       float* dS, float* dqkv, int64_t n_seq, int T, int D, int n_prefix,
+                                       float scale_div, float dbl, int act, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
+  GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
+  GHM_CHECK(D == 128 && T >= 1 && T <= 192, "shape (D == 128, T <= 192)");
+  GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (act == VACT_RELU)
+    launch_bwd_act<VACT_RELU>(T, g, ghm_stream(stream), qkv, P, Pd, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  else
+    launch_bwd_act<VACT_GELU>(T, g, ghm_stream(stream), qkv, P, Pd, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
   return ghm_launch_status();
 }

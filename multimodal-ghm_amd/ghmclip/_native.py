@@ -87,6 +87,8 @@ HIP_SIGNATURES = {
     "ghm_vlm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_attn_ext_fwd_x3": [_p, _p, _p, _p, _i64, _i, _i, _i, _f, _f, _p],
     "ghm_attn_ext_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _f, _p],
+    "ghm_attn_ext_fwd_x3_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _f, _i, _p],
+    "ghm_attn_ext_bwd_x3_act": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _f, _f, _i, _p],
     "ghm_gemm_x3": [_i, _i, _i, _p, _i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64,
                     _i, _p],
     "ghm_event_create": [_i],

@@ -62,11 +62,14 @@ class CdmPlan(EncoderPlan):
     split-K buffers part_w1 / part_b1)."""
 
     def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None, joint=False):
+                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax"):
         if precision is None:  # the joint model (T = 162) defaults to exact f32 (DESIGN.md §9)
             precision = default_precision("f32" if joint else "x3")
+        # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
+        # on the split-bf16 attention kernels (EncoderPlan: one-sequence up to 96 tokens,
+        # the multi-workgroup ghm_attn_ext_*_act past 96, the joint model's 162)
         super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
-                         normalize_attn=normalize_attn, device=device, precision=precision)
+                         normalize_attn=normalize_attn, device=device, precision=precision, activation=activation)
         if not 1 <= n_i_token <= n_token:
             raise ValueError("n_i_token must be in [1, n_token]")
         self.Ti = n_i_token
@@ -197,9 +200,9 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[1] * 2 + 1)
         self.sigma = sigma
-        if activation != "softmax" or not mlp or not layernorm or maxnorm or auto_regressive:
-            raise NotImplementedError("HIP CDM: softmax attention, mlp=True, layernorm=True, maxnorm=False, "
-                                      "auto_regressive=False")
+        if activation not in ("softmax", "relu", "gelu") or not mlp or not layernorm or maxnorm or auto_regressive:
+            raise NotImplementedError("HIP CDM: softmax / relu / gelu attention, mlp=True, layernorm=True, "
+                                      "maxnorm=False, auto_regressive=False")
         if guide and self.guided_layer_gap == 0:
             raise ValueError("guide=True needs n_layer >= 2 * n_guided_layers[1] + 1 (model.py:372)")
         if n_mlp_hidden != 4 * n_embd:
@@ -243,7 +246,8 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
             self._plans.clear()
             self._plans[key] = CdmPlan(self.n_layer, T, T_img, n_seq, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
-                                       precision=self.precision, joint=not self.sequential)
+                                       precision=self.precision, joint=not self.sequential,
+                                       activation=self.activation)
         return self._plans[key]
 
     def forward(self, xt, zi):

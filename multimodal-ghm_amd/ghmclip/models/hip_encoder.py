@@ -101,14 +101,16 @@ class EncoderPlan:
         self.long_attn = n_token > 96
         pad = 192 if self.long_attn else 96
         # attention activation (model.py:121-130): softmax, or elementwise relu / gelu
-        # on the split-bf16 one-sequence kernels (ghm_attn_{fwd,bwd}_x3_act)
+        # on the split-bf16 attention kernels: the one-sequence ones up to 96 tokens
+        # (ghm_attn_{fwd,bwd}_x3_act, x3 plans), the multi-workgroup ones past 96
+        # (ghm_attn_ext_{fwd,bwd}_x3_act, which every precision's long attention uses)
         acts = {"softmax": 0, "relu": 1, "gelu": 2}
         if activation not in acts:
             raise NotImplementedError(f"attention activation {activation!r}")
         self.act = acts[activation]
-        if self.act and (self.precision != "x3" or self.long_attn):
-            raise NotImplementedError(f"attention activation {activation!r} runs on the split-bf16 (x3) kernels "
-                                      f"for sequences of <= 96 tokens only")
+        if self.act and self.precision != "x3" and not self.long_attn:
+            raise NotImplementedError(f"attention activation {activation!r} runs on the split-bf16 (x3) kernels: "
+                                      f"precision 'x3' for sequences of <= 96 tokens")
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -132,6 +134,8 @@ class EncoderPlan:
         # selects the exact-f32 torch validation path instead
         self.attn_f32 = (self.long_attn and self.precision == "f32"
                          and os.environ.get("GHM_LONG_ATTN", "x3") == "f32")
+        if self.attn_f32 and self.act:
+            raise NotImplementedError("GHM_LONG_ATTN=f32 (the exact torch validation attention) is softmax only")
         if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2)
             self.G, self.Dg = e(M, D_HIDDEN), None
         else:
@@ -249,8 +253,7 @@ class EncoderPlan:
                 if self.attn_f32:
                     self._attn_fwd_f32(l)
                 elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
-                    c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
-                      _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+                    self._attn_ext_fwd(l, s)
                 elif self.act:
                     c("ghm_attn_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                       None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
@@ -267,8 +270,7 @@ class EncoderPlan:
             if self.attn_f32:
                 self._attn_fwd_f32(l)
             elif self.long_attn:
-                c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
-                  _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+                self._attn_ext_fwd(l, s)
             else:
                 c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   N, T, D_MODEL, self.scale_div, s)
@@ -276,6 +278,29 @@ class EncoderPlan:
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
               _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
               _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+
+    def _attn_ext_fwd(self, l, s):
+        """Attention past 96 tokens on the multi-workgroup split-bf16 kernels:
+        unmasked (n_prefix = T), plain residual (dbl = 0); relu / gelu via the _act
+        variants."""
+        N, T = self.N, self.T
+        if self.act:
+            _native.call("ghm_attn_ext_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                         _ptr(self.P[l]), None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, T,
+                         self.scale_div, 0.0, self.act, s)
+        else:
+            _native.call("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                         _ptr(self.P[l]), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+
+    def _attn_ext_bwd(self, l, cur, s):
+        N, T = self.N, self.T
+        if self.act:
+            _native.call("ghm_attn_ext_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
+                         None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv),
+                         N, T, D_MODEL, T, self.scale_div, 0.0, self.act, s)
+        else:
+            _native.call("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
+                         _ptr(self.dqkv), N, T, D_MODEL, T, self.scale_div, 0.0, s)
 
     def _attn_fwd_f32(self, l):
         """Exact-f32 single-head attention past 96 tokens (model.py:489-497 of the
@@ -466,8 +491,7 @@ class EncoderPlan:
             if self.attn_f32:
                 self._attn_bwd_f32(l, cur)
             elif self.long_attn:
-                c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur), _ptr(self.dS),
-                  _ptr(self.dqkv), N, T, D_MODEL, T, self.scale_div, 0.0, s)
+                self._attn_ext_bwd(l, cur, s)
             elif self.act:
                 c("ghm_attn_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
                   None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,

@@ -86,7 +86,7 @@ class CdmTrainer:
         self.T, self.Ti = T, Ti
         self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,
                             normalize_attn=model.normalize_attn, device=self.device, precision=precision,
-                            joint=self.joint)
+                            joint=self.joint, activation=getattr(model, "activation", "softmax"))
         self.precision = self.plan.precision
         if self.joint:
             self.clip_plan = None

@@ -141,10 +141,13 @@ class OracleCdm(nn.Module):
     the (then empty) ModuleLists, t_embedding, per layer q, k, v, ln1, mlp, ln2,
     then _read_out Linear(d -> 1) and the unused _out Linear(n_token -> 1)."""
 
-    def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512, sequential=True):
+    def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512, sequential=True,
+                 activation="softmax"):
         super().__init__()
         self.V, self.n_i_token, self.n_embd = num_class, n_i_token, n_embd
         self.sequential = sequential
+        # get_activation (model.py:121-130), applied to the scaled scores at :485
+        self.act = {"softmax": lambda x: F.softmax(x, dim=-1), "relu": F.relu, "gelu": F.gelu}[activation]
         self.position_embeddings = nn.Embedding(n_token, n_embd)
         self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         self._mlps, self._lns_1, self._lns_2 = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -178,7 +181,7 @@ class OracleCdm(nn.Module):
                                           self._lns_2):
             H1 = ln1(H)
             S = torch.einsum("bid,bjd->bij", q(H1), k(H1)) / np.sqrt(H.shape[2])  # :461-463
-            H = H + torch.einsum("bij,bjd->bid", F.softmax(S, dim=-1), v(H1))  # :466-467
+            H = H + torch.einsum("bij,bjd->bid", self.act(S), v(H1))  # :485-486
             H = H + mlp(ln2(H))  # :470-475
         return self._read_out(H)[:, :T2, 0]  # :527-531
 

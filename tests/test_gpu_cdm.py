@@ -72,12 +72,13 @@ def test_bp_dns_kernel_matches_reference():
         np.testing.assert_array_equal(z32.cpu().numpy(), f["z"][k])
 
 
-def _pair(L=2, seed=11, precision="f32"):
+def _pair(L=2, seed=11, precision="f32", activation="softmax"):
     from ghmclip import ConditionalDenoiseEncoderTransformer
     torch.manual_seed(seed)
-    prod = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True)
+    prod = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True,
+                                                activation=activation)
     torch.manual_seed(seed)
-    ref = CO.OracleCdm(82, 81, 10, 128, L, 512)
+    ref = CO.OracleCdm(82, 81, 10, 128, L, 512, activation=activation)
     for (kp, vp), (kr, vr) in zip(prod.state_dict().items(), ref.state_dict().items()):
         assert kp == kr and vp.shape == vr.shape
         assert torch.equal(vp, vr)
@@ -92,12 +93,15 @@ def _pair(L=2, seed=11, precision="f32"):
     return prod.to(DEV), ref
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision,activation", [("f32", "softmax"), ("x3", "softmax"), ("x3", "relu"),
+                                                  ("x3", "gelu")])
 @pytest.mark.parametrize("B", [7, 20])
-def test_cdm_module_forward_backward(B, precision):
+def test_cdm_module_forward_backward(B, precision, activation):
     """ConditionalDenoiseEncoderTransformer forward, parameter and conditioning
-    gradients vs the oracle restatement of model.py:337-532."""
-    prod, ref = _pair(precision=precision)
+    gradients vs the oracle restatement of model.py:337-532; the attention
+    activation (relu / gelu, model.py:485, train_CDNS.py --activation) on the
+    split-bf16 one-sequence kernels."""
+    prod, ref = _pair(precision=precision, activation=activation)
     g = torch.Generator().manual_seed(B)
     z = torch.randint(0, 10, (B, 81), generator=g).float() + torch.randn(B, 81, generator=g)
     cond = torch.randn(B, 1, 10, generator=g)

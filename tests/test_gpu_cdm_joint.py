@@ -38,20 +38,23 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-@pytest.mark.parametrize("B,mode", [(3, "x3"), (8, "x3"), (8, "f32"), (8, "f32_exact_attn")])
-def test_joint_cdm_module_forward_backward(B, mode, monkeypatch):
+@pytest.mark.parametrize("B,mode,act", [(3, "x3", "softmax"), (8, "x3", "softmax"), (8, "f32", "softmax"),
+                                        (8, "f32_exact_attn", "softmax"), (5, "x3", "relu"), (5, "f32", "gelu")])
+def test_joint_cdm_module_forward_backward(B, mode, act, monkeypatch):
     """ConditionalDenoiseEncoderTransformer(sequential=False) forward and every
     parameter gradient (t_embedding included) vs the oracle restatement, in
     the split-bf16 mode, the f32 mode (the joint default: exact projections and
-    MLP, split-bf16 attention core past 96 tokens) and the f32 mode's exact
-    torch attention (GHM_LONG_ATTN=f32, the validation path)."""
+    MLP, split-bf16 attention core past 96 tokens), the f32 mode's exact torch
+    attention (GHM_LONG_ATTN=f32, the validation path), and with the relu / gelu
+    attention of train_CDNS.py --activation (model.py:485; ghm_attn_ext_*_act)."""
     from ghmclip import ConditionalDenoiseEncoderTransformer
     if mode == "f32_exact_attn":
         monkeypatch.setenv("GHM_LONG_ATTN", "f32")
     torch.manual_seed(11)
-    prod = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 2, [4, 4], 4, 512, sequential=False)
+    prod = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 2, [4, 4], 4, 512, sequential=False,
+                                                activation=act)
     torch.manual_seed(11)
-    ref = CO.OracleCdm(162, 81, 10, 128, 2, 512, sequential=False)
+    ref = CO.OracleCdm(162, 81, 10, 128, 2, 512, sequential=False, activation=act)
     g = torch.Generator().manual_seed(B)
     with torch.no_grad():
         for (kp, vp), (_, vr) in zip(prod.named_parameters(), ref.named_parameters()):

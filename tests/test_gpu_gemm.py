@@ -322,3 +322,43 @@ def test_attention_ext_long_sequences(T, npre, dbl):
     got = dqkv.cpu().view(N, T, 3 * D).double()
     for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
         assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 2e-4 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
+
+
+@pytest.mark.parametrize("T,act", [(162, 1), (162, 2), (130, 2), (81, 1)])
+def test_attention_ext_activation(T, act):
+    """ghm_attn_ext_*_x3_act at D = 128 (the joint CDM's T = 162 under
+    train_CDNS.py --activation): relu / gelu of the scaled scores, no row
+    normalisation, plain residual; P, the output and dq / dk / dv against float64
+    autograd of model.py:485-486."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    N, D = 5, 128
+    pad = 96 if T <= 96 else 192
+    g = torch.Generator().manual_seed(T + act)
+    qkv = torch.randn(N, T, 3 * D, generator=g) * 0.5
+    H = torch.randn(N, T, D, generator=g)
+    dHm = torch.randn(N, T, D, generator=g)
+    q64, k64, v64 = (qkv[..., i * D:(i + 1) * D].double().requires_grad_(True) for i in range(3))
+    S = (q64 @ k64.transpose(1, 2)) / math.sqrt(D)
+    A = torch.relu(S) if act == 1 else torch.nn.functional.gelu(S)
+    want = H.double() + A @ v64
+    (want * dHm.double()).sum().backward()
+    qkv_d = qkv.to(DEV)
+    Hm = torch.empty(N * T, D, device=DEV)
+    P = torch.zeros(N, pad, pad, device=DEV)
+    Pd = torch.zeros(N, pad, pad, device=DEV)
+    dS = torch.zeros(N, pad, pad, device=DEV)
+    dqkv = torch.empty(N * T, 3 * D, device=DEV)
+    _native.call("ghm_attn_ext_fwd_x3_act", _ptr(qkv_d), _ptr(H.to(DEV)), _ptr(Hm), _ptr(P), _ptr(Pd), N, T, D, T,
+                 math.sqrt(D), 0.0, act, ctypes_stream())
+    _native.call("ghm_attn_ext_bwd_x3_act", _ptr(qkv_d), _ptr(P), _ptr(Pd), _ptr(dHm.to(DEV)), _ptr(dS), _ptr(dqkv),
+                 N, T, D, T, math.sqrt(D), 0.0, act, ctypes_stream())
+    torch.cuda.synchronize()
+    scale = lambda t: t.abs().max().item()  # noqa: E731
+    assert (Hm.cpu().view(N, T, D).double() - want.detach()).abs().max().item() <= 1e-4 * scale(want)
+    assert (P.cpu()[:, :T, :T].double() - A.detach()).abs().max().item() <= 1e-4 * scale(A)
+    assert P.cpu()[:, :T, T:].abs().max().item() == 0.0
+    got = dqkv.cpu().view(N, T, 3 * D).double()
+    for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
+        assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 2e-4 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
+
