@@ -262,11 +262,14 @@ int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, i
 /* ---- guided CLIP (clip_guide=True) ------------------------------------------
  * Exact BP_CLS messages of each sequence's GHM tree (data_random_GHM.py:185-208,
  * guided_info :526-549) from its leaves: trans = [L][C][V][V] f64 templates
- * (parent value, child value); msgs = [n_seq][n_total][V] f32 with
+ * (parent value, child value) of a translation-invariant tree (per_edge 0), or
+ * (per_edge 1) every edge's matrix, layer by layer: [sum_l C^(l+1)][V][V], layer
+ * l's edges in child order (parent * C + slot; GenTransition(translation_invariance=
+ * False), data_random_GHM.py:43-89); msgs = [n_seq][n_total][V] f32 with
  * n_total = (C^L - 1)/(C - 1), levels in guided-target order (depth L-1 first,
  * root last), log-domain, max-shifted per node. */
 int ghm_bp_cls(const double* trans, const uint8_t* tokens, float* msgs, int64_t n_seq, int L, int C, int V,
-               void* stream);
+               int per_edge, void* stream);
 /* part[n] = sum_{t,c<V} (H[n,t,c] - msgs[n][node_level(t)][c])^2 for guided target
  * `level` (model.py:790-800, 909-924); H is a [n_seq*T][128] residual stream. */
 int ghm_guide_fwd(const float* H, const float* msgs, float* part, int64_t n_seq, int L, int C, int V, int level,
@@ -331,13 +334,14 @@ int ghm_cdm_embed_joint_fwd(const float* z, const uint8_t* tok, const float* t_e
                             int64_t n_seq, int T, int T_img, int V, int D, void* stream);
 /* Exact BP, f64, one workgroup per sample: the text tree's BP_CLS root message
  * (data_random_GHM.py:185-208) conditions BP_DNS of the image tree (:467-523,
- * external message :875-877).  trans: [L][C][V][V] templates; t_tokens uint8
+ * external message :875-877).  trans: [L][C][V][V] templates, or per-edge tables
+ * as ghm_bp_cls (per_edge bit 0: the text tree, bit 1: the image tree); t_tokens uint8
  * [n_seq][C_t^L_t]; z f64 [n_seq][C_i^L_i] noisy observations.  Writes the
  * posterior means post (f32, the "Compare" target, train_sequential_DNS.py:145)
  * and z32 = (float)z, the model input (torch.tensor(noise, float32), :882). */
 int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
                double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i, int V,
-               void* stream);
+               int per_edge, void* stream);
 /* As ghm_bp_dns, and also the image tree's messages for the guided CDM
  * (data_random_GHM.py:551-592): msgs f32 [n_seq][3][n_nodes][V], planes hd, qd,
  * bu; n_nodes = non-root nodes + 1; depth d (1..L_i) nodes breadth-first from
@@ -345,7 +349,7 @@ int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_to
  * plane holds bu, as the reference's in-place `+=` aliases them, :501-504). */
 int ghm_bp_dns_msgs(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
                     double sigma, float* post, float* z32, float* msgs, int64_t n_seq, int L_t, int C_t, int L_i,
-                    int C_i, int V, void* stream);
+                    int C_i, int V, int per_edge, void* stream);
 /* pred[n, t] = H[n, t, :] . w_ro + b_ro for t < T_img (_read_out Linear(128, 1),
  * model.py:527-531).  H [n_seq][T][128]. */
 int ghm_cdm_readout_fwd(const float* H, const float* w_ro, const float* b_ro, float* pred, int64_t n_seq, int T,

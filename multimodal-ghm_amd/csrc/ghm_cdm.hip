@@ -113,7 +113,9 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
                                                const uint8_t* __restrict__ t_tok, const double* __restrict__ z,
                                                double sigma, float* __restrict__ post, float* __restrict__ z32,
                                                float* __restrict__ msgs, int n_nodes,
-                                               int Lt, int Ct, int Tt, int Li, int Ci, int Ti, int V) {
+                                               int Lt, int Ct, int Tt, int Li, int Ci, int Ti, int V,
+                                               int per_edge) {
+  const int pe_t = per_edge & 1, pe_i = (per_edge >> 1) & 1;
   __shared__ double hd[DNS_MAXNODES * DNS_MAXV];
   __shared__ double qd[DNS_MAXNODES * DNS_MAXV];
   __shared__ double bu_a[DNS_MAXLEAF * DNS_MAXV];
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
       for (int c = 0; c < Ct; ++c) {
         int xv = x[node * Ct + c];
         xv = xv < V ? xv : V - 1;
-        s += log(t_trans[((Lt - 1) * Ct + c) * V * V + v * V + xv]);
+        s += log(bp_edge(t_trans, Lt - 1, node * Ct + c, Ct, V, pe_t)[v * V + xv]);
       }
       cur[e] = s;
     }
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
         const int node = e / V, v = e % V;
         double s = 0.0;
         for (int c = 0; c < Ct; ++c) {
-          const double* tr = t_trans + ((d - 1) * Ct + c) * V * V + v * V;
+          const double* tr = bp_edge(t_trans, d - 1, node * Ct + c, Ct, V, pe_t) + v * V;
           const double* ch = cur + (node * Ct + c) * V;
           double a = 0.0;
           for (int u = 0; u < V; ++u) a += tr[u] * exp(ch[u]);
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
   for (int d = Li, cnt = Ti; d >= 1; --d, cnt /= Ci) {
     for (int e = tid; e < cnt * V; e += 64) {
       const int node = e / V, v = e % V;
-      const double* tr = i_trans + ((d - 1) * Ci + node % Ci) * V * V + v * V;
+      const double* tr = bp_edge(i_trans, d - 1, node, Ci, V, pe_i) + v * V;
       const double* h = hd + (off[d] + node) * V;
       double a = 0.0;
       for (int u = 0; u < V; ++u) a += tr[u] * exp(h[u]);
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(64) void k_bp_dns(const double* __restrict__ t_tran
     nodes *= Ci;
     for (int e = tid; e < nodes * V; e += 64) {
       const int node = e / V, v = e % V;
-      const double* tr = i_trans + ((d - 1) * Ci + node % Ci) * V * V + v;  // column v
+      const double* tr = bp_edge(i_trans, d - 1, node, Ci, V, pe_i) + v;  // column v
       const double* par = bu + (node / Ci) * V;
       const double* q = qd + (off[d] + node) * V;
       double a = 0.0;
@@ -419,7 +421,7 @@ static int tree_leaves(int L, int C) {
 
 static int bp_dns_launch(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
                          double sigma, float* post, float* z32, float* msgs, int64_t n_seq, int L_t, int C_t, int L_i,
-                         int C_i, int V, void* stream) {
+                         int C_i, int V, int per_edge, void* stream) {
   GHM_CHECK(t_trans && i_trans && t_tokens && z && post && z32, "null pointer");
   GHM_CHECK(L_t >= 1 && C_t >= 2 && L_i >= 1 && L_i <= 6 && C_i >= 2 && V >= 2 && V <= DNS_MAXV && n_seq >= 1 &&
                 sigma > 0.0,
@@ -430,21 +432,23 @@ static int bp_dns_launch(const double* t_trans, const double* i_trans, const uin
   GHM_CHECK(Tt <= DNS_MAXLEAF && Tt / C_t <= DNS_MAXLEAF && Ti <= DNS_MAXLEAF && nonroot <= DNS_MAXNODES,
             "tree too large (leaves <= 96)");
   hipLaunchKernelGGL(k_bp_dns, dim3(static_cast<unsigned>(n_seq)), dim3(64), 0, ghm_stream(stream), t_trans, i_trans,
-                     t_tokens, z, sigma, post, z32, msgs, nonroot + 1, L_t, C_t, Tt, L_i, C_i, Ti, V);
+                     t_tokens, z, sigma, post, z32, msgs, nonroot + 1, L_t, C_t, Tt, L_i, C_i, Ti, V, per_edge);
   return ghm_launch_status();
 }
 
 extern "C" int ghm_bp_dns(const double* t_trans, const double* i_trans, const uint8_t* t_tokens, const double* z,
                           double sigma, float* post, float* z32, int64_t n_seq, int L_t, int C_t, int L_i, int C_i,
-                          int V, void* stream) {
-  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, nullptr, n_seq, L_t, C_t, L_i, C_i, V, stream);
+                          int V, int per_edge, void* stream) {
+  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, nullptr, n_seq, L_t, C_t, L_i, C_i, V,
+                       per_edge, stream);
 }
 
 extern "C" int ghm_bp_dns_msgs(const double* t_trans, const double* i_trans, const uint8_t* t_tokens,
                                const double* z, double sigma, float* post, float* z32, float* msgs, int64_t n_seq,
-                               int L_t, int C_t, int L_i, int C_i, int V, void* stream) {
+                               int L_t, int C_t, int L_i, int C_i, int V, int per_edge, void* stream) {
   GHM_CHECK(msgs, "null pointer");
-  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, msgs, n_seq, L_t, C_t, L_i, C_i, V, stream);
+  return bp_dns_launch(t_trans, i_trans, t_tokens, z, sigma, post, z32, msgs, n_seq, L_t, C_t, L_i, C_i, V,
+                       per_edge, stream);
 }
 
 extern "C" int ghm_cdm_readout_fwd(const float* H, const float* w_ro, const float* b_ro, float* pred, int64_t n_seq,

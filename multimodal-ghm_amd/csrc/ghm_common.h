@@ -25,6 +25,27 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// Transition matrix of a GHM tree edge for the device BP kernels: layer `layer`
+// (parent at depth layer, child at depth layer + 1), child = the child's index
+// among the C^(layer+1) nodes of its depth (breadth first: parent * C + slot).
+// per_edge 0: translation-invariant templates [L][C][V][V] (slot = child % C);
+// per_edge 1: every edge's own matrix, layer by layer ([sum_l C^(l+1)][V][V],
+// GenTransition(translation_invariance=False), data_random_GHM.py:43-89).
+__device__ __forceinline__ const double* bp_edge(const double* tr, int layer, int child, int C, int V, int per_edge) {
+  int64_t idx;
+  if (per_edge) {
+    int64_t off = 0, w = C;
+    for (int k = 0; k < layer; ++k) {
+      off += w;
+      w *= C;
+    }
+    idx = off + child;
+  } else {
+    idx = static_cast<int64_t>(layer) * C + child % C;
+  }
+  return tr + idx * V * V;
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll

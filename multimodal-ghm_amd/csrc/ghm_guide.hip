@@ -17,7 +17,7 @@ constexpr int BP_MAXN = 32;  // nodes at depth L-1 (T / C <= 96 / 3)
 // (depth L-1 first, root last), nodes in breadth-first order within a level.
 __global__ __launch_bounds__(64) void k_bp_cls(const double* __restrict__ trans, const uint8_t* __restrict__ tok,
                                                float* __restrict__ msgs, int L, int C, int V, int T,
-                                               int n_total) {
+                                               int n_total, int per_edge) {
   __shared__ double cur[BP_MAXN * BP_MAXV];
   __shared__ double nxt[BP_MAXN * BP_MAXV];
   const int n = blockIdx.x, tid = threadIdx.x;
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(64) void k_bp_cls(const double* __restrict__ trans,
     for (int c = 0; c < C; ++c) {
       int xv = x[node * C + c];
       xv = xv < V ? xv : V - 1;
-      s += log(trans[((L - 1) * C + c) * V * V + v * V + xv]);
+      s += log(bp_edge(trans, L - 1, node * C + c, C, V, per_edge)[v * V + xv]);
     }
     cur[e] = s;
   }
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(64) void k_bp_cls(const double* __restrict__ trans,
       const int node = e / V, v = e % V;
       double s = 0.0;
       for (int c = 0; c < C; ++c) {
-        const double* tr = trans + ((d - 1) * C + c) * V * V + v * V;
+        const double* tr = bp_edge(trans, d - 1, node * C + c, C, V, per_edge) + v * V;
         const double* ch = cur + (node * C + c) * V;
         double a = 0.0;
         for (int u = 0; u < V; ++u) a += tr[u] * exp(ch[u]);
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_guide_total(const float* __restrict__ p
 // C-ABI launchers
 // ---------------------------------------------------------------------------
 extern "C" int ghm_bp_cls(const double* trans, const uint8_t* tokens, float* msgs, int64_t n_seq, int L, int C,
-                          int V, void* stream) {
+                          int V, int per_edge, void* stream) {
   GHM_CHECK(trans && tokens && msgs, "null pointer");
   GHM_CHECK(L >= 1 && C >= 2 && V >= 2 && V <= BP_MAXV && n_seq >= 1, "shape");
   int T = 1, n_total = 0;
@@ -150,7 +150,7 @@ extern "C" int ghm_bp_cls(const double* trans, const uint8_t* tokens, float* msg
   }
   GHM_CHECK(T <= GHM_MAXT && T / C <= BP_MAXN, "tree too large (leaves <= 96)");
   hipLaunchKernelGGL(k_bp_cls, dim3(static_cast<unsigned>(n_seq)), dim3(64), 0, ghm_stream(stream), trans, tokens,
-                     msgs, L, C, V, T, n_total);
+                     msgs, L, C, V, T, n_total, per_edge);
   return ghm_launch_status();
 }
 

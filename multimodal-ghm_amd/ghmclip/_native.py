@@ -62,8 +62,8 @@ HIP_SIGNATURES = {
     "ghm_split_weights": [_p, _i, _p],
     "ghm_cdm_embed_fwd": [_p, _p, _i, _p, _p, _i64, _i, _i, _i, _i, _p],
     "ghm_cdm_embed_joint_fwd": [_p, _p, _p, _p, _p, _i64, _i, _i, _i, _i, _p],
-    "ghm_bp_dns": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _i64, _i, _i, _i, _i, _i, _p],
-    "ghm_bp_dns_msgs": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _p],
+    "ghm_bp_dns": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _i64, _i, _i, _i, _i, _i, _i, _p],
+    "ghm_bp_dns_msgs": [_p, _p, _p, _p, ctypes.c_double, _p, _p, _p, _i64, _i, _i, _i, _i, _i, _i, _p],
     "ghm_guide_blk_fwd": [_p, _i, _i, _i, _i, _p, _i64, _i64, _i, _i, _p, _i64, _p],
     "ghm_guide_blk_bwd": [_p, _i, _i, _i, _i, _p, _i64, _i64, _i, _i, _p, _f, _i64, _p],
     "ghm_guide_blks_fwd": [_p, _p, _p, _p, _i, _p, _i64, _p],
@@ -119,7 +119,7 @@ HIP_SIGNATURES = {
     "ghm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_attn_fwd_x3_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
     "ghm_attn_bwd_x3_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
-    "ghm_bp_cls": [_p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_bp_cls": [_p, _p, _p, _i64, _i, _i, _i, _i, _p],
     "ghm_guide_fwd": [_p, _p, _p, _i64, _i, _i, _i, _i, _p],
     "ghm_guide_bwd": [_p, _p, _p, _i64, _i, _i, _i, _i, _f, _p],
     "ghm_guide_total": [_p, _i, _i64, _f, _p, _p, _p, _p],

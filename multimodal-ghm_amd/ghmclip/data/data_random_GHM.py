@@ -64,6 +64,30 @@ def _templates(transition, n_child):
     return np.ascontiguousarray(out)
 
 
+class DeviceTree:
+    """A GHM tree's transition matrices as the device BP kernels take them
+    (ghm_bp_cls / ghm_bp_dns, include/ghm_hip.h): the per-(layer, child slot)
+    templates [L][C][V][V] of a translation-invariant tree (per_edge 0), or every
+    edge's own matrix layer by layer, [sum_l C^(l+1)][V][V] with layer l's edges in
+    child order (per_edge 1: GenTransition(translation_invariance=False),
+    data_random_GHM.py:43-89)."""
+
+    def __init__(self, trans, L, C, V, per_edge):
+        self.trans = np.ascontiguousarray(trans, dtype=np.float64)
+        self.L, self.C, self.V, self.per_edge = int(L), int(C), int(V), int(per_edge)
+
+    @classmethod
+    def of(cls, x):
+        """A DeviceTree from itself, a template array [L][C][V][V], or a list of
+        per-layer edge tables ([C^(l+1)][V][V] each)."""
+        if isinstance(x, DeviceTree):
+            return x
+        if isinstance(x, np.ndarray) and x.ndim == 4:
+            return cls(x, x.shape[0], x.shape[1], x.shape[2], 0)
+        layers = [np.asarray(t, dtype=np.float64) for t in x]
+        return cls(np.concatenate(layers, axis=0), len(layers), layers[0].shape[0], layers[0].shape[-1], 1)
+
+
 def _edge_tables(transition):
     """Per-layer edge matrices [n_child^(l+1), V, V] (layer l, edge parent*C +
     child: the reference's transition[l] list as an array)."""
@@ -73,7 +97,12 @@ def _edge_tables(transition):
 def _tables(tr):
     """BP input as per-layer edge tables: a template array [L, C, V, V] is
     expanded (node n of layer l uses template n % C), a list of per-layer edge
-    tables passes through."""
+    tables passes through, a DeviceTree is split back into either."""
+    if isinstance(tr, DeviceTree):
+        if not tr.per_edge:
+            return _tables(tr.trans)
+        cuts = np.cumsum([tr.C ** (l + 1) for l in range(tr.L)])[:-1]
+        return np.split(tr.trans, cuts)
     if isinstance(tr, np.ndarray) and tr.ndim == 4:
         L, C = tr.shape[0], tr.shape[1]
         return [np.tile(tr[l], (C ** l, 1, 1)) for l in range(L)]
@@ -214,14 +243,14 @@ def guided_targets(templ, leaves, device="cpu"):
     leaves = np.asarray(leaves)
     B, T = leaves.shape
     dev = torch.device(device)
-    if dev.type == "cuda" and isinstance(templ, np.ndarray) and templ.ndim == 4:
-        templ = np.ascontiguousarray(templ, dtype=np.float64)
-        L, C, V, _ = templ.shape
+    if dev.type == "cuda":
+        dt = DeviceTree.of(templ)
+        L, C, V = dt.L, dt.C, dt.V
         n_total = (C ** L - 1) // (C - 1)
         tok = torch.from_numpy(np.ascontiguousarray(leaves, dtype=np.uint8)).to(dev)
-        tr = torch.from_numpy(templ).to(dev)
+        tr = torch.from_numpy(dt.trans).to(dev)
         msgs = torch.empty(B, n_total, V, dtype=torch.float32, device=dev)
-        _native.call("ghm_bp_cls", tr.data_ptr(), tok.data_ptr(), msgs.data_ptr(), B, L, C, V,
+        _native.call("ghm_bp_cls", tr.data_ptr(), tok.data_ptr(), msgs.data_ptr(), B, L, C, V, dt.per_edge,
                      torch.cuda.current_stream().cuda_stream)
         out, off, nodes = [], 0, T // C
         for _ in range(L):
@@ -290,12 +319,12 @@ class DoubleSampler:
         return NativeClipSampler(self.t_tables, self.i_tables, self.variable_type, K)
 
     def device_templates(self, what="this path"):
-        """(text, image) templates for the device BP kernels; raises for
-        non-translation-invariant trees (their BP runs on the host)."""
-        if self.t_templ is None or self.i_templ is None:
-            raise NotImplementedError(f"{what} needs translation-invariant trees: its BP targets / posteriors "
-                                      "run on the device from per-child-slot templates")
-        return self.t_templ, self.i_templ
+        """(text, image) transitions for the device BP kernels: the per-child-slot
+        templates of a translation-invariant tree, else a DeviceTree of its
+        per-edge tables (`what` names the caller; kept for the signature)."""
+        t = self.t_templ if self.t_templ is not None else DeviceTree.of(self.t_tables)
+        i = self.i_templ if self.i_templ is not None else DeviceTree.of(self.i_tables)
+        return t, i
 
     def get_zeroshot_batch(self, batch_size=128, return_tree=False):
         """:670-683: text and image trees sharing one root per sample (the draw of

@@ -25,6 +25,7 @@ import ctypes
 import numpy as np
 import torch
 
+from ..data.data_random_GHM import DeviceTree
 from .. import _native
 from . import distributed
 from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan, cdm_guide_blocks
@@ -101,13 +102,14 @@ class CdmTrainer:
                 self.clip_plan.split_weights(self.clip_p)  # frozen: split once
             self.t_tok = self.clip_plan.tokens
             n_text = clip_model.n_token
-        t_templ = np.ascontiguousarray(t_templ, dtype=np.float64)
-        i_templ = np.ascontiguousarray(i_templ, dtype=np.float64)
-        if i_templ.shape[1] ** i_templ.shape[0] != Ti or t_templ.shape[1] ** t_templ.shape[0] != n_text:
+        # templates [L][C][V][V], or per-edge tables of non-translation-invariant trees
+        tt, it = DeviceTree.of(t_templ), DeviceTree.of(i_templ)
+        if it.C ** it.L != Ti or tt.C ** tt.L != n_text:
             raise ValueError("transition templates do not match the token counts")
-        self.tree = (t_templ.shape[0], t_templ.shape[1], i_templ.shape[0], i_templ.shape[1], t_templ.shape[2])
-        self.t_trans = torch.from_numpy(t_templ).to(self.device)
-        self.i_trans = torch.from_numpy(i_templ).to(self.device)
+        self.tree = (tt.L, tt.C, it.L, it.C, tt.V)
+        self.per_edge = tt.per_edge | (it.per_edge << 1)  # ghm_bp_dns: bit 0 text, bit 1 image
+        self.t_trans = torch.from_numpy(tt.trans).to(self.device)
+        self.i_trans = torch.from_numpy(it.trans).to(self.device)
         # staged inputs (text leaves live in the CLIP plan's token buffer)
         self.i_tok = torch.empty(batch_size, Ti, dtype=torch.uint8, device=self.device)
         self.z64 = torch.empty(batch_size, Ti, dtype=torch.float64, device=self.device)
@@ -230,13 +232,14 @@ class CdmTrainer:
             ss = ctypes.c_void_p(side.cuda_stream)
             if self.guide:
                 _native.call("ghm_bp_dns_msgs", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
-                             self.sigma, _p(self.post), _p(self.z32), _p(self.imsgs), self.B, Lt, Ct, Li, Ci, V, ss)
+                             self.sigma, _p(self.post), _p(self.z32), _p(self.imsgs), self.B, Lt, Ct, Li, Ci, V,
+                             self.per_edge, ss)
                 if self.joint:  # (the sequential model's text blocks target the CLIP feature)
                     _native.call("ghm_bp_cls", _p(self.t_trans), _p(self.t_tok), _p(self.tmsgs), self.B, Lt, Ct, V,
-                                 ss)
+                                 self.per_edge & 1, ss)
             else:
                 _native.call("ghm_bp_dns", _p(self.t_trans), _p(self.i_trans), _p(self.t_tok), _p(self.z64),
-                             self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V, ss)
+                             self.sigma, _p(self.post), _p(self.z32), self.B, Lt, Ct, Li, Ci, V, self.per_edge, ss)
         emb = None if self.joint else self.clip_plan.forward(self.clip_p, split=False)  # train_sequential_DNS.py:141
         main.wait_stream(side)
         s = ctypes.c_void_p(main.cuda_stream)

@@ -24,6 +24,7 @@ import torch
 
 from .. import _native
 from . import distributed
+from ..data.data_random_GHM import DeviceTree
 from ..models.hip_encoder import EncoderPlan, default_precision, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
@@ -195,8 +196,8 @@ class ClipTrainer:
         self.penalty = float(penalty)
         self.glayers, self.gtrans, self.gmsgs, self.gtree = [], [], [], []
         for m, tr in zip(self.models, guide_trans):
-            tr = np.ascontiguousarray(tr, dtype=np.float64)
-            L, C, V = tr.shape[0], tr.shape[1], tr.shape[2]
+            dt = DeviceTree.of(tr)  # templates, or per-edge tables (non-translation-invariant trees)
+            tr, L, C, V = dt.trans, dt.L, dt.C, dt.V
             if C ** L != m.n_token or V != m.vocab_size:
                 raise ValueError("guide transitions do not match the encoder's token count / vocabulary")
             layers = [l for l, f in enumerate(m.guided_layer_flag) if f]
@@ -204,7 +205,7 @@ class ClipTrainer:
                 raise ValueError("more guided layers than tree levels")
             n_total = (C ** L - 1) // (C - 1)
             self.glayers.append(layers)
-            self.gtree.append((L, C, V))
+            self.gtree.append((L, C, V, dt.per_edge))
             self.gtrans.append(torch.from_numpy(tr).to(self.device))
             self.gmsgs.append(torch.zeros(self.n_seq, n_total, V, dtype=torch.float32, device=self.device))
         self.n_gparts = sum(len(x) for x in self.glayers)
@@ -214,11 +215,11 @@ class ClipTrainer:
     def _guide_fwd(self, tower, s):
         """BP guide targets from the staged tokens, then the penalty partials of
         the tower's guided layers (after its forward)."""
-        L, C, V = self.gtree[tower]
+        L, C, V, per_edge = self.gtree[tower]
         plan = self.plans[tower]
         base = sum(len(x) for x in self.glayers[:tower])
         _native.call("ghm_bp_cls", _p(self.gtrans[tower]), _p(plan.tokens), _p(self.gmsgs[tower]), self.n_seq,
-                     L, C, V, s)
+                     L, C, V, per_edge, s)
         for k, l in enumerate(self.glayers[tower]):
             _native.call("ghm_guide_fwd", _p(plan.H[l + 1]), _p(self.gmsgs[tower]), _p(self.gpart[base + k]),
                          self.n_seq, L, C, V, k, s)
@@ -227,7 +228,7 @@ class ClipTrainer:
         """{layer: fn(dH, stream)} adding d(penalty)/dH_{l+1} = 2 p (H - target) / N."""
         if not self.guide:
             return None
-        L, C, V = self.gtree[tower]
+        L, C, V, _ = self.gtree[tower]
         plan = self.plans[tower]
         msgs = self.gmsgs[tower]
         scale = 2.0 * self.penalty / self.n_seq

@@ -27,6 +27,8 @@ guide_bp.npz        get_batch(guide=True) at B=8 (p=0.2) after seed_everything(2
 guide_tiny.npz      guided CLIP (clip_guide=True, exp_clip_guidedTF.sh: lr 1e-3 -> 1e-6,
                     penalty 1e-3) at L=5, d=16, B=4 for 2 steps: loss, loss_nop, penalty,
                     raw grads, weights after each step.
+guide_nonti_tiny.npz  the same on --translation_invariance=False trees (--only
+                    guide_nonti_tiny), plus every edge's transition matrix of both trees.
 guide_curve.npz     the guided default config (L=5, d=128, B=128) ploss/loss history
                     for the first --guide-steps steps.
 
@@ -65,9 +67,9 @@ from ghmclip.data.data_random_GHM import ClipSampler  # noqa: E402
 P_Y = np.ones(10) / 10
 
 
-def make_sampler(p, seedtree=42, K=4):
+def make_sampler(p, seedtree=42, K=4, ti=True):
     return ClipSampler([4, 4], [3, 3], [P_Y, P_Y], [p, p], K=K, flip_scale=1,
-                       variable_type=10, translation_invariance=True, seedtree=seedtree)
+                       variable_type=10, translation_invariance=ti, seedtree=seedtree)
 
 
 def distinct_transitions(trans):
@@ -232,9 +234,10 @@ def guide_bp_fixture(B=8, p=0.2):
 
 
 def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, penalty=1e-3,
-                       lr_max=1e-3, lr_min=1e-6):
-    """train_CLIP.py:83-167 with clip_guide=True (exp_clip_guidedTF.sh)."""
-    s = make_sampler(p)
+                       lr_max=1e-3, lr_min=1e-6, ti=True):
+    """train_CLIP.py:83-167 with clip_guide=True (exp_clip_guidedTF.sh); ti=False:
+    --translation_invariance=False trees (one transition matrix per edge)."""
+    s = make_sampler(p, ti=ti)
     seed_everything(224)
     tm, im = build_guided(81, L, d)
     loss = GuidedClipLoss(4, B, penalty=penalty, guide=True)
@@ -268,6 +271,9 @@ def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, 
         out.update({f"s{it}.post.{k}": v for k, v in flat_state(im, "i").items()})
     out["meta"] = np.array([L, d, B, nsteps, total_iters], dtype=np.int64)
     out["hyper"] = np.array([p, penalty, lr_max, lr_min])
+    if not ti:
+        out["t_edges"] = np.concatenate([np.stack(layer) for layer in s.t_transition])
+        out["i_edges"] = np.concatenate([np.stack(layer) for layer in s.i_transition])
     np.savez_compressed(os.path.join(HERE, name), **out)
     print("wrote", name)
 
@@ -349,5 +355,7 @@ if __name__ == "__main__":
         guide_bp_fixture()
     if "guide_tiny" in jobs:
         guide_step_fixture("guide_tiny.npz")
+    if "guide_nonti_tiny" in jobs:
+        guide_step_fixture("guide_nonti_tiny.npz", ti=False)
     if "guide_curve" in jobs:
         guide_curve_fixture(a.guide_steps, out=a.guide_out)

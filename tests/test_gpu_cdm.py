@@ -66,10 +66,53 @@ def test_bp_dns_kernel_matches_reference():
         tok = torch.from_numpy(tl).to(DEV)  # held: the launch is asynchronous
         zd = torch.from_numpy(z).to(DEV)
         _native.call("ghm_bp_dns", tt.data_ptr(), it.data_ptr(), tok.data_ptr(), zd.data_ptr(), 1.0,
-                     post.data_ptr(), z32.data_ptr(), B, 4, 3, 4, 3, 10, torch.cuda.current_stream().cuda_stream)
+                     post.data_ptr(), z32.data_ptr(), B, 4, 3, 4, 3, 10, 0, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         np.testing.assert_allclose(post.cpu().numpy(), f["post"][k], rtol=0, atol=2e-6)
         np.testing.assert_array_equal(z32.cpu().numpy(), f["z"][k])
+
+
+def test_bp_dns_kernel_per_edge_matches_reference():
+    """ghm_bp_dns / ghm_bp_dns_msgs / ghm_bp_cls on per-edge tables (per_edge 3:
+    --translation_invariance=False text and image trees) == the reference's
+    posterior_mean_DNS and its text / image guided_info (cdm_nonti.npz)."""
+    from ghmclip import _native
+    g = np.load(os.path.join(GOLDEN, "cdm_nonti.npz"))
+    B, V, L, C, T = int(g["B"]), 10, 4, 3, 81
+    n_nodes = sum(C ** d for d in range(1, L + 1)) + 1
+    ss = torch.cuda.current_stream().cuda_stream
+    tt = torch.from_numpy(np.ascontiguousarray(g["t_edges"])).to(DEV)
+    it = torch.from_numpy(np.ascontiguousarray(g["i_edges"])).to(DEV)
+    tok = torch.from_numpy(np.ascontiguousarray(g["t_leaves"])).to(DEV)
+    zd = torch.from_numpy(np.ascontiguousarray(g["z"])).to(DEV)
+    post = torch.empty(B, T, dtype=torch.float32, device=DEV)
+    z32 = torch.empty_like(post)
+    _native.call("ghm_bp_dns", tt.data_ptr(), it.data_ptr(), tok.data_ptr(), zd.data_ptr(), 1.0,
+                 post.data_ptr(), z32.data_ptr(), B, L, C, L, C, V, 3, ss)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(post.cpu().numpy(), g["post"], rtol=0, atol=2e-6)
+    post2 = torch.empty_like(post)
+    imsgs = torch.empty(B, 3, n_nodes, V, dtype=torch.float32, device=DEV)
+    tmsgs = torch.empty(B, (C ** L - 1) // (C - 1), V, dtype=torch.float32, device=DEV)
+    _native.call("ghm_bp_dns_msgs", tt.data_ptr(), it.data_ptr(), tok.data_ptr(), zd.data_ptr(), 1.0,
+                 post2.data_ptr(), z32.data_ptr(), imsgs.data_ptr(), B, L, C, L, C, V, 3, ss)
+    _native.call("ghm_bp_cls", tt.data_ptr(), tok.data_ptr(), tmsgs.data_ptr(), B, L, C, V, 1, ss)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(post2, post, rtol=0, atol=0)
+    im = imsgs.cpu().numpy()
+    node0 = lambda d: n_nodes - 1 if d == 0 else sum(C ** e for e in range(1, d))  # noqa: E731
+    for k in range(2 * L + 1):  # downward depth L..1, the root (hd, bu), upward depth 1..L (hd, qd, bu)
+        depth = L - k if k <= L else k - L
+        planes = (0, 1) if k < L else (0, 2) if k == L else (0, 1, 2)
+        n0, nn = node0(depth), C ** depth
+        got = np.concatenate([im[:, pl, n0:n0 + nn] for pl in planes], axis=2)
+        np.testing.assert_allclose(got, g[f"image{k}"], rtol=1e-6, atol=2e-5, err_msg=f"image level {k}")
+    tm, off = tmsgs.cpu().numpy(), 0
+    for k in range(L):
+        want = g[f"text{k}"]
+        np.testing.assert_allclose(tm[:, off:off + want.shape[1]], want, rtol=1e-6, atol=1e-6,
+                                   err_msg=f"text level {k}")
+        off += want.shape[1]
 
 
 def _pair(L=2, seed=11, precision="f32", activation="softmax"):

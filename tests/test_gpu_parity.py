@@ -479,7 +479,7 @@ def test_bp_cls_kernel_matches_reference():
         leaves = torch.from_numpy(np.ascontiguousarray(g[f"{pref}_leaves"])).to(DEV)  # stored Fortran-order
         N = leaves.shape[0]
         msgs = torch.empty(N, 40, 10, dtype=torch.float32, device=DEV)
-        _native.call("ghm_bp_cls", trans.data_ptr(), leaves.data_ptr(), msgs.data_ptr(), N, 4, 3, 10,
+        _native.call("ghm_bp_cls", trans.data_ptr(), leaves.data_ptr(), msgs.data_ptr(), N, 4, 3, 10, 0,
                      torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         off = 0
@@ -488,6 +488,69 @@ def test_bp_cls_kernel_matches_reference():
             got = msgs[:, off:off + want.shape[1]].cpu().numpy()
             np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-6)
             off += want.shape[1]
+
+
+def test_bp_cls_kernel_per_edge_matches_reference():
+    """ghm_bp_cls on per-edge tables (per_edge 1: --translation_invariance=False
+    trees, unequal text 4x3 / image 3x2) == the reference's guided_info
+    (clip_nonti_guide.npz)."""
+    from ghmclip import _native
+    g = np.load(os.path.join(GOLDEN, "clip_nonti_guide.npz"))
+    for pref, L, C in (("t", 4, 3), ("i", 3, 2)):
+        trans = torch.from_numpy(np.ascontiguousarray(g[f"{pref}_edges"])).to(DEV)
+        assert trans.shape[0] == sum(C ** (l + 1) for l in range(L))
+        leaves = torch.from_numpy(np.ascontiguousarray(g[f"{pref}_leaves"])).to(DEV)
+        N = leaves.shape[0]
+        n_total = (C ** L - 1) // (C - 1)
+        msgs = torch.empty(N, n_total, 10, dtype=torch.float32, device=DEV)
+        _native.call("ghm_bp_cls", trans.data_ptr(), leaves.data_ptr(), msgs.data_ptr(), N, L, C, 10, 1,
+                     torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        off = 0
+        for k in range(L):
+            want = g[f"{pref}_msg{k}"]
+            got = msgs[:, off:off + want.shape[1]].cpu().numpy()
+            np.testing.assert_allclose(got, want, rtol=1e-6, atol=1e-6, err_msg=f"{pref} level {k}")
+            off += want.shape[1]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_guided_nonti_steps_vs_reference(precision):
+    """Guided CLIP on --translation_invariance=False trees: the fused step with
+    per-edge on-device BP targets == the reference's own two steps
+    (guide_nonti_tiny.npz: losses, penalty and raw gradients)."""
+    from ghmclip import ClipSampler, EncoderTransformer, get_lr_cosine_schedule, seed_everything
+    from ghmclip.training.clip_trainer import ClipTrainer
+    g = np.load(os.path.join(GOLDEN, "guide_nonti_tiny.npz"))
+    L, d, B, nsteps, total = [int(x) for x in g["meta"]]
+    p, penalty, lr_max, lr_min = [float(x) for x in g["hyper"]]
+    p_y = np.ones(10) / 10
+    sampler = ClipSampler([4, 4], [3, 3], [p_y, p_y], [p, p], K=4, translation_invariance=False, seedtree=42)
+    tt, it_ = sampler.device_templates("guided CLIP")
+    assert tt.per_edge == 1 and it_.per_edge == 1
+    np.testing.assert_array_equal(tt.trans, g["t_edges"])
+    np.testing.assert_array_equal(it_.trans, g["i_edges"])
+    seed_everything(224)
+    mk = lambda: EncoderTransformer(81, 10, d, L, n_guided_layer=4, guide=True)  # noqa: E731
+    tm, im = mk(), mk()
+    for pref, m in (("t", tm), ("i", im)):
+        for k, v in m.state_dict().items():
+            np.testing.assert_array_equal(v.numpy(), g[f"init.{pref}.{k}"])
+    tm, im = tm.to(DEV), im.to(DEV)
+    sched = [get_lr_cosine_schedule(s, lr_max, lr_min, 0, total) for s in range(total + 1)]
+    tr = ClipTrainer(tm, im, 4, B, sched, device=DEV, precision=precision, penalty=penalty,
+                     guide_trans=(tt, it_))
+    for it in range(nsteps):
+        tr.set_tokens(torch.from_numpy(g[f"s{it}.t_leaves"]), torch.from_numpy(g[f"s{it}.i_leaves"]))
+        tr.step()
+        torch.cuda.synchronize()
+        assert abs(tr.loss_history()[it] - float(g[f"s{it}.loss_nop"])) < 1e-5
+        ploss = float(g[f"s{it}.loss"])
+        assert abs(tr.ploss_history()[it] - ploss) <= 1e-5 * abs(ploss)
+        for pref, m in (("t", tm), ("i", im)):  # raw gradients (the fixture's are stored before clipping)
+            for k, prm in m.named_parameters():
+                want = torch.from_numpy(g[f"s{it}.grad.{pref}.{k}"])
+                assert _rel(prm.grad, want) < GRAD_TOL[precision], f"step {it} grad {pref}.{k}"
 
 
 def _guided_trainer(L, B, precision, total_iters=3000):

@@ -37,11 +37,24 @@ def test_clip_sampler_nonti_unequal_trees_bit_exact():
     np.testing.assert_allclose([m, se], g["bayes"], rtol=1e-12)
 
 
-def test_device_paths_refuse_nonti_templates():
+def test_device_tree_nonti_per_edge_tables():
+    """device_templates of a non-invariant tree: every edge's matrix, layer by
+    layer in child order (the per_edge layout of ghm_bp_cls / ghm_bp_dns), and
+    host BP on it == host BP on the reference's transition lists."""
     from ghmclip import ClipSampler
-    s = ClipSampler([2, 2], [3, 3], [P_Y, P_Y], [0.3, 0.3], K=4, translation_invariance=False, seedtree=42)
-    with pytest.raises(NotImplementedError):
-        s.device_templates("guided CLIP")
+    from ghmclip.data.data_random_GHM import DeviceTree, _bp_levels
+    s = ClipSampler([2, 3], [3, 2], [P_Y, P_Y], [0.3, 0.3], K=4, translation_invariance=False, seedtree=42)
+    t, i = s.device_templates("guided CLIP")
+    assert isinstance(t, DeviceTree) and t.per_edge == 1 and (t.L, t.C, t.V) == (2, 3, 10)
+    assert isinstance(i, DeviceTree) and i.per_edge == 1 and (i.L, i.C, i.V) == (3, 2, 10)
+    assert t.trans.shape == (3 + 9, 10, 10) and i.trans.shape == (2 + 4 + 8, 10, 10)
+    np.testing.assert_array_equal(t.trans, _edges(s.t_transition))
+    leaves = np.random.default_rng(0).integers(0, 10, size=(5, 8))
+    for a, b in zip(_bp_levels(i, leaves), _bp_levels(s.i_transition, leaves)):
+        np.testing.assert_array_equal(a, b)
+    ti = ClipSampler([2, 2], [3, 3], [P_Y, P_Y], [0.3, 0.3], K=4, seedtree=42)
+    t0, _ = ti.device_templates()
+    assert DeviceTree.of(t0).per_edge == 0 and t0.shape == (2, 3, 10, 10)
 
 
 def test_nwp_nonti_guided_batch_matches_reference():
@@ -89,3 +102,30 @@ def test_nwp_pipeline_nonti_matches_sampler():
         np.testing.assert_array_equal(gt.numpy(), vlm_guide_planes(tg, ig, 10))
     finally:
         pipe.close()
+
+
+def _tree(edges, L, C):
+    from ghmclip.data.data_random_GHM import DeviceTree
+    return DeviceTree(edges, L, C, edges.shape[-1], 1)
+
+
+def test_guided_targets_nonti_host_matches_reference():
+    """Host BP_CLS guided targets on per-edge tables == GHMTree.guided_info of the
+    reference's non-invariant trees (clip_nonti_guide.npz)."""
+    from ghmclip.data.data_random_GHM import guided_targets
+    g = np.load(os.path.join(GOLDEN, "clip_nonti_guide.npz"))
+    for pref, L, C in (("t", 4, 3), ("i", 3, 2)):
+        got = guided_targets(_tree(g[f"{pref}_edges"], L, C), g[f"{pref}_leaves"])
+        assert len(got) == L
+        for k, m in enumerate(got):
+            np.testing.assert_allclose(m.numpy()[:, ::C ** (k + 1)], g[f"{pref}_msg{k}"], rtol=1e-6, atol=1e-6)
+
+
+def test_bp_dns_nonti_host_matches_reference():
+    """Host BP_DNS posterior means on per-edge tables == the reference's
+    posterior_mean_DNS on a non-invariant tree (cdm_nonti.npz)."""
+    from ghmclip.data.data_random_GHM import _bp_levels, bp_dns_posterior
+    g = np.load(os.path.join(GOLDEN, "cdm_nonti.npz"))
+    ext = _bp_levels(_tree(g["t_edges"], 4, 3), g["t_leaves"])[-1][0]
+    post = bp_dns_posterior(_tree(g["i_edges"], 4, 3), g["z"].T, 1.0, ext)
+    np.testing.assert_allclose(post.T, g["post"], rtol=1e-12, atol=1e-12)
