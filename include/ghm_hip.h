@@ -121,6 +121,16 @@ int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float* stats, con
  * ghm_attn_fwd); dS: caller scratch [n_seq][96][96]  —  backward of model.py:778-782. */
 int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                  int64_t n_seq, int T, int D, float scale_div, void* stream);
+/* ghm_attn_fwd / ghm_attn_bwd with the attention activation of the reference's
+ * get_activation (models/model.py:121-130, applied at :781): act 0 softmax
+ * (identical to the plain entry points), 1 relu, 2 gelu (erf form) of the
+ * scaled scores, keys past T contributing 0.  P holds act(s); for gelu the
+ * forward also writes GELU'(s) to Pd (P's layout, required) and the backward
+ * reads it.  dS: caller scratch as in ghm_attn_bwd. */
+int ghm_attn_fwd_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq, int T,
+                     int D, float scale_div, int act, void* stream);
+int ghm_attn_bwd_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dS, float* dqkv,
+                     int64_t n_seq, int T, int D, float scale_div, int act, void* stream);
 
 /* QKV + LN1 backward: dH = dH_mid + dLN1(dqkv W); part_ln as in ghm_mlp_bwd
  * —  backward of model.py:772-775. */

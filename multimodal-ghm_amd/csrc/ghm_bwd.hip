@@ -206,13 +206,15 @@ __device__ __forceinline__ void stage_cols32_b(const float* __restrict__ base_ro
   }
 }
 
-template <int NKT>
+// ACT: dS = P (dP - rowsum(P dP)) / scale (softmax), [P > 0] dP / scale (relu),
+// GELU'(s) dP / scale (gelu, GELU' from the forward's Pd)
+template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q(const float* __restrict__ qkv,
                                                             const float* __restrict__ P,
                                                             const float* __restrict__ dHmid,
                                                             float* __restrict__ dS_out,
                                                             float* __restrict__ dqkv, int T,
-                                                            float scale_div) {
+                                                            float scale_div, const float* __restrict__ Pd = nullptr) {
   constexpr int TP = NKT * 32;
   __shared__ __attribute__((aligned(16))) float sbuf[TP * AK_PITCH];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
@@ -245,7 +247,8 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q(const float* __restr
     __syncthreads();
   }
   // P rows (dense, padded keys are 0); queries >= T contribute nothing
-  const float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
+  const int64_t poff = (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
+  const float* prow = (ACT == ACT_GELU ? Pd : P) + poff;  // gelu: the factor is GELU'(s)
   float delta = 0.f;
   f32x16 p[NKT];
 #pragma unroll
@@ -258,15 +261,24 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_bwd_q(const float* __restr
       p[kt][4 * qd + 2] = qv ? pv.z : 0.f;
       p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
     }
+    if (ACT == ACT_SOFTMAX) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+      for (int r = 0; r < 16; ++r) delta += p[kt][r] * dp[kt][r];
+    }
   }
-  delta += xhalf(delta);
-  float* srow = dS_out + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
+  if (ACT == ACT_SOFTMAX) delta += xhalf(delta);
+  float* srow = dS_out + poff;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dp[kt][r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+    for (int r = 0; r < 16; ++r) {
+      if (ACT == ACT_SOFTMAX)
+        dp[kt][r] = (p[kt][r] * (dp[kt][r] - delta)) / scale_div;
+      else if (ACT == ACT_RELU)
+        dp[kt][r] = (p[kt][r] > 0.f ? dp[kt][r] : 0.f) / scale_div;
+      else
+        dp[kt][r] = (p[kt][r] * dp[kt][r]) / scale_div;
+    }
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd)
       st4(srow + 32 * kt + quad_off(qd, h), dp[kt][4 * qd], dp[kt][4 * qd + 1], dp[kt][4 * qd + 2],
@@ -833,22 +845,42 @@ extern "C" int ghm_mlp_bwd(const float* dH_out, const float* H_mid, const float*
   return ghm_launch_status();
 }
 
+template <int ACT>
+static void attn_bwd_launch(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dS,
+                            float* dqkv, int64_t n_seq, int T, float scale_div, hipStream_t s) {
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (T <= 32) {
+    hipLaunchKernelGGL((k_attn_bwd_q<1, ACT>), dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div, Pd);
+    hipLaunchKernelGGL(k_attn_bwd_kv<1>, dim3(g), dim3(64), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else if (T <= 64) {
+    hipLaunchKernelGGL((k_attn_bwd_q<2, ACT>), dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div, Pd);
+    hipLaunchKernelGGL(k_attn_bwd_kv<2>, dim3(g), dim3(128), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  } else {
+    hipLaunchKernelGGL((k_attn_bwd_q<3, ACT>), dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div, Pd);
+    hipLaunchKernelGGL(k_attn_bwd_kv<3>, dim3(g), dim3(192), 0, s, qkv, P, dS, dH_mid, dqkv, T);
+  }
+}
+
 extern "C" int ghm_attn_bwd(const float* qkv, const float* P, const float* dH_mid, float* dS, float* dqkv,
                             int64_t n_seq, int T, int D, float scale_div, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
-  const unsigned g = static_cast<unsigned>(n_seq);
+  attn_bwd_launch<ACT_SOFTMAX>(qkv, P, nullptr, dH_mid, dS, dqkv, n_seq, T, scale_div, ghm_stream(stream));
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_bwd_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dS,
+                                float* dqkv, int64_t n_seq, int T, int D, float scale_div, int act, void* stream) {
+  GHM_CHECK(qkv && P && dH_mid && dS && dqkv && (act != ACT_GELU || Pd), "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  GHM_CHECK(act >= ACT_SOFTMAX && act <= ACT_GELU, "act: 0 softmax, 1 relu, 2 gelu");
   hipStream_t s = ghm_stream(stream);
-  if (T <= 32) {
-    hipLaunchKernelGGL(k_attn_bwd_q<1>, dim3(g), dim3(64), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
-    hipLaunchKernelGGL(k_attn_bwd_kv<1>, dim3(g), dim3(64), 0, s, qkv, P, dS, dH_mid, dqkv, T);
-  } else if (T <= 64) {
-    hipLaunchKernelGGL(k_attn_bwd_q<2>, dim3(g), dim3(128), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
-    hipLaunchKernelGGL(k_attn_bwd_kv<2>, dim3(g), dim3(128), 0, s, qkv, P, dS, dH_mid, dqkv, T);
-  } else {
-    hipLaunchKernelGGL(k_attn_bwd_q<3>, dim3(g), dim3(192), 0, s, qkv, P, dH_mid, dS, dqkv, T, scale_div);
-    hipLaunchKernelGGL(k_attn_bwd_kv<3>, dim3(g), dim3(192), 0, s, qkv, P, dS, dH_mid, dqkv, T);
-  }
+  if (act == ACT_SOFTMAX)
+    attn_bwd_launch<ACT_SOFTMAX>(qkv, P, Pd, dH_mid, dS, dqkv, n_seq, T, scale_div, s);
+  else if (act == ACT_RELU)
+    attn_bwd_launch<ACT_RELU>(qkv, P, Pd, dH_mid, dS, dqkv, n_seq, T, scale_div, s);
+  else
+    attn_bwd_launch<ACT_GELU>(qkv, P, Pd, dH_mid, dS, dqkv, n_seq, T, scale_div, s);
   return ghm_launch_status();
 }
 

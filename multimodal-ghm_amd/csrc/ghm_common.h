@@ -98,6 +98,10 @@ __device__ __forceinline__ void load64(const float* __restrict__ p, float* x) {
 __device__ __forceinline__ float gelu_f(float x) {
   return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
 }
+// attention activation (model.py:121-130 get_activation): the ACT template
+// parameter of the attention kernels and the `act` argument of their *_act entry points
+constexpr int ACT_SOFTMAX = 0, ACT_RELU = 1, ACT_GELU = 2;
+
 // GELU and its derivative from one erf evaluation (same formulas as torch's
 // forward and GeluBackward, approximate='none')
 __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& d) {

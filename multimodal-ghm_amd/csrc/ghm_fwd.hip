@@ -148,12 +148,15 @@ __device__ __forceinline__ void stage_cols32(const float* __restrict__ base_row,
   }
 }
 
-template <int NKT>
+// ACT (model.py:121-130, applied at :781): softmax, or the elementwise relu / gelu
+// of the scaled score (keys past T and padded queries 0; gelu also stores GELU'
+// of the score in Pd, P's layout, for the backward)
+template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restrict__ qkv,
                                                           const float* __restrict__ H,
                                                           float* __restrict__ Hmid,
                                                           float* __restrict__ P, int T,
-                                                          float scale_div) {
+                                                          float scale_div, float* __restrict__ Pd = nullptr) {
   constexpr int TP = NKT * 32;
   __shared__ __attribute__((aligned(16))) float sbuf[TP * AK_PITCH];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
@@ -185,33 +188,60 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
     }
     __syncthreads();
   }
-  // softmax over keys for query q (= this lane's column)
-  float mx = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = 32 * kt + acc_row(r, h);
-      const float v = key < T ? s[kt][r] / scale_div : -INFINITY;
-      s[kt][r] = v;
-      mx = fmaxf(mx, v);
-    }
-  }
-  mx = fmaxf(mx, xhalf(mx));
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = expf(s[kt][r] - mx);
-      s[kt][r] = e;
-      sum += e;
-    }
-  }
-  sum += xhalf(sum);
   // rows of padded queries (q >= T) are stored as 0: the key-block backward
   // kernel sums P over all 96 rows
-  const float inv = qv ? 1.f / sum : 0.f;
+  float inv;
+  if (ACT == ACT_SOFTMAX) {  // softmax over keys for query q (= this lane's column)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float v = key < T ? s[kt][r] / scale_div : -INFINITY;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, xhalf(mx));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = expf(s[kt][r] - mx);
+        s[kt][r] = e;
+        sum += e;
+      }
+    }
+    sum += xhalf(sum);
+    inv = qv ? 1.f / sum : 0.f;
+  } else {
+    inv = 1.f;
+    float* drow = ACT == ACT_GELU ? Pd + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P : nullptr;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      float dv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + acc_row(r, h);
+        const float x = s[kt][r] / scale_div;
+        float a, d = 0.f;
+        if (ACT == ACT_RELU)
+          a = fmaxf(x, 0.f);
+        else
+          gelu_and_grad(x, a, d);
+        const bool ok = key < T && qv;
+        s[kt][r] = ok ? a : 0.f;
+        dv[r] = ok ? d : 0.f;
+      }
+      if (ACT == ACT_GELU) {
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+          st4(drow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+      }
+    }
+  }
   float* prow = P + (static_cast<int64_t>(blockIdx.x) * AT_P + q) * AT_P;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
@@ -547,18 +577,38 @@ extern "C" int ghm_ln_qkv_fwd(const float* H, const float* ln_w, const float* ln
   return ghm_launch_status();
 }
 
+template <int ACT>
+static void attn_fwd_launch(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq,
+                            int T, float scale_div, hipStream_t s) {
+  const unsigned g = static_cast<unsigned>(n_seq);
+  if (T <= 32)
+    hipLaunchKernelGGL((k_attn_fwd<1, ACT>), dim3(g), dim3(64), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+  else if (T <= 64)
+    hipLaunchKernelGGL((k_attn_fwd<2, ACT>), dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+  else
+    hipLaunchKernelGGL((k_attn_fwd<3, ACT>), dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div, Pd);
+}
+
 extern "C" int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P,
                             int64_t n_seq, int T, int D, float scale_div, void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
   GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
-  const unsigned g = static_cast<unsigned>(n_seq);
+  attn_fwd_launch<ACT_SOFTMAX>(qkv, H, H_mid, P, nullptr, n_seq, T, scale_div, ghm_stream(stream));
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_attn_fwd_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq,
+                                int T, int D, float scale_div, int act, void* stream) {
+  GHM_CHECK(qkv && H && H_mid && P && (act != ACT_GELU || Pd), "null pointer");
+  GHM_CHECK(D == GHM_D && T >= 1 && T <= GHM_MAXT && n_seq >= 1, "shape (T <= 96, D == 128)");
+  GHM_CHECK(act >= ACT_SOFTMAX && act <= ACT_GELU, "act: 0 softmax, 1 relu, 2 gelu");
   hipStream_t s = ghm_stream(stream);
-  if (T <= 32)
-    hipLaunchKernelGGL(k_attn_fwd<1>, dim3(g), dim3(64), 0, s, qkv, H, H_mid, P, T, scale_div);
-  else if (T <= 64)
-    hipLaunchKernelGGL(k_attn_fwd<2>, dim3(g), dim3(128), 0, s, qkv, H, H_mid, P, T, scale_div);
+  if (act == ACT_SOFTMAX)
+    attn_fwd_launch<ACT_SOFTMAX>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
+  else if (act == ACT_RELU)
+    attn_fwd_launch<ACT_RELU>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
   else
-    hipLaunchKernelGGL(k_attn_fwd<3>, dim3(g), dim3(192), 0, s, qkv, H, H_mid, P, T, scale_div);
+    attn_fwd_launch<ACT_GELU>(qkv, H, H_mid, P, Pd, n_seq, T, scale_div, s);
   return ghm_launch_status();
 }
 

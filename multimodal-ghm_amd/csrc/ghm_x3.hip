@@ -1231,7 +1231,7 @@ __device__ __forceinline__ void rows_dot_half(const __bf16* ih, const __bf16* il
 // elementwise ACT_RELU / ACT_GELU of the scaled scores (no normalisation; keys
 // past T contribute 0).  The backward needs act'(s): relu' = [P > 0]; for gelu
 // the forward stores GELU'(s) beside P (Pd, same layout).
-constexpr int ACT_SOFTMAX = 0, ACT_RELU = 1, ACT_GELU = 2;
+// (ACT_SOFTMAX / ACT_RELU / ACT_GELU: ghm_common.h)
 
 template <int NKT, int ACT = ACT_SOFTMAX>
 __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd_x3(const float* __restrict__ qkv,

@@ -117,6 +117,8 @@ HIP_SIGNATURES = {
     "ghm_wgrad_x3": [_p, _i, _i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i64, _i, _p],
     "ghm_attn_fwd_x3": [_p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_attn_bwd_x3": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_attn_fwd_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
+    "ghm_attn_bwd_act": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
     "ghm_attn_fwd_x3_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
     "ghm_attn_bwd_x3_act": [_p, _p, _p, _p, _p, _i64, _i, _i, _f, _i, _p],
     "ghm_bp_cls": [_p, _p, _p, _i64, _i, _i, _i, _i, _p],

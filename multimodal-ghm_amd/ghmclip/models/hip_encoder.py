@@ -101,16 +101,14 @@ class EncoderPlan:
         self.long_attn = n_token > 96
         pad = 192 if self.long_attn else 96
         # attention activation (model.py:121-130): softmax, or elementwise relu / gelu
-        # on the split-bf16 attention kernels: the one-sequence ones up to 96 tokens
-        # (ghm_attn_{fwd,bwd}_x3_act, x3 plans), the multi-workgroup ones past 96
-        # (ghm_attn_ext_{fwd,bwd}_x3_act, which every precision's long attention uses)
+        # on every attention kernel: the one-sequence ones up to 96 tokens
+        # (ghm_attn_{fwd,bwd}_act exact f32, ghm_attn_{fwd,bwd}_x3_act split-bf16), the
+        # multi-workgroup ones past 96 (ghm_attn_ext_{fwd,bwd}_x3_act, which every
+        # precision's long attention uses)
         acts = {"softmax": 0, "relu": 1, "gelu": 2}
         if activation not in acts:
             raise NotImplementedError(f"attention activation {activation!r}")
         self.act = acts[activation]
-        if self.act and self.precision != "x3" and not self.long_attn:
-            raise NotImplementedError(f"attention activation {activation!r} runs on the split-bf16 (x3) kernels: "
-                                      f"precision 'x3' for sequences of <= 96 tokens")
         self.L, self.T, self.N, self.C, self.V = n_layer, n_token, n_seq, num_class, vocab
         self.M = M = n_seq * n_token
         self.eps = float(eps)
@@ -271,6 +269,9 @@ class EncoderPlan:
                 self._attn_fwd_f32(l)
             elif self.long_attn:
                 self._attn_ext_fwd(l, s)
+            elif self.act:
+                c("ghm_attn_fwd_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                  None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
             else:
                 c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   N, T, D_MODEL, self.scale_div, s)
@@ -492,10 +493,14 @@ class EncoderPlan:
                 self._attn_bwd_f32(l, cur)
             elif self.long_attn:
                 self._attn_ext_bwd(l, cur, s)
-            elif self.act:
+            elif self.act and x3:
                 c("ghm_attn_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
                   None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,
                   self.scale_div, self.act, s)
+            elif self.act:
+                c("ghm_attn_bwd_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
+                  None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
+                  D_MODEL, self.scale_div, self.act, s)
             else:
                 c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
                   _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)

@@ -27,8 +27,10 @@ guide_bp.npz        get_batch(guide=True) at B=8 (p=0.2) after seed_everything(2
 guide_tiny.npz      guided CLIP (clip_guide=True, exp_clip_guidedTF.sh: lr 1e-3 -> 1e-6,
                     penalty 1e-3) at L=5, d=16, B=4 for 2 steps: loss, loss_nop, penalty,
                     raw grads, weights after each step.
-guide_nonti_tiny.npz  the same on --translation_invariance=False trees (--only
-                    guide_nonti_tiny), plus every edge's transition matrix of both trees.
+guide_nonti_tiny.npz  the same at d=128 (the HIP encoder's width) on
+                    --translation_invariance=False trees (--only guide_nonti_tiny), with
+                    (sum, sum of squares, abs-max) checksums of the weight / gradient
+                    tensors, plus every edge's transition matrix of both trees.
 guide_curve.npz     the guided default config (L=5, d=128, B=128) ploss/loss history
                     for the first --guide-steps steps.
 
@@ -234,7 +236,7 @@ def guide_bp_fixture(B=8, p=0.2):
 
 
 def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, penalty=1e-3,
-                       lr_max=1e-3, lr_min=1e-6, ti=True):
+                       lr_max=1e-3, lr_min=1e-6, ti=True, checksum_only=False):
     """train_CLIP.py:83-167 with clip_guide=True (exp_clip_guidedTF.sh); ti=False:
     --translation_invariance=False trees (one transition matrix per edge)."""
     s = make_sampler(p, ti=ti)
@@ -271,6 +273,11 @@ def guide_step_fixture(name, L=5, d=16, B=4, nsteps=2, p=0.2, total_iters=3000, 
         out.update({f"s{it}.post.{k}": v for k, v in flat_state(im, "i").items()})
     out["meta"] = np.array([L, d, B, nsteps, total_iters], dtype=np.int64)
     out["hyper"] = np.array([p, penalty, lr_max, lr_min])
+    if checksum_only:  # as step_fixture: (sum, sum of squares, abs-max) of the big tensors
+        out = {k + ".cks" if (".grad." in k or k.startswith("init.") or ".post." in k) and v.size > 64 else k:
+               np.array([v.astype(np.float64).sum(), (v.astype(np.float64) ** 2).sum(), np.abs(v).max()])
+               if (".grad." in k or k.startswith("init.") or ".post." in k) and v.size > 64 else v
+               for k, v in out.items()}
     if not ti:
         out["t_edges"] = np.concatenate([np.stack(layer) for layer in s.t_transition])
         out["i_edges"] = np.concatenate([np.stack(layer) for layer in s.i_transition])
@@ -356,6 +363,6 @@ if __name__ == "__main__":
     if "guide_tiny" in jobs:
         guide_step_fixture("guide_tiny.npz")
     if "guide_nonti_tiny" in jobs:
-        guide_step_fixture("guide_nonti_tiny.npz", ti=False)
+        guide_step_fixture("guide_nonti_tiny.npz", d=128, ti=False, checksum_only=True)
     if "guide_curve" in jobs:
         guide_curve_fixture(a.guide_steps, out=a.guide_out)

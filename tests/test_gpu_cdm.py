@@ -177,6 +177,31 @@ def _trainer(L, B, precision, total_iters=30000):
     return s, bayes, tr
 
 
+def test_trainer_nonti_trees_bp_targets_match_reference():
+    """CdmTrainer on --translation_invariance=False trees (DeviceTree per-edge
+    tables from ConditionalDenoiseSampler.device_templates): the step's BP_DNS
+    targets == the reference's posterior means on its own draw (cdm_nonti.npz)."""
+    from ghmclip import ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, EncoderTransformer
+    from ghmclip import get_lr_cosine_schedule
+    from ghmclip.training.cdm_trainer import CdmTrainer
+    g = np.load(os.path.join(GOLDEN, "cdm_nonti.npz"))
+    B = int(g["B"])
+    s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1, translation_invariance=False)
+    tt, it = s.device_templates("the CDM trainer")
+    np.testing.assert_array_equal(tt.trans, g["t_edges"])
+    np.testing.assert_array_equal(it.trans, g["i_edges"])
+    clip = EncoderTransformer(81, 10, 128, 5).to(DEV)
+    model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 1, [1, 4], 4, 512, sequential=True).to(DEV)
+    sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, 100) for k in range(101)]
+    tr = CdmTrainer(model, clip, B, sched, tt, it, sigma=1.0, device=DEV)
+    assert tr.per_edge == 3
+    tr.set_batch(torch.from_numpy(g["t_leaves"]), torch.from_numpy(g["i_leaves"]), torch.from_numpy(g["z"]))
+    tr.step()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(tr.post.cpu().numpy(), g["post"], rtol=0, atol=2e-6)
+    assert np.isfinite(tr.loss_history()).all()
+
+
 def _run(s, tr, B, steps, graph_after=None):
     for k in range(steps):
         tl, _, z, il = s.draw_numpy(B)

@@ -362,3 +362,42 @@ def test_attention_ext_activation(T, act):
     for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
         assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 2e-4 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
 
+
+
+@pytest.mark.parametrize("T,act", [(81, 1), (81, 2), (40, 2), (17, 1)])
+def test_attention_f32_activation(T, act):
+    """ghm_attn_{fwd,bwd}_act (exact-f32 one-sequence kernels; the guided CLIP's
+    default precision under train_CLIP --clip_activation): relu / gelu of the
+    scaled scores, no row normalisation; P, the output and dq / dk / dv against
+    float64 autograd of model.py:778-782 with get_activation (:121-130)."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    N, D, pad = 5, 128, 96
+    g = torch.Generator().manual_seed(T + 10 * act)
+    qkv = torch.randn(N, T, 3 * D, generator=g) * 0.5
+    H = torch.randn(N, T, D, generator=g)
+    dHm = torch.randn(N, T, D, generator=g)
+    q64, k64, v64 = (qkv[..., i * D:(i + 1) * D].double().requires_grad_(True) for i in range(3))
+    S = (q64 @ k64.transpose(1, 2)) / math.sqrt(D)
+    A = torch.relu(S) if act == 1 else torch.nn.functional.gelu(S)
+    want = H.double() + A @ v64
+    (want * dHm.double()).sum().backward()
+    qkv_d = qkv.to(DEV)
+    Hm = torch.empty(N * T, D, device=DEV)
+    P = torch.zeros(N, pad, pad, device=DEV)
+    Pd = torch.zeros(N, pad, pad, device=DEV)
+    dS = torch.zeros(N, pad, pad, device=DEV)
+    dqkv = torch.empty(N * T, 3 * D, device=DEV)
+    _native.call("ghm_attn_fwd_act", _ptr(qkv_d), _ptr(H.to(DEV)), _ptr(Hm), _ptr(P), _ptr(Pd), N, T, D,
+                 math.sqrt(D), act, ctypes_stream())
+    _native.call("ghm_attn_bwd_act", _ptr(qkv_d), _ptr(P), _ptr(Pd), _ptr(dHm.to(DEV)), _ptr(dS), _ptr(dqkv),
+                 N, T, D, math.sqrt(D), act, ctypes_stream())
+    torch.cuda.synchronize()
+    scale = lambda t: t.abs().max().item()  # noqa: E731
+    # exact f32 products (k-ordered fmaf chains): f32-rounding-level bounds
+    assert (Hm.cpu().view(N, T, D).double() - want.detach()).abs().max().item() <= 5e-6 * scale(want)
+    assert (P.cpu()[:, :T, :T].double() - A.detach()).abs().max().item() <= 5e-6 * scale(A)
+    assert P.cpu()[:, :T, T:].abs().max().item() == 0.0 and P.cpu()[:, T:, :].abs().max().item() == 0.0
+    got = dqkv.cpu().view(N, T, 3 * D).double()
+    for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
+        assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 1e-5 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
