@@ -468,7 +468,7 @@ def final_risk(a, ws):
     CLIP run, exp_clip_{standard,guided}TF.sh at p = 0.2, total_iters = 3000, through
     the drop-in CLI code path (train_CLIP.run: RNG order sampler(42) -> get_Bayes ->
     seed(224) -> encoders; live native sampler in its producer thread + pinned
-    H2D, HIP-graph steps), global batch 128 split over the ranks (strong scaling,
+    H2D, the trainer's steps), global batch 128 split over the ranks (strong scaling,
     the same objective as one GPU).  final_risk = mean(loss_history[-100:])
     (figures/eval-clip-risk.py:29), against the published value
     (figures/data/ghm-data/clip-risk.json).  The run's loop time is the
@@ -507,7 +507,7 @@ def final_risk(a, ws):
             "live_sampler": {"steps": r["steps"], "seconds": round(loop, 3),
                              "ms_per_step": round(1000 * loop / r["steps"], 4),
                              "samples_per_s": round(128 * r["steps"] / loop, 1),
-                             "note": "train_CLIP loop: native sampler producer thread + pinned H2D + graph step + "
+                             "note": "train_CLIP loop: native sampler producer thread + pinned H2D + the step (eager issue) + "
                                      "the reference's log-line history sync every 20 steps"}}
 
 
@@ -607,6 +607,7 @@ def main():
     kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
     risk = None if a.no_final_risk else final_risk(a, ws)
     rc = tr.precision == "x3"
+    graphed = tr.graphs is not None
     del ring, tr
     if rank != 0:
         teardown()
@@ -694,7 +695,7 @@ def main():
                    + (" + on-device BP guide targets and penalty on 4 layers" if a.guide else ""),
                    "batch_rows_per_rank": a.batch, "sequences_per_encoder_per_rank": a.batch * 5,
                    "global_batch_rows": a.global_batch, "n_layer": a.layers, "parallelism": f"dp{ws}",
-                   "hip_graph": not a.no_graph},
+                   "hip_graph": graphed},
         "roofline": roofline,
         "steps_per_s": round(steps_per_s, 3),
         "sequences_per_s": round(samples * 10 / elapsed, 1),
@@ -790,7 +791,7 @@ def main_cdm(a, ws, rank):
                                 f"CLIP text EncoderTransformer(L=5) forward + on-device BP_DNS compare, "
                                 f"fwd+bwd+clip+AdamW"),
                    "batch_rows_per_rank": a.batch, "global_batch_rows": a.batch * ws, "n_layer": L,
-                   "parallelism": f"dp{ws}", "hip_graph": not a.no_graph},
+                   "parallelism": f"dp{ws}", "hip_graph": tr.graphs is not None},
         "roofline": {"bound": "hbm", "kernel": f"{kname} (LN2+MLP fwd, one CDM layer, M={M})",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": mlp_bytes,
@@ -873,7 +874,7 @@ def main_vlm(a, ws, rank):
                                 f"+ frozen CLIP image EncoderTransformer(L=5) forward, CE + KL compare, "
                                 f"fwd+bwd+clip+AdamW"),
                    "batch_rows_per_rank": a.batch, "global_batch_rows": a.batch * ws, "n_layer": L,
-                   "parallelism": f"dp{ws}", "hip_graph": not a.no_graph},
+                   "parallelism": f"dp{ws}", "hip_graph": tr.graphs is not None},
         "roofline": roofline,
         "step_tflops": round(step_gflop * ws * a.steps / elapsed / 1e3, 2),
         "loss_finite": bool(np.isfinite(losses).all()),

@@ -425,7 +425,12 @@ class ClipTrainer:
                 self._order(st, self.comm, ("early", t))
                 with torch.cuda.stream(self.comm):
                     self._single(self.plans[t].flush_pending, graphs, ("flush", t))
-            self._phase(self._bwd_b_gen, graphs, "bwd_b", fork=False)
+            # one join on the main stream's path: the comm stream (its early
+            # reductions long done) waits for the side tower, the main stream for
+            # the comm stream -- instead of two waits in series on the main stream
+            self._phase(self._bwd_b_gen, graphs, "bwd_b", fork=False, join=False)
+            _, _, s1 = self._tower_streams()
+            self._order(s1, self.comm, "side_join")
             self._order(self.comm, torch.cuda.current_stream(), "early_join")
         elif not dp:
             self._phase(self._bwd_gen, graphs, "bwd", fork=False)
@@ -560,10 +565,16 @@ class ClipTrainer:
         torch.cuda.current_stream().wait_stream(s)
         return graphs
 
-    def capture(self):
-        """Capture the step into HIP graphs (call after >= 1 eager step so all
-        lazy initialisation has happened).  Replays reuse the staged tokens."""
-        self.graphs = self._capture_graphs()
+    def capture(self, graphs=None):
+        """Switch the step to replaying HIP piece graphs (call after >= 1 eager step
+        so all lazy initialisation has happened; replays reuse the staged tokens)
+        -- if graphs is True, or if graphs is None and GHM_GRAPH=1.  The default
+        keeps the step eager: the host issues each kernel far ahead of the GPU, and
+        every piece-graph launch costs its stream ~9 us of idle queue at the piece
+        boundary (eager 4.014 vs piece graphs 4.052 ms per step, r4_ab13)."""
+        if graphs is None:
+            graphs = os.environ.get("GHM_GRAPH", "0") == "1"
+        self.graphs = self._capture_graphs() if graphs else None
 
     # -- host-side views -----------------------------------------------------------
     def loss_history(self, upto=None):

@@ -214,7 +214,7 @@ def _run(sampler, tr, B, steps, graph_after=None):
         tr.set_tokens(torch.from_numpy(tl), torch.from_numpy(il))
         tr.step()
         if graph_after is not None and s + 1 == graph_after:
-            tr.capture()
+            tr.capture(graphs=True)  # the replayed piece graphs (GHM_GRAPH=1), eager before
     torch.cuda.synchronize()
     return tr.loss_history()
 
