@@ -84,7 +84,11 @@ def allreduce_ranges_mean_(flat, ranges, group=None):
     the SUM of the ranks' values times 1/world; at world 2 that sum is one
     addition, so bucketed == flat bit for bit (tests/test_dp_gloo.py); beyond 2
     ranks a ring may add an element's terms in an order that depends on its
-    chunk, which can change its last bit (the same on every rank)."""
+    chunk, which can change its last bit (the same on every rank).  Overlap: on
+    RCCL the collective is enqueued on the caller's (comm) stream and the host
+    returns at once, so the towers' later launches run beside it; gloo's
+    all_reduce blocks the host until done, so the gloo-based data-parallel tests
+    check the bucketed arithmetic and the stream ordering, not that overlap."""
     for a, b in ranges:
         allreduce_mean_(flat[a:b], group=group)
     return flat
