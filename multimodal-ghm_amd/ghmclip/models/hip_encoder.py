@@ -141,7 +141,7 @@ class EncoderPlan:
         self.st1 = e(L, M, 2)
         self.st2 = e(L, M, 2)
         self.emb = e(N, num_class)
-        self.tokens = torch.empty(N, T, dtype=torch.uint8, device=dev)
+        self.tokens = self.token_buf = torch.empty(N, T, dtype=torch.uint8, device=dev)
         # backward scratch
         self.dH = e(2, M, D_MODEL)
         self.dqkv = e(M, 3 * D_MODEL)
