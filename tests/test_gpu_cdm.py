@@ -231,6 +231,45 @@ def test_cdm_steps_vs_reference_fixture(precision):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
+def test_cdm_nonti_steps_vs_reference_fixture(precision):
+    """train_sequential_DNS --translation_invariance=False: the native sampler's
+    Bayes risk and draws on per-edge trees, then two fused steps (per-edge BP_DNS
+    targets on the device) against the reference's own run (cdm_nonti_tiny.npz:
+    initial weights, loss, compare)."""
+    from ghmclip import (ConditionalDenoiseEncoderTransformer, ConditionalDenoiseSampler, EncoderTransformer,
+                         get_lr_cosine_schedule, seed_everything)
+    from ghmclip.training.cdm_trainer import CdmTrainer
+    f = np.load(os.path.join(GOLDEN, "cdm_nonti_tiny.npz"))
+    seed_everything(224)
+    s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1, translation_invariance=False)
+    bayes = s.get_Bayes(n_eval=10000)
+    np.testing.assert_allclose(bayes, f["bayes"], rtol=1e-10)
+    tt, it = s.device_templates("the CDM trainer")
+    np.testing.assert_array_equal(tt.trans, f["t_edges"])
+    np.testing.assert_array_equal(it.trans, f["i_edges"])
+    clip = EncoderTransformer(81, 10, 128, 5).to(DEV)
+    model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, 1, [1, 4], 4, 512, sequential=True).to(DEV)
+    sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, 30000) for k in range(30001)]
+    tr = CdmTrainer(model, clip, 4, sched, tt, it, sigma=1.0, device=DEV, precision=precision)
+    for (n, p), want in zip(tr.model.named_parameters(), f["init_stats"]):
+        assert abs((p.double() ** 2).sum().item() - want[1]) <= 1e-12 * want[1] + 1e-12, n
+    for (n, p), want in zip(tr.clip.named_parameters(), f["clip_stats"]):
+        assert abs((p.double() ** 2).sum().item() - want[1]) <= 1e-12 * want[1] + 1e-12, n
+    for k in range(2):
+        tl, _, z, il = s.draw_numpy(4)
+        np.testing.assert_array_equal(tl, f[f"t_leaves{k}"])
+        np.testing.assert_array_equal(il, f[f"i_leaves{k}"])
+        np.testing.assert_array_equal(z.astype(np.float32), f[f"z{k}"])
+        tr.set_batch(torch.from_numpy(tl), torch.from_numpy(il), torch.from_numpy(z))
+        tr.step()
+    torch.cuda.synchronize()
+    hist, chist = tr.loss_history(), tr.compare_history()
+    for k in range(2):
+        assert abs(hist[k] - float(f[f"ploss{k}"])) <= 2e-5 * float(f[f"ploss{k}"]), (k, hist[k])
+        assert abs(chist[k] - float(f[f"compare{k}"])) <= 2e-5 * float(f[f"compare{k}"]), (k, chist[k])
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 def test_cdm_steps_vs_oracle(precision):
     """Fused step == the oracle's step on identical draws: predictions, gradients
     (the trainer keeps them unclipped; the clip coefficient is hyper[1])."""
