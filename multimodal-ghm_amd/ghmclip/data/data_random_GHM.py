@@ -453,16 +453,18 @@ class ConditionalDenoiseSampler(DoubleSampler):
                          translation_invariance, seedtree)
         self.sigma = sigma
         self.native = self._native_sampler(2)
-        self.T = self.native.T
+        self.T = self.native.T  # None for trees of different leaf counts
+        self.T_t, self.T_i = self.native.T_t, self.native.T_i
 
     def draw_numpy(self, batch_size):
         """One reference-identical draw from numpy's global state: (text leaves uint8
-        [B, T], roots uint8 [B], z float64 [B, T], image leaves uint8 [B, T])."""
-        B, T = batch_size, self.T
-        tl = np.empty((B, T), np.uint8)
-        il = np.empty((B, T), np.uint8)
+        [B, T_t], roots uint8 [B], z float64 [B, T_i], image leaves uint8 [B, T_i])
+        (the noise lives on the image leaves, :862)."""
+        B = batch_size
+        tl = np.empty((B, self.T_t), np.uint8)
+        il = np.empty((B, self.T_i), np.uint8)
         root = np.empty(B, np.uint8)
-        z = np.empty((B, T), np.float64)
+        z = np.empty((B, self.T_i), np.float64)
         self.native.pull_numpy_state()
         self.native.next_cdm_into(B, self.sigma, tl, il, z, root)
         self.native.push_numpy_state()

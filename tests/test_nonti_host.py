@@ -129,3 +129,37 @@ def test_bp_dns_nonti_host_matches_reference():
     ext = _bp_levels(_tree(g["t_edges"], 4, 3), g["t_leaves"])[-1][0]
     post = bp_dns_posterior(_tree(g["i_edges"], 4, 3), g["z"].T, 1.0, ext)
     np.testing.assert_allclose(post.T, g["post"], rtol=1e-12, atol=1e-12)
+
+
+def test_cdm_sampler_unequal_trees_matches_reference():
+    """ConditionalDenoiseSampler on the trees of the reference's own unit tests
+    (tests/test_data_randomghm.py: n_layers [3, 4], sigma 0.1): text and image
+    leaf counts differ (27 / 81); draws, BP_DNS posterior means and get_Bayes
+    against the reference (cdm_unequal.npz)."""
+    from ghmclip import ConditionalDenoiseSampler, seed_everything
+    g = np.load(os.path.join(GOLDEN, "cdm_unequal.npz"))
+    s = ConditionalDenoiseSampler([3, 4], [3, 3], [P_Y, P_Y], [0.1, 0.1], sigma=0.1)
+    assert (s.T_t, s.T_i) == (27, 81)
+    seed_everything(3)
+    for k in range(2):
+        rt, ri = s.get_batch(batch_size=int(g["B"]))
+        np.testing.assert_array_equal(rt[0].numpy(), g[f"t_leaves{k}"])
+        np.testing.assert_array_equal(rt[1].numpy(), g[f"root{k}"])
+        np.testing.assert_array_equal(ri[0].numpy(), g[f"z{k}"])
+        np.testing.assert_array_equal(ri[1].numpy(), g[f"i_leaves{k}"])
+        np.testing.assert_allclose(ri[3], g[f"post{k}"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(s.get_Bayes(n_eval=500), g["bayes"], rtol=1e-8)
+
+
+def test_conditional_denoising_posterior_identity():
+    """The reference's own unit test (tests/test_data_randomghm.py:38-45) on this
+    package: with exact posterior means x_hat, E[x_hat^2] = E[x_hat x] over a
+    10,000-sample batch, |difference| < 3e-3 (guide=False: this package computes
+    the guided CDM targets on the device)."""
+    from ghmclip import ConditionalDenoiseSampler
+    s = ConditionalDenoiseSampler([3, 4], [3, 3], [P_Y, P_Y], [0.1, 0.1], sigma=0.1, flip_scale=1,
+                                  translation_invariance=True, variable_type=10)
+    _, res_image = s.get_batch(batch_size=10000)
+    true, pred = np.asarray(res_image[1]), np.asarray(res_image[-1])
+    err = abs(np.mean(np.mean(pred ** 2, 1)) - np.mean(np.mean(pred * true, 1)))
+    assert err < 3e-3, err
