@@ -412,6 +412,14 @@ def bp_dns_posterior(templ, z, sigma, ext):
     layer (translation invariance: node n uses its child-slot matrix n % C).
     z: noisy leaf observations [n_leaves, B] float64; ext: external root message
     [V, B].  Returns the posterior means [n_leaves, B]."""
+    return bp_dns_levels(templ, z, sigma, ext)[-1]
+
+
+def bp_dns_levels(templ, z, sigma, ext):
+    """bp_dns_posterior's messages as well: (hd, qd, bu, root_bu, post) with hd / qd /
+    bu dicts depth 1..L -> [n_nodes, V, B] (the per-node hd_message, qd_message and
+    bu_message of data_random_GHM.py:481-512), the root's bu [V, B] (its hd aliases
+    it, :501-504) and the posterior means [n_leaves, B]."""
     tab = _tables(templ)
     n_layer, C, V = len(tab), tab[0].shape[0], tab[0].shape[1]
     vt = np.linspace(0, V - 1, V).reshape(1, V, 1)
@@ -435,11 +443,13 @@ def bp_dns_posterior(templ, z, sigma, ext):
     bu = children_sum(qd[1])  # root (:499-504)
     bu -= bu.max(axis=1, keepdims=True)
     bu = bu + np.asarray(ext)[None]
+    root_bu, bus = bu[0], {}
     for layer in range(1, n_layer + 1):  # root -> leaves (:507-512)
         b = hd[layer] + up(np.repeat(bu, C, axis=0) - qd[layer], tab[layer - 1], transpose=True)
         bu = b - b.max(axis=1, keepdims=True)
+        bus[layer] = bu
     w = np.exp(bu)
-    return ((vt * w).sum(axis=1) / w.sum(axis=1))
+    return hd, qd, bus, root_bu, ((vt * w).sum(axis=1) / w.sum(axis=1))
 
 
 class ConditionalDenoiseSampler(DoubleSampler):
@@ -478,17 +488,39 @@ class ConditionalDenoiseSampler(DoubleSampler):
         return t_pp, bp_dns_posterior(self.i_tables, np.asarray(z).T, self.sigma, ext).T
 
     def get_batch(self, batch_size=128, device="cpu", guide=False):
-        """:854-884.  Returns (text_leaves int64 [B, T], text_root int64 [B], None,
-        t_pp [V, B]), (z float32 [B, T], image_leaves int64 [B, T], None,
-        posterior means float64 [B, T])."""
-        if guide:
-            raise NotImplementedError("guided CDM targets (guided_info) are computed on the device inside the "
-                                      "fused CdmTrainer step (ghm_bp_dns_msgs / ghm_bp_cls), not by the sampler")
+        """:854-884.  Returns (text_leaves int64 [B, T_t], text_root int64 [B],
+        text guided_info, t_pp [V, B]), (z float32 [B, T_i], image_leaves int64
+        [B, T_i], image guided_info, posterior means float64 [B, T_i]).  guide=True:
+        the host BP's guided_info lists (:526-592) -- the text tree's BP_CLS
+        message of every leaf's ancestor, depth L_t-1 first ([B, T_t, V] each), and
+        the image tree's BP_DNS messages: (hd, qd) of depths L_i .. 1, the root's
+        (hd, bu), then (hd, qd, bu) of depths 1 .. L_i ([B, T_i, 2V] / [B, T_i, 3V],
+        float32); guide=False: None (the fused CdmTrainer step computes its targets
+        on the device, ghm_bp_dns_msgs / ghm_bp_cls)."""
         tl, root, z, il = self.draw_numpy(batch_size)
-        t_pp, post = self.posterior(tl, z)
+        p_y = np.ones(self.variable_type) / self.variable_type
+        t_levels = _bp_levels(self.t_tables, tl)
+        t_pp = bp_cls_posterior(self.t_tables, tl, p_y).T
+        hd, qd, bu, root_bu, post = bp_dns_levels(self.i_tables, np.asarray(z).T, self.sigma, t_levels[-1][0])
+        post = post.T
+        t_info = i_info = None
+        if guide:
+            T_t, T_i = tl.shape[1], il.shape[1]
+            t_info = [torch.from_numpy(np.repeat(m.transpose(2, 0, 1), T_t // m.shape[0], axis=1)
+                                       .astype(np.float32)).to(device) for m in t_levels]
+
+            def rep(*ms):  # [n_nodes, V, B] each -> [B, T_i, k V]
+                cat = np.concatenate(ms, axis=1)
+                return torch.from_numpy(np.repeat(cat.transpose(2, 0, 1), T_i // cat.shape[0], axis=1)
+                                        .astype(np.float32)).to(device)
+
+            L = len(hd)
+            i_info = [rep(hd[d], qd[d]) for d in range(L, 0, -1)]
+            i_info.append(rep(root_bu[None], root_bu[None]))
+            i_info += [rep(hd[d], qd[d], bu[d]) for d in range(1, L + 1)]
         to = lambda a: torch.from_numpy(a.astype(np.int64)).to(device)  # noqa: E731
-        return ((to(tl), to(root), None, t_pp),
-                (torch.from_numpy(z.astype(np.float32)).to(device), to(il), None, post))
+        return ((to(tl), to(root), t_info, t_pp),
+                (torch.from_numpy(z.astype(np.float32)).to(device), to(il), i_info, post))
 
     def get_Bayes(self, n_eval=30000):
         """:886-894 — mean and standard error of the Bayes (posterior-mean) squared error."""

@@ -153,13 +153,33 @@ def test_cdm_sampler_unequal_trees_matches_reference():
 
 def test_conditional_denoising_posterior_identity():
     """The reference's own unit test (tests/test_data_randomghm.py:38-45) on this
-    package: with exact posterior means x_hat, E[x_hat^2] = E[x_hat x] over a
-    10,000-sample batch, |difference| < 3e-3 (guide=False: this package computes
-    the guided CDM targets on the device)."""
+    package, as written there: with exact posterior means x_hat, E[x_hat^2] =
+    E[x_hat x] over a 10,000-sample guide=True batch, |difference| < 3e-3."""
     from ghmclip import ConditionalDenoiseSampler
     s = ConditionalDenoiseSampler([3, 4], [3, 3], [P_Y, P_Y], [0.1, 0.1], sigma=0.1, flip_scale=1,
                                   translation_invariance=True, variable_type=10)
-    _, res_image = s.get_batch(batch_size=10000)
+    _, res_image = s.get_batch(batch_size=10000, guide=True)
+    assert len(res_image[2]) == 2 * 4 + 1
     true, pred = np.asarray(res_image[1]), np.asarray(res_image[-1])
     err = abs(np.mean(np.mean(pred ** 2, 1)) - np.mean(np.mean(pred * true, 1)))
     assert err < 3e-3, err
+
+
+def test_cdm_guided_info_nonti_matches_reference():
+    """ConditionalDenoiseSampler.get_batch(guide=True) on non-invariant trees: the
+    text BP_CLS and image BP_DNS guided_info levels (data_random_GHM.py:526-592)
+    against the reference's own batch (cdm_nonti.npz, stored one column per node)."""
+    from ghmclip import ConditionalDenoiseSampler, seed_everything
+    g = np.load(os.path.join(GOLDEN, "cdm_nonti.npz"))
+    s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1, translation_invariance=False)
+    seed_everything(5)
+    rt, ri = s.get_batch(batch_size=int(g["B"]), guide=True)
+    np.testing.assert_array_equal(rt[0].numpy(), g["t_leaves"])
+    np.testing.assert_allclose(ri[3], g["post"], rtol=1e-10, atol=1e-12)
+    assert len(rt[2]) == 4 and len(ri[2]) == 9
+    for k, m in enumerate(rt[2]):
+        np.testing.assert_allclose(m.numpy()[:, ::3 ** (k + 1)], g[f"text{k}"], rtol=1e-6, atol=1e-6)
+    for k, m in enumerate(ri[2]):
+        depth = 4 - k if k <= 4 else k - 4
+        np.testing.assert_allclose(m.numpy()[:, ::3 ** (4 - depth)], g[f"image{k}"], rtol=1e-6, atol=1e-5,
+                                   err_msg=f"image level {k}")
