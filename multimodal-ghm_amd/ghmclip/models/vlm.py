@@ -29,6 +29,7 @@ HBM layout (M = n_seq * T tokens, D = n_embd, F = 4 D, fp32 row-major):
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -131,7 +132,7 @@ class VlmPlan:
             self.dqkv = e(M, 3 * D)
             self.dS = torch.zeros(N, pad, pad, dtype=torch.float32, device=self.device)
         # split-k weight-gradient slabs, column-sum partials
-        self.nsplit = max(1, min(32, M // 256))
+        self.nsplit = max(1, min(int(os.environ.get("GHM_VLM_NSPLIT", "16")), M // 256))
         self.slab = e(self.nsplit * max(D * F, 3 * D * D))
         lib = _native.hip_lib()
         self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
