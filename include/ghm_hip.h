@@ -467,7 +467,9 @@ int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const float* Pd, c
  * k for tb = 0), b_chunk rows each (0: B0 only).  N % 128 == 0.
  * epi: 0 C = acc; 1 (u = acc + bias[n]) C = GELU(u), C2 = GELU'(u); 2 C = acc +
  * bias[n] + R[m][n]; 3 C = acc * R[m][n]; 4 split-k partials C[z][M][N] (nsplit
- * slabs of ghm_gemm_slab_elems floats in total), summed by ghm_gemm_reduce. */
+ * slabs of ghm_gemm_slab_elems floats in total), summed by ghm_gemm_reduce; with
+ * ta = 1 and C2 set, also C2[z][m] = the split's sum over k of A(m, k) (nsplit x M
+ * floats: the Linear bias gradient as a by-product of its weight gradient). */
 int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit);
 int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
                 const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2, const float* bias,
@@ -482,6 +484,11 @@ int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda, const flo
  * D0, D1, D2 by chunk (0: D0 only). */
 int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
                     int64_t chunk, void* stream);
+/* ghm_gemm_reduce plus, in the same launch, bdst[m] = sum_z bslab[z][m] (the row
+ * sums of a ta = 1 slab GEMM; M % 4 == 0).  bslab = bdst = NULL: ghm_gemm_reduce.
+ * Replaces the bias-gradient column sums of the MLP Linears (model.py:344-347). */
+int ghm_gemm_reduce_bias(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
+                         int64_t chunk, const float* bslab, float* bdst, void* stream);
 /* out[n] = sum_m X[m][n] (deterministic two-stage), X [M][N] fp32, N % 4 == 0 and
  * N/4 dividing 256 or >= 256; part scratch of ghm_colsum_part_elems(M, N) floats.
  * The bias gradients of the Linear layers and the position-embedding gradient

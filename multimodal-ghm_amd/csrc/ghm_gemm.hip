@@ -33,6 +33,7 @@
 //   EPI_RESID   C = acc + bias[n] + R[m][n]                     (MLP down + residual)
 //   EPI_MUL     C = acc * R[m][n]                               (dG * GELU'(U))
 //   EPI_SLAB    slab[z][m][n] = acc                             (split-k wgrad)
+//               C2[z][m] = sum over the split's k of A(m, k)      (ta = 1, C2 set: bias grad)
 #include "ghm_launch.h"
 #include "ghm_split.h"
 
@@ -228,8 +229,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
       load_oc<GB_N>(vb, b + (lk - k0) * g.ldb, g.ldb, k0, ke, n0);
     }
   };
+  // split-k wgrad with C2 set: per-thread row sums of A (the bias gradient, sum
+  // over tokens of dY) accumulated from the staged registers, tile by tile in k order
+  float4 rs = make_float4(0.f, 0.f, 0.f, 0.f);
   // k0: the K tile being stored (zeroes A's token tail in split-k)
   auto store = [&](const float4* va, const float4* vb, int buf, int64_t k0) {
+    if constexpr (TA && EPI == EPI_SLAB) {
+      if (g.C2) {
+        const int kg = threadIdx.x / (BM / 4);
+#pragma unroll
+        for (int i = 0; i < NA; ++i)
+          if (k0 + NA * kg + i < ke) {
+            rs.x += va[i].x; rs.y += va[i].y; rs.z += va[i].z; rs.w += va[i].w;
+          }
+      }
+    }
     if constexpr (F32) {
       if constexpr (TA) store_oc_f32<BM, true>(va, af[buf], k0, ke);
       else store_kc_f32<BM>(va, af[buf]);
@@ -344,6 +358,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     }
   }
 
+  if constexpr (TA && EPI == EPI_SLAB) {
+    // row-sum partial C2[z][m]: the 256 / (BM / 4) row groups of a column quad
+    // combined in group order through LDS, once per (m block, split)
+    if (g.C2 && tbx == 0) {
+      constexpr int C4 = BM / 4, G = 256 / C4;
+      float4* red = reinterpret_cast<float4*>(smem);
+      __syncthreads();
+      red[threadIdx.x] = rs;
+      __syncthreads();
+      if (threadIdx.x < C4) {
+        float4 a = red[threadIdx.x];
+#pragma unroll
+        for (int q = 1; q < G; ++q) {
+          const float4 v = red[threadIdx.x + q * C4];
+          a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        const int64_t m = m0 + 4 * threadIdx.x;
+        if (m < g.M) *reinterpret_cast<float4*>(g.C2 + static_cast<int64_t>(tbz) * g.M + m) = a;
+      }
+    }
+  }
+
   // epilogue: lane row m = m0 + 32(TM wm + i) + r; register quad qd of acc[i][j] holds
   // n = n0 + 32(2 wn + j) + 8 qd + 4 h + 0..3 -> one 16-byte access per quad
 #pragma unroll
@@ -390,9 +426,23 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   }
 }
 
-// dst rows (stacked as B is): out = sum_z slab[z] in z order
+// dst rows (stacked as B is): out = sum_z slab[z] in z order.  Workgroups past the
+// slab's (nmain) sum the row-sum partials bslab[z][M] into bdst (bias gradient).
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ slab, int nsplit, int64_t M, int64_t N,
-                                                      float* d0, float* d1, float* d2, int64_t chunk) {
+                                                      float* d0, float* d1, float* d2, int64_t chunk,
+                                                      const float* __restrict__ bslab, float* bdst, int64_t nmain) {
+  if (static_cast<int64_t>(blockIdx.x) >= nmain) {
+    const int64_t b4 = (static_cast<int64_t>(blockIdx.x) - nmain) * 256 + threadIdx.x;
+    if (4 * b4 >= M) return;
+    const float4* s = reinterpret_cast<const float4*>(bslab) + b4;
+    float4 a = s[0];
+    for (int z = 1; z < nsplit; ++z) {
+      const float4 b = s[static_cast<int64_t>(z) * (M / 4)];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    reinterpret_cast<float4*>(bdst)[b4] = a;
+    return;
+  }
   const int64_t i4 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const int64_t total = M * N;
   if (4 * i4 >= total) return;
@@ -731,6 +781,7 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
   GHM_CHECK(epi >= EPI_STORE && epi <= EPI_SLAB, "epilogue");
   GHM_CHECK(nsplit == 1 || epi == EPI_SLAB, "split k needs the slab epilogue");
   GHM_CHECK(epi != EPI_GELU || (bias && C2), "GELU epilogue needs bias and C2");
+  GHM_CHECK(!C2 || epi == EPI_GELU || (epi == EPI_SLAB && ta && M % 4 == 0), "C2: GELU' or the ta = 1 slab row sums");
   GHM_CHECK(epi != EPI_RESID || (bias && R), "residual epilogue needs bias and R");
   GHM_CHECK(epi != EPI_MUL || R, "product epilogue needs R");
   GHM_CHECK(lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && ldr % 4 == 0, "row strides % 4 == 0");
@@ -788,14 +839,22 @@ extern "C" int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda
                      stream);
 }
 
-extern "C" int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
-                               int64_t chunk, void* stream) {
+extern "C" int ghm_gemm_reduce_bias(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1,
+                                    float* D2, int64_t chunk, const float* bslab, float* bdst, void* stream) {
   GHM_CHECK(slab && D0 && nsplit >= 1 && M >= 1 && N >= 4 && N % 4 == 0, "bad arguments");
   GHM_CHECK(chunk <= 0 || (M <= 3 * chunk && D1 && (M <= 2 * chunk || D2)), "stacked destination");
-  const int64_t n4 = M * N / 4;
-  hipLaunchKernelGGL(k_gemm_reduce, dim3(static_cast<unsigned>((n4 + 255) / 256)), dim3(256), 0, ghm_stream(stream),
-                     slab, nsplit, M, N, D0, D1, D2, chunk);
+  GHM_CHECK(!bslab == !bdst && (!bslab || M % 4 == 0), "row sums: bslab and bdst together, M % 4 == 0");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(bslab) | reinterpret_cast<uintptr_t>(bdst)) & 15) == 0,
+            "16-byte aligned row sums");
+  const int64_t nmain = (M * N / 4 + 255) / 256, nb = bslab ? (M / 4 + 255) / 256 : 0;
+  hipLaunchKernelGGL(k_gemm_reduce, dim3(static_cast<unsigned>(nmain + nb)), dim3(256), 0, ghm_stream(stream), slab,
+                     nsplit, M, N, D0, D1, D2, chunk, bslab, bdst, nmain);
   return ghm_launch_status();
+}
+
+extern "C" int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,
+                               int64_t chunk, void* stream) {
+  return ghm_gemm_reduce_bias(slab, nsplit, M, N, D0, D1, D2, chunk, nullptr, nullptr, stream);
 }
 
 extern "C" int64_t ghm_colsum_part_elems(int64_t M, int64_t N) {

@@ -134,6 +134,7 @@ class VlmPlan:
         # split-k weight-gradient slabs, column-sum partials
         self.nsplit = max(1, min(int(os.environ.get("GHM_VLM_NSPLIT", "16")), M // 256))
         self.slab = e(self.nsplit * max(D * F, 3 * D * D))
+        self.bslab = e(self.nsplit * F)  # MLP bias-gradient row-sum partials
         lib = _native.hip_lib()
         self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
                              lib.ghm_colsum_part_elems(N, n_token * D),
@@ -204,12 +205,16 @@ class VlmPlan:
         self._gen += 1
         return self.logits
 
-    def _wgrad(self, A, lda, m, B, ldb, n, dst, chunk, s):
-        """dst (rows stacked by chunk) = A^T B over the M tokens: split-k slabs + fixed-order reduce."""
-        self._gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.M, nsplit=self.nsplit, s=s)
+    def _wgrad(self, A, lda, m, B, ldb, n, dst, chunk, s, bias=None):
+        """dst (rows stacked by chunk) = A^T B over the M tokens: split-k slabs + fixed-order reduce.
+        bias: also its gradient, the column sums of A over the tokens, from the same
+        staged tiles (C2 row-sum partials) and the same reduce launch."""
+        bs = None if bias is None else self.bslab
+        self._gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.M, C2=bs, nsplit=self.nsplit, s=s)
         d = list(dst) + [None] * (3 - len(dst))
         pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
-        _native.call("ghm_gemm_reduce", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk, s)
+        _native.call("ghm_gemm_reduce_bias", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk,
+                     pp(bs), pp(bias), s)
 
     def _backward_hip(self, p, g, dlogits=None, layer_grad=None):
         s = _stream()
@@ -224,11 +229,9 @@ class VlmPlan:
             if layer_grad and l in layer_grad:
                 layer_grad[l](cur, s)
             w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
-            self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s)
-            self._colsum(cur, M, D, g[f"_mlps.{l}.2.bias"], s)
+            self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s, bias=g[f"_mlps.{l}.2.bias"])
             self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
-            self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s)
-            self._colsum(self.dG, M, F, g[f"_mlps.{l}.0.bias"], s)
+            self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s, bias=g[f"_mlps.{l}.0.bias"])
             self._gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
               _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)

@@ -149,6 +149,41 @@ def test_wgrad_split_k(M_tok, nsplit, f32):
     assert torch.equal(res[0], res[1])
 
 
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("m,n", [(256, 1024), (1024, 256)])  # 128- and 64-row tiles (launch_tm)
+@pytest.mark.parametrize("M_tok,nsplit", [(2000, 7), (10368 + 5, 16)])
+def test_wgrad_split_k_bias_rows(m, n, M_tok, nsplit, f32):
+    """The slab GEMM's C2 row sums + ghm_gemm_reduce_bias: the MLP bias gradient
+    (sum over tokens of dY, model.py:344-347 autograd) from the weight-gradient
+    launch, beside the weight gradient itself; split tails zeroed, bit-identical
+    when repeated."""
+    REL = RELS[f32]
+    g = torch.Generator().manual_seed(M_tok + m)
+    dY = torch.randn(M_tok, m, generator=g)
+    X = torch.randn(M_tok, n, generator=g)
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    slab = torch.empty(nsplit * m * n, device=DEV)
+    bslab = torch.full((nsplit * m,), float("nan"), device=DEV)
+    out, bias = torch.empty(m, n, device=DEV), torch.empty(m, device=DEV)
+    dY_big = torch.full((M_tok + 64, m), float("nan"), device=DEV)
+    X_big = torch.full((M_tok + 64, n), float("nan"), device=DEV)
+    dY_big[:M_tok] = dY.to(DEV)
+    X_big[:M_tok] = X.to(DEV)
+    res = []
+    for _ in range(2):
+        _gemm(1, 0, EPI_SLAB, dY_big, m, (X_big,), n, 0, slab, n, m, n, M_tok, C2=bslab, nsplit=nsplit, f32=f32)
+        _native.call("ghm_gemm_reduce_bias", _ptr(slab), nsplit, m, n, _ptr(out), None, None, 0, _ptr(bslab),
+                     _ptr(bias), ctypes_stream())
+        torch.cuda.synchronize()
+        res.append((out.cpu(), bias.cpu()))
+    _check(res[0][0], dY.double().t() @ X.double(), REL * (dY.double().abs().t() @ X.double().abs()) + 1e-6, "wgrad")
+    want_b = dY.double().sum(0)
+    bound_b = 1e-6 * dY.double().abs().sum(0) + 1e-6  # f32 sums in a fixed order
+    _check(res[0][1], want_b, bound_b, "bias rows")
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
 def ctypes_stream():
     import ctypes
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
