@@ -804,6 +804,8 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
   g.C = C; g.ldc = ldc; g.C2 = C2; g.bias = bias; g.R = R; g.ldr = ldr;
   g.M = M; g.N = N; g.K = K;
   g.k_per_split = ((K + nsplit - 1) / nsplit + GB_K - 1) / GB_K * GB_K;
+  // an empty split would stage (unused) A columns past K: only ta = 1 clamps them
+  GHM_CHECK(ta || (nsplit - 1) * g.k_per_split < K, "ta = 0 split k: every split needs a K tile");
   hipStream_t s = ghm_stream(stream);
 #define GHM_GEMM_CASE(TA_, TB_, E_)                                    \
   if (ta == TA_ && tb == TB_ && epi == E_) {                           \
@@ -817,6 +819,7 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
   GHM_GEMM_CASE(0, 0, EPI_STORE)
   GHM_GEMM_CASE(0, 0, EPI_MUL)
   GHM_GEMM_CASE(0, 0, EPI_RESID)  // the f32 VLM's dX += dk Wk, dv Wv
+  GHM_GEMM_CASE(0, 0, EPI_SLAB)  // split-k data gradient (VLM dX over K = 768 / 1024)
   GHM_GEMM_CASE(1, 0, EPI_SLAB)
   GHM_GEMM_CASE(1, 0, EPI_STORE)
 #undef GHM_GEMM_CASE

@@ -135,6 +135,10 @@ class VlmPlan:
         self.nsplit = max(1, min(int(os.environ.get("GHM_VLM_NSPLIT", "16")), M // 256))
         self.slab = e(self.nsplit * max(D * F, 3 * D * D))
         self.bslab = e(self.nsplit * F)  # MLP bias-gradient row-sum partials
+        # data gradients dX = dY W over K = 4D / 3D: k split in dsplit slabs (the
+        # N = D products have only 2 x M / 64 output tiles: ~1.3 workgroups per CU)
+        self.dsplit = max(1, int(os.environ.get("GHM_VLM_DSPLIT", "1")))
+        self.dslab = e(self.dsplit * M * D) if self.dsplit > 1 else None
         lib = _native.hip_lib()
         self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
                              lib.ghm_colsum_part_elems(N, n_token * D),
@@ -216,6 +220,17 @@ class VlmPlan:
         _native.call("ghm_gemm_reduce_bias", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk,
                      pp(bs), pp(bias), s)
 
+    def _dgrad(self, A, lda, Bs, b_chunk, K, s):
+        """self.dX [M][D] = A [M][K] @ B (B [K][D] rows stacked by b_chunk), split-k
+        over dsplit slabs + the fixed-order reduce when dsplit > 1."""
+        M, D = self.M, self.D
+        ns = self.dsplit
+        if ns > 1 and (ns - 1) * ((-(-K // ns) + 31) // 32 * 32) < K:
+            self._gemm(0, 0, EPI_SLAB, A, lda, Bs, D, b_chunk, self.dslab, D, M, D, K, nsplit=ns, s=s)
+            _native.call("ghm_gemm_reduce", _ptr(self.dslab), ns, M, D, _ptr(self.dX), None, None, 0, s)
+        else:
+            self._gemm(0, 0, EPI_STORE, A, lda, Bs, D, b_chunk, self.dX, D, M, D, K, s=s)
+
     def _backward_hip(self, p, g, dlogits=None, layer_grad=None):
         s = _stream()
         c = _native.call
@@ -232,7 +247,7 @@ class VlmPlan:
             self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s, bias=g[f"_mlps.{l}.2.bias"])
             self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
             self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s, bias=g[f"_mlps.{l}.0.bias"])
-            self._gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
+            self._dgrad(self.dG, F, (w1,), 0, F, s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
               _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 2, l, s)
@@ -254,7 +269,7 @@ class VlmPlan:
                 c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS),
                   _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
                 self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D, gqkv, D, s)
-                self._gemm(0, 0, EPI_STORE, self.dqkv, 3 * D, wqkv, D, D, self.dX, D, M, D, 3 * D, s=s)
+                self._dgrad(self.dqkv, 3 * D, wqkv, D, 3 * D, s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
               _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
             self._reduce_ln(g, 1, l, s)

@@ -184,6 +184,27 @@ def test_wgrad_split_k_bias_rows(m, n, M_tok, nsplit, f32):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("f32", [False, True])
+@pytest.mark.parametrize("K,stacked,nsplit", [(1024, False, 2), (1024, False, 3), (768, True, 2)])
+def test_dgrad_split_k(K, stacked, nsplit, f32):
+    """dX = dY W (ta = 0, tb = 0) in split-k slabs + the fixed-order reduce (the
+    VLM's GHM_VLM_DSPLIT path), W as one tensor or three stacked along k."""
+    REL = RELS[f32]
+    D, M = 256, 10368 + 5
+    g = torch.Generator().manual_seed(K + nsplit)
+    dY = torch.randn(M, K, generator=g)
+    W = torch.randn(K, D, generator=g) * 0.05
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    Bs = tuple(W[i * D:(i + 1) * D].to(DEV) for i in range(3)) if stacked else (W.to(DEV),)
+    slab = torch.empty(nsplit * M * D, device=DEV)
+    out = torch.empty(M, D, device=DEV)
+    _gemm(0, 0, EPI_SLAB, dY.to(DEV), K, Bs, D, D if stacked else 0, slab, D, M, D, K, nsplit=nsplit, f32=f32)
+    _native.call("ghm_gemm_reduce", _ptr(slab), nsplit, M, D, _ptr(out), None, None, 0, ctypes_stream())
+    torch.cuda.synchronize()
+    _check(out, dY.double() @ W.double(), REL * (dY.double().abs() @ W.double().abs()) + 1e-6, "dgrad split")
+
+
 def ctypes_stream():
     import ctypes
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
