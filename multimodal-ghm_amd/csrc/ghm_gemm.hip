@@ -92,13 +92,17 @@ __device__ __forceinline__ void store_kc(const float4* v, __bf16* hi, __bf16* lo
 }
 
 // [k][outer] tile: k rows k0..k0+31, outer columns c0..c0+COLS-1; thread = (k group
-// of RPT rows, 4 columns).  Rows >= kend read a clamped row; with ZERO the store
+// of RPT rows, 4 columns), k groups fastest across the lanes: the transposed LDS
+// stores of a wave then spread over the k offsets of a row (distinct banks) rather
+// than over 4-row groups whose 2 GP-dword stride maps onto 4 banks (PMC r4_m3: 10-17
+// conflict cycles per LDS instruction in the ta = 1 / tb = 0 GEMMs); each global
+// load still covers whole 128-B row segments.  Rows >= kend read a clamped row; with ZERO the store
 // writes zeros for them (the split-k token tail: one operand zeroed suffices).
 template <int COLS>
 __device__ __forceinline__ void load_oc(float4* v, const float* __restrict__ base, int64_t ld, int64_t k0,
                                         int64_t kend, int64_t c0) {
-  constexpr int C4 = COLS / 4, RPT = COLS / 32;
-  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+  constexpr int RPT = COLS / 32, KG = 32 / RPT;
+  const int kg = threadIdx.x % KG, c4 = threadIdx.x / KG;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
     const int64_t k = k0 + RPT * kg + i;
@@ -108,8 +112,8 @@ __device__ __forceinline__ void load_oc(float4* v, const float* __restrict__ bas
 }
 template <int COLS, bool ZERO>
 __device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo, int64_t k0, int64_t kend) {
-  constexpr int C4 = COLS / 4, RPT = COLS / 32;
-  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+  constexpr int RPT = COLS / 32, KG = 32 / RPT;
+  const int kg = threadIdx.x % KG, c4 = threadIdx.x / KG;  // k groups fastest: see load_oc
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     __bf16 h[RPT], l[RPT];
@@ -152,8 +156,8 @@ __device__ __forceinline__ void store_kc_f32(const float4* v, float* img) {
 }
 template <int COLS, bool ZERO>
 __device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_t k0, int64_t kend) {
-  constexpr int C4 = COLS / 4, RPT = COLS / 32;
-  const int kg = threadIdx.x / C4, c4 = threadIdx.x % C4;
+  constexpr int RPT = COLS / 32, KG = 32 / RPT;
+  const int kg = threadIdx.x % KG, c4 = threadIdx.x / KG;  // k groups fastest: see load_oc
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     float x[RPT];
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   auto store = [&](const float4* va, const float4* vb, int buf, int64_t k0) {
     if constexpr (TA && EPI == EPI_SLAB) {
       if (g.C2) {
-        const int kg = threadIdx.x / (BM / 4);
+        const int kg = threadIdx.x % (32 / NA);  // load_oc's lane mapping
 #pragma unroll
         for (int i = 0; i < NA; ++i)
           if (k0 + NA * kg + i < ke) {
@@ -359,19 +363,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   }
 
   if constexpr (TA && EPI == EPI_SLAB) {
-    // row-sum partial C2[z][m]: the 256 / (BM / 4) row groups of a column quad
-    // combined in group order through LDS, once per (m block, split)
+    // row-sum partial C2[z][m]: the 32 / NA k groups of a column quad combined in
+    // group order through LDS, once per (m block, split)
     if (g.C2 && tbx == 0) {
-      constexpr int C4 = BM / 4, G = 256 / C4;
+      constexpr int C4 = BM / 4, G = 32 / NA;  // lane = c4 * G + k group
       float4* red = reinterpret_cast<float4*>(smem);
       __syncthreads();
       red[threadIdx.x] = rs;
       __syncthreads();
       if (threadIdx.x < C4) {
-        float4 a = red[threadIdx.x];
+        float4 a = red[threadIdx.x * G];
 #pragma unroll
         for (int q = 1; q < G; ++q) {
-          const float4 v = red[threadIdx.x + q * C4];
+          const float4 v = red[threadIdx.x * G + q];
           a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
         }
         const int64_t m = m0 + 4 * threadIdx.x;
