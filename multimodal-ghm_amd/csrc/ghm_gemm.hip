@@ -64,6 +64,16 @@ struct GemmArgs {
 // unconditional and their data is consumed only by the split store: a guard or
 // select on the loaded value forces a vmcnt wait right after the load, which
 // serialises every prefetch.
+// Row of a k-contiguous tile staged by element idx (8 lanes per row): within each
+// 16-row group a half-wave takes rows 4 apart (0, 4, 8, 12 | 2, 6, 10, 14, and the
+// odd rows in the next wave), whose 20-dword pitch offsets land in the 4 disjoint
+// 16-bank windows of the LDS: conflict-free stores (plain idx >> 3 put rows 0-3
+// of a half-wave on overlapping windows).  ROWS % 16 == 0.
+__device__ __forceinline__ int kc_row(int idx) {
+  const int w8 = idx >> 6, q = (idx >> 3) & 7;
+  return 16 * (w8 >> 1) + 4 * (q & 3) + 2 * (q >> 2) + (w8 & 1);
+}
+
 template <int ROWS>
 __device__ __forceinline__ void load_kc(float4* v, const float* __restrict__ base, int64_t ld, int64_t r0,
                                         int64_t nrows, int64_t k0) {
@@ -71,7 +81,7 @@ __device__ __forceinline__ void load_kc(float4* v, const float* __restrict__ bas
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int idx = threadIdx.x + 256 * i;
-    const int row = idx >> 3, k4 = idx & 7;
+    const int row = kc_row(idx), k4 = idx & 7;
     const int64_t r = r0 + row;
     const int64_t rc = r < nrows ? r : nrows - 1;
     v[i] = *reinterpret_cast<const float4*>(base + rc * ld + k0 + 4 * k4);
@@ -83,7 +93,7 @@ __device__ __forceinline__ void store_kc(const float4* v, __bf16* hi, __bf16* lo
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int idx = threadIdx.x + 256 * i;
-    const int row = idx >> 3, k4 = idx & 7;
+    const int row = kc_row(idx), k4 = idx & 7;
     bf16x4 a, b;
     split4(v[i], a, b);
     stb4(hi + row * GP + 4 * k4, a);
@@ -151,7 +161,7 @@ __device__ __forceinline__ void store_kc_f32(const float4* v, float* img) {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int idx = threadIdx.x + 256 * i;
-    *reinterpret_cast<float4*>(img + (idx >> 3) * GPF + 4 * (idx & 7)) = v[i];
+    *reinterpret_cast<float4*>(img + kc_row(idx) * GPF + 4 * (idx & 7)) = v[i];
   }
 }
 template <int COLS, bool ZERO>
