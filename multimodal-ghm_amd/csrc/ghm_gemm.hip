@@ -772,8 +772,13 @@ template <bool TA, bool TB, int EPI, bool F32>
 void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   // measured (VLM shapes, M = 10,368): 128 x 128 tiles with one K tile in flight
   // are faster for N >= 768; 64 x 128 tiles with two K tiles in flight for N = 256
+  // GHM_GEMM_TM2_MIN_N: A/B knob for that cut (read once)
+  static const int64_t tm2_min = [] {
+    const char* e = getenv("GHM_GEMM_TM2_MIN_N");
+    return e ? static_cast<int64_t>(atoll(e)) : static_cast<int64_t>(768);
+  }();
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
-  if (g.N >= 768)
+  if (g.N >= tm2_min)
     hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit),
                        dim3(256), 0, s, g);
   else
