@@ -11,6 +11,13 @@ HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h $(SRC)/ghm_split.h $(SRC)/gh
 
 all: $(LIBDIR)/libghm_hip.so $(LIBDIR)/libghm_host.so
 
+# source hash baked into both libraries (ghm_build_id / ghm_sampler_build_id;
+# multimodal-ghm_amd/ghmclip/_buildid.py): the generated file changes only with it
+BUILD_ID_SRC := build/obj/ghm_build_id.cpp
+$(BUILD_ID_SRC): FORCE
+	@python3 tools/build_id.py $@ > /dev/null
+FORCE:
+
 OBJDIR := build/obj
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 
@@ -19,13 +26,16 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HIP_HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPOBJFLAGS) -c -o $@ $<
 
-$(LIBDIR)/libghm_hip.so: $(HIP_OBJS)
-	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS)
+$(OBJDIR)/ghm_build_id.o: $(BUILD_ID_SRC)
+	$(CXX) -O2 -fPIC -c -o $@ $<
 
-$(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h
+$(LIBDIR)/libghm_hip.so: $(HIP_OBJS) $(OBJDIR)/ghm_build_id.o
 	@mkdir -p $(LIBDIR)
-	$(CXX) -O3 -std=c++17 -fPIC -shared -pthread -o $@ $(SRC)/ghm_sampler.cpp
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $(HIP_OBJS) $(OBJDIR)/ghm_build_id.o
+
+$(LIBDIR)/libghm_host.so: $(SRC)/ghm_sampler.cpp include/ghm_sampler.h $(BUILD_ID_SRC)
+	@mkdir -p $(LIBDIR)
+	$(CXX) -O3 -std=c++17 -fPIC -shared -pthread -DGHM_HOST_LIB -o $@ $(SRC)/ghm_sampler.cpp -x c++ $(BUILD_ID_SRC)
 
 resource-usage: $(HIP_SRCS) $(HIP_HDRS)
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -Rpass-analysis=kernel-resource-usage $(SRC)/ghm_fwd.hip -o /tmp/ghm_fwd.o
@@ -35,4 +45,4 @@ resource-usage: $(HIP_SRCS) $(HIP_HDRS)
 clean:
 	rm -f $(LIBDIR)/*.so $(OBJDIR)/*.o
 
-.PHONY: all clean resource-usage
+.PHONY: all clean resource-usage FORCE

@@ -24,6 +24,10 @@ extern "C" {
 const char* ghm_last_error_string(void);
 /* 1 when the library was built for gfx950 and a device is visible, else 0. */
 int ghm_device_ok(void);
+/* 16 hex digits: the hash of the sources this library was built from
+ * (multimodal-ghm_amd/csrc/*, include/*.h, Makefile; ghmclip/_buildid.py).
+ * smoke() and bench.py require it to equal the hash of the tree they run in. */
+const char* ghm_build_id(void);
 /* Cross-stream ordering (the two-tower step's fork / join / cross waits,
  * replacing torch Stream.wait_stream in train_CLIP's step, which has no
  * reference counterpart: the reference runs the towers one after the other).

@@ -40,6 +40,8 @@ ghm_sampler* ghm_sampler_create(const double* t_trans, const double* i_trans, in
 ghm_sampler* ghm_sampler_create_edges(const double* t_edges, int t_layer, int t_child, const double* i_edges,
                                       int i_layer, int i_child, int V, int K);
 void ghm_sampler_destroy(ghm_sampler* s);
+/* the source hash of this library's build (as ghm_build_id in ghm_hip.h) */
+const char* ghm_sampler_build_id(void);
 
 /* Seed like numpy.random.seed(int) (init_genrand). */
 int ghm_sampler_seed(ghm_sampler* s, uint32_t seed);

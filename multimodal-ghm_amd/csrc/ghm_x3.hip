@@ -26,8 +26,12 @@
 #error "GHM_ABL timing ablations give wrong results: only with -DGHM_ABLATION_BUILD (tools/, never the product library)"
 #endif
 
+// 1: k_qkv_bwd_x3 reads the forward's LN1 statistics (system-scope load); 0 (the
+// product): it recomputes them from H, one more read of H (+0.85 % of the step,
+// r4_ab8).  The recompute stays the default until the wrong-statistics mechanism
+// beside k_wgrad_x3 is known (DESIGN.md section 4 "Determinism").
 #ifndef GHM_QKV_STATS_LOAD
-#define GHM_QKV_STATS_LOAD 1  // 0: k_qkv_bwd_x3 recomputes the LN1 statistics from H (one more read of H)
+#define GHM_QKV_STATS_LOAD 0
 #endif
 #ifndef GHM_WGRAD_FAST
 #define GHM_WGRAD_FAST 1  // 0: the run-time-stride weight gradients only (k_wgrad_x3 LDA / LDB = 0)

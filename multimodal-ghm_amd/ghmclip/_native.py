@@ -39,6 +39,7 @@ _u32 = ctypes.c_uint32
 HIP_SIGNATURES = {
     "ghm_last_error_string": [],
     "ghm_device_ok": [],
+    "ghm_build_id": [],
     "ghm_token_blocks": [_i64],
     "ghm_mlp_bwd_rc_x3_blocks": [_i64],
     "ghm_embed_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
@@ -132,7 +133,7 @@ HIP_SIGNATURES = {
     "ghm_adamw": [_p, _p, _p, _p, _i64, _p, _f, _f, _f, _f, _f, _p],
     "ghm_zsc_logits": [_p, _i64, _p, _i, _p, _i, _i, _p, _i, _p, _p],
 }
-_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_event_create": ctypes.c_void_p, "ghm_embed_bwd_part_elems": _i64, "ghm_embed_bwd_splits": _i, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
+_RESTYPE = {"ghm_last_error_string": ctypes.c_char_p, "ghm_build_id": ctypes.c_char_p, "ghm_event_create": ctypes.c_void_p, "ghm_embed_bwd_part_elems": _i64, "ghm_embed_bwd_splits": _i, "ghm_guide_max_blocks": _i, "ghm_token_blocks": _i64,
             "ghm_mlp_bwd_rc_x3_blocks": _i64,
             "ghm_ln_rows_blocks": _i64, "ghm_gemm_slab_elems": _i64, "ghm_colsum_part_elems": _i64,
             "ghm_wcolsum_part_elems": _i64,
@@ -142,6 +143,7 @@ HOST_SIGNATURES = {
     "ghm_sampler_create": [_p, _p, _i, _i, _i, _i],
     "ghm_sampler_create_edges": [_p, _i, _i, _p, _i, _i, _i, _i],
     "ghm_sampler_destroy": [_p],
+    "ghm_sampler_build_id": [],
     "ghm_sampler_seed": [_p, _u32],
     "ghm_sampler_set_state": [_p, _p, _i],
     "ghm_sampler_get_state": [_p, _p, _p],
@@ -155,7 +157,7 @@ HOST_SIGNATURES = {
     "ghm_sampler_randn": [_p, _p, _i64],
 }
 _HOST_RESTYPE = {"ghm_sampler_create": ctypes.c_void_p, "ghm_sampler_create_edges": ctypes.c_void_p,
-                 "ghm_sampler_destroy": None}
+                 "ghm_sampler_destroy": None, "ghm_sampler_build_id": ctypes.c_char_p}
 
 _hip = None
 _host = None
@@ -186,6 +188,20 @@ def host_lib():
     if _host is None:
         _host = _load(HOST_LIB, HOST_SIGNATURES, _HOST_RESTYPE)
     return _host
+
+
+def check_build_id():
+    """The source hash both loaded libraries were built from, checked against the
+    tree this process runs in (ghmclip/_buildid.py); raises on a mismatch (a
+    stale or foreign binary).  Returns the id."""
+    from ._buildid import source_build_id
+    want = source_build_id()
+    got = hip_lib().ghm_build_id().decode()
+    got_host = host_lib().ghm_sampler_build_id().decode()
+    if got != want or got_host != want:
+        raise RuntimeError(f"native libraries were built from other sources: libghm_hip {got}, "
+                           f"libghm_host {got_host}, tree {want} (run `make`)")
+    return got
 
 
 def check(rc, what):

@@ -315,6 +315,12 @@ class DoubleSampler:
         self.i_templ = _templates(self.i_transition, n_childs[1])
         self._zs = None
 
+    def _p_y(self, tree):
+        """The root prior of the text (0) or image (1) tree, as the reference builds
+        each GHMTree with p_ys[0] / p_ys[1] (data_random_GHM.py:665-666, 762-764,
+        860-861, 908-909) and BP_CLS combines it with the root message (:213)."""
+        return np.asarray(self.p_ys[tree], np.float64)
+
     def _native_sampler(self, K):
         return NativeClipSampler(self.t_tables, self.i_tables, self.variable_type, K)
 
@@ -387,17 +393,15 @@ class ClipSampler(DoubleSampler):
         if guide:
             tg = guided_targets(self.t_templ if self.t_templ is not None else self.t_tables, tl, device)
             ig = guided_targets(self.i_templ if self.i_templ is not None else self.i_tables, il, device)
-            p_y = np.ones(self.variable_type) / self.variable_type
-            tp = bp_cls_posterior(self.t_tables, tl, p_y)
-            ip = bp_cls_posterior(self.i_tables, il, p_y)
+            tp = bp_cls_posterior(self.t_tables, tl, self._p_y(0))
+            ip = bp_cls_posterior(self.i_tables, il, self._p_y(1))
         return [to(tl), to(tr), tg, tp], [to(il), to(ir), ig, ip]
 
     def get_Bayes(self, n_eval=10000):
         """:786-817 — exact Bayes CLIP loss from BP posteriors (host, once per run)."""
         tl, _, il, _ = self.draw_numpy(n_eval)
-        p_y = np.ones(self.variable_type) / self.variable_type
-        tp = bp_cls_posterior(self.t_tables, tl, p_y).T
-        ip = bp_cls_posterior(self.i_tables, il, p_y).T
+        tp = bp_cls_posterior(self.t_tables, tl, self._p_y(0)).T
+        ip = bp_cls_posterior(self.i_tables, il, self._p_y(1)).T
         return PPCLIPLoss(tp, ip, n_eval, self.K, self.variable_type)
 
 
@@ -482,8 +486,7 @@ class ConditionalDenoiseSampler(DoubleSampler):
 
     def posterior(self, tl, z):
         """(text BP_CLS posteriors [V, B], image BP_DNS posterior means [B, T])."""
-        p_y = np.ones(self.variable_type) / self.variable_type
-        t_pp = bp_cls_posterior(self.t_tables, tl, p_y).T
+        t_pp = bp_cls_posterior(self.t_tables, tl, self._p_y(0)).T
         ext = bp_cls_root_message(self.t_tables, tl)
         return t_pp, bp_dns_posterior(self.i_tables, np.asarray(z).T, self.sigma, ext).T
 
@@ -498,9 +501,8 @@ class ConditionalDenoiseSampler(DoubleSampler):
         float32); guide=False: None (the fused CdmTrainer step computes its targets
         on the device, ghm_bp_dns_msgs / ghm_bp_cls)."""
         tl, root, z, il = self.draw_numpy(batch_size)
-        p_y = np.ones(self.variable_type) / self.variable_type
         t_levels = _bp_levels(self.t_tables, tl)
-        t_pp = bp_cls_posterior(self.t_tables, tl, p_y).T
+        t_pp = bp_cls_posterior(self.t_tables, tl, self._p_y(0)).T
         hd, qd, bu, root_bu, post = bp_dns_levels(self.i_tables, np.asarray(z).T, self.sigma, t_levels[-1][0])
         post = post.T
         t_info = i_info = None
@@ -655,9 +657,8 @@ class NextWordPredictSampler(DoubleSampler):
         guide=True: (posteriors, image posteriors, text guide targets (the 2L + 1
         arrays of bp_nwp_posterior), image guide targets (GHMTree.guided_info of the
         image tree: L float32 [B, T, V]))."""
-        p_y = np.ones(self.variable_type) / self.variable_type
         ext = bp_cls_root_message(self.i_tables, il)
-        i_pp = bp_cls_posterior(self.i_tables, il, p_y)
+        i_pp = bp_cls_posterior(self.i_tables, il, self._p_y(1))
         if not guide:
             return bp_nwp_posterior(self.t_tables, tl, ext), i_pp
         post, tg = bp_nwp_posterior(self.t_tables, tl, ext, guide=True)

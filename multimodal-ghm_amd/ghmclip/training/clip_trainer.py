@@ -17,6 +17,7 @@ Design:
   layers' backward runs, then the rest) before the optimizer.
 """
 import ctypes
+import weakref
 import os
 
 import numpy as np
@@ -79,6 +80,13 @@ def dp_bucket_ranges(bucket_a, n):
     a = [(ta, tb), (ia, ib)]
     b = [(tb, ia), (ib, n)]
     return [r for r in a if r[1] > r[0]], [r for r in b if r[1] > r[0]]
+
+
+def _destroy_events(evs):
+    lib = _native.hip_lib()
+    for ev in evs.values():
+        lib.ghm_event_destroy(ev)
+    evs.clear()
 
 
 class ClipTrainer:
@@ -173,6 +181,7 @@ class ClipTrainer:
         # idle queue, a satisfied one 5.7 (tools/xq_latency.py, profiles/r4_xq_report.txt)
         self.fast_events = int(os.environ.get("GHM_FAST_EVENTS", "2"))
         self._evs = {}
+        self._ev_fin = None
         # data-parallel timing (bench.py): None, or a list that each step appends
         # (bucket A ms, bucket B ms, exposed ms) event triples to
         self.comm_timing = None
@@ -348,11 +357,20 @@ class ClipTrainer:
     def _event(self, key):
         ev = self._evs.get(key)
         if ev is None:
+            if self._ev_fin is None:  # destroy the native events with the trainer (or at close())
+                self._ev_fin = weakref.finalize(self, _destroy_events, self._evs)
+                self._ev_fin.atexit = False  # not from interpreter shutdown (the HIP runtime may be gone)
             ev = _native.hip_lib().ghm_event_create(self.fast_events)
             if not ev:
                 _native.check(-1, "ghm_event_create")
             self._evs[key] = ev = ctypes.c_void_p(ev)
         return ev
+
+    def close(self):
+        """Release the native cross-stream events (also done when the trainer is
+        garbage collected)."""
+        if self._ev_fin is not None:
+            self._ev_fin()
 
     def _order(self, producer, consumer, key):
         """consumer waits for the work enqueued on producer so far."""
@@ -503,17 +521,20 @@ class ClipTrainer:
     def _dp(self):
         return self.pg is not None or distributed.is_on()
 
-    def set_tokens(self, t_tokens, i_tokens):
+    def set_tokens(self, t_tokens, i_tokens, alias=False):
         """Stage one batch (uint8 [n_seq, T] host-pinned or device tensors) into
         the plans' token buffers, async on the current stream (the side stream
-        is ordered after it by the fork of each phase).  An eager step reads a
-        contiguous uint8 device tensor of the right shape in place (the bench's
-        HBM ring: no copy kernel at the head of the step); graph replays read the
-        plans' own buffers, whose addresses the graphs hold."""
+        is ordered after it by the fork of each phase); the caller may reuse its
+        tensors as soon as this returns (stream-ordered copies).  alias=True (the
+        bench's HBM ring): an eager step reads a contiguous uint8 device tensor of
+        the right shape in place instead -- no copy kernel at the head of the step
+        -- and the caller must then leave the tensor unmodified until the step
+        has completed on the GPU.  Graph replays always read the plans' own
+        buffers, whose addresses the graphs hold."""
         for plan, t in ((self.plans[0], t_tokens), (self.plans[1], i_tokens)):
             own = plan.token_buf
-            if (self.graphs is None and t.device == own.device and t.dtype == torch.uint8 and t.is_contiguous()
-                    and t.shape == own.shape):
+            if (alias and self.graphs is None and t.device == own.device and t.dtype == torch.uint8
+                    and t.is_contiguous() and t.shape == own.shape):
                 plan.tokens = t
             else:
                 plan.tokens = own

@@ -328,3 +328,38 @@ def test_sguided_flags_and_blocks_match_reference_layout():
     # upward layers: h, q one block back, u from 2 n_t V = 20 upwards
     assert [[b[3] for b in blocks[k] if b[0] == "i"] for k in range(5, 9)] == [[40, 50, 20], [30, 40, 30],
                                                                                [20, 30, 40], [10, 20, 50]]
+
+
+@pytest.mark.parametrize("kind", ["cdm", "vlm", "clip"])
+def test_cls_posteriors_use_each_trees_root_prior(kind):
+    """The BP_CLS posteriors a sampler returns use the tree's own root prior p_ys[0]
+    (text) / p_ys[1] (image), as the reference's GHMTree(p_ys[k]) + BP_CLS
+    (data_random_GHM.py:213, 665-666, 860-861, 908-909): with a non-uniform prior
+    the posterior is the uniform-prior one reweighted by p_y and renormalised, on
+    the same draws (the roots are drawn uniformly either way)."""
+    from ghmclip import ClipSampler, ConditionalDenoiseSampler, NextWordPredictSampler, seed_everything
+    rng = np.random.RandomState(3)
+    pt, pi = rng.dirichlet(np.ones(10)), rng.dirichlet(np.ones(10))
+
+    def draw(p_ys):
+        seed_everything(11)
+        if kind == "cdm":
+            s = ConditionalDenoiseSampler([3, 3], [3, 3], p_ys, [0.2, 0.2], sigma=1)
+            (_, _, _, tpp), _ = s.get_batch(6)
+            return [(tpp, 0)]
+        if kind == "vlm":
+            s = NextWordPredictSampler([3, 3], [3, 3], p_ys, [0.2, 0.2])
+            _, (_, _, _, ipp) = s.get_batch(6)
+            return [(ipp.T, 1)]
+        s = ClipSampler([3, 3], [3, 3], p_ys, [0.2, 0.2], K=2)
+        (_, _, _, tp), (_, _, _, ip) = s.get_batch("cpu", 6, guide=True)
+        return [(tp, 0), (ip, 1)]
+
+    uni = draw([P_Y, P_Y])
+    non = draw([pt, pi])
+    for (u, k), (n, _) in zip(uni, non):
+        u, n = np.asarray(u, np.float64), np.asarray(n, np.float64)
+        prior = (pt, pi)[k].reshape(-1, 1) if u.shape[0] == 10 else (pt, pi)[k].reshape(1, -1)
+        w = u * prior
+        axis = 0 if u.shape[0] == 10 else 1
+        np.testing.assert_allclose(n, w / w.sum(axis=axis, keepdims=True), rtol=1e-9, atol=1e-12)

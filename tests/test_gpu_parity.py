@@ -240,13 +240,14 @@ def test_step_bit_identical_across_runs(precision):
 
 def test_qkv_backward_unperturbed_beside_weight_gradient():
     """The QKV backward on fixed inputs gives bit-identical outputs while the
-    weight-gradient kernel runs on another stream.  k_qkv_bwd_x3 reads the
-    forward's LN1 statistics with a system-scope load (round 4; rounds 2-3
-    recomputed them from H): a plain load of that buffer gave wrong 16-token
-    row groups in 2 of 14 / 39 of 39 repetitions under this aggressor and an
-    agent-scope load in 32 of 39, the system-scope load in none of 92
-    (tools/race_probe.py, profiles/r3_probe.txt, r4_*_probe_xcc.txt; DESIGN.md
-    section 4 "Determinism")."""
+    weight-gradient kernel runs on another stream.  k_qkv_bwd_x3 recomputes
+    the LN1 statistics from H (rounds 2-3 and again from round 5; round 4 read
+    them with a system-scope load): a plain load of the forward's statistics
+    buffer gave wrong 16-token row groups in 2 of 14 / 39 of 39 repetitions under
+    this aggressor and an agent-scope load in 32 of 39; with no mechanism known
+    the product path does not read that buffer here (tools/race_probe.py,
+    profiles/r3_probe.txt, r4_*_probe_xcc.txt; DESIGN.md section 4
+    "Determinism")."""
     import ctypes
     from ghmclip import _native
     sampler, tr = _trainer(5, 128, 0.2, precision="x3")

@@ -1,9 +1,11 @@
 """Sequential VLM (BASELINE config 5) on the HIP path vs the CPU oracle and the
 reference's own fixtures (tests/golden/make_golden_vlm.py).
 
-The VLM's projections are fp32 library GEMMs (rocBLAS / hipBLASLt) and its other
-operators hand-written kernels (csrc/ghm_vlm.hip); tolerances: forward 2e-5 and
-gradients 1e-4 relative to the tensor's max-abs, losses 2e-5 relative."""
+Every VLM projection runs on the hand-written GEMM template of csrc/ghm_gemm.hip
+(`ghm_gemm_x3` split-bf16, or `ghm_gemm_f32` exact-f32 MFMA in the f32 mode; no
+library GEMM), attention and the other operators on csrc/ghm_vlm.hip /
+ghm_vlm_x3.hip; tolerances: forward 2e-5 and gradients 1e-4 relative to the
+tensor's max-abs, losses 2e-5 relative (f32 mode; x3 as stated per test)."""
 import os
 
 import numpy as np

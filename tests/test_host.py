@@ -29,6 +29,89 @@ def test_hip_library_exports_every_declared_symbol():
     assert set(names) == set(_native.HIP_SIGNATURES), "ctypes table out of sync with ghm_hip.h"
 
 
+def _prototypes(header):
+    """name -> list of parameter types (ctypes) of every declaration in the header."""
+    import ctypes
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//.*", "", src)
+    scalar = {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+              "double": ctypes.c_double, "uint32_t": ctypes.c_uint32, "int32_t": ctypes.c_int32}
+    out = {}
+    for m in re.finditer(r"\b(ghm_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src):
+        params = [p.strip() for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
+        types = []
+        for p in params:
+            p = re.sub(r"\b(const|struct)\b", "", p).strip()
+            types.append(ctypes.c_void_p if "*" in p else scalar[p.split()[0]])
+        out[m.group(1)] = types
+    return out
+
+
+@pytest.mark.parametrize("header,table", [("ghm_hip.h", "HIP_SIGNATURES"), ("ghm_sampler.h", "HOST_SIGNATURES")])
+def test_ctypes_table_matches_header_prototypes(header, table):
+    """Every ctypes argtypes list has the header's arity and parameter types
+    (pointer -> c_void_p, int64_t -> c_int64, ...), so no caller can shift an
+    argument into the wrong slot."""
+    from ghmclip import _native
+    protos = _prototypes(header)
+    sigs = getattr(_native, table)
+    assert set(protos) == set(sigs)
+    for name, want in protos.items():
+        got = sigs[name]
+        assert len(got) == len(want) and all(a is b for a, b in zip(got, want)), name
+
+
+def test_integration_doc_bindings_match_header():
+    """The reference-side bindings shown in INTEGRATION.md (`_lib.<fn>.argtypes = ...`
+    and the calls `_lib.<fn>(...)` / `_h.<fn>(...)`) have the header's arity and
+    types: the doc fails this test as soon as it drifts from include/*.h."""
+    import ast
+    import ctypes
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", doc, flags=re.S)
+    assert blocks
+    protos = {**_prototypes("ghm_hip.h"), **_prototypes("ghm_sampler.h")}
+    n_argtypes = n_calls = 0
+    for code in blocks:
+        tree = ast.parse(code)
+        for node in ast.walk(tree):
+            if (isinstance(node, ast.Assign) and isinstance(node.targets[0], ast.Attribute)
+                    and node.targets[0].attr == "argtypes"):
+                name = node.targets[0].value.attr
+                got = eval(compile(ast.Expression(node.value), "doc", "eval"), {"ctypes": ctypes})
+                want = protos[name]
+                assert len(got) == len(want) and all(a is b for a, b in zip(got, want)), name
+                n_argtypes += 1
+            if (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                    and isinstance(node.func.value, ast.Name) and node.func.value.id in ("_lib", "_h")
+                    and node.func.attr.startswith("ghm_")):
+                name = node.func.attr
+                nargs = 0
+                for a in node.args:  # *x[i:j] with constant bounds counts j - i arguments
+                    if isinstance(a, ast.Starred):
+                        sl = a.value.slice
+                        nargs += sl.upper.value - sl.lower.value
+                    else:
+                        nargs += 1
+                if name in protos:
+                    assert nargs == len(protos[name]), f"{name}: {nargs} args"
+                    n_calls += 1
+    assert n_argtypes >= 1 and n_calls >= 4
+
+
+def test_libraries_carry_the_source_build_id():
+    """Both libraries were built from the sources of this tree (the hash the
+    Makefile baked in == the hash recomputed here); smoke() and bench.py make the
+    same check on the GPU box."""
+    from ghmclip import _native
+    from ghmclip._buildid import source_build_id, source_files
+    files = source_files()
+    assert "Makefile" in files and any(f.endswith("ghm_x3.hip") for f in files)
+    assert any(f.endswith("ghm_hip.h") for f in files)
+    assert _native.check_build_id() == source_build_id()
+
+
 def test_host_library_exports_every_declared_symbol():
     import ctypes
     from ghmclip import _native
