@@ -415,34 +415,56 @@ def time_mlp_bwd_in_graph(trainer, replays=10, serial=True):
 def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     """The oracle (PyTorch-CPU restatement) timed on the box's host CPUs, twice:
     with the GPU job's CPU share ($OMP_NUM_THREADS, 16 per GPU on the pool; the
-    headline `value`) and with every host CPU (os.cpu_count(), BASELINE.md §3.2,
-    fewer steps: `all_cores`)."""
+    headline `value`) and with os.cpu_count() threads (BASELINE.md §3.2 "all host
+    cores", `all_cores`: fewer steps, and given up after a warm-up step slower than
+    30 s -- on a box whose job is held to a 16-CPU share, os.cpu_count() threads
+    oversubscribe that share).  Progress goes to stderr step by step."""
     host_cpus = os.cpu_count() or 1
     share = min(host_cpus, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = host_cpus
     out = _cpu_baseline_at(share, B, L, steps, guide, workload)
     out["host_cpus"] = host_cpus
+    out["affinity_cpus"] = usable
     out["cores_note"] = ("cores = threads used for value: the GPU job's CPU share on the box ($OMP_NUM_THREADS, 16 "
                          "per GPU); all_cores = the same restatement on os.cpu_count() threads")
     if host_cpus > share:
-        allc = _cpu_baseline_at(host_cpus, B, L, max(2, steps // 2), guide, workload)
-        out["all_cores"] = {"value": allc["value"], "cores": host_cpus, "sample": allc["sample"]}
+        allc = _cpu_baseline_at(host_cpus, B, L, max(2, steps // 4), guide, workload, warmup_limit_s=30.0)
+        out["all_cores"] = {k: allc[k] for k in ("value", "cores", "sample") if k in allc}
     torch.set_num_threads(share)
     return out
 
 
-def _cpu_baseline_at(threads, B, L, steps, guide, workload):
+def _cpu_baseline_at(threads, B, L, steps, guide, workload, warmup_limit_s=None):
     from oracle import ghm_oracle as O
     torch.set_num_threads(threads)
     cores = {"cores": threads}
+
+    def timed(tr):
+        t0 = time.time()
+        tr.step()  # warm-up
+        w = time.time() - t0
+        log(f"cpu baseline ({threads} threads): warm-up step {w:.2f} s")
+        if warmup_limit_s is not None and w > warmup_limit_s:
+            return None, w
+        t0 = time.time()
+        for k in range(steps):
+            tr.step()
+            log(f"cpu baseline ({threads} threads): step {k + 1}/{steps}, {time.time() - t0:.2f} s")
+        return (time.time() - t0) / steps, w
+
+    def skipped(w):
+        return {"value": None, "unit": "samples/s", **cores, "kind": "port",
+                "sample": f"not measured: the warm-up step took {w:.1f} s on {threads} threads (> {warmup_limit_s} s)"}
     if workload in ("cdm", "cdm_joint", "cdm_guided"):
         from oracle import cdm_oracle as CO
         joint = workload != "cdm"
         tr = CO.OracleCdmJointTrainer(B=B, L=L) if joint else CO.OracleCdmTrainer(B=B, L=L, n_bayes=0)
-        tr.step()
-        t0 = time.time()
-        for _ in range(steps):
-            tr.step()
-        dt = (time.time() - t0) / steps
+        dt, w = timed(tr)
+        if dt is None:
+            return skipped(w)
         note = (" (unguided: the oracle has no guided step; guidance adds BP messages and 26 small penalty "
                 "blocks)" if workload == "cdm_guided" else "")
         return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
@@ -454,11 +476,9 @@ def _cpu_baseline_at(threads, B, L, steps, guide, workload):
         from oracle import vlm_oracle as VO
         jt = workload != "vlm"
         tr = VO.OracleVlmJointTrainer(B=B, L=L) if jt else VO.OracleVlmTrainer(B=B, L=L)
-        tr.step()
-        t0 = time.time()
-        for _ in range(steps):
-            tr.step()
-        dt = (time.time() - t0) / steps
+        dt, w = timed(tr)
+        if dt is None:
+            return skipped(w)
         return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
                 "sample": f"{steps} steps (after 1 warm-up) of the {'joint' if jt else 'sequential'} "
                           f"{'(unguided: the oracle has no guided VLM step) ' if workload == 'vlm_guided' else ''}"
@@ -466,11 +486,9 @@ def _cpu_baseline_at(threads, B, L, steps, guide, workload):
                           f"(oracle/vlm_oracle.py, host BP posteriors included); {dt:.3f} s/step"}
     tr = (O.OracleTrainer(p=0.2, B=B, L=L, lr_max=1e-3, lr_min=1e-6, guide=True, penalty=1e-3) if guide
           else O.OracleTrainer(p=0.2, B=B, L=L))
-    tr.step()  # warm-up
-    t0 = time.time()
-    for _ in range(steps):
-        tr.step()
-    dt = (time.time() - t0) / steps
+    dt, w = timed(tr)
+    if dt is None:
+        return skipped(w)
     return {"value": round(B / dt, 3), "unit": "samples/s", **cores, "kind": "port",
             "sample": f"{steps} steps (after 1 warm-up) of the {'guided' if guide else 'default'} CLIP config, B={B}, fp32 "
                       f"PyTorch-CPU restatement of the reference (oracle/ghm_oracle.py); "

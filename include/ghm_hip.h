@@ -25,7 +25,8 @@ const char* ghm_last_error_string(void);
 /* 1 when the library was built for gfx950 and a device is visible, else 0. */
 int ghm_device_ok(void);
 /* 16 hex digits: the hash of the sources this library was built from
- * (multimodal-ghm_amd/csrc/*, include/*.h, Makefile; ghmclip/_buildid.py).
+ * (every file of multimodal-ghm_amd/csrc, the headers in include, the Makefile;
+ * ghmclip/_buildid.py).
  * smoke() and bench.py require it to equal the hash of the tree they run in. */
 const char* ghm_build_id(void);
 /* Cross-stream ordering (the two-tower step's fork / join / cross waits,
@@ -221,19 +222,23 @@ int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b,
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),
  * dH_mid = dH_out + dLN2 (must not alias dH_out) and part_ln as ghm_mlp_bwd
- * (n_blocks = ghm_mlp_bwd_rc_x3_blocks(M))  —  backward of model.py:741-747,784-788. */
+ * (n_blocks = ghm_mlp_bwd_rc_x3_blocks(M))  —  backward of model.py:741-747,784-788.
+ * split_out 0: G and dU f32 [M][F]; 1: pre-split bf16 planes for
+ * ghm_wgrad_ring_x3's format 2 (hi [M][F] at the pointer, lo [M][F] right after
+ * it: the same bytes), the columns of every 32-group in perm32 order (k-slot
+ * 8g + i holds unit 4g + i for i < 4, 16 + 4g + i - 4 else). */
 int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
-                      const float* ln_b, const void* pack, const float* b1, float* G, float* dU, float* dH_mid,
-                      float* part_ln, int64_t M, int D, int F, void* stream);
+                      const float* ln_b, const void* pack, const float* b1, void* G, void* dU, float* dH_mid,
+                      float* part_ln, int64_t M, int D, int F, int split_out, void* stream);
 /* The same launch with per-workgroup clock stamps for bench.py's in-graph
  * kernel timing: stamps[2 b], stamps[2 b + 1] = s_memrealtime (100 MHz) at
  * workgroup b's start and end, 2 x ghm_mlp_bwd_rc_x3_blocks(M) uint64.  twin
  * (1 or 2) picks one of two identical kernel instantiations, so a profiler
  * trace separates two measurements. */
 int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
-                              const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
-                              float* dH_mid, float* part_ln, int64_t M, int D, int F, uint64_t* stamps,
-                              int twin, void* stream);
+                              const float* ln_b, const void* pack, const float* b1, void* G, void* dU,
+                              float* dH_mid, float* part_ln, int64_t M, int D, int F, int split_out,
+                              uint64_t* stamps, int twin, void* stream);
 /* As ghm_qkv_bwd (backward of model.py:772-775), with the LN1 statistics
  * recomputed from H exactly as the forward computed them (eps = the LayerNorm
  * eps); stats (the forward's [M][2] buffer) is accepted and not read
@@ -272,6 +277,21 @@ int ghm_attn_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const
 int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
                  const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,
                  int tok_per_split, void* stream);
+/* Split-K weight (and bias) gradient partials of the encoder projections on an
+ * LDS-DMA ring with producer / consumer waves (csrc/ghm_wgrad.hip):
+ *   part[z][a][b] = sum_{m in split z} A[m][a] op(B)[m][b], bias_part[z][a] = sum A[m][a]
+ * (bias_part may be NULL), z over ceil(M / tok_per_split) splits, A_cols and
+ * B_cols multiples of 128.  Operand formats: 0 f32 rows of ld elements; 1 (B
+ * only) f32 through LayerNorm with stats [M][2] (mean, rstd), ln_w, ln_b;
+ * 2 pre-split bf16 planes of ghm_mlp_bwd_rc_x3(split_out = 1): hi [M][ld] at
+ * the pointer, lo `plane` elements on, perm32 column order (the output rows /
+ * columns are in natural order).  One operand must be format 0 or 1.  The
+ * weight gradients of model.py:773-775 (dWq|k|v = dqkv^T LN1(H)) and :787-788
+ * (dW2 = dY^T G, db2; dW1 = dU^T LN2(H_mid), db1) under autograd (train_CLIP.py:158). */
+int ghm_wgrad_ring_x3(const void* A, int lda, int A_cols, int a_fmt, int64_t a_plane, const void* B, int ldb,
+                      int B_cols, int b_fmt, int64_t b_plane, const float* stats, const float* ln_w,
+                      const float* ln_b, float* part, float* bias_part, int64_t M, int tok_per_split,
+                      void* stream);
 
 /* ---- guided CLIP (clip_guide=True) ------------------------------------------
  * Exact BP_CLS messages of each sequence's GHM tree (data_random_GHM.py:185-208,

@@ -546,9 +546,14 @@ __device__ __forceinline__ void store_g_du(const float* gv, const float* du, flo
 //   rc_ud:  U = W1[c] LN2(Hmid)^T + b1 (recomputed), dG = W2^T[c] dY^T,
 //           G = GELU(U), dU = dG GELU'(U) -> HBM; returns dU split (dh, dl)
 //   rc_dx2: dX2^T += W1^T[:, c] dU^T
+// SPLITOUT: G and dU leave as pre-split bf16 planes (the weight gradients'
+// WG_SPLIT operands, ghm_wgrad.hip): grow / drow point at the lane's 8 k-slots
+// 32c + 8g .. + 7 of the hi plane (perm32 column order, one 16-B store per plane),
+// the lo plane `plane` elements on; else f32 [M][512] rows at 32c + 4g
+template <bool SPLITOUT>
 __device__ __forceinline__ void rc_ud(const __bf16* cb, const float4* bb, const bf16x8* xh, const bf16x8* xl,
-                                      const bf16x8* yh, const bf16x8* yl, float* grow, float* drow, int t, int g,
-                                      bf16x8& dh, bf16x8& dl) {
+                                      const bf16x8* yh, const bf16x8* yl, void* grow, void* drow, int64_t plane,
+                                      int t, int g, bf16x8& dh, bf16x8& dl) {
   const __bf16* w1h = cb;
   const __bf16* w1l = cb + PLANE;
   const __bf16* w2h = cb + 2 * PLANE;
@@ -576,8 +581,19 @@ __device__ __forceinline__ void rc_ud(const __bf16* cb, const float4* bb, const 
       du[4 * jt + r] = dg[jt][r] * gd;
     }
   }
-  store_g_du(gv, du, grow, drow);
   split8(du, dh, dl);
+  if (SPLITOUT) {
+    bf16x8 gh, gl;
+    split8(gv, gh, gl);
+    __bf16* gp = static_cast<__bf16*>(grow);
+    __bf16* dp = static_cast<__bf16*>(drow);
+    *reinterpret_cast<bf16x8*>(gp) = gh;
+    *reinterpret_cast<bf16x8*>(gp + plane) = gl;
+    *reinterpret_cast<bf16x8*>(dp) = dh;
+    *reinterpret_cast<bf16x8*>(dp + plane) = dl;
+  } else {
+    store_g_du(gv, du, static_cast<float*>(grow), static_cast<float*>(drow));
+  }
 }
 
 // dX2^T tile j: A[d = 16 j + t][k-slot 8 g + i] = W1[unit perm32(8 g + i)][d],
@@ -600,12 +616,12 @@ __device__ __forceinline__ void rc_dx2(const __bf16* cb, bf16x8 dh, bf16x8 dl, f
 // 4-7 one dX2 behind on a 3-buffer ring, so the two waves of a SIMD sit in
 // opposite MFMA / GELU phases (isolated 119 -> 124 us, step +1 %,
 // profiles/r3_ab5).
-template <int NW>
+template <int NW, bool SPLITOUT>
 __device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
                                                 const __bf16* W1n, const __bf16* W2Tn, const float4* bb,
                                                 const bf16x8* xh, const bf16x8* xl, const bf16x8* yh,
-                                                const bf16x8* yl, f32x4* dx, float* grow, float* drow, int t,
-                                                int g, int lane) {
+                                                const bf16x8* yl, f32x4* dx, void* grow, void* drow, int64_t plane,
+                                                int t, int g, int lane) {
   fill_r32t_w8<NW>(W1n, GHM_D, PK_W, nb, nb + PLANE);
   fill_r32_w8<NW>(W2Tn, GHM_D, PK_W, nb + 2 * PLANE, nb + 3 * PLANE);
   bf16x8 dh, dl;
@@ -613,7 +629,7 @@ __device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, _
   // 115.7 us, 186 instead of 226 VGPRs, step -1.2 % (profiles/r3_ab14; the same
   // hint in the MLP forward made the step slower)
   __builtin_amdgcn_iglp_opt(0);
-  rc_ud(cb, bb, xh, xl, yh, yl, grow, drow, t, g, dh, dl);
+  rc_ud<SPLITOUT>(cb, bb, xh, xl, yh, yl, grow, drow, plane, t, g, dh, dl);
   // the dX2 products as a scheduling region of their own, under the same hint:
   // isolated 116.1 -> 113.1 us, step unchanged (4.12 / 4.12 ms, r3_sr / r3_ab20)
   __builtin_amdgcn_sched_barrier(0);
@@ -627,7 +643,7 @@ __device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, _
 // of each workgroup writes the 100 MHz constant clock (s_memrealtime) at its
 // start and after its last store to stamps[2 blockIdx.x + {0, 1}]; the launch
 // spans min(start) .. max(end).  Nothing else differs.
-template <int NW, int STAMP = 0>
+template <int NW, int STAMP = 0, bool SPLITOUT = false>
 __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
     const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
@@ -696,9 +712,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
     issue_fence();
     const int cn = c + 1 < NC ? c + 1 : NC - 1;  // branch-free: the last iteration refills chunk NC-1
-    mlp_bwd_rc_iter<NW>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
-                        W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, Gout + mc * GHM_F + 32 * c + 4 * g,
-                        dU + mc * GHM_F + 32 * c + 4 * g, t, g, lane);
+    void* grow = SPLITOUT ? static_cast<void*>(reinterpret_cast<__bf16*>(Gout) + mc * GHM_F + 32 * c + 8 * g)
+                          : static_cast<void*>(Gout + mc * GHM_F + 32 * c + 4 * g);
+    void* drow = SPLITOUT ? static_cast<void*>(reinterpret_cast<__bf16*>(dU) + mc * GHM_F + 32 * c + 8 * g)
+                          : static_cast<void*>(dU + mc * GHM_F + 32 * c + 4 * g);
+    mlp_bwd_rc_iter<NW, SPLITOUT>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
+                                  W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, grow, drow, M * GHM_F, t, g, lane);
     // retire this iteration's LDS-DMA fills: vmcnt(0), also covering the G / dU
     // stores issued after them (see k_ln_mlp_fwd_x3b).  Storing them one chunk
     // later instead, so this wait would not cover fresh stores, measured slower
@@ -1763,22 +1782,45 @@ extern "C" int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M) {
   return (M + tok - 1) / tok;
 }
 
+template <int NW, int STAMP, bool SPLITOUT>
+static void mlp_bwd_rc_launch(unsigned nblk, hipStream_t s, const float* dH_out, const float* H_mid,
+                              const float* stats, const float* ln_w, const float* ln_b, const void* pack,
+                              const float* b1, void* G, void* dU, float* dH_mid, float* part_ln, int64_t M,
+                              uint64_t* stamps) {
+  hipLaunchKernelGGL((k_mlp_bwd_rc_x3<NW, STAMP, SPLITOUT>), dim3(nblk), dim3(64 * NW), 0, s, dH_out, H_mid,
+                     reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
+                     static_cast<float*>(G), static_cast<float*>(dU), dH_mid, part_ln, M, stamps);
+}
+template <int STAMP>
+static void mlp_bwd_rc_dispatch(int64_t M, int split_out, hipStream_t s, const float* dH_out, const float* H_mid,
+                                const float* stats, const float* ln_w, const float* ln_b, const void* pack,
+                                const float* b1, void* G, void* dU, float* dH_mid, float* part_ln,
+                                uint64_t* stamps) {
+  const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
+  if (rc_waves(M) == 8) {
+    if (split_out)
+      mlp_bwd_rc_launch<8, STAMP, true>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    else
+      mlp_bwd_rc_launch<8, STAMP, false>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+  } else {
+    if (split_out)
+      mlp_bwd_rc_launch<4, STAMP, true>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    else
+      mlp_bwd_rc_launch<4, STAMP, false>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+  }
+}
+
 extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const float* stats, const float* ln_w,
-                                 const float* ln_b, const void* pack, const float* b1, float* G, float* dU,
-                                 float* dH_mid, float* part_ln, int64_t M, int D, int F, void* stream) {
+                                 const float* ln_b, const void* pack, const float* b1, void* G, void* dU,
+                                 float* dH_mid, float* part_ln, int64_t M, int D, int F, int split_out,
+                                 void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln, "null pointer");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  GHM_CHECK(split_out == 0 || split_out == 1, "split_out");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
-  const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
-  if (rc_waves(M) == 8)
-    hipLaunchKernelGGL(k_mlp_bwd_rc_x3<8>, dim3(nblk), dim3(512), 0, ghm_stream(stream), dH_out, H_mid,
-                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
-                       G, dU, dH_mid, part_ln, M);
-  else
-    hipLaunchKernelGGL(k_mlp_bwd_rc_x3<4>, dim3(nblk), dim3(256), 0, ghm_stream(stream), dH_out, H_mid,
-                       reinterpret_cast<const float2*>(stats), ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), b1,
-                       G, dU, dH_mid, part_ln, M);
+  mlp_bwd_rc_dispatch<0>(M, split_out, ghm_stream(stream), dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid,
+                         part_ln, nullptr);
   return ghm_launch_status();
 }
 
@@ -1786,33 +1828,20 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
 // per-workgroup clock stamps (2 x ghm_mlp_bwd_rc_x3_blocks(M) uint64).
 extern "C" int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid, const float* stats,
                                          const float* ln_w, const float* ln_b, const void* pack, const float* b1,
-                                         float* G, float* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
-                                         uint64_t* stamps, int twin, void* stream) {
+                                         void* G, void* dU, float* dH_mid, float* part_ln, int64_t M, int D, int F,
+                                         int split_out, uint64_t* stamps, int twin, void* stream) {
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln && stamps,
             "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
+  GHM_CHECK(split_out == 0 || split_out == 1, "split_out");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
   GHM_CHECK(twin == 1 || twin == 2, "twin must be 1 or 2");
-  const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
-  const float2* st = reinterpret_cast<const float2*>(stats);
-  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
   hipStream_t s = ghm_stream(stream);
-  if (rc_waves(M) == 8) {
-    if (twin == 1)
-      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, 1>), dim3(nblk), dim3(512), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
-                         dU, dH_mid, part_ln, M, stamps);
-    else
-      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<8, 2>), dim3(nblk), dim3(512), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
-                         dU, dH_mid, part_ln, M, stamps);
-  } else {
-    if (twin == 1)
-      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, 1>), dim3(nblk), dim3(256), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
-                         dU, dH_mid, part_ln, M, stamps);
-    else
-      hipLaunchKernelGGL((k_mlp_bwd_rc_x3<4, 2>), dim3(nblk), dim3(256), 0, s, dH_out, H_mid, st, ln_w, ln_b, pk, b1, G,
-                         dU, dH_mid, part_ln, M, stamps);
-  }
+  if (twin == 1)
+    mlp_bwd_rc_dispatch<1>(M, split_out, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, stamps);
+  else
+    mlp_bwd_rc_dispatch<2>(M, split_out, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, stamps);
   return ghm_launch_status();
 }
 

@@ -51,6 +51,21 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def perm32(q):
+    """k-slot q of a 32-group of the MLP backward's split G / dU planes holds unit
+    perm32(q) (csrc/ghm_x3.hip perm32)."""
+    base, r = q & ~31, q & 31
+    return base + (4 * ((r >> 3) & 3) + (r & 3) if (r & 7) < 4 else 16 + 4 * ((r >> 3) & 3) + (r & 3))
+
+
+def inv_perm32_index(device):
+    """index tensor idx with natural[:, u] = permuted[:, idx[u]] over 512 units."""
+    inv = [0] * D_HIDDEN
+    for q in range(D_HIDDEN):
+        inv[perm32(q)] = q
+    return torch.tensor(inv, dtype=torch.long, device=device)
+
+
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -134,7 +149,17 @@ class EncoderPlan:
                          and os.environ.get("GHM_LONG_ATTN", "x3") == "f32")
         if self.attn_f32 and self.act:
             raise NotImplementedError("GHM_LONG_ATTN=f32 (the exact torch validation attention) is softmax only")
-        if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2)
+        # x3 weight gradients on the LDS-DMA ring kernel (ghm_wgrad_ring_x3, producer /
+        # consumer waves) instead of ghm_wgrad_x3: $GHM_WGRAD_RING bit mask, 1 | 2 = dW2
+        # and dW1 (the MLP backward then writes G / dU as pre-split planes), 4 = dWq|k|v.
+        # Default 0: isolated the ring is faster (33.3 / 39.9 / 32.7 vs 42.3 / 45.3 /
+        # 35.8 us) but the two-tower step slower (4.19-4.21 vs 4.05-4.09 ms, r5_ring4:
+        # its 130-150 KB of LDS hold a whole CU)
+        ring = int(os.environ.get("GHM_WGRAD_RING", "0")) if self.precision == "x3" else 0
+        self.wgrad_ring = bool(ring & 3)      # dW2 / dW1 on the ring, G / dU pre-split
+        self.wgrad_ring_qkv = bool(ring & 4)  # dWq|k|v on the ring
+        if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2): f32 [M][512], or the
+            # bf16 hi / lo planes [2][M][512] of the ring path in the same bytes
             self.G, self.Dg = e(M, D_HIDDEN), None
         else:
             self.G, self.Dg = e(L, M, D_HIDDEN), e(L, M, D_HIDDEN)
@@ -198,6 +223,17 @@ class EncoderPlan:
             npk = int(_native.GHM_SPLIT_PACK_ELEMS)
             self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
         self._gen = 0
+
+    def mlp_scratch_f32(self, name="G"):
+        """The MLP backward's G or dU scratch as f32 [M][512] in natural column
+        order (inspection / tests): the ring path stores them as bf16 hi / lo
+        planes with the columns of each 32-group in perm32 order."""
+        t = getattr(self, name)
+        if not self.wgrad_ring:
+            return t
+        planes = t.view(torch.bfloat16).view(2, self.M, D_HIDDEN).float()
+        v = planes[0] + planes[1]
+        return v[:, inv_perm32_index(v.device)]
 
     def probs_dense(self, l):
         """Layer l's attention probabilities [n_seq, T, T] (inspection helper)."""
@@ -468,7 +504,8 @@ class EncoderPlan:
             if x3:  # recomputes U; writes G (scratch) and dU
                 args = (_ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                         _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]), _ptr(p[f"_mlps.{l}.0.bias"]),
-                        _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN)
+                        _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN,
+                        int(self.wgrad_ring))
                 if getattr(self, "stamps", None) is not None:  # bench.py's in-graph timing
                     c("ghm_mlp_bwd_rc_x3_stamped", *args, _ptr(self.stamps[l]), self.stamp_twin, s)
                 else:
@@ -480,13 +517,22 @@ class EncoderPlan:
             nb2 = self.nblk_rc if (x3 and self.mlp_rc) else self.nblk
             jobs.append(J(P_ln2, nb2, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
-            c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G if self.mlp_rc else self.G[l]), D_HIDDEN, D_HIDDEN, 0,
-              None, None, None, _ptr(P_w2), _ptr(P_b2), M, tps, s)
+            if self.wgrad_ring:  # dY f32 (format 0) x G pre-split (format 2)
+                c("ghm_wgrad_ring_x3", _ptr(cur), D_MODEL, D_MODEL, 0, 0, _ptr(self.G), D_HIDDEN, D_HIDDEN, 2,
+                  M * D_HIDDEN, None, None, None, _ptr(P_w2), _ptr(P_b2), M, tps, s)
+            else:
+                c(wgrad, _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G if self.mlp_rc else self.G[l]), D_HIDDEN,
+                  D_HIDDEN, 0, None, None, None, _ptr(P_w2), _ptr(P_b2), M, tps, s)
             jobs += [J(P_w2, ns, [g[f"_mlps.{l}.2.weight"]]), J(P_b2, ns, [g[f"_mlps.{l}.2.bias"]])]
             tps, ns = self.wg["w1"]  # dW1[hid][in] = sum dU[m][hid] LN2(Hmid)[m][in]; db1 = sum dU
-            c(wgrad, _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
-              _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
-              _ptr(P_w1), _ptr(P_b1), M, tps, s)
+            if self.wgrad_ring:  # dU pre-split (format 2) x LN2(Hmid) (format 1)
+                c("ghm_wgrad_ring_x3", _ptr(self.dU), D_HIDDEN, D_HIDDEN, 2, M * D_HIDDEN, _ptr(self.Hmid[l]),
+                  D_MODEL, D_MODEL, 1, 0, _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                  _ptr(p[f"_lns_2.{l}.bias"]), _ptr(P_w1), _ptr(P_b1), M, tps, s)
+            else:
+                c(wgrad, _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
+                  _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
+                  _ptr(P_w1), _ptr(P_b1), M, tps, s)
             jobs += [J(P_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(P_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
             if self.attn_f32:
@@ -505,9 +551,14 @@ class EncoderPlan:
                 c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
                   _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
-            c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
-              _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-              _ptr(P_wq), None, M, tps, s)
+            if self.wgrad_ring_qkv:  # dqkv f32 (format 0) x LN1(H) (format 1)
+                c("ghm_wgrad_ring_x3", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, 0, 0, _ptr(self.H[l]), D_MODEL,
+                  D_MODEL, 1, 0, _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+                  _ptr(P_wq), None, M, tps, s)
+            else:
+                c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
+                  _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+                  _ptr(P_wq), None, M, tps, s)
             jobs.append(J(P_wq, ns, [g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"],
                                              g[f"_values.{l}.weight"]]))
             if x3:

@@ -186,6 +186,7 @@ class ClipTrainer:
         # (bucket A ms, bucket B ms, exposed ms) event triples to
         self.comm_timing = None
         self._bwd_it = [None, None]  # the towers' running backward launch generators
+        self._pending = []  # started data-parallel collectives (distributed.allreduce_ranges_start)
         self._setup_guide(penalty, guide_trans)
 
     def _setup_guide(self, penalty, guide_trans):
@@ -436,13 +437,14 @@ class ClipTrainer:
         # the schedule the graphs were captured with (bench.py replays them with the
         # towers on one stream, where _early() would say no)
         early = self._early() if graphs is None else ("flush", 0) in graphs
-        if not dp and early:
+        if early:  # the upper layers' partials reduced on the comm stream, off the towers' paths
             self._phase(lambda t: self._bwd_a_gen(t, flush=False), graphs, "bwd_a", fork=False, join=False)
             _, s0, s1 = self._tower_streams()
             for t, st in ((1, s1), (0, s0)):  # each tower's upper partials, after its bwd_a, on the comm stream
                 self._order(st, self.comm, ("early", t))
                 with torch.cuda.stream(self.comm):
                     self._single(self.plans[t].flush_pending, graphs, ("flush", t))
+        if early and not dp:
             # one join on the main stream's path: the comm stream (its early
             # reductions long done) waits for the side tower, the main stream for
             # the comm stream -- instead of two waits in series on the main stream
@@ -454,13 +456,25 @@ class ClipTrainer:
             self._phase(self._bwd_gen, graphs, "bwd", fork=False)
             self._order(self.comm, main, "loss_join")
         else:
+            # data parallel, the same schedule: bucket A (the top layers' gradients,
+            # final once both towers' upper partials are reduced) is all-reduced on the
+            # comm stream right behind those reductions while the towers run their
+            # lower layers; bucket B after the backward; the collectives are started
+            # asynchronously (the host goes on issuing the towers' launches, with gloo
+            # too) and waited for before the optimizer
             ev = [] if self.comm_timing is not None else None
-            self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a", fork=False, join=False)
             bucket_a, bucket_b = self.dp_buckets()
-            self._allreduce_ranges(bucket_a, ev, both=True)
+            if early:
+                self._allreduce_async(bucket_a, ev)  # the comm stream already follows both towers
+            else:
+                self._phase(lambda t: self._bwd_a_gen(t, flush=True), graphs, "bwd_a", fork=False, join=False)
+                self._allreduce_async(bucket_a, ev, after=self._tower_streams()[1:])
             self._phase(self._bwd_b_gen, graphs, "bwd_b", fork=False)
-            self._allreduce_ranges(bucket_b, ev)
             main = torch.cuda.current_stream()
+            self._allreduce_async(bucket_b, ev, after=(main,))
+            with torch.cuda.stream(self.comm):
+                distributed.allreduce_finish(self._pending)
+            self._pending = []
             if ev is not None:  # exposed: the main stream's wait for the collectives after its backward
                 ev.append(torch.cuda.Event(enable_timing=True))
                 ev[-1].record(main)
@@ -485,24 +499,28 @@ class ClipTrainer:
         B = the rest."""
         return dp_bucket_ranges(self.bucket_a, self.n_params)
 
-    def _allreduce_ranges(self, ranges, ev=None, both=False):
-        """Mean over ranks of gflat[a:b] for each range, issued on the comm
-        stream after the work already queued on the current stream (both: and on
-        the side tower's stream), so the towers' streams run on while the
-        collective is in flight.  ev: a list to append the collective's start /
-        end events (comm stream) to."""
+    def _allreduce_async(self, ranges, ev=None, after=()):
+        """Start the mean over ranks of gflat[a:b] for each range on the comm stream,
+        after the work already queued on the streams in `after`; the pending
+        collectives are finished (waited for, scaled) before the optimizer.  ev
+        (bench.py's timing mode): a list to append the bucket's start / end events
+        on the comm stream to -- the bucket is then finished right away, so the
+        end event follows the collective (the towers' streams run on either way)."""
         comm = self.comm
-        comm.wait_stream(torch.cuda.current_stream())
-        if both:
-            comm.wait_stream(self._tower_streams()[2])
+        for st in after:
+            if st != comm:
+                comm.wait_stream(st)
         with torch.cuda.stream(comm):
             if ev is not None:
                 ev.append(torch.cuda.Event(enable_timing=True))
                 ev[-1].record(comm)
-            distributed.allreduce_ranges_mean_(self.gflat, ranges, group=self.pg)
+            pend = distributed.allreduce_ranges_start(self.gflat, ranges, group=self.pg)
             if ev is not None:
+                distributed.allreduce_finish(pend)
+                pend = []
                 ev.append(torch.cuda.Event(enable_timing=True))
                 ev[-1].record(comm)
+        self._pending += pend
 
     def comm_stats(self):
         """Per-step averages (ms) of the recorded data-parallel timing: bucket A
@@ -577,7 +595,7 @@ class ClipTrainer:
         for t in (0, 1):
             graphs[("fwd", t)] = pieces(self._fwd_gen(t))
         graphs["loss"] = one(self._loss)
-        if not dp and self._early():
+        if self._early():  # one process or data parallel: the same early-reduce schedule
             for t in (0, 1):
                 graphs[("bwd_a", t)] = pieces(self._bwd_a_gen(t, flush=False))
                 graphs[("flush", t)] = one(self.plans[t].flush_pending)

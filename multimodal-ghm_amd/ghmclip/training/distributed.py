@@ -77,20 +77,37 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+def allreduce_ranges_start(flat, ranges, group=None):
+    """Start the mean over ranks of flat[a:b] for each (a, b) of `ranges`, in order
+    (the bucketed gradient all-reduce of ClipTrainer.step): one SUM collective per
+    bucket with async_op=True, issued by every rank with the same ranges.  Returns
+    the pending (work, view, world) triples for allreduce_finish, which waits for
+    each and applies the 1/world scale.  Overlap: RCCL enqueues the collective on
+    its own stream behind the caller's current (comm) stream and the host returns
+    at once; gloo runs it on a background thread and returns at once too, so the
+    towers' later launches are issued (and run) while it is in flight in both
+    backends.  Each element is the SUM of the ranks' values times 1/world; at world
+    2 that sum is one addition, so bucketed == flat bit for bit
+    (tests/test_dp_gloo.py); beyond 2 ranks a ring may add an element's terms in an
+    order that depends on its chunk, which can change its last bit (the same on
+    every rank; the world-4 test bounds it)."""
+    import torch.distributed as dist
+    n = dist.get_world_size(group)
+    return [(dist.all_reduce(flat[a:b], op=dist.ReduceOp.SUM, group=group, async_op=True), flat[a:b], n)
+            for a, b in ranges]
+
+
+def allreduce_finish(pending):
+    """Wait for allreduce_ranges_start's collectives (the current stream is ordered
+    after each) and scale each bucket by 1/world, on the current stream."""
+    for work, view, n in pending:
+        work.wait()
+        view.mul_(1.0 / n)
+
+
 def allreduce_ranges_mean_(flat, ranges, group=None):
-    """allreduce_mean_ of flat[a:b] for each (a, b) of `ranges`, in order: one
-    collective per bucket, issued by every rank with the same ranges (the
-    bucketed gradient all-reduce of ClipTrainer.step).  Each element is still
-    the SUM of the ranks' values times 1/world; at world 2 that sum is one
-    addition, so bucketed == flat bit for bit (tests/test_dp_gloo.py); beyond 2
-    ranks a ring may add an element's terms in an order that depends on its
-    chunk, which can change its last bit (the same on every rank).  Overlap: on
-    RCCL the collective is enqueued on the caller's (comm) stream and the host
-    returns at once, so the towers' later launches run beside it; gloo's
-    all_reduce blocks the host until done, so the gloo-based data-parallel tests
-    check the bucketed arithmetic and the stream ordering, not that overlap."""
-    for a, b in ranges:
-        allreduce_mean_(flat[a:b], group=group)
+    """allreduce_mean_ of flat[a:b] for each (a, b) of `ranges`: start + finish."""
+    allreduce_finish(allreduce_ranges_start(flat, ranges, group))
     return flat
 
 

@@ -115,7 +115,8 @@ def test_encoder_forward_stages(T, nseq, precision):
     if plan.mlp_rc:  # the backward recomputes U: its G scratch ends with layer 0's GELU(U)
         emb.sum().backward()
         torch.cuda.synchronize()
-        assert _rel(plan.G[:M].view(nseq, T, 512), want["G"][0]) < tol, "G[0] (recomputed)"
+        G = plan.mlp_scratch_f32("G")  # (hi + lo of the ring path's split planes, natural columns)
+        assert _rel(G[:M].view(nseq, T, 512), want["G"][0]) < tol, "G[0] (recomputed)"
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
@@ -267,14 +268,19 @@ def test_qkv_backward_unperturbed_beside_weight_gradient():
     for _ in range(15):
         sa.wait_stream(torch.cuda.current_stream())
         sb.wait_stream(torch.cuda.current_stream())
+        def aggressor():  # the product's dW2 launch (the ring kernel on the split G planes)
+            if p1.wgrad_ring:
+                _native.call("ghm_wgrad_ring_x3", P(p1.H[l + 1]), 128, 128, 0, 0, P(p1.G), 512, 512, 2, M * 512,
+                             None, None, None, P(p1.part_w2), P(p1.part_b2), M, tps, B)
+            else:
+                _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
+                             P(p1.part_w2), P(p1.part_b2), M, tps, B)
         for _ in range(3):
-            _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
-                         P(p1.part_w2), P(p1.part_b2), M, tps, B)
+            aggressor()
         _native.call("ghm_qkv_bwd_x3", P(dqkv), P(p0.H[l]), P(p0.st1[l]), P(w0[f"_lns_1.{l}.weight"]),
                      P(p0.pack[l]), P(dHmid), P(outH), P(outP), M, 128, p0.eps, A)
         for _ in range(3):
-            _native.call("ghm_wgrad_x3", P(p1.H[l + 1]), 128, 128, P(p1.G), 512, 512, 0, None, None, None,
-                         P(p1.part_w2), P(p1.part_b2), M, tps, B)
+            aggressor()
         torch.cuda.synchronize()
         got = (outH.clone(), outP.clone())
         if ref is None:

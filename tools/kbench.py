@@ -86,7 +86,8 @@ def main():
                                gf(4 * M * 128 * 512)),
             "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
-                                        P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512, sp),
+                                        P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512,
+                                        int(plan.wgrad_ring), sp),
                               gf(6 * M * 128 * 512)),
             "qkv_bwd_x3": (lambda: c("ghm_qkv_bwd_x3", P(plan.dqkv), P(plan.H[l]), P(plan.st1[l]), P(p["_lns_1.0.weight"]), pk,
                                      P(plan.dH[1]), P(plan.dH[0]), P(plan.part_ln), M, 128, plan.eps, sp),
@@ -102,6 +103,16 @@ def main():
             "wgrad_qkv_x3": (lambda: c("ghm_wgrad_x3", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2,
                                        P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                        P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
+            # the ring weight gradients (ghm_wgrad_ring_x3) on the MLP backward's split G / dU planes
+            "wgrad_ring_w2": (lambda: c("ghm_wgrad_ring_x3", P(plan.H[l + 1]), 128, 128, 0, 0, P(plan.G), 512, 512,
+                                        2, M * 512, None, None, None, P(plan.part_w2), P(plan.part_b2), M, tps_w2,
+                                        sp), gf(2 * M * 128 * 512)),
+            "wgrad_ring_w1": (lambda: c("ghm_wgrad_ring_x3", P(plan.dU), 512, 512, 2, M * 512, P(plan.Hmid[l]), 128,
+                                        128, 1, 0, P(plan.st2[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+                                        P(plan.part_w1), P(plan.part_b1), M, tps_w1, sp), gf(2 * M * 128 * 512)),
+            "wgrad_ring_qkv": (lambda: c("ghm_wgrad_ring_x3", P(plan.dqkv), 384, 384, 0, 0, P(plan.H[l]), 128, 128,
+                                         1, 0, P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
+                                         P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
         })
     kernels.update({
         "reduce_w2": (lambda: plan._reduce(plan.part_w2, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),

@@ -155,7 +155,7 @@ def main():
         if aggr == "mlp_bwd":
             c("ghm_mlp_bwd_rc_x3", P(p1.H[l + 1]), P(p1.Hmid[l]), P(p1.st2[l]), P(w1[f"_lns_2.{l}.weight"]),
               P(w1[f"_lns_2.{l}.bias"]), P(p1.pack[l]), P(w1[f"_mlps.{l}.0.bias"]), P(p1.G), P(p1.dU), P(xH), P(xP),
-              M, 128, 512, B)
+              M, 128, 512, 0, B)
         elif aggr == "fwd_mlp":
             c("ghm_ln_mlp_fwd_x3b", P(p1.Hmid[l]), P(w1[f"_lns_2.{l}.weight"]), P(w1[f"_lns_2.{l}.bias"]),
               P(p1.pack[l]), P(w1[f"_mlps.{l}.0.bias"]), P(w1[f"_mlps.{l}.2.bias"]), P(xH),
