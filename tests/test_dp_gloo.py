@@ -235,3 +235,73 @@ def test_flat_layout_unequal_towers():
                 ly = _layer_of(name)
                 in_a = lo <= off and off + k <= hi
                 assert in_a == (ly is not None and ly >= m.n_layer - min(top, m.n_layer)), (top, name)
+
+
+def _world4_worker(rank, world, port, B, K, out):
+    """A strong split of the global batch over `world` ranks (B / world rows of
+    every block per rank, pipeline.shard_rows), the per-rank oracle gradient, and
+    the product's bucketed asynchronous all-reduce (distributed.allreduce_ranges_start
+    / allreduce_finish: both buckets started before either is waited for, as
+    ClipTrainer.step issues bucket A while the lower layers' backward runs)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "multimodal-ghm_amd")]
+    from ghmclip.training import distributed
+    from ghmclip.training.pipeline import shard_rows
+    from oracle import ghm_oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    s = O.ClipSamplerOracle([3, 3], [3, 3], [0.2, 0.2], K=K, seedtree=42)
+    O.seed_everything(224)
+    tm, im = O.build_encoders(27, 1, 16)
+    batch = s.get_batch(B)  # every rank draws the same global batch
+    idx = shard_rows(B, K + 1, rank, world)
+    t = tm(torch.as_tensor(batch[0][idx]))[0]
+    i = im(torch.as_tensor(batch[2][idx]))[0]
+    loss = O.clip_loss(t, i, K, B // world)
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in list(tm.parameters()) + list(im.parameters())])
+    n = g.numel()
+    pa = distributed.allreduce_ranges_start(g, [(0, n // 3)])
+    pb = distributed.allreduce_ranges_start(g, [(n // 3, n)])
+    lt = loss.detach().reshape(1).clone()
+    distributed.allreduce_mean_(lt)
+    distributed.allreduce_finish(pa + pb)
+    allg = [torch.empty_like(g) for _ in range(world)]
+    dist.all_gather(allg, g)
+    if rank == 0:
+        out.put((g.numpy(), float(lt.item()), [x.numpy() for x in allg]))
+    dist.destroy_process_group()
+
+
+def test_world4_strong_split_equals_one_rank():
+    """World 4, global B = 128 split into 32 rows per rank (review
+    item 5): the mean over ranks of the shard losses and gradients equals the
+    1-rank full-batch loss and gradient to the ring-order bound (4-term sums in a
+    rank-order-dependent association: 1e-5 relative per element, 2e-7 on the
+    loss), and every rank ends with the same bytes."""
+    from oracle import ghm_oracle as O
+    B, K, world = 128, 4, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_world4_worker, args=(r, world, port, B, K, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    g_dp, loss_dp, per_rank = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for x in per_rank:
+        assert x.tobytes() == g_dp.tobytes()
+    s = O.ClipSamplerOracle([3, 3], [3, 3], [0.2, 0.2], K=K, seedtree=42)
+    O.seed_everything(224)
+    tm, im = O.build_encoders(27, 1, 16)
+    batch = s.get_batch(B)
+    loss = O.clip_loss(tm(torch.as_tensor(batch[0]))[0], im(torch.as_tensor(batch[2]))[0], K, B)
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in list(tm.parameters()) + list(im.parameters())]).numpy()
+    assert abs(loss_dp - loss.item()) <= 2e-7 * abs(loss.item())
+    scale = np.abs(g).max()
+    assert np.abs(g_dp - g).max() <= 1e-5 * scale
