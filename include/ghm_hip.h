@@ -474,7 +474,8 @@ int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float* dH_mid, f
  * applied at :485 for the CDM): act 1 relu, 2 gelu of the scaled score,
  * elementwise (no row normalisation; masked entries 0); gelu writes GELU'(score)
  * to Pd (same shape as P) for the backward, which takes dS = act'(score) dA /
- * scale_div.  D == 128 (the joint CDM at T = 162 under train_CDNS.py --activation). */
+ * scale_div.  D == 128 (the joint CDM at T = 162 under train_CDNS.py --activation) or
+ * 256 (the VLM, AutoRegressiveTransformer(activation="relu"), model.py:163, 287). */
 int ghm_attn_ext_fwd_x3_act(const float* qkv, const float* H, float* H_mid, float* P, float* Pd, int64_t n_seq,
                             int T, int D, int n_prefix, float scale_div, float dbl, int act, void* stream);
 int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const float* dH_mid, float* dS,

@@ -512,26 +512,15 @@ void launch_fwd_n(unsigned g, hipStream_t s, const float* qkv, const float* H, f
                      npre, sd, dbl, Pd);
 }
 
-template <int ACT>
-void launch_fwd_act(int T, unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P,
-                    float* Pd, int npre, float sd, float dbl) {
-  if (T <= 32) launch_fwd_n<1, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-  else if (T <= 64) launch_fwd_n<2, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-  else if (T <= 96) launch_fwd_n<3, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-  else if (T <= 128) launch_fwd_n<4, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-  else if (T <= 160) launch_fwd_n<5, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-  else launch_fwd_n<6, 128, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
-}
-
-template <int DD>
+template <int DD, int ACT = VACT_SOFTMAX>
 void launch_fwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int npre,
-                float sd, float dbl) {
-  if (T <= 32) launch_fwd_n<1, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 64) launch_fwd_n<2, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 96) launch_fwd_n<3, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 128) launch_fwd_n<4, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else if (T <= 160) launch_fwd_n<5, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);
-  else launch_fwd_n<6, DD>(g, s, qkv, H, Hm, P, T, npre, sd, dbl);  // D = 256: spills 5-12 VGPRs (correct, slower)
+                float sd, float dbl, float* Pd = nullptr) {
+  if (T <= 32) launch_fwd_n<1, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 64) launch_fwd_n<2, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 96) launch_fwd_n<3, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 128) launch_fwd_n<4, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else if (T <= 160) launch_fwd_n<5, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);
+  else launch_fwd_n<6, DD, ACT>(g, s, qkv, H, Hm, P, T, npre, sd, dbl, Pd);  // D = 256: spills 5-12 VGPRs (correct, slower)
 }
 
 template <int NKT, int DD, int ACT = VACT_SOFTMAX>
@@ -544,26 +533,15 @@ void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, c
                      dqkv, T, npre, dbl);
 }
 
-template <int ACT>
-void launch_bwd_act(int T, unsigned g, hipStream_t s, const float* qkv, const float* P, const float* Pd,
-                    const float* dHm, float* dS, float* dqkv, int npre, float sd, float dbl) {
-  if (T <= 32) launch_bwd_n<1, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-  else if (T <= 64) launch_bwd_n<2, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-  else if (T <= 96) launch_bwd_n<3, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-  else if (T <= 128) launch_bwd_n<4, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-  else if (T <= 160) launch_bwd_n<5, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-  else launch_bwd_n<6, 128, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
-}
-
-template <int DD>
+template <int DD, int ACT = VACT_SOFTMAX>
 void launch_bwd(int T, unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
-                float* dqkv, int npre, float sd, float dbl) {
-  if (T <= 32) launch_bwd_n<1, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
-  else if (T <= 64) launch_bwd_n<2, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
-  else if (T <= 96) launch_bwd_n<3, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
-  else if (T <= 128) launch_bwd_n<4, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
-  else if (T <= 160) launch_bwd_n<5, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
-  else launch_bwd_n<6, DD>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl);
+                float* dqkv, int npre, float sd, float dbl, const float* Pd = nullptr) {
+  if (T <= 32) launch_bwd_n<1, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 64) launch_bwd_n<2, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 96) launch_bwd_n<3, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 128) launch_bwd_n<4, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else if (T <= 160) launch_bwd_n<5, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
+  else launch_bwd_n<6, DD, ACT>(g, s, qkv, P, dHm, dS, dqkv, T, npre, sd, dbl, Pd);
 }
 
 }  // namespace
@@ -613,11 +591,17 @@ extern "C" int ghm_attn_ext_fwd_x3_act(const float* qkv, const float* H, float* 
                                        void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
   GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
-  GHM_CHECK(D == 128 && T >= 1 && T <= 192, "shape (D == 128, T <= 192)");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  if (act == VACT_RELU) launch_fwd_act<VACT_RELU>(T, g, ghm_stream(stream), qkv, H, H_mid, P, Pd, n_prefix, scale_div, dbl);
-  else launch_fwd_act<VACT_GELU>(T, g, ghm_stream(stream), qkv, H, H_mid, P, Pd, n_prefix, scale_div, dbl);
+  hipStream_t s = ghm_stream(stream);
+  if (D == 128) {
+    if (act == VACT_RELU) launch_fwd<128, VACT_RELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+    else launch_fwd<128, VACT_GELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+  } else {  // D = 256: the VLM (AutoRegressiveTransformer(activation=...), model.py:163, 287)
+    if (act == VACT_RELU) launch_fwd<256, VACT_RELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+    else launch_fwd<256, VACT_GELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+  }
   return ghm_launch_status();
 }
 
@@ -626,12 +610,16 @@ extern "C" int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const f
                                        float scale_div, float dbl, int act, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
-  GHM_CHECK(D == 128 && T >= 1 && T <= 192, "shape (D == 128, T <= 192)");
+  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  if (act == VACT_RELU)
-    launch_bwd_act<VACT_RELU>(T, g, ghm_stream(stream), qkv, P, Pd, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
-  else
-    launch_bwd_act<VACT_GELU>(T, g, ghm_stream(stream), qkv, P, Pd, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  hipStream_t s = ghm_stream(stream);
+  if (D == 128) {
+    if (act == VACT_RELU) launch_bwd<128, VACT_RELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+    else launch_bwd<128, VACT_GELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+  } else {
+    if (act == VACT_RELU) launch_bwd<256, VACT_RELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+    else launch_bwd<256, VACT_GELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+  }
   return ghm_launch_status();
 }

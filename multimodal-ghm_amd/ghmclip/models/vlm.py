@@ -88,7 +88,7 @@ EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
 
 class VlmPlan:
     def __init__(self, n_layer, n_token, n_seq, n_prefix=1, num_class=10, n_embd=256, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None, joint=False):
+                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax"):
         if n_embd not in (128, 256, 512):
             raise ValueError(f"the HIP VLM kernels take n_embd in (128, 256, 512) (got {n_embd})")
         self.L, self.T, self.N, self.P, self.V, self.D = n_layer, n_token, n_seq, n_prefix, num_class, n_embd
@@ -102,6 +102,12 @@ class VlmPlan:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         if self.precision == "x3" and n_embd not in (128, 256):
             raise ValueError(f"the split-bf16 VLM kernels take n_embd in (128, 256) (got {n_embd})")
+        # attention activation (model.py:121-130): softmax, or relu on the split-bf16
+        # kernels (gelu of the -inf-masked scores is NaN in the reference: refused)
+        if activation not in ("softmax", "relu") or (activation == "relu" and self.precision != "x3"):
+            raise NotImplementedError(f"HIP VLM attention: softmax, or relu with precision x3 (got {activation}, "
+                                      f"{self.precision})")
+        self.act = 1 if activation == "relu" else 0
         if n_token > 192 or (n_token > 96 and self.precision != "x3"):
             raise ValueError(f"the HIP attention kernels take sequences of <= 96 tokens, <= 192 with the split-bf16 "
                              f"(x3) kernels (got {n_token}, precision {self.precision})")
@@ -195,8 +201,12 @@ class VlmPlan:
                   _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, s)
             else:
                 self._gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
-                c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.Pm[l]),
-                  N, T, D, self.P, self.scale_div, 1.0 / D, s)
+                if self.act:  # relu(score) (model.py:287), masked entries 0
+                    c("ghm_attn_ext_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                      _ptr(self.Pm[l]), None, N, T, D, self.P, self.scale_div, 1.0 / D, self.act, s)
+                else:
+                    c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
+                      _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, 1.0 / D, s)
             c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
             self._gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
@@ -266,8 +276,12 @@ class VlmPlan:
                     self._gemm(0, 0, EPI_RESID, d, D, (w,), D, 0, self.dX, D, M, D, D, bias=self.zero_b, R=self.dX,
                                ldr=D, s=s)
             else:
-                c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS),
-                  _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
+                if self.act:  # dS = [P > 0] dA / scale_div
+                    c("ghm_attn_ext_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.Pm[l]), None, _ptr(nxt),
+                      _ptr(self.dS), _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, self.act, s)
+                else:
+                    c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS),
+                      _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
                 self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D, gqkv, D, s)
                 self._dgrad(self.dqkv, 3 * D, wqkv, D, 3 * D, s)
             c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
@@ -308,7 +322,7 @@ def vlm_guide_blocks(model, n_text, V):
     the leaf, text root, text upward, image).  Text block k (k-th text-guided
     layer): k = 0 the leaf q at columns index_q; 0 < k <= n_t the (h, q) pair at
     (index_h, index_q); k > n_t the u at index_u; image blocks at index_i."""
-    n_t, n_i, P = model.n_t_guided_layer, model.n_i_guided_layer, model.n_i_token
+    n_t, P = model.n_t_guided_layer, model.n_i_token
     n_tplanes = 3 * n_t + 1
     tplane = lambda k: n_text * V * k  # noqa: E731
     iplane = lambda j: n_text * V * n_tplanes + P * V * j  # noqa: E731
@@ -357,8 +371,15 @@ def _guided_slices(model, n_text):
 
 
 def vlm_guide_plane_elems(model, n_text, V):
-    """Floats per sample of the guide target planes (vlm_guide_planes)."""
-    return n_text * V * (3 * model.n_t_guided_layer + 1) + model.n_i_token * V * model.n_i_guided_layer
+    """Floats per sample of the guide target planes (vlm_guide_planes): the text
+    blocks, then (joint model) one [n_i_token][V] plane per image-guided layer.  The
+    sequential model's image guides all target the frozen CLIP feature
+    (train_sequential_NWP.py:165), which the fused trainer reads from the CLIP
+    encoder's output in place: no image planes."""
+    n = n_text * V * (3 * model.n_t_guided_layer + 1)
+    if not model.sequential:
+        n += model.n_i_token * V * sum(model.i_guided_layer_flag)
+    return n
 
 
 class _VlmFn(torch.autograd.Function):
@@ -425,8 +446,9 @@ class AutoRegressiveTransformer(nn.Module):
     covers the configurations the VLM experiments train: sequential
     (exp_vlm_{standard,shallow}TF.sh: a frozen-CLIP image feature prefix token, T = 81)
     and joint (exp_vlm_jointtrain.sh: the 81 image leaves through i_embedding as the
-    prefix, T = 161, split-bf16 only); prefix-causal mask, softmax attention,
-    LayerNorm, MLP, no guide; n_embd in (128, 256, 512) (joint: 128, 256)."""
+    prefix, T = 161, split-bf16 only); prefix-causal mask, softmax attention (relu on
+    the split-bf16 kernels), LayerNorm, MLP; guide=True for both (train_NWP.py /
+    train_sequential_NWP.py --guide=True); n_embd in (128, 256, 512) (joint: 128, 256)."""
 
     def __init__(self, n_token=9, n_i_token=4, num_class=10, n_embd=128, n_layer=12, n_guided_layers=(3, 3),
                  n_head=4, n_mlp_hidden=512, activation="softmax", mlp=True, normalize_attn=True,
@@ -451,11 +473,8 @@ class AutoRegressiveTransformer(nn.Module):
         self.n_t_guided_layer = n_guided_layers[0]
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[0] * 2 + 1)
-        if activation != "softmax" or not mlp or not layernorm:
-            raise NotImplementedError("HIP VLM: softmax attention, mlp=True, layernorm=True")
-        if guide and sequential:
-            raise NotImplementedError("HIP VLM: guide=True is built for the joint model (train_NWP.py, "
-                                      "exp_vlm_guidedTF.sh)")
+        if activation not in ("softmax", "relu") or not mlp or not layernorm:
+            raise NotImplementedError("HIP VLM: softmax or relu attention, mlp=True, layernorm=True")
         if not auto_regressive or (sequential and n_i_token != 1):
             raise NotImplementedError("HIP VLM: auto_regressive=True; sequential=True takes one prefix token "
                                       "(train_sequential_NWP.py), sequential=False the image leaves "
@@ -505,7 +524,8 @@ class AutoRegressiveTransformer(nn.Module):
             self._plans.clear()
             self._plans[key] = VlmPlan(self.n_layer, T, n_seq, n_prefix=P, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
-                                       precision=self.precision, joint=not self.sequential)
+                                       precision=self.precision, joint=not self.sequential,
+                                       activation=self.activation)
         return self._plans[key]
 
     def forward(self, xt, zi):

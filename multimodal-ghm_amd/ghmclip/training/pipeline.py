@@ -167,21 +167,24 @@ class NwpBatchPipeline(BatchPipeline):
     """The same producer for NextWordPredictSampler draws: text inputs / targets
     uint8 [B, T-1], the exact next-word posteriors float32 [B, T-1, V] (host BP,
     bp_nwp_posterior) and image leaves uint8 [B, T]; guide=True also the packed
-    BP guide targets float32 [B, n] (vlm_guide_planes: train_NWP.py --guide=True).
+    BP guide targets float32 [B, n] (vlm_guide_planes: train_NWP.py --guide=True;
+    image_guide=False packs the text blocks only: train_sequential_NWP.py, whose
+    image guides target the CLIP feature on the device).
     sampler: the NextWordPredictSampler (its native MT state already pulled from
     numpy).  row_slice: optional (rank, world) — a contiguous 1/world of the
     samples (the VLM loss is a mean over samples, model.py:1087-1098)."""
 
-    def __init__(self, sampler, batch_size, n_slots=3, row_slice=None, guide=False):
+    def __init__(self, sampler, batch_size, n_slots=3, row_slice=None, guide=False, image_guide=True):
         self.sampler = sampler
         self.guide = guide
+        self.image_guide = image_guide
         super().__init__(sampler.native, batch_size, n_slots, row_slice)
 
     def _make_slots(self, n_slots):
         B, T, Ti, V = self.B, self.s.T_t, self.s.T_i, self.sampler.variable_type
         self.T = T
         L = self.sampler.n_layers
-        ng = (T - 1) * V * (3 * L[0] + 1) + Ti * V * L[1] if self.guide else 0
+        ng = (T - 1) * V * (3 * L[0] + 1) + (Ti * V * L[1] if self.image_guide else 0) if self.guide else 0
 
         def slot():
             return (_host_buffer((B, T - 1), torch.uint8), _host_buffer((B, T - 1), torch.uint8),
@@ -203,7 +206,7 @@ class NwpBatchPipeline(BatchPipeline):
         if self.guide:
             p, _, tg, ig = self.sampler.posterior(tl, il.numpy(), guide=True)
             post.numpy()[:] = p
-            vlm_guide_planes(tg, ig, self.sampler.variable_type, out=gt.numpy())
+            vlm_guide_planes(tg, ig if self.image_guide else [], self.sampler.variable_type, out=gt.numpy())
         else:
             post.numpy()[:] = self.sampler.posterior(tl, il.numpy())[0]
 

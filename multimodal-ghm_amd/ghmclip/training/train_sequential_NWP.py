@@ -10,7 +10,11 @@ image encoder, AutoRegressiveTransformer forward/backward, next-token cross
 entropy, KL "Compare" against the exact BP posterior, clip and AdamW; the
 native sampler and the host BP posteriors run in a producer thread.
 Differences, by design:
-  * --device must be a HIP device; guide=True is not built (NotImplementedError);
+  * --device must be a HIP device;
+  * --guide=True: the producer thread computes the text BP guide targets on the
+    host (bp_nwp_posterior(guide=True)) and stages them with the batch; the image
+    guides target the frozen CLIP feature on the device (:165); penalties and
+    their gradients run inside the fused step (VlmTrainer guide branch);
   * checkpoints are read with the weights-only unpickler, and the saved 'loss'
     entry is a plain dict (type, penalty, guide) instead of the pickled module;
   * wandb/s3fs are optional (skipped with a warning when not installed);
@@ -56,8 +60,6 @@ def parse(argv=None):
 
 def main(argv=None):
     c = parse(argv)
-    if c.guide:
-        raise NotImplementedError("guided VLM (guide=True) is not built on the HIP path yet")
     ws, rank, device = distributed.setup()
     if ws == 1:
         print(f"Using GPU: {torch.cuda.get_device_name(0)}")
@@ -126,17 +128,18 @@ def main(argv=None):
     sched = [get_lr_cosine_schedule(i, c.lr_max, c.lr_min, c.warmup_iters, c.total_iters)
              for i in range(c.total_iters)]
     trainer = VlmTrainer(model, clip_image_model, c.batch_size // ws, sched, max_norm=c.max_norm, device=device,
-                         t_offset=t_offset)
+                         t_offset=t_offset, penalty=c.penalty)
     if t_offset:
         trainer.load_optimizer_state(optimizer)
     sampler.native.pull_numpy_state()  # the producer owns numpy's MT stream from here on
-    pipe = NwpBatchPipeline(sampler, c.batch_size, n_slots=3, row_slice=(rank, ws) if ws > 1 else None)
+    pipe = NwpBatchPipeline(sampler, c.batch_size, n_slots=3, row_slice=(rank, ws) if ws > 1 else None,
+                            guide=c.guide, image_guide=False)
 
     def sync_hist(upto):
-        h, ch = trainer.loss_history(upto), trainer.compare_history(upto)
-        h, ch = distributed.mean_histories([h, ch], device)  # every rank
+        h, ph, ch = trainer.loss_history(upto), trainer.ploss_history(upto), trainer.compare_history(upto)
+        h, ph, ch = distributed.mean_histories([h, ph, ch], device)  # every rank
         loss_history[:upto] = h
-        ploss_history[:upto] = h  # guide=False: the penalised loss is the loss
+        ploss_history[:upto] = ph  # equals the loss without guidance
         compare_history[:upto] = ch
 
     def save(iter_num):
@@ -158,10 +161,13 @@ def main(argv=None):
                 sync_hist(iter_num + 1)
                 finish_time = time.time()
                 h = iter_num // 2
+                # the last step's output[1:5] (a collective under DP: every rank logs)
+                pen = distributed.mean_histories([trainer.guide_penalties()], device)[0] if c.guide \
+                    else [0.0, 0.0, 0.0, 0.0]
                 logger.info(f"Iter: {iter_num}, "
                             f"Penalty train loss: {np.mean(ploss_history[h:iter_num]):.4f}, "
                             f"Train loss: {np.mean(loss_history[h:iter_num]):.4f}, "
-                            f"Penalty: [{0:.4f}, {0:.4f}, {0:.4f}, {0:.4f}], "
+                            f"Penalty: [{pen[0]:.4f}, {pen[1]:.4f}, {pen[2]:.4f}, {pen[3]:.4f}], "
                             f"Compare: {np.mean(compare_history[h:iter_num]):.4f},"
                             f"Bayes: {Bayes_loss:.4f}, "
                             f"LR: {lr:.6f}, "

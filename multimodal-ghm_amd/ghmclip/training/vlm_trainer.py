@@ -74,7 +74,8 @@ class VlmTrainer:
         self.T, self.P, self.V = model.n_token, model.n_i_token, model.vocab_size
         self.plan = VlmPlan(model.n_layer, model.n_token, batch_size, n_prefix=model.n_i_token,
                             num_class=model.vocab_size, n_embd=model.n_embd, normalize_attn=model.normalize_attn,
-                            device=self.device, precision=precision, joint=self.joint)
+                            device=self.device, precision=precision, joint=self.joint,
+                            activation=getattr(model, "activation", "softmax"))
         if self.joint:
             self.clip_plan = None
             self.precision = self.plan.precision
@@ -111,17 +112,19 @@ class VlmTrainer:
         self._setup_guide(penalty)
 
     def _setup_guide(self, penalty):
-        """Guided joint VLM (train_NWP.py --guide=True, exp_vlm_guidedTF.sh): the
-        host stages per-position BP targets (bp_nwp_posterior(guide=True) and the
-        image guided_info, packed by vlm_guide_planes); the penalty partials of
-        every guided block (model.py:303-331, 1122-1144) are one launch after the
-        forward, their gradients one launch per guided layer in the backward."""
+        """Guided VLM (train_NWP.py / train_sequential_NWP.py --guide=True,
+        exp_vlm_guidedTF.sh): the host stages per-position BP targets
+        (bp_nwp_posterior(guide=True), and for the joint model the image
+        guided_info, packed by vlm_guide_planes); the penalty partials of every
+        guided block (model.py:303-331, 1122-1144) are one launch after the forward,
+        their gradients one launch per guided layer in the backward.  The sequential
+        model's image blocks target the frozen CLIP feature itself
+        (train_sequential_NWP.py:165: [clip_image_output] * 2), read in place from
+        the CLIP encoder's output [B][V] (no host staging)."""
         self.guide = bool(getattr(self.model, "guide", False))
         self.phist = None
         if not self.guide:
             return
-        if not self.joint or self.precision != "x3":
-            raise NotImplementedError("guided VLM runs on the joint model's split-bf16 path")
         Tt = self.T - self.P
         self.penalty = float(penalty)
         self.gblocks = vlm_guide_blocks(self.model, Tt, self.V)
@@ -141,12 +144,17 @@ class VlmTrainer:
         """Host arrays of ghm_guide_blks_{fwd,bwd}_d (kept alive: graphs replay them)."""
         n = len(items)
         H = (ctypes.c_void_p * n)(*[self.plan.H[l + 1].data_ptr() for l, _ in items])
-        M = (ctypes.c_void_p * n)(*[self.gtgt.data_ptr()] * n)
+        M = (ctypes.c_void_p * n)()
         desc = (ctypes.c_int32 * (6 * n))()
         desc64 = (ctypes.c_int64 * (2 * n))()
-        for k, (_, (tok0, ntok, col, off, _)) in enumerate(items):
+        for k, (_, (tok0, ntok, col, off, grp)) in enumerate(items):
             desc[6 * k:6 * k + 6] = [self.T, tok0, ntok, col, 1, self.V]
-            desc64[2 * k:2 * k + 2] = [self.n_gelems, off]
+            if grp == "loss3" and not self.joint:  # the CLIP feature [B][V] (one prefix token)
+                M[k] = self.clip_plan.emb.data_ptr()
+                desc64[2 * k:2 * k + 2] = [self.V, 0]
+            else:
+                M[k] = self.gtgt.data_ptr()
+                desc64[2 * k:2 * k + 2] = [self.n_gelems, off]
         lst = (H, M, desc, desc64, n)
         self._glists.append(lst)
         return lst
@@ -194,7 +202,8 @@ class VlmTrainer:
     def set_batch(self, xt, yt, post, i_tokens, guide_targets=None):
         """Stage one batch: text inputs / targets uint8 [B, T-1], BP posteriors
         float32 [B, T-1, V], image leaves uint8 [B, 81] (host-pinned or device);
-        guided: the packed guide targets float32 [B, n_gelems] (vlm_guide_planes)."""
+        guided: the packed guide targets float32 [B, n_gelems] (vlm_guide_planes; the
+        sequential model's hold the text blocks only)."""
         self.plan.xt.copy_(xt, non_blocking=True)
         self.yt.copy_(yt, non_blocking=True)
         self.post.copy_(post, non_blocking=True)

@@ -136,10 +136,12 @@ class OracleVlm(nn.Module):
     the (then empty) ModuleLists, t_embedding, i_embedding, per layer q, k, v, ln1,
     mlp, ln2, then _read_out Linear(d -> V) and the unused _out."""
 
-    def __init__(self, n_token, n_i_token=1, num_class=10, n_embd=256, n_layer=9, n_mlp_hidden=1024, sequential=True):
+    def __init__(self, n_token, n_i_token=1, num_class=10, n_embd=256, n_layer=9, n_mlp_hidden=1024, sequential=True,
+                 activation="softmax"):
         super().__init__()
         self.V, self.n_i_token, self.n_embd, self.n_token = num_class, n_i_token, n_embd, n_token
         self.sequential = sequential
+        self.activation = activation  # get_activation (model.py:121-130): softmax / relu
         self.position_embeddings = nn.Embedding(n_token, n_embd)
         self._queries, self._keys, self._values = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
         self._mlps, self._lns_1, self._lns_2 = nn.ModuleList(), nn.ModuleList(), nn.ModuleList()
@@ -177,7 +179,7 @@ class OracleVlm(nn.Module):
             S = torch.matmul(q(H1), k(H1).transpose(-2, -1))  # :329
             S = S + mask  # :333
             S = S / np.sqrt(self.n_embd)  # :335-336
-            A = F.softmax(S, dim=-1)
+            A = F.softmax(S, dim=-1) if self.activation == "softmax" else F.relu(S)  # :287
             Vv = v(H1)
             H = H + torch.einsum("bij,bjd->bid", A, Vv)  # :338
             A = A / H.shape[2]  # :339-340
@@ -205,14 +207,14 @@ class OracleVlmTrainer:
     just before its construction; the script loads a trained CLIP checkpoint)."""
 
     def __init__(self, p=0.2, B=128, L=9, d=256, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
-                 max_norm=1.0, seed=224, seedtree=42, clip_seed=7, n_layer_tree=4, n_child=3):
+                 max_norm=1.0, seed=224, seedtree=42, clip_seed=7, n_layer_tree=4, n_child=3, activation="softmax"):
         self.sampler = NwpSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], seedtree=seedtree)
         T = n_child ** n_layer_tree
         torch.manual_seed(clip_seed)
         self.clip = OracleEncoder(T, 10, 128, 5)
         torch.manual_seed(seed)  # seed_everything(seed) before the model (:120)
         np.random.seed(seed)
-        self.model = OracleVlm(T, 1, 10, d, L, 4 * d)
+        self.model = OracleVlm(T, 1, 10, d, L, 4 * d, activation=activation)
         self.params = list(self.model.parameters())
         self.opt = OracleAdamW(self.params)
         self.B = B

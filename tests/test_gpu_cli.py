@@ -238,3 +238,34 @@ def test_guided_sequential_cdm_cli(tmp_path, monkeypatch, capsys):
     with open(os.path.join(os.path.dirname(ck[0]), "training.log")) as f:
         lines = [ln for ln in f if "Penalty: [" in ln]
     assert lines and "Penalty: [0.00,0.00,0.00,0.00]" not in lines[-1], lines[-1:]
+
+
+def test_guided_sequential_vlm_cli(tmp_path, monkeypatch):
+    """scripts/examples/eg_snwp.sh with --guide=True (shortened: batch 8, 5
+    iterations, log every 2): train_sequential_NWP finds the standard CLIP run
+    (--clip_feature=TF) as its frozen image encoder, trains the guided next-word
+    model (n_guided_layers = [4, 1]: text BP guides, the CLIP feature as the image
+    guide) and writes logs/exp_snwp/<tree>/GT_L9H4D256/ with the penalised loss in
+    ploss_history and the four penalty groups in the log line."""
+    from ghmclip.training import train_CLIP, train_sequential_NWP
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    clip_flags = [f for f in CLIP_FLAGS if not f.startswith(("--p_ttree_flip", "--p_itree_flip"))]
+    train_CLIP.main(clip_flags + ["--p_ttree_flip=0.02", "--p_itree_flip=0.02"])
+    assert len(glob.glob("logs/CLIP/K4_L4C3p2_L4C3p2sc10/TF_L5H4D128_L5H4D128/*/checkpoint.pth")) == 1
+    flags = ["--job_name=exp_snwp", "--clip_feature=TF", "--model_type=TF", "--n_ttree_layer=4", "--n_itree_layer=4",
+             "--n_ttree_child=3", "--n_itree_child=3", "--p_ttree_flip=0.02", "--p_itree_flip=0.02", "--flip_scale=1",
+             "--batch_size=8", "--variable_type=10", "--d_eb=256", "--n_model_layer=9", "--n_head=4",
+             "--layernorm=True", "--normalize_attn=True", "--lr_max=1e-3", "--lr_min=1e-6", "--guide=True",
+             "--total_iters=5", "--penalty=0.001", "--raw=False", "--log_interval=2", "--eval_interval=2"]
+    loss, compare = train_sequential_NWP.main(flags)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/exp_snwp/K4_L4C3p2_L4C3p2sc10/GT_L9H4D256/*/checkpoint.pth")
+    assert len(ck) == 1
+    d = load_checkpoint(ck[0], "cpu")
+    assert d["iter"] == 5 and d["loss"]["guide"] is True
+    np.testing.assert_allclose(d["loss_history"], loss)
+    assert (d["ploss_history"] > d["loss_history"]).all()
+    with open(os.path.join(os.path.dirname(ck[0]), "training.log")) as f:
+        lines = [ln for ln in f if "Penalty: [" in ln]
+    assert lines and "Penalty: [0.0000, 0.0000, 0.0000, 0.0000]" not in lines[-1], lines[-1:]

@@ -65,3 +65,41 @@ def test_guide_planes_layout():
     np.testing.assert_array_equal(blk[:, 7], tg[4][:, :, :V])
     np.testing.assert_array_equal(blk[:, 9], tg[5])
     np.testing.assert_array_equal(pl[:, 13 * n * V:].reshape(B, 4, 81, V)[:, 3], ig[3])
+
+
+def test_sequential_guided_blocks_and_planes():
+    """train_sequential_NWP.py --guide=True (n_guided_layers = [n_ttree_layer, 1],
+    L = 9): every layer text-guided, layers 0 and 3 image-guided (model.py:207-216);
+    text blocks start at token 1 (one prefix token), the two image blocks are
+    columns 0:10 / 10:20 of the prefix row; the packed planes hold the 13 text
+    blocks only (the image targets are the CLIP feature, read on the device)."""
+    from ghmclip import AutoRegressiveTransformer
+    from ghmclip.models.vlm import vlm_guide_blocks, vlm_guide_plane_elems
+    from ghmclip.training.pipeline import NwpBatchPipeline
+    m = AutoRegressiveTransformer(81, 1, 10, 256, 9, [4, 1], 4, 1024, auto_regressive=True, sequential=True,
+                                  guide=True)
+    assert m.t_guided_layer_flag == [True] * 9
+    assert m.i_guided_layer_flag == [True, False, False, True] + [False] * 5
+    blocks = vlm_guide_blocks(m, 80, 10)
+    assert sorted(blocks) == list(range(9))
+    img = [(l, b[:3]) for l in sorted(blocks) for b in blocks[l] if b[4] == "loss3"]
+    assert img == [(0, (0, 1, 0)), (3, (0, 1, 10))]
+    text = [b for l in sorted(blocks) for b in blocks[l] if b[4] != "loss3"]
+    assert all(b[0] == 1 and b[1] == 80 for b in text) and len(text) == 13
+    assert sorted(b[3] for b in text) == [800 * k for k in range(13)]
+    assert vlm_guide_plane_elems(m, 80, 10) == 13 * 800
+    # the joint model keeps one plane per image-guided layer
+    mj = AutoRegressiveTransformer(161, 81, 10, 256, 9, [4, 4], 4, 1024, auto_regressive=True, sequential=False,
+                                   guide=True)
+    assert vlm_guide_plane_elems(mj, 80, 10) == 13 * 800 + 4 * 810
+    pipe = NwpBatchPipeline.__new__(NwpBatchPipeline)
+    pipe.sampler, pipe.guide, pipe.image_guide = _sampler(), True, False
+    pipe.B, pipe.slice = 2, None
+    pipe.s = pipe.sampler.native
+    pipe._make_slots(1)
+    assert tuple(pipe.slots[0][4].shape) == (2, 13 * 800)
+    pipe._fill(0)
+    xt, _, post, il, gt = pipe.slots[0]
+    from ghmclip.data.data_random_GHM import vlm_guide_planes
+    _, _, tg, _ = pipe.sampler.posterior(pipe.tl, il.numpy(), guide=True)
+    np.testing.assert_array_equal(gt.numpy(), vlm_guide_planes(tg, [], 10))
