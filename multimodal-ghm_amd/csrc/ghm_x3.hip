@@ -463,6 +463,240 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
 }
 
 // ---------------------------------------------------------------------------
+// Wave-specialised LN2 + MLP forward (8 waves, 128 tokens per workgroup).
+// The same products as k_ln_mlp_fwd_x3b, scheduled so that the two waves a
+// SIMD holds (waves w and w + 4 of a workgroup sit on one SIMD) are in opposite
+// phases: an M phase (the chunk's down-projection Y += W2(c-1) G(c-1) and the
+// next up-projection U(c) = W1(c) X: 48 MFMAs, 32 operand reads) and a V phase
+// (G(c) = GELU(U(c) + b1) and its split: VALU only).  Waves 0-3 run
+// M(p), V(p), M(p+1), ... and waves 4-7 the same one interval later; the
+// intervals are separated by s_barrier, so the compiler cannot merge the two
+// phases of one wave (the software-pipelined x3b variants of rounds 3-4 lost
+// because the scheduler re-clustered the MFMAs).  Ring: interval pair p (2p,
+// 2p+1) reads slot p & 1 = {W1(p), W2(p-1)}; the fills of pair p + 1 are issued
+// at the start of interval 2p into the other slot, which pair p - 1 released
+// at the barrier ending interval 2p - 1, and retired at the barrier ending
+// interval 2p + 1: the same 64 KB double buffer as x3b.
+// ---------------------------------------------------------------------------
+struct WsState {
+  f32x4 u[2];
+  bf16x8 gh, gl;
+};
+
+// M phase on ring slot cb (W1 hi|lo, W2 hi|lo): Y += W2 G (DOWN) and U = W1 X (UP)
+template <bool DOWN, bool UP>
+__device__ __forceinline__ void ws_mphase(const __bf16* __restrict__ cb, const bf16x8* xh, const bf16x8* xl,
+                                          f32x4* y, WsState& st, int t, int g) {
+  __builtin_amdgcn_iglp_opt(0);  // interleave the operand reads with the MFMAs
+  if (DOWN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = r128_off(16 * j + t, g);
+      y[j] = mfma16_x3(ldsb8(cb + 2 * PLANE + o), ldsb8(cb + 3 * PLANE + o), st.gh, st.gl, y[j]);
+    }
+  }
+  if (UP) {
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      st.u[jt] = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int o = r32_off(16 * jt + t, 4 * s2 + g);
+        st.u[jt] = mfma16_x3(ldsb8(cb + o), ldsb8(cb + PLANE + o), xh[s2], xl[s2], st.u[jt]);
+      }
+    }
+  }
+}
+
+// V phase: G = GELU(U + b1) -> (gh, gl)
+__device__ __forceinline__ void ws_vphase(const float4* bb, WsState& st) {
+  float gv[8], dg[8];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    gv[4 * jt + 0] = st.u[jt][0] + bb[jt].x;
+    gv[4 * jt + 1] = st.u[jt][1] + bb[jt].y;
+    gv[4 * jt + 2] = st.u[jt][2] + bb[jt].z;
+    gv[4 * jt + 3] = st.u[jt][3] + bb[jt].w;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) gelu_fast(gv[r], gv[r], dg[r]);
+  split8(gv, st.gh, st.gl);
+}
+
+// the interval barriers are scheduling barriers too: without sched_barrier the
+// machine scheduler moved the (memory-free) GELU VALU and the last MFMAs of a
+// phase across the asm s_barrier into the next interval
+__device__ __forceinline__ void ws_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void ws_bar_fills() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// fills of pair p + 1 = {W1(p + 1), W2(p)} into ring slot nb
+template <int NW>
+__device__ __forceinline__ void ws_fill(__bf16* nb, const __bf16* W1, const __bf16* W2, int p) {
+  constexpr int NC = GHM_F / 32;
+  if (p + 1 < NC) fill_r32_w8<NW>(W1 + (p + 1) * 32 * GHM_D, GHM_D, PK_W, nb, nb + PLANE);
+  fill_r128_w8<NW>(W2 + p * 32, GHM_F, PK_W, nb + 2 * PLANE, nb + 3 * PLANE);
+}
+
+// one interval pair 0 < p < NC, straight-line per group: fills of pair p + 1,
+// then A: M(p) | V(p), B: V(p-1) | M(p).  cb / nb: __restrict__ parameters of one
+// inlined function (alias scopes: no vmcnt wait for the fresh fills before the
+// operand reads)
+template <int NW, bool GRP_A>
+__device__ __forceinline__ void ws_pair(const __bf16* __restrict__ cb, __bf16* __restrict__ nb, int p,
+                                        const __bf16* W1, const __bf16* W2, const float4* bb, const bf16x8* xh,
+                                        const bf16x8* xl, f32x4* y, WsState& st, int t, int g) {
+  ws_fill<NW>(nb, W1, W2, p);
+  if (GRP_A) {
+    ws_mphase<true, true>(cb, xh, xl, y, st, t, g);
+    ws_bar();
+    ws_vphase(bb, st);
+  } else {
+    ws_vphase(bb, st);
+    ws_bar();
+    ws_mphase<true, true>(cb, xh, xl, y, st, t, g);
+  }
+  ws_bar_fills();
+}
+
+// a group's whole chunk loop: pair 0 (U(0) only), pairs 1 .. NC-1, pair NC (Y(NC-1) only)
+template <int NW, bool GRP_A>
+__device__ __forceinline__ void ws_loop(__bf16* lds, const __bf16* W1, const __bf16* W2, const float* sb1,
+                                        const bf16x8* xh, const bf16x8* xl, f32x4* y, int t, int g) {
+  constexpr int NC = GHM_F / 32;
+  WsState st;
+  float4 bb[2];
+  auto read_b1 = [&](int q) {  // b1 of chunk q, read before the pair's fills (see k_ln_mlp_fwd_x3b)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * q + 16 * jt + 4 * g);
+    issue_fence();
+  };
+  // pair 0: slot 0 = {W1(0)}
+  if (GRP_A) read_b1(0);
+  ws_fill<NW>(lds + 4 * PLANE, W1, W2, 0);
+  if (GRP_A) {
+    ws_mphase<false, true>(lds, xh, xl, y, st, t, g);
+    ws_bar();
+    ws_vphase(bb, st);
+  } else {
+    ws_bar();
+    ws_mphase<false, true>(lds, xh, xl, y, st, t, g);
+  }
+  ws_bar_fills();
+#pragma unroll 1
+  for (int p = 1; p < NC; ++p) {
+    const int cur = p & 1;
+    read_b1(GRP_A ? p : p - 1);
+    ws_pair<NW, GRP_A>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), p, W1, W2, bb, xh, xl, y, st, t, g);
+  }
+  // pair NC: slot NC & 1 = {W2(NC-1)}
+  const __bf16* cb = lds + 4 * PLANE * (NC & 1);
+  if (GRP_A) {
+    ws_mphase<true, false>(cb, xh, xl, y, st, t, g);
+    ws_bar();
+  } else {
+    read_b1(NC - 1);
+    ws_vphase(bb, st);
+    ws_bar();
+    ws_mphase<true, false>(cb, xh, xl, y, st, t, g);
+  }
+  ws_bar();
+}
+
+// 4 waves per SIMD (HIP's second bound: minimum waves per EU), i.e. two
+// workgroups per CU as x3b; at the bound 2 the compiler spent 153 VGPRs (one
+// workgroup per CU)
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 4) void k_ln_mlp_fwd_x3w(
+    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
+    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
+  constexpr int NC = GHM_F / 32;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE + 2 * GHM_F];
+  float* sb1 = reinterpret_cast<float*>(lds + 8 * PLANE);
+  const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const bool grpA = wave < NW / 2;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + (threadIdx.x >> 6)) * 16 + t;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W1 = pack + PK_W1_N;
+  const __bf16* W2 = pack + PK_W2_P32;
+  fill_r32_w8<NW>(W1, GHM_D, PK_W, lds, lds + PLANE);  // pair 0 = {W1(0)} into slot 0
+  if (threadIdx.x < GHM_F / 4)
+    reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
+  bf16x8 xh[4], xl[4];
+  {  // LN2 of the token row (as k_ln_mlp_fwd_x3b), lane holds features 32s + 8g + i
+    const float* row = Hmid + mc * GHM_D;
+    float x[32];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const float4 a = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g);
+      const float4 b = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g + 4);
+      x[8 * s2 + 0] = a.x; x[8 * s2 + 1] = a.y; x[8 * s2 + 2] = a.z; x[8 * s2 + 3] = a.w;
+      x[8 * s2 + 4] = b.x; x[8 * s2 + 5] = b.y; x[8 * s2 + 6] = b.z; x[8 * s2 + 7] = b.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) sm += x[k];
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    const float mean = sm * (1.f / 128.f);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float d = x[k] - mean;
+      v += d * d;
+    }
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const float rstd = 1.f / sqrtf(v * (1.f / 128.f) + eps);
+    if (g == 0 && valid) stats[m] = make_float2(mean, rstd);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int f = 32 * s2 + 8 * g + i;
+        x[8 * s2 + i] = (x[8 * s2 + i] - mean) * rstd * lnw[f] + lnb[f];
+      }
+      split8(x + 8 * s2, xh[s2], xl[s2]);
+    }
+  }
+  f32x4 y[8];  // seeded with the residual and b2 (as x3b)
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const float* hr = Hmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
+      y[j][0] = hv.x + bv.x;
+      y[j][1] = hv.y + bv.y;
+      y[j][2] = hv.z + bv.z;
+      y[j][3] = hv.w + bv.w;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (grpA)
+    ws_loop<NW, true>(lds, W1, W2, sb1, xh, xl, y, t, g);
+  else
+    ws_loop<NW, false>(lds, W1, W2, sb1, xh, xl, y, t, g);
+  if (valid) {
+    float* orow = Hout + m * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st4(orow + 16 * j + 4 * g, y[j][0], y[j][1], y[j][2], y[j][3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // MLP + LN2 backward with the up-projection recomputed       (model.py:784-788)
 // 16 tokens per wave, 8 waves (128 tokens) per workgroup, weight tiles by
 // LDS-DMA as in k_ln_mlp_fwd_x3b.  The forward saved only Hmid and the LN2
@@ -2056,7 +2290,16 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
   hipStream_t s = ghm_stream(stream);
   const bool big = (M + 127) / 128 >= 256;  // enough 128-token workgroups to give every CU one
   const dim3 g8(static_cast<unsigned>((M + 127) / 128)), g4(static_cast<unsigned>((M + 63) / 64));
-  if (big)
+  // GHM_MLP_FWD_WS=1: the wave-specialised schedule (k_ln_mlp_fwd_x3w); read per
+  // call (a graph captures the choice made at capture time)
+  const char* ws_env = std::getenv("GHM_MLP_FWD_WS");
+  const int ws = ws_env ? std::atoi(ws_env) : 0;  // 1: 8 waves (two workgroups per CU), 2: 16 waves (one)
+  if (big && ws == 2)
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3w<16>, dim3(static_cast<unsigned>((M + 255) / 256)), dim3(1024), 0, s, H_mid,
+                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+  else if (big && ws)
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3w<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+  else if (big)
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
   else
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);

@@ -24,6 +24,19 @@ PEAK = 157.3e12       # f32 MFMA, dense
 BF16_PEAK = 2.5e15    # bf16 MFMA, dense (x3 issues 3 bf16 products per f32 product)
 
 
+def _with_env(key, val, fn):
+    """Run fn() with os.environ[key] = val (the library reads some switches per call)."""
+    old = os.environ.get(key)
+    os.environ[key] = val
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[key]
+        else:
+            os.environ[key] = old
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
@@ -83,6 +96,14 @@ def main():
             "ln_mlp_fwd_x3b": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                          P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
                                          P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp),
+                               gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3w": (lambda: _with_env("GHM_MLP_FWD_WS", "1", lambda: c(
+                "ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk,
+                P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp)),
+                               gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3w16": (lambda: _with_env("GHM_MLP_FWD_WS", "2", lambda: c(
+                "ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk,
+                P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp)),
                                gf(4 * M * 128 * 512)),
             "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
