@@ -1043,6 +1043,259 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
   }
 }
 
+#ifdef GHM_FUSED_DW_PROTO
+#ifndef GHM_ABLATION_BUILD
+#error "GHM_FUSED_DW_PROTO is a timing prototype: only with -DGHM_ABLATION_BUILD (tools/, never the product library)"
+#endif
+// ---------------------------------------------------------------------------
+// TIMING PROTOTYPE (review item 2; results are not the weight gradients): the MLP
+// backward at 64 tokens per workgroup with dW2 / dW1 accumulated inside it per
+// hidden chunk, instead of writing G / dU for k_wgrad_x3.  Everything the fused
+// design must do is here at its real size: the dY and LN2(Hmid) token images
+// staged once into LDS (bf16 hi / lo, [64 tokens][128]: 64 KB), per chunk the
+// G_c / dU_c images written (16 KB) and a barrier, 48 more MFMAs per wave per chunk
+// whose tokens-on-k operands come from those images through ds_read_b64_tr_b16,
+// and the per-chunk partials (dW2_c + dW1_c: 2 x 128 x 32 f32 = 32 KB per
+// workgroup and chunk) stored for a fixed-order reduction over the workgroups.
+// The operand indexing inside the images is schematic (conflict-free offsets of
+// the right instruction count); the U / dG / dU / dX2 / LN2 work is the product's.
+// LDS: 66 KB ring + 80 KB images = 146 KB: one workgroup (4 waves) per CU.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void rc_ud_vals(const __bf16* cb, const float4* bb, const bf16x8* xh, const bf16x8* xl,
+                                           const bf16x8* yh, const bf16x8* yl, int t, int g, float* gv, float* du) {
+  const __bf16* w1h = cb;
+  const __bf16* w1l = cb + PLANE;
+  const __bf16* w2h = cb + 2 * PLANE;
+  const __bf16* w2l = cb + 3 * PLANE;
+  f32x4 u[2], dg[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    u[jt] = zero4();
+    dg[jt] = zero4();
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int o1 = r32t_off(16 * jt + t, 4 * s2 + g), o = r32_off(16 * jt + t, 4 * s2 + g);
+      u[jt] = mfma16_x3(ldsb8(w1h + o1), ldsb8(w1l + o1), xh[s2], xl[s2], u[jt]);
+      dg[jt] = mfma16_x3(ldsb8(w2h + o), ldsb8(w2l + o), yh[s2], yl[s2], dg[jt]);
+    }
+  }
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const float bs[4] = {bb[jt].x, bb[jt].y, bb[jt].z, bb[jt].w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float gd;
+      gelu_fast(u[jt][r] + bs[r], gv[4 * jt + r], gd);
+      du[4 * jt + r] = dg[jt][r] * gd;
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 proto_tr(const __bf16* img, int off) {
+  typedef __attribute__((address_space(3))) bf16x4 lds4_t;
+  const bf16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds4_t*)(img + off));
+  const bf16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds4_t*)(img + off + 16 * 64));
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r[i] = a[i];
+    r[4 + i] = b[i];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(256, 1) void k_mlp_bwd_fused_proto(
+    const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
+    const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
+    float* __restrict__ part_w, float* __restrict__ dHmid, float* __restrict__ part_ln, int64_t M) {
+  constexpr int NW = 4, NC = GHM_F / 32;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE + 2 * GHM_F];
+  // token images: dY hi|lo, X2 hi|lo [64][128] (4 x 16 KB), G_c hi|lo, dU_c hi|lo [64][32] (4 x 4 KB)
+  __shared__ __attribute__((aligned(16))) __bf16 img[4 * 64 * 128 + 4 * 64 * 32];
+  float* sb1 = reinterpret_cast<float*>(lds + 8 * PLANE);
+  auto sw1h = [&](int b) { return lds + 4 * PLANE * b; };
+  auto sw1l = [&](int b) { return lds + 4 * PLANE * b + PLANE; };
+  auto sw2h = [&](int b) { return lds + 4 * PLANE * b + 2 * PLANE; };
+  auto sw2l = [&](int b) { return lds + 4 * PLANE * b + 3 * PLANE; };
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int tok = 16 * wave + t;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + wave) * 16 + t;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W1 = pack + PK_W1_N;
+  const __bf16* W2T = pack + PK_W2_T;
+  fill_r32t_w8<NW>(W1, GHM_D, PK_W, sw1h(0), sw1l(0));
+  fill_r32_w8<NW>(W2T, GHM_D, PK_W, sw2h(0), sw2l(0));
+  if (threadIdx.x < GHM_F / 4)
+    reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
+  bf16x8 xh[4], xl[4], yh[4], yl[4];
+  const float2 st = ld_stats_sys(stats, mc);
+  {
+    const float* row = Hmid + mc * GHM_D;
+    const float* dyr = dHout + mc * GHM_D;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int f0 = 32 * s2 + 8 * g;
+      const float4 a = *reinterpret_cast<const float4*>(row + f0);
+      const float4 b = *reinterpret_cast<const float4*>(row + f0 + 4);
+      const float4 ga = *reinterpret_cast<const float4*>(lnw + f0);
+      const float4 gb = *reinterpret_cast<const float4*>(lnw + f0 + 4);
+      const float4 ba = *reinterpret_cast<const float4*>(lnb + f0);
+      const float4 bb = *reinterpret_cast<const float4*>(lnb + f0 + 4);
+      float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const float gw[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+      const float bw[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = (x[i] - st.x) * st.y * gw[i] + bw[i];
+      split8(x, xh[s2], xl[s2]);
+      const float4 c = *reinterpret_cast<const float4*>(dyr + f0);
+      const float4 d = *reinterpret_cast<const float4*>(dyr + f0 + 4);
+      const float y[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+      split8(y, yh[s2], yl[s2]);
+      // the token images of dY and X2 (once)
+      const int o = tok * 128 + 8 * ((4 * s2 + g) ^ (tok & 15));
+      *reinterpret_cast<bf16x8*>(img + o) = yh[s2];
+      *reinterpret_cast<bf16x8*>(img + 64 * 128 + o) = yl[s2];
+      *reinterpret_cast<bf16x8*>(img + 2 * 64 * 128 + o) = xh[s2];
+      *reinterpret_cast<bf16x8*>(img + 3 * 64 * 128 + o) = xl[s2];
+    }
+  }
+  __bf16* gimg = img + 4 * 64 * 128;
+  f32x4 dx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dx[j] = zero4();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const int cur = c & 1;
+    float4 bb[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
+    issue_fence();
+    const int cn = c + 1 < NC ? c + 1 : NC - 1;
+    fill_r32t_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, sw1h(cur ^ 1), sw1l(cur ^ 1));
+    fill_r32_w8<NW>(W2T + cn * 32 * GHM_D, GHM_D, PK_W, sw2h(cur ^ 1), sw2l(cur ^ 1));
+    float gv[8], du[8];
+    rc_ud_vals(lds + 4 * PLANE * cur, bb, xh, xl, yh, yl, t, g, gv, du);
+    bf16x8 gh, gl, dh, dl;
+    split8(gv, gh, gl);
+    split8(du, dh, dl);
+    rc_dx2(lds + 4 * PLANE * cur, dh, dl, dx, lane);
+    // G_c / dU_c token images [64][32], then every wave's quarter of dW2_c / dW1_c
+    const int go = tok * 32 + 8 * (g ^ (tok & 3));
+    *reinterpret_cast<bf16x8*>(gimg + go) = gh;
+    *reinterpret_cast<bf16x8*>(gimg + 64 * 32 + go) = gl;
+    *reinterpret_cast<bf16x8*>(gimg + 2 * 64 * 32 + go) = dh;
+    *reinterpret_cast<bf16x8*>(gimg + 3 * 64 * 32 + go) = dl;
+    __syncthreads();
+    f32x4 w2a[4], w1a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w2a[q] = w1a[q] = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {  // 64 tokens = 2 k-steps of 32
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // dW2_c rows 32 wave + 16 (q >> 1) (features o), cols 16 (q & 1) (units): A = dY^T, B = G_c
+        const int ao = (32 * ks + 4 * (lane >> 4)) * 128 + 32 * wave + 16 * (q >> 1) + (lane & 15);
+        const int bo = (32 * ks + 4 * (lane >> 4)) * 32 + 16 * (q & 1) + (lane & 15);
+        w2a[q] = mfma16_x3(proto_tr(img, ao), proto_tr(img + 64 * 128, ao), proto_tr(gimg, bo),
+                           proto_tr(gimg + 64 * 32, bo), w2a[q]);
+        // dW1_c rows 16 (q >> 1) (units), cols 32 wave + 16 (q & 1) (inputs): A = dU_c^T, B = X2
+        const int ao1 = (32 * ks + 4 * (lane >> 4)) * 32 + 16 * (q >> 1) + (lane & 15);
+        const int bo1 = (32 * ks + 4 * (lane >> 4)) * 128 + 32 * wave + 16 * (q & 1) + (lane & 15);
+        w1a[q] = mfma16_x3(proto_tr(gimg + 2 * 64 * 32, ao1), proto_tr(gimg + 3 * 64 * 32, ao1),
+                           proto_tr(img + 2 * 64 * 128, bo1), proto_tr(img + 3 * 64 * 128, bo1), w1a[q]);
+      }
+    }
+    // this workgroup's chunk partials: [blk][c][wave][lane][32]
+    float* pp = part_w + ((static_cast<int64_t>(blockIdx.x) * NC + c) * NW + wave) * 64 * 32 + lane * 32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      st4(pp + 4 * q, w2a[q][0], w2a[q][1], w2a[q][2], w2a[q][3]);
+      st4(pp + 16 + 4 * q, w1a[q][0], w1a[q][1], w1a[q][2], w1a[q][3]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  // LN2 backward (as k_mlp_bwd_rc_x3)
+  const float mean = st.x, rstd = st.y;
+  float xhat[32], dyg[32];
+  float s1 = 0.f, s2 = 0.f;
+  {
+    const float* row = Hmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 xv = *reinterpret_cast<const float4*>(row + f);
+      const float4 gv = *reinterpret_cast<const float4*>(lnw + f);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float xh_ = (xs[r] - mean) * rstd;
+        xhat[4 * j + r] = xh_;
+        const float v = dx[j][r] * gs[r];
+        dyg[4 * j + r] = v;
+        s1 += v;
+        s2 += v * xh_;
+      }
+    }
+  }
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  const float m1 = s1 * (1.f / GHM_D), m2 = s2 * (1.f / GHM_D);
+  {
+    const float* dres = dHout + mc * GHM_D;
+    float* orow = dHmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 rv = *reinterpret_cast<const float4*>(dres + f);
+      const float rs[4] = {rv.x, rv.y, rv.z, rv.w};
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = rs[r] + rstd * (dyg[4 * j + r] - m1 - xhat[4 * j + r] * m2);
+      st4(orow + f, o[0], o[1], o[2], o[3]);
+    }
+  }
+  float vg[32], vb[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const float d = valid ? dx[k >> 2][k & 3] : 0.f;
+    vb[k] = d;
+    vg[k] = d * xhat[k];
+  }
+  const float2 rg = reduce_scatter32_t16(vg, t);
+  const float2 rb = reduce_scatter32_t16(vb, t);
+  float* red = reinterpret_cast<float*>(lds);
+  {
+    const int k0 = 2 * t;
+    const int f0 = 16 * (k0 >> 2) + 4 * g + (k0 & 3);
+    red[wave * GHM_D + f0] = rg.x;
+    red[wave * GHM_D + f0 + 1] = rg.y;
+    red[NW * GHM_D + wave * GHM_D + f0] = rb.x;
+    red[NW * GHM_D + wave * GHM_D + f0 + 1] = rb.y;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * GHM_D) {
+    const int q = threadIdx.x >> 7, f = threadIdx.x & 127;
+    const float* rr = red + q * NW * GHM_D + f;
+    part_ln[static_cast<int64_t>(blockIdx.x) * 2 * GHM_D + q * GHM_D + f] =
+        (rr[0] + rr[GHM_D]) + (rr[2 * GHM_D] + rr[3 * GHM_D]);
+  }
+}
+
+extern "C" int ghm_mlp_bwd_fused_proto(const float* dH_out, const float* H_mid, const float* stats,
+                                       const float* ln_w, const float* ln_b, const void* pack, const float* b1,
+                                       float* part_w, float* dH_mid, float* part_ln, int64_t M, void* stream) {
+  GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && part_w && dH_mid && part_ln, "null pointer");
+  hipLaunchKernelGGL(k_mlp_bwd_fused_proto, dim3(static_cast<unsigned>((M + 63) / 64)), dim3(256), 0,
+                     ghm_stream(stream), dH_out, H_mid, reinterpret_cast<const float2*>(stats), ln_w, ln_b,
+                     reinterpret_cast<const __bf16*>(pack), b1, part_w, dH_mid, part_ln, M);
+  return ghm_launch_status();
+}
+#endif  // GHM_FUSED_DW_PROTO
+
 // ---------------------------------------------------------------------------
 // QKV + LN1 backward                                          (model.py:772-775)
 //   dX1^T = Wq^T dQ^T + Wk^T dK^T + Wv^T dV^T, then LN1 backward + residual.

@@ -198,6 +198,8 @@ def check_build_id():
     from ._buildid import source_build_id
     want = source_build_id()
     got = hip_lib().ghm_build_id().decode()
+    if os.environ.get("GHM_HIP_LIB") and got.startswith("variant-"):
+        return got  # an explicit A/B variant library (tools/build_variant.sh): reported, not the tree's
     got_host = host_lib().ghm_sampler_build_id().decode()
     if got != want or got_host != want:
         raise RuntimeError(f"native libraries were built from other sources: libghm_hip {got}, "

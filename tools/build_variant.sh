@@ -17,6 +17,10 @@ for f in $SRC/multimodal-ghm_amd/csrc/*.hip; do
   objs="$objs $o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libghm_hip.so $objs
+# a variant id: the variant's sources hashed (flags appended), so check_build_id reports it
+printf '// variant build (tools/build_variant.sh)\nextern "C" const char* ghm_build_id(void) { return "variant-%s"; }\n' \
+  "$(cat $SRC/multimodal-ghm_amd/csrc/* $SRC/include/*.h | sha256sum | cut -c1-12)$(echo $EXTRA | tr -d ' ')" > $SRC/bid.cpp
+g++ -O2 -fPIC -c -o $SRC/bid.o $SRC/bid.cpp
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libghm_hip.so $objs $SRC/bid.o
 rm -rf $SRC
 echo built $OUT/libghm_hip.so

@@ -135,6 +135,28 @@ def main():
                                          1, 0, P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                          P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
         })
+    lib = _native.hip_lib()
+    if plan.pack is not None and hasattr(lib, "ghm_mlp_bwd_fused_proto"):
+        # review item 2 timing prototype (ablation build only: tools/build_variant.sh ...
+        # -DGHM_ABLATION_BUILD -DGHM_FUSED_DW_PROTO): MLP backward with dW2 / dW1 fused
+        # at 64 tokens per workgroup, and the fixed-order reduction of its partials
+        nb = (M + 63) // 64
+        pw = torch.empty(nb, 16 * 4 * 64 * 32, device=plan.H.device)
+        red_out = torch.empty(16 * 4 * 64 * 32, device=plan.H.device)
+        pln = torch.empty(nb, 2, 128, device=plan.H.device)
+        fp = lib.ghm_mlp_bwd_fused_proto
+        fp.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_int64, ctypes.c_void_p]
+        job = _native.ReduceJob()
+        job.part, job.n_split, job.n_seg, job.n = pw.data_ptr(), nb, 1, pw.shape[1]
+        job.dst[0] = red_out.data_ptr()
+        job.off[0], job.off[1] = 0, pw.shape[1]
+        jobs = (_native.ReduceJob * 1)(job)
+        kernels.update({
+            "mlp_bwd_fused_proto": (lambda: _native.check(fp(
+                P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]),
+                pk, P(p["_mlps.0.0.bias"]), P(pw), P(xo["dHm"]), P(pln), M, sp), "proto"), gf(10 * M * 128 * 512)),
+            "fused_proto_reduce": (lambda: c("ghm_reduce_batch", jobs, 1, sp), None),
+        })
     kernels.update({
         "reduce_w2": (lambda: plan._reduce(plan.part_w2, ns_w2, 128 * 512, [g["_mlps.0.2.weight"]], sp), None),
         "reduce_ln": (lambda: plan._reduce(plan.part_ln, plan.nblk, 256, [g["_lns_1.0.weight"], g["_lns_1.0.bias"]],
