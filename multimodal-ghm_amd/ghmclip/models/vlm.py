@@ -37,7 +37,7 @@ import torch.nn as nn
 from .. import _native
 from .hip_encoder import PRECISIONS, default_precision, require_hip
 
-__all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names",
+__all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "VlmPlan", "vlm_param_names", "vlm_untrained",
            "vlm_guide_blocks", "vlm_guide_plane_elems",
            "VLM_UNTRAINED", "VLM_JOINT_UNTRAINED"]
 
@@ -46,6 +46,17 @@ __all__ = ["AutoRegressiveTransformer", "ConditionalGuidedCELoss", "KLdiv", "Vlm
 VLM_UNTRAINED = ("i_embedding.weight", "_out.weight", "_out.bias")
 # joint model (sequential=False, train_NWP.py): the image leaves go through i_embedding
 VLM_JOINT_UNTRAINED = ("_out.weight", "_out.bias")
+
+
+def vlm_untrained(model):
+    """Parameters the reference never gives a gradient (AdamW and clip_grad_norm_
+    skip them): VLM_UNTRAINED / VLM_JOINT_UNTRAINED, and with layernorm=False the
+    unused LayerNorms (model.py:269-277, 294-301)."""
+    names = VLM_UNTRAINED if model.sequential else VLM_JOINT_UNTRAINED
+    if not getattr(model, "layernorm", True):
+        names = names + tuple(f"_lns_{k}.{l}.{w}" for k in (1, 2) for l in range(model.n_layer)
+                              for w in ("weight", "bias"))
+    return names
 
 
 def vlm_param_names(n_layer):
@@ -88,7 +99,8 @@ EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL, EPI_SLAB = range(5)
 
 class VlmPlan:
     def __init__(self, n_layer, n_token, n_seq, n_prefix=1, num_class=10, n_embd=256, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax"):
+                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax",
+                 layernorm=True):
         if n_embd not in (128, 256, 512):
             raise ValueError(f"the HIP VLM kernels take n_embd in (128, 256, 512) (got {n_embd})")
         self.L, self.T, self.N, self.P, self.V, self.D = n_layer, n_token, n_seq, n_prefix, num_class, n_embd
@@ -119,7 +131,14 @@ class VlmPlan:
         L, D, F, N = n_layer, n_embd, self.F, n_seq
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         self.H = e(L + 1, M, D)
-        self.Hmid, self.X1, self.X2 = e(L, M, D), e(L, M, D), e(L, M, D)
+        self.Hmid = e(L, M, D)
+        # layernorm=False (model.py:269-277, 294-301): Q / K / V read H and the MLP
+        # reads Hmid directly; their backward adds dX into the residual gradient
+        self.layernorm = bool(layernorm)
+        if self.layernorm:
+            self.X1, self.X2 = e(L, M, D), e(L, M, D)
+        else:
+            self.X1, self.X2 = self.H[:L], self.Hmid
         self.G, self.Dg = e(L, M, F), e(L, M, F)
         self.Pm = torch.zeros(L, N, pad, pad, dtype=torch.float32, device=self.device)
         self.st1, self.st2 = e(L, M, 2), e(L, M, 2)
@@ -191,8 +210,9 @@ class VlmPlan:
             c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
               _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), None, N, T, self.P, self.V, D, s)
         for l in range(self.L):
-            c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-              _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
+            if self.layernorm:
+                c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
+                  _ptr(self.X1[l]), _ptr(self.st1[l]), M, D, self.eps, s)
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
             if self.f32:
                 for w, out in zip(wqkv, (self.q[l], self.k[l], self.v[l])):
@@ -207,8 +227,9 @@ class VlmPlan:
                 else:
                     c("ghm_attn_ext_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
                       _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, 1.0 / D, s)
-            c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
-              _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
+            if self.layernorm:
+                c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
+                  _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
             self._gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
                   C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
             self._gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
@@ -258,9 +279,12 @@ class VlmPlan:
             self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
             self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s, bias=g[f"_mlps.{l}.0.bias"])
             self._dgrad(self.dG, F, (w1,), 0, F, s)
-            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-              _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
-            self._reduce_ln(g, 2, l, s)
+            if self.layernorm:
+                c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]),
+                  _ptr(p[f"_lns_2.{l}.weight"]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
+                self._reduce_ln(g, 2, l, s)
+            else:
+                c("ghm_add", _ptr(cur), _ptr(self.dX), _ptr(nxt), M * D, s)
             # attention (nxt = dHmid) -> dq | dk | dv
             wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
             gqkv = (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"])
@@ -284,9 +308,12 @@ class VlmPlan:
                       _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
                 self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D, gqkv, D, s)
                 self._dgrad(self.dqkv, 3 * D, wqkv, D, 3 * D, s)
-            c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-              _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
-            self._reduce_ln(g, 1, l, s)
+            if self.layernorm:
+                c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]),
+                  _ptr(p[f"_lns_1.{l}.weight"]), _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)
+                self._reduce_ln(g, 1, l, s)
+            else:
+                c("ghm_add", _ptr(nxt), _ptr(self.dX), _ptr(cur), M * D, s)
         self._colsum(cur, self.N, self.T * D, g["position_embeddings.weight"], s)  # sum over sequences
         # token-embedding gradients: rows of dH0 summed per token value (text rows
         # t >= P; the joint model's prefix rows through i_embedding)
@@ -429,7 +456,7 @@ class _VlmFn(torch.autograd.Function):
                                "activations saved for backward")
         params = ctx.saved_tensors
         names = ctx.module._names
-        untrained = VLM_JOINT_UNTRAINED if plan.joint else VLM_UNTRAINED
+        untrained = vlm_untrained(ctx.module)
         grads = {n: torch.empty_like(p) for n, p in zip(names, params) if n not in untrained}
         dz = torch.zeros(plan.N, plan.T, plan.V, dtype=torch.float32, device=dlog.device)
         dz[:, plan.P:, :] = dlog
@@ -473,8 +500,8 @@ class AutoRegressiveTransformer(nn.Module):
         self.n_t_guided_layer = n_guided_layers[0]
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[0] * 2 + 1)
-        if activation not in ("softmax", "relu") or not mlp or not layernorm:
-            raise NotImplementedError("HIP VLM: softmax or relu attention, mlp=True, layernorm=True")
+        if activation not in ("softmax", "relu") or not mlp:
+            raise NotImplementedError("HIP VLM: softmax or relu attention, mlp=True")
         if not auto_regressive or (sequential and n_i_token != 1):
             raise NotImplementedError("HIP VLM: auto_regressive=True; sequential=True takes one prefix token "
                                       "(train_sequential_NWP.py), sequential=False the image leaves "
@@ -525,7 +552,7 @@ class AutoRegressiveTransformer(nn.Module):
             self._plans[key] = VlmPlan(self.n_layer, T, n_seq, n_prefix=P, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
                                        precision=self.precision, joint=not self.sequential,
-                                       activation=self.activation)
+                                       activation=self.activation, layernorm=self.layernorm)
         return self._plans[key]
 
     def forward(self, xt, zi):

@@ -20,7 +20,7 @@ from .. import _native
 from . import distributed
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
-from ..models.vlm import VLM_JOINT_UNTRAINED, VLM_UNTRAINED, VlmPlan, vlm_guide_blocks, vlm_guide_plane_elems
+from ..models.vlm import VlmPlan, vlm_guide_blocks, vlm_guide_plane_elems, vlm_untrained
 
 
 def _p(t):
@@ -41,7 +41,7 @@ class VlmTrainer:
         self.joint = clip_model is None  # train_NWP.py: image leaves through i_embedding, no CLIP
         if self.joint == bool(model.sequential):
             raise ValueError("a sequential model needs its frozen CLIP image encoder; the joint model takes none")
-        untrained = VLM_JOINT_UNTRAINED if self.joint else VLM_UNTRAINED
+        untrained = vlm_untrained(model)
         self.B = batch_size
         self.max_norm = float(max_norm)
         self.pg = process_group
@@ -75,7 +75,8 @@ class VlmTrainer:
         self.plan = VlmPlan(model.n_layer, model.n_token, batch_size, n_prefix=model.n_i_token,
                             num_class=model.vocab_size, n_embd=model.n_embd, normalize_attn=model.normalize_attn,
                             device=self.device, precision=precision, joint=self.joint,
-                            activation=getattr(model, "activation", "softmax"))
+                            activation=getattr(model, "activation", "softmax"),
+                            layernorm=getattr(model, "layernorm", True))
         if self.joint:
             self.clip_plan = None
             self.precision = self.plan.precision

@@ -137,8 +137,9 @@ class OracleVlm(nn.Module):
     mlp, ln2, then _read_out Linear(d -> V) and the unused _out."""
 
     def __init__(self, n_token, n_i_token=1, num_class=10, n_embd=256, n_layer=9, n_mlp_hidden=1024, sequential=True,
-                 activation="softmax"):
+                 activation="softmax", layernorm=True):
         super().__init__()
+        self.layernorm = layernorm  # model.py:269-277, 294-301: False = Q / K / V and the MLP on H itself
         self.V, self.n_i_token, self.n_embd, self.n_token = num_class, n_i_token, n_embd, n_token
         self.sequential = sequential
         self.activation = activation  # get_activation (model.py:121-130): softmax / relu
@@ -175,7 +176,7 @@ class OracleVlm(nn.Module):
         H = emb + self.position_embeddings(torch.arange(T).expand(B, T))  # :305
         for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
                                           self._lns_2):
-            H1 = ln1(H)
+            H1 = ln1(H) if self.layernorm else H
             S = torch.matmul(q(H1), k(H1).transpose(-2, -1))  # :329
             S = S + mask  # :333
             S = S / np.sqrt(self.n_embd)  # :335-336
@@ -184,7 +185,7 @@ class OracleVlm(nn.Module):
             H = H + torch.einsum("bij,bjd->bid", A, Vv)  # :338
             A = A / H.shape[2]  # :339-340
             H = H + torch.einsum("bij,bjd->bid", A, Vv)  # :341
-            H = H + mlp(ln2(H))  # :344-347
+            H = H + mlp(ln2(H) if self.layernorm else H)  # :344-347
         return self._read_out(H)[:, self.n_i_token:, :]  # :397-401
 
 
@@ -207,14 +208,15 @@ class OracleVlmTrainer:
     just before its construction; the script loads a trained CLIP checkpoint)."""
 
     def __init__(self, p=0.2, B=128, L=9, d=256, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
-                 max_norm=1.0, seed=224, seedtree=42, clip_seed=7, n_layer_tree=4, n_child=3, activation="softmax"):
+                 max_norm=1.0, seed=224, seedtree=42, clip_seed=7, n_layer_tree=4, n_child=3, activation="softmax",
+                 layernorm=True):
         self.sampler = NwpSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], seedtree=seedtree)
         T = n_child ** n_layer_tree
         torch.manual_seed(clip_seed)
         self.clip = OracleEncoder(T, 10, 128, 5)
         torch.manual_seed(seed)  # seed_everything(seed) before the model (:120)
         np.random.seed(seed)
-        self.model = OracleVlm(T, 1, 10, d, L, 4 * d, activation=activation)
+        self.model = OracleVlm(T, 1, 10, d, L, 4 * d, activation=activation, layernorm=layernorm)
         self.params = list(self.model.parameters())
         self.opt = OracleAdamW(self.params)
         self.B = B

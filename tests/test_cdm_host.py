@@ -281,6 +281,24 @@ def test_vlm_relu_oracle_two_steps_match_reference():
         np.testing.assert_allclose(ps[:, 1], g[f"param_stats{k}"][:, 1], rtol=1e-9)
 
 
+def test_vlm_noln_oracle_two_steps_match_reference():
+    """AutoRegressiveTransformer(layernorm=False) (model.py:269-277, 294-301): two
+    full training steps at d=256, L=2, B=4 (vlm_noln_tiny.npz); the unused
+    LayerNorms get no gradient and no AdamW update."""
+    from oracle import vlm_oracle as VO
+    g = _fix("vlm_noln_tiny.npz")
+    assert not bool(g["layernorm"])
+    tr = VO.OracleVlmTrainer(B=4, L=2, layernorm=False)
+    for k in range(2):
+        ploss, loss, cmp = tr.step()
+        assert abs(ploss - float(g[f"ploss{k}"])) <= 1e-6 * ploss
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-5 * cmp
+        np.testing.assert_allclose(tr.last_logits.numpy(), g[f"logits{k}"], rtol=1e-5, atol=1e-5)
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps[:, 1], g[f"param_stats{k}"][:, 1], rtol=1e-9)
+    assert not any("_lns_" in n for n in g["grad_names0"])
+
+
 def test_vlm_joint_oracle_two_steps_match_reference():
     """Joint VLM (train_NWP.py, sequential=False, T = 161), two full training steps at
     d=256, L=1, B=4 (vlm_joint_tiny.npz): draws, initial weights, logits, losses."""

@@ -1,7 +1,8 @@
 """Guided sequential VLM (train_sequential_NWP.py --guide=True: L = 9, d = 256,
-n_guided_layers = [4, 1], penalty 0.001) and the relu-attention VLM
-(AutoRegressiveTransformer(activation="relu"), model.py:121-130, 287) on the HIP
-path vs the reference's own fixtures (tests/golden/make_golden_vlm.py).
+n_guided_layers = [4, 1], penalty 0.001), the relu-attention VLM
+(AutoRegressiveTransformer(activation="relu"), model.py:121-130, 287) and the VLM
+without LayerNorm (layernorm=False, model.py:269-277, 294-301) on the HIP path vs
+the reference's own fixtures (tests/golden/make_golden_vlm.py).
 
 Guided sequential: every layer is text-guided (gap 9 // 9 = 1) and layers 0 and 3
 image-guided (model.py:207-216: counter < 1, and counter == n_t - 1 with n_i < n_t);
@@ -30,7 +31,7 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def _trainer(B, L=9, guide=True, activation="softmax", total_iters=30000):
+def _trainer(B, L=9, guide=True, activation="softmax", total_iters=30000, layernorm=True, precision="x3"):
     """train_sequential_NWP.py order (raw=True): sampler, the CLIP image encoder
     (torch.manual_seed(7), as the fixtures), seed_everything(224), the model."""
     from ghmclip import AutoRegressiveTransformer, EncoderTransformer, NextWordPredictSampler, seed_everything
@@ -41,9 +42,9 @@ def _trainer(B, L=9, guide=True, activation="softmax", total_iters=30000):
     clip = EncoderTransformer(81, 10, 128, 5).to(DEV)
     seed_everything(224)
     model = AutoRegressiveTransformer(81, 1, 10, 256, L, [4, 1], 4, 1024, auto_regressive=True, sequential=True,
-                                      guide=guide, activation=activation).to(DEV)
+                                      guide=guide, activation=activation, layernorm=layernorm).to(DEV)
     sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, total_iters) for k in range(total_iters)]
-    tr = VlmTrainer(model, clip, B, sched, device=DEV, precision="x3", penalty=0.001)
+    tr = VlmTrainer(model, clip, B, sched, device=DEV, precision=precision, penalty=0.001)
     return s, clip, tr
 
 
@@ -227,3 +228,71 @@ def test_relu_vlm_module_vs_oracle(B):
             continue
         assert rel(pp.grad, pr.grad) < 5e-4, k
     assert rel(fd.grad, fr.grad) < 5e-4
+
+
+TOL = {"f32": (2e-5, 1e-4), "x3": (1e-4, 5e-4)}  # (losses, parameter checksums) relative, as test_gpu_vlm.py
+
+
+@pytest.mark.parametrize("precision", ["f32", "x3"])
+def test_noln_vlm_steps_vs_reference_fixture(precision):
+    """layernorm=False, d=256, L=2, B=4: two fused steps (vlm_noln_tiny.npz); the
+    LayerNorm parameters stay untouched (no gradient, no AdamW step)."""
+    f = np.load(os.path.join(GOLDEN, "vlm_noln_tiny.npz"))
+    assert not bool(f["layernorm"])
+    tl_, tp = TOL[precision]
+    B = int(f["B"])
+    s, _, tr = _trainer(B, L=2, guide=False, layernorm=False, precision=precision)
+    assert not tr.plan.layernorm and all("_lns_" not in n for n in tr.gd)
+    ln0 = {n: p.detach().clone() for n, p in tr.model.named_parameters() if "_lns_" in n}
+    for k in range(2):
+        tl, il = _stage(s, tr, B, guide=False)
+        np.testing.assert_array_equal(tl[:, :-1], f[f"xt{k}"])
+        tr.step()
+        torch.cuda.synchronize()
+        sd = dict(tr.model.named_parameters())
+        for n, st in zip(list(f["param_names"]), f[f"param_stats{k}"]):
+            got = (sd[n].detach().double() ** 2).sum().item()
+            assert abs(got - st[1]) <= tp * st[1] + 1e-12, (k, n, got, st[1])
+    for n, v in ln0.items():
+        assert torch.equal(dict(tr.model.named_parameters())[n].detach(), v), n
+    h, c = tr.loss_history(), tr.compare_history()
+    for k in range(2):
+        assert abs(h[k] - float(f[f"ploss{k}"])) <= tl_ * float(f[f"ploss{k}"]), (k, h[k])
+        assert abs(c[k] - float(f[f"compare{k}"])) <= tl_ * float(f[f"compare{k}"]), (k, c[k])
+
+
+@pytest.mark.parametrize("precision", ["f32", "x3"])
+def test_noln_vlm_module_vs_oracle(precision):
+    """Module forward / backward with layernorm=False vs OracleVlm(layernorm=False)
+    (pinned by vlm_noln_tiny.npz in tests/test_cdm_host.py): logits, gradients, no
+    LayerNorm gradients."""
+    import oracle.vlm_oracle as VO
+    from ghmclip import AutoRegressiveTransformer
+    tf, tg = TOL[precision]
+    torch.manual_seed(17)
+    prod = AutoRegressiveTransformer(81, 1, 10, 256, 2, [4, 1], 4, 1024, auto_regressive=True, sequential=True,
+                                     layernorm=False)
+    torch.manual_seed(17)
+    ref = VO.OracleVlm(81, 1, 10, 256, 2, 1024, layernorm=False)
+    prod.precision = precision
+    prod = prod.to(DEV)
+    g = torch.Generator().manual_seed(5)
+    xt = torch.randint(0, 10, (4, 80), generator=g)
+    feat = torch.randn(4, 1, 10, generator=g)
+    R = torch.randn(4, 80, 10, generator=g)
+    fd = feat.to(DEV).requires_grad_(True)
+    logits, _ = prod(xt.to(DEV), fd)
+    (logits * R.to(DEV)).sum().backward()
+    fr = feat.clone().requires_grad_(True)
+    want = ref(xt, fr)
+    (want * R).sum().backward()
+    torch.cuda.synchronize()
+    rel = lambda a, b: ((a.detach().cpu().double() - b.detach().double()).abs().max()  # noqa: E731
+                        / b.detach().double().abs().max()).item()
+    assert rel(logits, want) < tf
+    for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
+        if pr.grad is None:
+            assert pp.grad is None, k
+            continue
+        assert rel(pp.grad, pr.grad) < tg, k
+    assert rel(fd.grad, fr.grad) < tg
