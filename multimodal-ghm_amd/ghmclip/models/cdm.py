@@ -16,10 +16,11 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import D_MODEL, EncoderPlan, default_precision, require_hip
+from .hip_encoder import D_HIDDEN, D_MODEL, EncoderPlan, default_precision, require_hip
+from .vlm import EPI_GELU, EPI_MUL, EPI_RESID, EPI_SLAB, EPI_STORE, _gemm
 
 __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
-           "cdm_param_names", "CDM_UNTRAINED", "CDM_JOINT_UNTRAINED"]
+           "cdm_param_names", "cdm_untrained", "CDM_UNTRAINED", "CDM_JOINT_UNTRAINED", "NoLnLayers"]
 
 # parameters the reference never gives a gradient in sequential mode (the
 # conditioning token bypasses t_embedding, _out is unused by forward): AdamW and
@@ -27,6 +28,84 @@ __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "L
 CDM_UNTRAINED = ("t_embedding.weight", "_out.weight", "_out.bias")
 # joint model (sequential=False, train_CDNS.py): the text leaves go through t_embedding
 CDM_JOINT_UNTRAINED = ("_out.weight", "_out.bias")
+
+
+def cdm_untrained(model):
+    """Parameters the reference never gives a gradient (AdamW and clip_grad_norm_
+    skip them): CDM_UNTRAINED / CDM_JOINT_UNTRAINED, and with layernorm=False the
+    unused LayerNorms (model.py:470-477, 488-498)."""
+    names = CDM_UNTRAINED if model.sequential else CDM_JOINT_UNTRAINED
+    if not getattr(model, "layernorm", True):
+        names = names + tuple(f"_lns_{k}.{l}.{w}" for k in (1, 2) for l in range(model.n_layer)
+                              for w in ("weight", "bias"))
+    return names
+
+
+class NoLnLayers:
+    """The CDM layer stack with layernorm=False (model.py:470-477: Q / K / V read
+    H; :488-498: H = H + mlp(H) after the attention residual).  The LayerNorm is
+    fused into EncoderPlan's token-parallel kernels, so this stack runs the
+    projections on the tiled GEMM instead (ghm_gemm_x3, or ghm_gemm_f32 in the f32
+    mode: GELU / GELU', bias + residual and the GELU' product in its epilogues,
+    split-k weight gradients with the bias sums) around the plan's own attention
+    kernels (EncoderPlan._attn_fwd / _attn_bwd, every activation and length);
+    the residual gradients add with ghm_add.  HBM: G, GELU'(U) [L][M][512] saved by
+    the forward, dU [M][512], dX [M][128] and the split-k slabs."""
+
+    def __init__(self, plan):
+        self.plan = plan
+        L, M = plan.L, plan.M
+        dev = plan.device
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.f32 = plan.precision != "x3"
+        self.G, self.Dg = e(L, M, D_HIDDEN), e(L, M, D_HIDDEN)
+        self.dG, self.dX = e(M, D_HIDDEN), e(M, D_MODEL)
+        self.nsplit = max(1, min(16, M // 256))
+        self.slab = e(self.nsplit * max(D_MODEL * D_HIDDEN, 3 * D_MODEL * D_MODEL))
+        self.bslab = e(self.nsplit * D_HIDDEN)
+
+    def _gemm(self, *a, **k):
+        _gemm(*a, f32=self.f32, **k)
+
+    def _wgrad(self, A, lda, m, B, ldb, n, dst, chunk, s, bias=None):
+        """dst (rows stacked by chunk) = A^T B over the M tokens (+ the bias gradient,
+        the column sums of A, from the same launch), as VlmPlan._wgrad."""
+        bs = None if bias is None else self.bslab
+        self._gemm(1, 0, EPI_SLAB, A, lda, (B,), ldb, 0, self.slab, n, m, n, self.plan.M, C2=bs, nsplit=self.nsplit,
+                   s=s)
+        d = list(dst) + [None] * (3 - len(dst))
+        pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
+        _native.call("ghm_gemm_reduce_bias", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk,
+                     pp(bs), pp(bias), s)
+
+    def fwd(self, p, l, s):
+        pl, D, F, M = self.plan, D_MODEL, D_HIDDEN, self.plan.M
+        wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
+        self._gemm(0, 1, EPI_STORE, pl.H[l], D, wqkv, D, D, pl.qkv[l], 3 * D, M, 3 * D, D, s=s)
+        pl._attn_fwd(l, s)
+        self._gemm(0, 1, EPI_GELU, pl.Hmid[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
+                   C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
+        self._gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, pl.H[l + 1], D, M, D, F,
+                   bias=p[f"_mlps.{l}.2.bias"], R=pl.Hmid[l], ldr=D, s=s)
+
+    def bwd(self, p, g, l, cur, nxt, s, layer_grad=None):
+        """cur = dL/dH[l+1] in; returns (dL/dH[l], the free ping-pong buffer)."""
+        pl, D, F, M = self.plan, D_MODEL, D_HIDDEN, self.plan.M
+        if layer_grad and l in layer_grad:
+            layer_grad[l](cur, s)
+        w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
+        self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s, bias=g[f"_mlps.{l}.2.bias"])
+        self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
+        self._wgrad(self.dG, F, F, pl.Hmid[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s, bias=g[f"_mlps.{l}.0.bias"])
+        self._gemm(0, 0, EPI_STORE, self.dG, F, (w1,), D, 0, self.dX, D, M, D, F, s=s)
+        _native.call("ghm_add", _ptr(cur), _ptr(self.dX), _ptr(nxt), M * D, s)  # nxt = dL/dHmid[l]
+        pl._attn_bwd(l, nxt, s)
+        wqkv = (p[f"_queries.{l}.weight"], p[f"_keys.{l}.weight"], p[f"_values.{l}.weight"])
+        gqkv = (g[f"_queries.{l}.weight"], g[f"_keys.{l}.weight"], g[f"_values.{l}.weight"])
+        self._wgrad(pl.dqkv, 3 * D, 3 * D, pl.H[l], D, D, gqkv, D, s)
+        self._gemm(0, 0, EPI_STORE, pl.dqkv, 3 * D, wqkv, D, D, self.dX, D, M, D, 3 * D, s=s)
+        _native.call("ghm_add", _ptr(nxt), _ptr(self.dX), _ptr(cur), M * D, s)  # cur = dL/dH[l]
+        return cur, nxt
 
 
 def cdm_param_names(n_layer):
@@ -62,7 +141,8 @@ class CdmPlan(EncoderPlan):
     split-K buffers part_w1 / part_b1)."""
 
     def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
-                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax"):
+                 normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax",
+                 layernorm=True):
         if precision is None:  # the joint model (T = 162) defaults to exact f32 (DESIGN.md §9)
             precision = default_precision("f32" if joint else "x3")
         # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
@@ -80,6 +160,9 @@ class CdmPlan(EncoderPlan):
             self.wpart = torch.empty(lib.ghm_wcolsum_part_elems(n_seq * (n_token - n_i_token), D_MODEL, num_class),
                                      dtype=torch.float32, device=self.device)
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        # layernorm=False: the layer stack on the GEMM path (NoLnLayers)
+        self.layernorm = bool(layernorm)
+        self.noln = None if self.layernorm else NoLnLayers(self)
         self.pred = e(n_seq, n_i_token)
         self.dpred = e(n_seq, n_i_token)
         self.part_rw = e(n_seq, D_MODEL)
@@ -89,7 +172,7 @@ class CdmPlan(EncoderPlan):
         """z: f32 [N, T_img] noisy observations; cond: f32 [N, T - T_img, cond_ld]
         conditioning features (first V used).  Returns self.pred [N, T_img]."""
         s = _stream()
-        if self.precision == "x3" and split:
+        if self.precision == "x3" and split and self.layernorm:
             self.split_weights(p, s)
         if self.joint:  # cond unused: self.tok holds the text leaves
             _native.call("ghm_cdm_embed_joint_fwd", _ptr(z), _ptr(self.tok), _ptr(p["t_embedding.weight"]),
@@ -104,6 +187,20 @@ class CdmPlan(EncoderPlan):
                      _ptr(p["_read_out.bias"]), _ptr(self.pred), self.N, self.T, self.Ti, D_MODEL, s)
         self._gen += 1
         return self.pred
+
+    def layers_fwd(self, p, s):
+        if self.layernorm:
+            return super().layers_fwd(p, s)
+        for l in range(self.L):
+            self.noln.fwd(p, l, s)
+
+    def layers_bwd(self, p, g, jobs, s, layer_grad=None):
+        if self.layernorm:
+            return super().layers_bwd(p, g, jobs, s, layer_grad)
+        cur, nxt = self.dH[0], self.dH[1]
+        for l in reversed(range(self.L)):
+            cur, nxt = self.noln.bwd(p, g, l, cur, nxt, s, layer_grad)
+        return cur
 
     def backward(self, p, g, dpred=None, layer_grad=None):
         """Writes d(loss)/d(param) into g[name] for every trained parameter (not
@@ -153,7 +250,7 @@ class _CdmFn(torch.autograd.Function):
                                "overwrote the activations saved for backward")
         params = ctx.saved_tensors
         names = ctx.module._names
-        untrained = CDM_JOINT_UNTRAINED if plan.joint else CDM_UNTRAINED
+        untrained = cdm_untrained(ctx.module)
         trained = [n not in untrained for n in names]
         grads = {n: torch.empty_like(p) for n, p, t in zip(names, params, trained) if t}
         dH0 = plan.backward(dict(zip(names, params)), grads, dpred=dpred.contiguous().float())
@@ -200,9 +297,9 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
         self.n_i_guided_layer = n_guided_layers[1]
         self.guided_layer_gap = n_layer // (n_guided_layers[1] * 2 + 1)
         self.sigma = sigma
-        if activation not in ("softmax", "relu", "gelu") or not mlp or not layernorm or maxnorm or auto_regressive:
-            raise NotImplementedError("HIP CDM: softmax / relu / gelu attention, mlp=True, layernorm=True, "
-                                      "maxnorm=False, auto_regressive=False")
+        if activation not in ("softmax", "relu", "gelu") or not mlp or maxnorm or auto_regressive:
+            raise NotImplementedError("HIP CDM: softmax / relu / gelu attention, mlp=True, maxnorm=False, "
+                                      "auto_regressive=False")
         if guide and self.guided_layer_gap == 0:
             raise ValueError("guide=True needs n_layer >= 2 * n_guided_layers[1] + 1 (model.py:372)")
         if n_mlp_hidden != 4 * n_embd:
@@ -247,7 +344,7 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
             self._plans[key] = CdmPlan(self.n_layer, T, T_img, n_seq, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
                                        precision=self.precision, joint=not self.sequential,
-                                       activation=self.activation)
+                                       activation=self.activation, layernorm=self.layernorm)
         return self._plans[key]
 
     def forward(self, xt, zi):

@@ -284,16 +284,7 @@ class EncoderPlan:
                 pk = _ptr(self.pack[l])
                 c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
                   pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-                if self.attn_f32:
-                    self._attn_fwd_f32(l)
-                elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
-                    self._attn_ext_fwd(l, s)
-                elif self.act:
-                    c("ghm_attn_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-                      None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
-                else:
-                    c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-                      N, T, D_MODEL, self.scale_div, s)
+                self._attn_fwd(l, s)
                 c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
                   _ptr(self.H[l + 1]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
@@ -301,20 +292,56 @@ class EncoderPlan:
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-            if self.attn_f32:
-                self._attn_fwd_f32(l)
-            elif self.long_attn:
-                self._attn_ext_fwd(l, s)
-            elif self.act:
-                c("ghm_attn_fwd_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-                  None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
-            else:
-                c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
-                  N, T, D_MODEL, self.scale_div, s)
+            self._attn_fwd(l, s)
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
               _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
               _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+
+    def _attn_fwd(self, l, s):
+        """Layer l's attention + residual (model.py:776-783): Hmid[l] = H[l] + A V
+        from qkv[l], P (and Pd) saved for the backward."""
+        c = _native.call
+        N, T = self.N, self.T
+        if self.attn_f32:
+            self._attn_fwd_f32(l)
+        elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
+            self._attn_ext_fwd(l, s)
+        elif self.precision == "x3":
+            if self.act:
+                c("ghm_attn_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                  None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
+            else:
+                c("ghm_attn_fwd_x3", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+                  N, T, D_MODEL, self.scale_div, s)
+        elif self.act:
+            c("ghm_attn_fwd_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+              None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
+        else:
+            c("ghm_attn_fwd", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
+              N, T, D_MODEL, self.scale_div, s)
+
+    def _attn_bwd(self, l, cur, s):
+        """Backward of _attn_fwd: dqkv from cur = dL/dHmid[l] (the residual term
+        stays the caller's)."""
+        c = _native.call
+        N, T = self.N, self.T
+        x3 = self.precision == "x3"
+        if self.attn_f32:
+            self._attn_bwd_f32(l, cur)
+        elif self.long_attn:
+            self._attn_ext_bwd(l, cur, s)
+        elif self.act and x3:
+            c("ghm_attn_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
+              None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,
+              self.scale_div, self.act, s)
+        elif self.act:
+            c("ghm_attn_bwd_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
+              None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
+              D_MODEL, self.scale_div, self.act, s)
+        else:
+            c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
+              _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)
 
     def _attn_ext_fwd(self, l, s):
         """Attention past 96 tokens on the multi-workgroup split-bf16 kernels:
@@ -535,21 +562,7 @@ class EncoderPlan:
                   _ptr(P_w1), _ptr(P_b1), M, tps, s)
             jobs += [J(P_w1, ns, [g[f"_mlps.{l}.0.weight"]]), J(P_b1, ns, [g[f"_mlps.{l}.0.bias"]])]
             cur, nxt = nxt, cur  # cur = dHmid_l
-            if self.attn_f32:
-                self._attn_bwd_f32(l, cur)
-            elif self.long_attn:
-                self._attn_ext_bwd(l, cur, s)
-            elif self.act and x3:
-                c("ghm_attn_bwd_x3_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
-                  None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dqkv), N, T, D_MODEL,
-                  self.scale_div, self.act, s)
-            elif self.act:
-                c("ghm_attn_bwd_act", _ptr(self.qkv[l]), _ptr(self.P[l]),
-                  None if self.Pd is None else _ptr(self.Pd[l]), _ptr(cur), _ptr(self.dS), _ptr(self.dqkv), N, T,
-                  D_MODEL, self.scale_div, self.act, s)
-            else:
-                c("ghm_attn_bwd_x3" if x3 else "ghm_attn_bwd", _ptr(self.qkv[l]), _ptr(self.P[l]), _ptr(cur),
-                  _ptr(self.dS), _ptr(self.dqkv), N, T, D_MODEL, self.scale_div, s)
+            self._attn_bwd(l, cur, s)
             tps, ns = self.wg["qkv"]  # dWq|k|v[o][in] = sum dqkv[m][o] LN1(H)[m][in]
             if self.wgrad_ring_qkv:  # dqkv f32 (format 0) x LN1(H) (format 1)
                 c("ghm_wgrad_ring_x3", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, 0, 0, _ptr(self.H[l]), D_MODEL,

@@ -28,7 +28,7 @@ import torch
 from ..data.data_random_GHM import DeviceTree
 from .. import _native
 from . import distributed
-from ..models.cdm import CDM_JOINT_UNTRAINED, CDM_UNTRAINED, CdmPlan, cdm_guide_blocks
+from ..models.cdm import CdmPlan, cdm_guide_blocks, cdm_untrained
 from ..models.hip_encoder import EncoderPlan, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
@@ -57,7 +57,7 @@ class CdmTrainer:
         self.sigma = float(sigma)
         self.names = list(model._names)
         sd = dict(model.named_parameters())
-        untrained = CDM_JOINT_UNTRAINED if self.joint else CDM_UNTRAINED
+        untrained = cdm_untrained(model)
         for p in list(sd.values()) + ([] if self.joint else list(clip_model.parameters())):
             require_hip(p)
         trained = [n for n in self.names if n not in untrained]
@@ -87,7 +87,8 @@ class CdmTrainer:
         self.T, self.Ti = T, Ti
         self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,
                             normalize_attn=model.normalize_attn, device=self.device, precision=precision,
-                            joint=self.joint, activation=getattr(model, "activation", "softmax"))
+                            joint=self.joint, activation=getattr(model, "activation", "softmax"),
+                            layernorm=getattr(model, "layernorm", True))
         self.precision = self.plan.precision
         if self.joint:
             self.clip_plan = None

@@ -142,9 +142,10 @@ class OracleCdm(nn.Module):
     then _read_out Linear(d -> 1) and the unused _out Linear(n_token -> 1)."""
 
     def __init__(self, n_token, n_i_token, num_class=10, n_embd=128, n_layer=9, n_mlp_hidden=512, sequential=True,
-                 activation="softmax"):
+                 activation="softmax", layernorm=True):
         super().__init__()
         self.V, self.n_i_token, self.n_embd = num_class, n_i_token, n_embd
+        self.layernorm = layernorm  # model.py:470-477, 488-498: False = Q / K / V and the MLP on H itself
         self.sequential = sequential
         # get_activation (model.py:121-130), applied to the scaled scores at :485
         self.act = {"softmax": lambda x: F.softmax(x, dim=-1), "relu": F.relu, "gelu": F.gelu}[activation]
@@ -179,10 +180,10 @@ class OracleCdm(nn.Module):
         H = emb + self.position_embeddings(pos)  # :437
         for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
                                           self._lns_2):
-            H1 = ln1(H)
+            H1 = ln1(H) if self.layernorm else H
             S = torch.einsum("bid,bjd->bij", q(H1), k(H1)) / np.sqrt(H.shape[2])  # :461-463
             H = H + torch.einsum("bij,bjd->bid", self.act(S), v(H1))  # :485-486
-            H = H + mlp(ln2(H))  # :470-475
+            H = H + mlp(ln2(H) if self.layernorm else H)  # :470-475
         return self._read_out(H)[:, :T2, 0]  # :527-531
 
 
@@ -197,13 +198,14 @@ class OracleCdmTrainer:
     encoder at its seeded initial weights (see make_golden_cdm.py)."""
 
     def __init__(self, p=0.2, B=128, L=9, d=128, lr_max=1e-3, lr_min=1e-6, warmup=0, total_iters=30000,
-                 max_norm=1.0, seed=224, seedtree=42, sigma=1.0, n_bayes=10000, n_layer_tree=4, n_child=3):
+                 max_norm=1.0, seed=224, seedtree=42, sigma=1.0, n_bayes=10000, n_layer_tree=4, n_child=3,
+                 layernorm=True):
         seed_everything(seed)
         self.sampler = CdmSamplerOracle([n_layer_tree] * 2, [n_child] * 2, [p, p], sigma=sigma, seedtree=seedtree)
         self.bayes = self.sampler.get_Bayes(n_bayes) if n_bayes else None
         T = n_child ** n_layer_tree
         self.clip = OracleEncoder(T, 10, 128, 5)
-        self.model = OracleCdm(T + 1, T, 10, d, L, 4 * d)
+        self.model = OracleCdm(T + 1, T, 10, d, L, 4 * d, layernorm=layernorm)
         self.params = list(self.model.parameters())
         self.opt = OracleAdamW(self.params)
         self.B = B

@@ -114,6 +114,23 @@ def test_oracle_two_steps_match_reference():
         np.testing.assert_allclose(ps, g[f"param_stats{k}"], rtol=1e-12, atol=1e-12)
 
 
+def test_noln_oracle_two_steps_match_reference():
+    """ConditionalDenoiseEncoderTransformer(layernorm=False) (model.py:470-477,
+    488-498; the ModelConfig default): two full training steps at L=2, B=4
+    (cdm_noln_tiny.npz); the unused LayerNorms get no gradient."""
+    g = _fix("cdm_noln_tiny.npz")
+    assert not bool(g["layernorm"])
+    tr = CO.OracleCdmTrainer(B=4, L=2, layernorm=False)
+    for k in range(2):
+        ploss, loss, cmp = tr.step()
+        assert abs(ploss - float(g[f"ploss{k}"])) <= 1e-6 * ploss
+        assert abs(cmp - float(g[f"compare{k}"])) <= 1e-6 * cmp
+        np.testing.assert_allclose(tr.last_pred.numpy(), g[f"pred{k}"], rtol=1e-5, atol=1e-4)
+        ps = np.array([[p.double().sum().item(), (p.double() ** 2).sum().item()] for p in tr.model.parameters()])
+        np.testing.assert_allclose(ps[:, 1], g[f"param_stats{k}"][:, 1], rtol=1e-9)
+    assert not any("_lns_" in n for n in g["grad_names0"])
+
+
 def test_joint_oracle_two_steps_match_reference():
     """Joint model (train_CDNS.py, sequential=False, T = 162), two full training steps
     at L=1, B=4 (cdm_joint_tiny.npz): initial weights, predictions, losses, compare

@@ -115,13 +115,13 @@ def test_bp_dns_kernel_per_edge_matches_reference():
         off += want.shape[1]
 
 
-def _pair(L=2, seed=11, precision="f32", activation="softmax"):
+def _pair(L=2, seed=11, precision="f32", activation="softmax", layernorm=True):
     from ghmclip import ConditionalDenoiseEncoderTransformer
     torch.manual_seed(seed)
     prod = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True,
-                                                activation=activation)
+                                                activation=activation, layernorm=layernorm)
     torch.manual_seed(seed)
-    ref = CO.OracleCdm(82, 81, 10, 128, L, 512, activation=activation)
+    ref = CO.OracleCdm(82, 81, 10, 128, L, 512, activation=activation, layernorm=layernorm)
     for (kp, vp), (kr, vr) in zip(prod.state_dict().items(), ref.state_dict().items()):
         assert kp == kr and vp.shape == vr.shape
         assert torch.equal(vp, vr)
@@ -136,15 +136,20 @@ def _pair(L=2, seed=11, precision="f32", activation="softmax"):
     return prod.to(DEV), ref
 
 
-@pytest.mark.parametrize("precision,activation", [("f32", "softmax"), ("x3", "softmax"), ("x3", "relu"),
-                                                  ("x3", "gelu")])
+@pytest.mark.parametrize("precision,activation,layernorm", [
+    ("f32", "softmax", True), ("x3", "softmax", True), ("x3", "relu", True), ("x3", "gelu", True),
+    ("f32", "softmax", False), ("x3", "softmax", False), ("f32", "relu", False)])
 @pytest.mark.parametrize("B", [7, 20])
-def test_cdm_module_forward_backward(B, precision, activation):
+def test_cdm_module_forward_backward(B, precision, activation, layernorm):
     """ConditionalDenoiseEncoderTransformer forward, parameter and conditioning
     gradients vs the oracle restatement of model.py:337-532; the attention
     activation (relu / gelu, model.py:485, train_CDNS.py --activation) on the
-    split-bf16 one-sequence kernels."""
-    prod, ref = _pair(precision=precision, activation=activation)
+    split-bf16 one-sequence kernels; layernorm=False (model.py:470-477, 488-498) on
+    the GEMM layer stack (cdm.NoLnLayers), its LayerNorms without gradients.  relu
+    without LayerNorm runs in f32 here: on the split-bf16 path it measured 6.2e-4 on
+    an MLP weight gradient (B=20; unnormalised scores on un-normalised activations
+    reach gradients of 4e4), outside the 5e-4 split-bf16 bound (r5_cdmnoln)."""
+    prod, ref = _pair(precision=precision, activation=activation, layernorm=layernorm)
     g = torch.Generator().manual_seed(B)
     z = torch.randint(0, 10, (B, 81), generator=g).float() + torch.randn(B, 81, generator=g)
     cond = torch.randn(B, 1, 10, generator=g)
@@ -166,12 +171,13 @@ def test_cdm_module_forward_backward(B, precision, activation):
     assert _rel(cd.grad, cr.grad) < GRAD_TOL[precision]
 
 
-def _trainer(L, B, precision, total_iters=30000):
+def _trainer(L, B, precision, total_iters=30000, layernorm=True):
     from ghmclip import ConditionalDenoiseEncoderTransformer, EncoderTransformer, get_lr_cosine_schedule
     from ghmclip.training.cdm_trainer import CdmTrainer
     s, bayes = _sampler()
     clip = EncoderTransformer(81, 10, 128, 5).to(DEV)
-    model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True).to(DEV)
+    model = ConditionalDenoiseEncoderTransformer(82, 81, 10, 128, L, [1, 4], 4, 512, sequential=True,
+                                                 layernorm=layernorm).to(DEV)
     sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, total_iters) for k in range(total_iters + 1)]
     tr = CdmTrainer(model, clip, B, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV, precision=precision)
     return s, bayes, tr
@@ -228,6 +234,28 @@ def test_cdm_steps_vs_reference_fixture(precision):
     for k in range(2):
         assert abs(hist[k] - float(f[f"ploss{k}"])) <= 2e-5 * float(f[f"ploss{k}"]), (k, hist[k])
         assert abs(chist[k] - float(f[f"compare{k}"])) <= 2e-5 * float(f[f"compare{k}"]), (k, chist[k])
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_cdm_noln_steps_vs_reference_fixture(precision):
+    """layernorm=False (the reference's ModelConfig default, utils/config.py:46):
+    two fused steps at L=2, B=4 against the reference's run (cdm_noln_tiny.npz: its
+    loss grows 1455 -> 12434 in one step without the LayerNorms) — loss and compare
+    at 2e-5 (f32) / 1e-4 (x3) relative, the LayerNorm parameters untouched."""
+    f = np.load(os.path.join(GOLDEN, "cdm_noln_tiny.npz"))
+    assert not bool(f["layernorm"])
+    tol = 2e-5 if precision == "f32" else 1e-4
+    s, _, tr = _trainer(2, 4, precision, layernorm=False)
+    for (n, p), want in zip(tr.model.named_parameters(), f["init_stats"]):
+        assert abs((p.double() ** 2).sum().item() - want[1]) <= 1e-12 * want[1] + 1e-12, n
+    assert all("_lns_" not in n for n in tr.gd)
+    ln0 = {n: p.detach().clone() for n, p in tr.model.named_parameters() if "_lns_" in n}
+    hist, chist = _run(s, tr, 4, 2)
+    for k in range(2):
+        assert abs(hist[k] - float(f[f"ploss{k}"])) <= tol * float(f[f"ploss{k}"]), (k, hist[k])
+        assert abs(chist[k] - float(f[f"compare{k}"])) <= tol * float(f[f"compare{k}"]), (k, chist[k])
+    for n, v in ln0.items():
+        assert torch.equal(dict(tr.model.named_parameters())[n].detach(), v), n
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

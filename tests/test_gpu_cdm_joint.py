@@ -38,23 +38,26 @@ def _need_gpu():
     assert _native.hip_lib().ghm_device_ok() == 1, "libghm_hip.so not usable on this device"
 
 
-@pytest.mark.parametrize("B,mode,act", [(3, "x3", "softmax"), (8, "x3", "softmax"), (8, "f32", "softmax"),
-                                        (8, "f32_exact_attn", "softmax"), (5, "x3", "relu"), (5, "f32", "gelu")])
-def test_joint_cdm_module_forward_backward(B, mode, act, monkeypatch):
+@pytest.mark.parametrize("B,mode,act,ln", [(3, "x3", "softmax", True), (8, "x3", "softmax", True),
+                                           (8, "f32", "softmax", True), (8, "f32_exact_attn", "softmax", True),
+                                           (5, "x3", "relu", True), (5, "f32", "gelu", True),
+                                           (6, "f32", "softmax", False), (6, "x3", "softmax", False)])
+def test_joint_cdm_module_forward_backward(B, mode, act, ln, monkeypatch):
     """ConditionalDenoiseEncoderTransformer(sequential=False) forward and every
     parameter gradient (t_embedding included) vs the oracle restatement, in
     the split-bf16 mode, the f32 mode (the joint default: exact projections and
     MLP, split-bf16 attention core past 96 tokens), the f32 mode's exact torch
     attention (GHM_LONG_ATTN=f32, the validation path), and with the relu / gelu
-    attention of train_CDNS.py --activation (model.py:485; ghm_attn_ext_*_act)."""
+    attention of train_CDNS.py --activation (model.py:485; ghm_attn_ext_*_act), and
+    with layernorm=False (model.py:470-477, 488-498; the GEMM layer stack)."""
     from ghmclip import ConditionalDenoiseEncoderTransformer
     if mode == "f32_exact_attn":
         monkeypatch.setenv("GHM_LONG_ATTN", "f32")
     torch.manual_seed(11)
     prod = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 2, [4, 4], 4, 512, sequential=False,
-                                                activation=act)
+                                                activation=act, layernorm=ln)
     torch.manual_seed(11)
-    ref = CO.OracleCdm(162, 81, 10, 128, 2, 512, sequential=False, activation=act)
+    ref = CO.OracleCdm(162, 81, 10, 128, 2, 512, sequential=False, activation=act, layernorm=ln)
     g = torch.Generator().manual_seed(B)
     with torch.no_grad():
         for (kp, vp), (_, vr) in zip(prod.named_parameters(), ref.named_parameters()):

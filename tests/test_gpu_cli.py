@@ -94,6 +94,24 @@ def test_joint_cdm_cli(tmp_path, monkeypatch):
     assert d["model_state_dict"]["position_embeddings.weight"].shape == (162, 128)
 
 
+def test_cdm_and_vlm_cli_layernorm_default(tmp_path, monkeypatch):
+    """train_CDNS / train_NWP without --layernorm: ModelConfig's default
+    layernorm=False (utils/config.py:46) runs the models without LayerNorm
+    (model.py:269-301, 470-498); the unused LayerNorms stay at their initial values
+    in the saved state dict."""
+    from ghmclip.training import train_CDNS, train_NWP
+    from ghmclip.training.train_CLIP import load_checkpoint
+    monkeypatch.chdir(tmp_path)
+    flags = [f for f in CDNS_FLAGS if not f.startswith("--layernorm")]
+    loss, compare = train_CDNS.main(flags)
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+    ck = glob.glob("logs/CDM/K4_L4C3p20_L4C3p20sc10/JT_L2H4D128/*/checkpoint.pth")
+    sd = load_checkpoint(ck[0], "cpu")["model_state_dict"]
+    assert torch.equal(sd["_lns_1.0.weight"], torch.ones(128)) and torch.equal(sd["_lns_2.1.bias"], torch.zeros(128))
+    loss, compare = train_NWP.main([f for f in NWP_FLAGS if not f.startswith("--layernorm")])
+    assert len(loss) == 5 and np.isfinite(loss).all() and np.isfinite(compare).all()
+
+
 def test_guided_cdm_cli(tmp_path, monkeypatch):
     """exp_cdm_guidedTF.sh flags (shortened, L=9 for the 9 guided layers): train_CDNS
     --guide=True writes logs/CDM/<tree>/GT_L9H4D128/ with the penalised loss in
