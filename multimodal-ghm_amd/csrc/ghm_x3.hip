@@ -508,6 +508,49 @@ __device__ __forceinline__ void ws_mphase(const __bf16* __restrict__ cb, const b
   }
 }
 
+// The same with every operand read issued before the first MFMA (64 VGPRs per
+// product): the scheduler otherwise keeps one read ahead and waits lgkmcnt(0)
+// every 3 MFMAs; here the waits count down (lgkmcnt(N)) while the MFMAs run.
+// For the 256-VGPR build (one workgroup per CU) only.
+template <bool DOWN, bool UP>
+__device__ __forceinline__ void ws_mphase_deep(const __bf16* __restrict__ cb, const bf16x8* xh, const bf16x8* xl,
+                                               f32x4* y, WsState& st, int t, int g) {
+  bf16x8 dh[8], dl[8], uh[8], ul[8];
+  if (DOWN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = r128_off(16 * j + t, g);
+      dh[j] = ldsb8(cb + 2 * PLANE + o);
+      dl[j] = ldsb8(cb + 3 * PLANE + o);
+    }
+  }
+  if (UP) {
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int o = r32_off(16 * jt + t, 4 * s2 + g);
+        uh[4 * jt + s2] = ldsb8(cb + o);
+        ul[4 * jt + s2] = ldsb8(cb + PLANE + o);
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (DOWN) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = mfma16_x3(dh[j], dl[j], st.gh, st.gl, y[j]);
+  }
+  if (UP) {
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      st.u[jt] = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        st.u[jt] = mfma16_x3(uh[4 * jt + s2], ul[4 * jt + s2], xh[s2], xl[s2], st.u[jt]);
+    }
+  }
+}
+
 // V phase: G = GELU(U + b1) -> (gh, gl)
 __device__ __forceinline__ void ws_vphase(const float4* bb, WsState& st) {
   float gv[8], dg[8];
@@ -549,25 +592,34 @@ __device__ __forceinline__ void ws_fill(__bf16* nb, const __bf16* W1, const __bf
 // then A: M(p) | V(p), B: V(p-1) | M(p).  cb / nb: __restrict__ parameters of one
 // inlined function (alias scopes: no vmcnt wait for the fresh fills before the
 // operand reads)
-template <int NW, bool GRP_A>
+template <bool DEEP, bool DOWN, bool UP>
+__device__ __forceinline__ void ws_m(const __bf16* __restrict__ cb, const bf16x8* xh, const bf16x8* xl, f32x4* y,
+                                     WsState& st, int t, int g) {
+  if (DEEP)
+    ws_mphase_deep<DOWN, UP>(cb, xh, xl, y, st, t, g);
+  else
+    ws_mphase<DOWN, UP>(cb, xh, xl, y, st, t, g);
+}
+
+template <int NW, bool GRP_A, bool DEEP = false>
 __device__ __forceinline__ void ws_pair(const __bf16* __restrict__ cb, __bf16* __restrict__ nb, int p,
                                         const __bf16* W1, const __bf16* W2, const float4* bb, const bf16x8* xh,
                                         const bf16x8* xl, f32x4* y, WsState& st, int t, int g) {
   ws_fill<NW>(nb, W1, W2, p);
   if (GRP_A) {
-    ws_mphase<true, true>(cb, xh, xl, y, st, t, g);
+    ws_m<DEEP, true, true>(cb, xh, xl, y, st, t, g);
     ws_bar();
     ws_vphase(bb, st);
   } else {
     ws_vphase(bb, st);
     ws_bar();
-    ws_mphase<true, true>(cb, xh, xl, y, st, t, g);
+    ws_m<DEEP, true, true>(cb, xh, xl, y, st, t, g);
   }
   ws_bar_fills();
 }
 
 // a group's whole chunk loop: pair 0 (U(0) only), pairs 1 .. NC-1, pair NC (Y(NC-1) only)
-template <int NW, bool GRP_A>
+template <int NW, bool GRP_A, bool DEEP = false>
 __device__ __forceinline__ void ws_loop(__bf16* lds, const __bf16* W1, const __bf16* W2, const float* sb1,
                                         const bf16x8* xh, const bf16x8* xl, f32x4* y, int t, int g) {
   constexpr int NC = GHM_F / 32;
@@ -582,30 +634,30 @@ __device__ __forceinline__ void ws_loop(__bf16* lds, const __bf16* W1, const __b
   if (GRP_A) read_b1(0);
   ws_fill<NW>(lds + 4 * PLANE, W1, W2, 0);
   if (GRP_A) {
-    ws_mphase<false, true>(lds, xh, xl, y, st, t, g);
+    ws_m<DEEP, false, true>(lds, xh, xl, y, st, t, g);
     ws_bar();
     ws_vphase(bb, st);
   } else {
     ws_bar();
-    ws_mphase<false, true>(lds, xh, xl, y, st, t, g);
+    ws_m<DEEP, false, true>(lds, xh, xl, y, st, t, g);
   }
   ws_bar_fills();
 #pragma unroll 1
   for (int p = 1; p < NC; ++p) {
     const int cur = p & 1;
     read_b1(GRP_A ? p : p - 1);
-    ws_pair<NW, GRP_A>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), p, W1, W2, bb, xh, xl, y, st, t, g);
+    ws_pair<NW, GRP_A, DEEP>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), p, W1, W2, bb, xh, xl, y, st, t, g);
   }
   // pair NC: slot NC & 1 = {W2(NC-1)}
   const __bf16* cb = lds + 4 * PLANE * (NC & 1);
   if (GRP_A) {
-    ws_mphase<true, false>(cb, xh, xl, y, st, t, g);
+    ws_m<DEEP, true, false>(cb, xh, xl, y, st, t, g);
     ws_bar();
   } else {
     read_b1(NC - 1);
     ws_vphase(bb, st);
     ws_bar();
-    ws_mphase<true, false>(cb, xh, xl, y, st, t, g);
+    ws_m<DEEP, true, false>(cb, xh, xl, y, st, t, g);
   }
   ws_bar();
 }
@@ -613,8 +665,8 @@ __device__ __forceinline__ void ws_loop(__bf16* lds, const __bf16* W1, const __b
 // 4 waves per SIMD (HIP's second bound: minimum waves per EU), i.e. two
 // workgroups per CU as x3b; at the bound 2 the compiler spent 153 VGPRs (one
 // workgroup per CU)
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 4) void k_ln_mlp_fwd_x3w(
+template <int NW, int MINW = 4>
+__global__ __launch_bounds__(64 * NW, MINW) void k_ln_mlp_fwd_x3w(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
     float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
@@ -686,9 +738,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ln_mlp_fwd_x3w(
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (grpA)
-    ws_loop<NW, true>(lds, W1, W2, sb1, xh, xl, y, t, g);
+    ws_loop<NW, true, MINW == 2>(lds, W1, W2, sb1, xh, xl, y, t, g);
   else
-    ws_loop<NW, false>(lds, W1, W2, sb1, xh, xl, y, t, g);
+    ws_loop<NW, false, MINW == 2>(lds, W1, W2, sb1, xh, xl, y, t, g);
   if (valid) {
     float* orow = Hout + m * GHM_D;
 #pragma unroll
@@ -2546,8 +2598,14 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
   // GHM_MLP_FWD_WS=1: the wave-specialised schedule (k_ln_mlp_fwd_x3w); read per
   // call (a graph captures the choice made at capture time)
   const char* ws_env = std::getenv("GHM_MLP_FWD_WS");
-  const int ws = ws_env ? std::atoi(ws_env) : 0;  // 1: 8 waves (two workgroups per CU), 2: 16 waves (one)
-  if (big && ws == 2)
+  // 1: 8 waves (two workgroups per CU), 2: 16 waves (one), 3: 8 waves at up to 256 VGPRs (one)
+  const int ws = ws_env ? std::atoi(ws_env) : 0;
+  if (big && ws == 4)  // the plain schedule at 16 waves / 256 tokens: half the weight streaming per token
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<16>, dim3(static_cast<unsigned>((M + 255) / 256)), dim3(1024), 0, s, H_mid,
+                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+  else if (big && ws == 3)  // 8 waves at <= 256 VGPRs: one workgroup per CU, deeper operand prefetch
+    hipLaunchKernelGGL((k_ln_mlp_fwd_x3w<8, 2>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+  else if (big && ws == 2)
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3w<16>, dim3(static_cast<unsigned>((M + 255) / 256)), dim3(1024), 0, s, H_mid,
                        ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
   else if (big && ws)

@@ -49,7 +49,7 @@ def _run(plan, p, Hmid, M, ws):
     return H, st
 
 
-@pytest.mark.parametrize("ws", [1, 2])
+@pytest.mark.parametrize("ws", [1, 2, 3, 4])
 @pytest.mark.parametrize("M", [51840, 40001, 32768])
 def test_ws_forward_bit_identical(M, ws):
     """Every M that takes the 128-token workgroups (>= 256 of them), ragged tails included."""
@@ -68,7 +68,7 @@ def test_ws_forward_bit_identical(M, ws):
     assert torch.equal(s0, s1)
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "3", "4"])
 def test_ws_step_gradients_bit_identical(mode):
     grads = []
     for ws in (mode, "0"):

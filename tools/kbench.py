@@ -105,6 +105,14 @@ def main():
                 "ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk,
                 P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp)),
                                gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3w82": (lambda: _with_env("GHM_MLP_FWD_WS", "3", lambda: c(
+                "ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk,
+                P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp)),
+                               gf(4 * M * 128 * 512)),
+            "ln_mlp_fwd_x3b16": (lambda: _with_env("GHM_MLP_FWD_WS", "4", lambda: c(
+                "ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk,
+                P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp)),
+                               gf(4 * M * 128 * 512)),
             "mlp_bwd_rc_x3": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
                                         P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512,
