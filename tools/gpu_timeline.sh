@@ -14,3 +14,5 @@ f=$(find gpurun_out/tl_$TAG -name '*kernel_trace.csv' | head -1)
 python tools/timeline.py "$f" k_adamw -26 -v > gpurun_out/tl_$TAG/timeline.txt
 s=$(find gpurun_out/tl_$TAG -name '*kernel_stats.csv' | head -1)
 python tools/kstats.py "$s" 26 30 > gpurun_out/tl_$TAG/kstats.txt
+# keep the derived timeline / stats, drop the per-dispatch trace (gpurun merges back at most 64 MiB)
+find gpurun_out/tl_$TAG -name '*kernel_trace.csv' -size +4M -delete
