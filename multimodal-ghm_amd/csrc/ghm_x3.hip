@@ -417,6 +417,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
       fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1h(cur ^ 1), s1l(cur ^ 1));
       fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2h(cur ^ 1), s2l(cur ^ 1));
     }
+#endif
     f32x4 u[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -454,7 +455,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     if (GHM_ABL != 5)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-#endif
   if (valid) {
     float* orow = Hout + m * GHM_D;
 #pragma unroll
