@@ -292,7 +292,7 @@ def pmc_traffic(kernel):
     with open(path) as f:
         t = json.load(f)
     ks = t.get("kernels", {})
-    for suffix in ("", "<8>", "<8, 0>", "<8, false>"):  # the instantiation the step launches (NW = 8)
+    for suffix in ("", "<8>", "<8, 0>", "<8, false>", "<8, 0, false>"):  # the instantiation the step launches (NW = 8)
         if kernel + suffix in ks:
             return ks[kernel + suffix]["hbm_bytes"]
     return None
@@ -337,6 +337,18 @@ def _kname(raw):
     return name[5:] if name.startswith("void ") else name
 
 
+def _rc_twin(inst, stamp):
+    """k_mlp_bwd_rc_x3<NW, STAMP[, SPLITOUT]> with STAMP replaced (the stamped twins
+    are STAMP 1 / 2 of the same instantiation), or None for other kernels."""
+    if not inst or not inst.startswith("k_mlp_bwd_rc_x3<") or not inst.endswith(">"):
+        return None
+    args = [x.strip() for x in inst[len("k_mlp_bwd_rc_x3<"):-1].split(",")]
+    if len(args) < 2:
+        return None
+    args[1] = str(stamp)
+    return "k_mlp_bwd_rc_x3<" + ", ".join(args) + ">"
+
+
 def profiled_kernels():
     """(path, {kernel instantiation: (total ns, calls, average ns)}) of the committed
     rocprofv3 --kernel-trace --stats summary of graph-replayed CLIP bench steps."""
@@ -347,8 +359,8 @@ def profiled_kernels():
     agg = {}
     for r in csv.DictReader(open(path)):
         k = _kname(r["Name"])  # instantiation (template arguments kept)
-        if k.startswith("k_mlp_bwd_rc_x3<") and k.endswith(", 2>"):  # the concurrent-step stamped twin
-            k = k[:-len(", 2>")] + ", 0>"
+        if _rc_twin(k, 2) == k:  # the concurrent-step stamped twin counts as the kernel itself
+            k = _rc_twin(k, 0)
         t, n = agg.get(k, (0.0, 0))
         agg[k] = (t + float(r["TotalDurationNs"]), n + int(r["Calls"]))
     return path, {k: (t, n, t / max(1, n)) for k, (t, n) in agg.items()}
@@ -625,7 +637,8 @@ def main():
     top = max(prof, key=lambda k: prof[k][0]) if prof else None
     # the largest single call site: k_wgrad_x3<2, .> totals two different GEMMs (dW1 and
     # dWqkv, one instantiation), so the candidates are the one-call-site kernels
-    cands = [k for k in prof if k.split("<")[0] in DOMINANT_CANDIDATES and not k.endswith(", 1>")]
+    cands = [k for k in prof if k.split("<")[0] in DOMINANT_CANDIDATES and not k.endswith(", 1>")
+             and _rc_twin(k, 1) != k]  # not the serialized-measurement twin
     dom_inst = max(cands, key=lambda k: prof[k][0]) if cands else None
     dom = dom_inst.split("<")[0] if dom_inst else "k_mlp_bwd_rc_x3"
     if tr.precision != "x3":
@@ -637,7 +650,7 @@ def main():
             dom_ms_conc, n_c = time_mlp_bwd_in_graph(tr, serial=False)
             dom_how = (f"graph replay with the two towers' launches on one stream (the kernel alone on the GPU): "
                        f"every launch's first-workgroup start to last-workgroup end (s_memrealtime stamps of the "
-                       f"kernel's stamped twin k_mlp_bwd_rc_x3<8, 1>), {n_l} launches; the rocprofv3 average of "
+                       f"kernel's stamped twin k_mlp_bwd_rc_x3<8, 1, false>), {n_l} launches; the rocprofv3 average of "
                        f"that twin in the same command is profile_avg_ms")
         else:
             dom_ms = time_kernel_in_step(tr, DOMINANT_CANDIDATES[dom]["entry"])
@@ -686,7 +699,7 @@ def main():
         dtraffic = pmc_traffic(dom_inst or dom)
         if dtraffic is None and dom == "k_mlp_bwd_rc_x3":  # names of older profiles
             dtraffic = pmc_traffic("k_mlp_bwd_rc_x3<8, false>") or pmc_traffic("k_mlp_bwd_rc_x3<8>")
-        twin = (dom_inst or "")[:-len(", 0>")] + ", 1>" if (dom_inst or "").endswith(", 0>") else None
+        twin = _rc_twin(dom_inst, 1) if _rc_twin(dom_inst, 0) == dom_inst else None
         prof_avg_ms = prof[twin][2] / 1e6 if twin in prof else None  # the serialized-measurement twin
         roofline = {"bound": "mfma",
                     "kernel": f"{dom} ({d['what']})",
@@ -699,7 +712,7 @@ def main():
                     "algorithmic_bytes": round(d["bytes"] * scale), "design_bytes": round(d["design_bytes"] * scale),
                     "kernel_ms": round(dom_ms, 4), "timing": dom_how,
                     "kernel_ms_concurrent": None if dom_ms_conc is None else round(dom_ms_conc, 4),
-                    "concurrent_note": "span of the same launches in the real step (twin k_mlp_bwd_rc_x3<8, 2>), "
+                    "concurrent_note": "span of the same launches in the real step (twin k_mlp_bwd_rc_x3<8, 2, false>), "
                                        "where the other tower's kernels share the CUs",
                     "dominant_by": (f"{dom_inst}: {100 * prof[dom_inst][0] / ptot:.1f} % of kernel time in "
                                     f"{os.path.relpath(prof_path, ROOT)}, the largest single call site"
