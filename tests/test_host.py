@@ -330,3 +330,22 @@ def test_sampler_usable_after_fork():
     os.waitpid(pid, 0)
     s.native.next_into(B, t, i)
     assert buf == t.tobytes() + i.tobytes()
+
+
+def test_bench_finds_the_dominant_kernels_stamped_twin():
+    """bench.py's roofline line reads the dominant kernel and its serialized-measurement
+    twin (STAMP 1 of the same instantiation) from the newest committed kernel
+    statistics; a template argument added to the kernel must not lose the twin
+    (round 5: profile_avg_ms was null until the lookup parsed the arguments)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b._rc_twin("k_mlp_bwd_rc_x3<8, 0, false>", 1) == "k_mlp_bwd_rc_x3<8, 1, false>"
+    assert b._rc_twin("k_mlp_bwd_rc_x3<8, 0>", 2) == "k_mlp_bwd_rc_x3<8, 2>"
+    assert b._rc_twin("k_wgrad_x3<0, 4, 128, 512>", 1) is None
+    path, prof = b.profiled_kernels()
+    assert path is not None
+    rc = [k for k in prof if k.startswith("k_mlp_bwd_rc_x3<") and b._rc_twin(k, 0) == k]
+    assert rc and all(b._rc_twin(k, 1) in prof for k in rc), (path, sorted(prof))
+    assert b.pmc_traffic("k_mlp_bwd_rc_x3") is not None
