@@ -277,7 +277,7 @@ class EncoderPlan:
 
     def _layer_fwd(self, p, l, s):
         c = _native.call
-        M, T, N = self.M, self.T, self.N
+        M = self.M
         x3 = self.precision == "x3"
         if True:
             if x3:
@@ -518,7 +518,7 @@ class EncoderPlan:
         ping-pong buffer)."""
         c = _native.call
         J = self._job
-        M, T, N = self.M, self.T, self.N
+        M = self.M
         x3 = self.precision == "x3"
         wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
         P_ln, P_ln2 = self._lp("ln", l), self._lp("ln2", l)
