@@ -163,6 +163,12 @@ class OracleCdm(nn.Module):
             self._lns_2.append(nn.LayerNorm([n_embd]))
         self._read_out = nn.Linear(n_embd, 1)
         self._out = nn.Linear(n_token, 1)
+        # test-only probe (not the reference): per-layer boolean masks [B, T, T] that
+        # replace relu's own (S > 0) -- e.g. the kernels' masks, read back from their
+        # saved P -- so the float64 gradient is taken with the same derivative of
+        # relu at near-zero scores; the forward value S * mask differs from relu(S)
+        # only at such scores
+        self.relu_masks = None
 
     def forward(self, xt, zi):
         """xt: CLIP text features [B, T1, V] (sequential) or text leaves [B, T1] (joint,
@@ -178,11 +184,12 @@ class OracleCdm(nn.Module):
             emb[:, T2:, :] = self.t_embedding(xt)  # :422-423
         pos = torch.arange(T1 + T2).expand(B, T1 + T2)
         H = emb + self.position_embeddings(pos)  # :437
-        for q, k, v, mlp, ln1, ln2 in zip(self._queries, self._keys, self._values, self._mlps, self._lns_1,
-                                          self._lns_2):
+        for li, (q, k, v, mlp, ln1, ln2) in enumerate(zip(self._queries, self._keys, self._values, self._mlps,
+                                                          self._lns_1, self._lns_2)):
             H1 = ln1(H) if self.layernorm else H
             S = torch.einsum("bid,bjd->bij", q(H1), k(H1)) / np.sqrt(H.shape[2])  # :461-463
-            H = H + torch.einsum("bij,bjd->bid", self.act(S), v(H1))  # :485-486
+            A = self.act(S) if self.relu_masks is None else S * self.relu_masks[li]
+            H = H + torch.einsum("bij,bjd->bid", A, v(H1))  # :485-486
             H = H + mlp(ln2(H) if self.layernorm else H)  # :470-475
         return self._read_out(H)[:, :T2, 0]  # :527-531
 

@@ -38,3 +38,49 @@ def curve_bound(ref, ref_t2, floor=1e-4, factor=2.0):
     bound = np.maximum(floor, factor * spread)
     window = int(np.argmax(spread > floor)) if (spread > floor).any() else len(spread)
     return bound, window, spread
+
+
+def kernel_relu_masks(module):
+    """The relu masks the split-bf16 attention kernels used in a module's last
+    forward: P > 0 of each layer's saved scores ([L] x bool [N, T, T], on the CPU;
+    the backward takes relu's derivative from the same P)."""
+    (plan,) = module._plans.values()
+    return [(plan.probs_dense(l) > 0).cpu() for l in range(plan.L)]
+
+
+def masked_relu_oracle(ref, masks, loss):
+    """A float64 copy of an oracle module with relu replaced by the given masks
+    (OracleCdm.relu_masks), its gradients from loss(model).backward() in float64.
+    Checks first that the masks are relu's own up to near-zero scores: they agree
+    with the float64 scores' signs everywhere but a handful of entries."""
+    import copy
+
+    import torch
+    dt = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        r64 = copy.deepcopy(ref).double()
+        r64.zero_grad()
+        S = []
+        orig = torch.einsum
+
+        def capture(eq, *a):
+            y = orig(eq, *a)
+            if eq == "bid,bjd->bij":
+                S.append(y.detach())
+            return y
+        torch.einsum = capture
+        try:
+            with torch.no_grad():
+                loss(r64)
+        finally:
+            torch.einsum = orig
+        assert len(S) == len(masks)
+        for s, m in zip(S, masks):
+            assert s.shape == m.shape
+            assert int(((s > 0) != m).sum()) <= 16, "kernel masks differ from relu(S > 0) beyond near-zero scores"
+        r64.relu_masks = [m.double() for m in masks]
+        loss(r64).backward()
+    finally:
+        torch.set_default_dtype(dt)
+    return r64

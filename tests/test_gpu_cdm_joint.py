@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN, curve_bound
+from conftest import GOLDEN, curve_bound, kernel_relu_masks, masked_relu_oracle
 from oracle import cdm_oracle as CO
 
 pytestmark = pytest.mark.gpu
@@ -78,15 +78,22 @@ def test_joint_cdm_module_forward_backward(B, mode, act, ln, monkeypatch):
     (want * R).sum().backward()
     torch.cuda.synchronize()
     assert _rel(pred, want) < 1e-4
-    # relu on the split-bf16 kernels: unnormalised scores (no softmax) make the
-    # 162-key sums and their gradients larger; measured 6.2e-4 on the position
-    # embeddings' gradient (a sum over every sequence), so 1e-3 there
-    gtol = 1e-3 if (mode, act) == ("x3", "relu") else 5e-4
+    if act == "relu":
+        # relu's derivative steps at a zero score: a score inside the split-bf16
+        # rounding band (~2^-17 of |q||k|) can land on the other side of zero, and
+        # that one mask entry moves the position / token-embedding gradients by up
+        # to 2e-2 (the float64 oracle moves by 1e-3 to 3e-2 under a 2^-17 perturbation
+        # of the q / k weights: tools/diag_cdm_relu.py, profiles/r5_relu_mask.txt).  So the
+        # gradients are held, at the same 5e-4, against the float64 oracle taken with
+        # the kernels' own relu masks (read back from the saved P; they agree with
+        # the float64 scores' signs but for a handful of near-zero entries).
+        masks = kernel_relu_masks(prod)
+        ref = masked_relu_oracle(ref, masks, lambda m: (m(xt, z.double()) * R.double()).sum())
     for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
         if pr.grad is None:
             assert pp.grad is None, k
             continue
-        assert _rel(pp.grad, pr.grad) < gtol, k
+        assert _rel(pp.grad, pr.grad) < 5e-4, k
 
 
 def _trainer(L, B, total_iters=30000, precision="x3"):
