@@ -151,6 +151,43 @@ __device__ __forceinline__ void store_oc(const float4* v, __bf16* hi, __bf16* lo
   }
 }
 
+// Buffer-load staging (BUF): each thread's byte offsets inside a K tile are
+// fixed (computed once, the same row / column mapping as load_kc / load_oc); a
+// tile moves only the SGPR descriptor's base, and its record count ends the
+// operand at the last valid row, so rows past M (k-contiguous A), past the
+// split's last token (the [k][outer] operands) or past the end of K read as
+// zeros in hardware: no per-tile 64-bit address arithmetic, row clamps or
+// zeroing selects on the VALU.
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t rs, int voff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
+  return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const float* p, int64_t bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes > 0 ? bytes : 0));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>((static_cast<uint64_t>(hi) << 32) | lo),
+                                           static_cast<short>(0), n, 0x00020000);
+}
+// a thread's byte offsets: k-contiguous tile (row kc_row(idx), 4 floats at k4)
+template <int ROWS>
+__device__ __forceinline__ void voff_kc(int* vo, int64_t ld) {
+#pragma unroll
+  for (int i = 0; i < ROWS * 8 / 256; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    vo[i] = static_cast<int>((kc_row(idx) * ld + 4 * (idx & 7)) * 4);
+  }
+}
+// [k][outer] tile: rows RPT kg + i, columns 4 c4 (load_oc's mapping)
+template <int COLS>
+__device__ __forceinline__ void voff_oc(int* vo, int64_t ld) {
+  constexpr int RPT = COLS / 32, KG = 32 / RPT;
+  const int kg = threadIdx.x % KG, c4 = threadIdx.x / KG;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) vo[i] = static_cast<int>(((RPT * kg + i) * ld + 4 * c4) * 4);
+}
+
 // exact-f32 variant (F32): [row][k] f32 images with a 36-float pitch, staged
 // without a split; lane (r, h) of a v_mfma_f32_32x32x2f32 takes k = 16 h + kk at
 // step kk (both operands alike), so a lane's 16 operands are four 16-byte reads.
@@ -184,8 +221,13 @@ __device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_
 
 // F32 = true: the exact-f32 product (the VLM's precision "f32" mode) on the same
 // tiling, prefetch schedule and epilogues; GELU then uses the erf form.
-template <bool TA, bool TB, int EPI, int TM, bool F32>
+// V bit 0 (BUF): stage through buffer loads (bload4 / brsrc above) instead of
+// pointer loads; bit 1 (IL, with BUF): the next tile's split store is issued in
+// the same scheduling region as the current tile's MFMAs, interleaved with them
+// by sched_group_barrier (a wave's staging VALU fills its own MFMA gaps)
+template <bool TA, bool TB, int EPI, int TM, bool F32, int V = 0>
 __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
+  constexpr bool BUF = (V & 1) != 0, IL = (V & 3) == 3;
   constexpr int BM = 64 * TM;
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
   constexpr int NB = TB ? GB_N * 8 / 256 : GB_N / 32;
@@ -230,7 +272,42 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     return g.B[q];
   };
 
+  int voa[BUF ? NA : 1], vob[BUF ? NB : 1];
+  if constexpr (BUF) {
+    if constexpr (TA) voff_oc<BM>(voa, g.lda);
+    else voff_kc<BM>(voa, g.lda);
+    if constexpr (TB) voff_kc<GB_N>(vob, g.ldb);
+    else voff_oc<GB_N>(vob, g.ldb);
+  }
   auto load = [&](float4* va, float4* vb, int64_t k0) {
+    if constexpr (BUF) {
+      // the tile's rows from its first: k0 on for [k][outer], m0 / n0 on for k-contiguous
+      const int64_t krows = ke - k0 < GB_K ? ke - k0 : GB_K;
+      if constexpr (TA) {
+        const auto rs = brsrc(g.A + k0 * g.lda + m0, krows * g.lda * 4);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
+      } else {
+        const int64_t mrows = g.M - m0 < BM ? g.M - m0 : BM;
+        const auto rs = brsrc(g.A + m0 * g.lda + k0, mrows * g.lda * 4);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
+      }
+      if constexpr (TB) {
+        int64_t ln;
+        const float* b = bbase(n0, ln);
+        const auto rs = brsrc(b + ln * g.ldb + k0, GB_N * g.ldb * 4);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) vb[i] = bload4(rs, vob[i]);
+      } else {
+        int64_t lk;
+        const float* b = bbase(k0, lk);
+        const auto rs = brsrc(b + lk * g.ldb + n0, krows * g.ldb * 4);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) vb[i] = bload4(rs, vob[i]);
+      }
+      return;
+    }
     if constexpr (TA) load_oc<BM>(va, g.A, g.lda, k0, ke, m0);
     else load_kc<BM>(va, g.A, g.lda, m0, g.M, k0);
     if constexpr (TB) {
@@ -253,19 +330,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
         const int kg = threadIdx.x % (32 / NA);  // load_oc's lane mapping
 #pragma unroll
         for (int i = 0; i < NA; ++i)
-          if (k0 + NA * kg + i < ke) {
+          if (BUF || k0 + NA * kg + i < ke) {  // BUF: rows past the split read as zeros
             rs.x += va[i].x; rs.y += va[i].y; rs.z += va[i].z; rs.w += va[i].w;
           }
       }
     }
     if constexpr (F32) {
-      if constexpr (TA) store_oc_f32<BM, true>(va, af[buf], k0, ke);
+      if constexpr (TA) store_oc_f32<BM, !BUF>(va, af[buf], k0, ke);
       else store_kc_f32<BM>(va, af[buf]);
       if constexpr (TB) store_kc_f32<GB_N>(vb, bf[buf]);
       else store_oc_f32<GB_N, false>(vb, bf[buf], k0, ke);
       return;
     }
-    if constexpr (TA) store_oc<BM, true>(va, ah[buf], al[buf], k0, ke);
+    if constexpr (TA) store_oc<BM, !BUF>(va, ah[buf], al[buf], k0, ke);
     else store_kc<BM>(va, ah[buf], al[buf]);
     if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
     else store_oc<GB_N, false>(vb, bh[buf], bl[buf], k0, ke);
@@ -324,6 +401,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     }
   };
 
+  // IL: one MFMA, then up to 6 VALU (the split of the next tile) and one LDS
+  // write, repeated over the tile's MFMAs
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM * 2 * 2 * 3; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+  };
+
   // two K tiles in flight in registers (sets p, q) ahead of the LDS tile being
   // multiplied: the global loads of a tile are issued two compute phases before
   // their split store, which keeps enough bytes in flight per CU to cover HBM
@@ -337,10 +425,16 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     int buf = 0;
     for (int64_t k0 = kb; k0 < ke; k0 += GB_K) {
       const bool more = k0 + GB_K < ke;
-      load(pa, pb, more ? k0 + GB_K : k0);  // unconditional: no branch around the loads
+      // unconditional: no branch around the loads (BUF: a tile past ke reads zeros)
+      load(pa, pb, more || BUF ? k0 + GB_K : k0);
       issue_fence();
       compute(buf);
-      if (more) store(pa, pb, buf ^ 1, k0 + GB_K);
+      if constexpr (IL) {
+        store(pa, pb, buf ^ 1, k0 + GB_K);  // past the end: zeros into a buffer nobody reads
+        interleave();
+      } else if (more) {
+        store(pa, pb, buf ^ 1, k0 + GB_K);
+      }
       __syncthreads();
       buf ^= 1;
     }
@@ -348,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     float4 pa[NA], pb[NB], qa[NA], qb[NB];
     // loads are unconditional (past the last tile they re-read it, unused): a load
     // under a branch made the wait-count pass drain every load at the next store
-    auto kt = [&](int64_t k) { return k < ke ? k : klast; };
+    auto kt = [&](int64_t k) { return BUF || k < ke ? k : klast; };  // BUF: past ke reads zeros
     load(pa, pb, kb);
     load(qa, qb, kt(kb + GB_K));
     issue_fence();
@@ -359,13 +453,23 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     for (int64_t k0 = kb; k0 < ke; k0 += 2 * GB_K) {
       // LDS[0] = tile k0; q = tile k0 + 32; p = tile k0 + 64 (in flight)
       compute(0);
-      if (k0 + GB_K < ke) store(qa, qb, 1, k0 + GB_K);
+      if constexpr (IL) {
+        store(qa, qb, 1, k0 + GB_K);
+        interleave();
+      } else if (k0 + GB_K < ke) {
+        store(qa, qb, 1, k0 + GB_K);
+      }
       __syncthreads();
       load(qa, qb, kt(k0 + 3 * GB_K));
       issue_fence();
       if (k0 + GB_K >= ke) break;
       compute(1);
-      if (k0 + 2 * GB_K < ke) store(pa, pb, 0, k0 + 2 * GB_K);
+      if constexpr (IL) {
+        store(pa, pb, 0, k0 + 2 * GB_K);
+        interleave();
+      } else if (k0 + 2 * GB_K < ke) {
+        store(pa, pb, 0, k0 + 2 * GB_K);
+      }
       __syncthreads();
       load(pa, pb, kt(k0 + 4 * GB_K));
       issue_fence();
@@ -777,13 +881,21 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
     const char* e = getenv("GHM_GEMM_TM2_MIN_N");
     return e ? static_cast<int64_t>(atoll(e)) : static_cast<int64_t>(768);
   }();
+  // GHM_GEMM_BUF: staging variant V (A/B knob, read per call): 0 pointer loads,
+  // 1 buffer loads, 3 buffer loads + interleaved split stores (split-bf16 only)
+  const char* be = getenv("GHM_GEMM_BUF");
+  const int v = be ? atoi(be) : 0;
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
-  if (g.N >= tm2_min)
-    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit),
-                       dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit),
-                       dim3(256), 0, s, g);
+  const dim3 g2(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), g1(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit);
+  if (g.N >= tm2_min) {
+    if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, 1>), g2, dim3(256), 0, s, g);
+    else if (!F32 && v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, F32 ? 1 : 3>), g2, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), g2, dim3(256), 0, s, g);
+  } else {
+    if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1>), g1, dim3(256), 0, s, g);
+    else if (!F32 && v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, F32 ? 1 : 3>), g1, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), g1, dim3(256), 0, s, g);
+  }
 }
 
 }  // namespace
@@ -804,6 +916,8 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
   GHM_CHECK(epi != EPI_RESID || (bias && R), "residual epilogue needs bias and R");
   GHM_CHECK(epi != EPI_MUL || R, "product epilogue needs R");
   GHM_CHECK(lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 && ldr % 4 == 0, "row strides % 4 == 0");
+  // buffer-load staging: a tile's byte offsets (up to 128 rows) fit 31 bits
+  GHM_CHECK(lda < (1 << 20) && ldb < (1 << 20), "row strides < 2^20 floats");
   GHM_CHECK(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(R) |
               reinterpret_cast<uintptr_t>(C2) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0,
             "16-byte aligned operands");

@@ -457,3 +457,72 @@ def test_attention_f32_activation(T, act):
     got = dqkv.cpu().view(N, T, 3 * D).double()
     for i, ref in enumerate((q64.grad, k64.grad, v64.grad)):
         assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 1e-5 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
+
+
+@pytest.mark.parametrize("variant", ["1", "3"])
+def test_buffer_load_staging_bit_identical(variant, monkeypatch):
+    """GHM_GEMM_BUF=1 (buffer-load staging: rows past M, past a split's last
+    token or past K read as hardware zeros instead of clamped re-reads + zeroing
+    selects) and =3 (the same with the next tile's split store interleaved into
+    the current tile's MFMAs) change only how and when tiles are loaded and
+    stored: every shape class -- forward
+    store / GELU / residual, data gradient store / product / split-k, split-k
+    weight gradient with bias rows, token tails and an empty trailing split, both
+    tile heights -- is bit-identical to the pointer-load staging.  The guard rows
+    past every operand are NaN, so a read past the end would show."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(77)
+    M = 10368 + 5
+    cases = []
+
+    def nan_pad(t):
+        big = torch.full((t.shape[0] + 64, t.shape[1]), float("nan"), device=DEV)
+        big[:t.shape[0]] = t.to(DEV)
+        return big
+
+    for K, N in [(256, 1024), (256, 256), (1024, 256)]:
+        X = nan_pad(torch.randn(M, K, generator=g))
+        W, W2 = (torch.randn(N, K, generator=g) / 16).to(DEV), (torch.randn(K, N, generator=g) / 16).to(DEV)
+        b, R = torch.randn(N, generator=g).to(DEV), torch.randn(M, N, generator=g).to(DEV)
+
+        def run(X=X, W=W, b=b, R=R, W2=W2, K=K, N=N):
+            C, C2, C3, C4, C5 = (torch.empty(M, N, device=DEV) for _ in range(5))
+            _gemm(0, 1, EPI_STORE, X, K, (W,), K, 0, C, N, M, N, K)
+            _gemm(0, 1, EPI_GELU, X, K, (W,), K, 0, C2, N, M, N, K, C2=C3, bias=b)
+            _gemm(0, 1, EPI_RESID, X, K, (W,), K, 0, C4, N, M, N, K, bias=b, R=R, ldr=N)
+            _gemm(0, 0, EPI_MUL, X, K, (W2,), N, 0, C5, N, M, N, K, R=R, ldr=N)
+            return C, C2, C3, C4, C5
+        cases.append(run)
+    Wq = [(torch.randn(256, 256, generator=g) / 16).to(DEV) for _ in range(3)]
+    dQ = nan_pad(torch.randn(M, 768, generator=g))
+
+    def run_dsplit():
+        slab = torch.empty(3 * M * 256, device=DEV)
+        out = torch.empty(M, 256, device=DEV)
+        _gemm(0, 0, EPI_SLAB, dQ, 768, Wq, 256, 256, slab, 256, M, 256, 768, nsplit=3)
+        _native.call("ghm_gemm_reduce", _ptr(slab), 3, M, 256, _ptr(out), None, None, 0, ctypes_stream())
+        return (out,)
+    cases.append(run_dsplit)
+    for m, n, Mt, ns in [(1024, 256, 10368 + 5, 16), (256, 1024, 2000, 7), (768, 256, 405, 4), (256, 256, 40, 3)]:
+        dY = nan_pad(torch.randn(Mt, m, generator=g))
+        Xw = nan_pad(torch.randn(Mt, n, generator=g))
+
+        def runw(dY=dY, Xw=Xw, m=m, n=n, Mt=Mt, ns=ns):
+            slab = torch.empty(ns * m * n, device=DEV)
+            bslab = torch.empty(ns * m, device=DEV)
+            out, bias = torch.empty(m, n, device=DEV), torch.empty(m, device=DEV)
+            _gemm(1, 0, EPI_SLAB, dY, m, (Xw,), n, 0, slab, n, m, n, Mt, C2=bslab, nsplit=ns)
+            _native.call("ghm_gemm_reduce_bias", _ptr(slab), ns, m, n, _ptr(out), None, None, 0, _ptr(bslab),
+                         _ptr(bias), ctypes_stream())
+            return out, bias
+        cases.append(runw)
+    monkeypatch.delenv("GHM_GEMM_BUF", raising=False)
+    base = [[t.cpu() for t in c()] for c in cases]
+    monkeypatch.setenv("GHM_GEMM_BUF", variant)
+    got = [[t.cpu() for t in c()] for c in cases]
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(base, got)):
+        for j, (x, y) in enumerate(zip(a, b)):
+            assert torch.isfinite(x).all(), (i, j)
+            assert torch.equal(x, y), (i, j)
