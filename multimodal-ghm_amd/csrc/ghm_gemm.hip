@@ -21,7 +21,12 @@
 // per 128-B row segment); operands whose storage is [k][outer] are loaded as
 // 4 (or 2) consecutive k rows x 4 columns per thread and transposed in
 // registers before the split store.  The next K tile's global loads are issued
-// before the current tile's MFMAs.
+// before the current tile's MFMAs.  Loads are buffer loads (round 5): per-thread
+// byte offsets fixed for the whole K loop, a tile moves only the SGPR descriptor,
+// whose record count makes rows past M / past a split's last token read as zeros
+// (no per-tile 64-bit address arithmetic, row clamps or zeroing selects); for the
+// weight gradients the next tile's split store is interleaved into the current
+// tile's MFMAs (sched_group_barrier).
 //
 // The MFMA computes C^T tiles (B image rows as its A operand) so each lane owns
 // one output row and 4 consecutive columns per register quad: the epilogue reads
@@ -281,22 +286,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   }
   auto load = [&](float4* va, float4* vb, int64_t k0) {
     if constexpr (BUF) {
-      // the tile's rows from its first: k0 on for [k][outer], m0 / n0 on for k-contiguous
+      // the tile's rows from its first: k0 on for [k][outer], m0 / n0 on for
+      // k-contiguous.  A tile at or past ke (the prefetch past the last one) gets
+      // no records at all: its k-contiguous rows would otherwise run past the end
+      // of the operand's last row.
       const int64_t krows = ke - k0 < GB_K ? ke - k0 : GB_K;
+      const bool live = k0 < ke;
       if constexpr (TA) {
         const auto rs = brsrc(g.A + k0 * g.lda + m0, krows * g.lda * 4);
 #pragma unroll
         for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
       } else {
         const int64_t mrows = g.M - m0 < BM ? g.M - m0 : BM;
-        const auto rs = brsrc(g.A + m0 * g.lda + k0, mrows * g.lda * 4);
+        const auto rs = brsrc(g.A + m0 * g.lda + k0, live ? mrows * g.lda * 4 : 0);
 #pragma unroll
         for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
       }
       if constexpr (TB) {
         int64_t ln;
         const float* b = bbase(n0, ln);
-        const auto rs = brsrc(b + ln * g.ldb + k0, GB_N * g.ldb * 4);
+        const auto rs = brsrc(b + ln * g.ldb + k0, live ? GB_N * g.ldb * 4 : 0);
 #pragma unroll
         for (int i = 0; i < NB; ++i) vb[i] = bload4(rs, vob[i]);
       } else {
@@ -881,19 +890,22 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
     const char* e = getenv("GHM_GEMM_TM2_MIN_N");
     return e ? static_cast<int64_t>(atoll(e)) : static_cast<int64_t>(768);
   }();
-  // GHM_GEMM_BUF: staging variant V (A/B knob, read per call): 0 pointer loads,
-  // 1 buffer loads, 3 buffer loads + interleaved split stores (split-bf16 only)
+  // staging variant V: buffer loads (1), with the split stores interleaved into
+  // the MFMAs (3, split-bf16 only) for the weight gradients (ta = 1), where it
+  // measured 39.6 -> 37.6 us; the forward / data-gradient shapes ran slower with
+  // it (profiles/r5_vlm_gemm_buf.txt).  GHM_GEMM_BUF = 0 / 1 / 3 forces one
+  // variant for every shape (A/B knob, read per call).
   const char* be = getenv("GHM_GEMM_BUF");
-  const int v = be ? atoi(be) : 0;
+  const int v = be ? atoi(be) : (TA ? 3 : 1);
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
   const dim3 g2(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), g1(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit);
   if (g.N >= tm2_min) {
     if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, 1>), g2, dim3(256), 0, s, g);
-    else if (!F32 && v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, F32 ? 1 : 3>), g2, dim3(256), 0, s, g);
+    else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, F32 ? 1 : 3>), g2, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), g2, dim3(256), 0, s, g);
   } else {
     if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1>), g1, dim3(256), 0, s, g);
-    else if (!F32 && v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, F32 ? 1 : 3>), g1, dim3(256), 0, s, g);
+    else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, F32 ? 1 : 3>), g1, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), g1, dim3(256), 0, s, g);
   }
 }

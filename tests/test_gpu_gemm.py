@@ -459,13 +459,15 @@ def test_attention_f32_activation(T, act):
         assert (got[..., i * D:(i + 1) * D] - ref).abs().max().item() <= 1e-5 * scale(ref), "dq dk dv"[3 * i:3 * i + 2]
 
 
+@pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("variant", ["1", "3"])
-def test_buffer_load_staging_bit_identical(variant, monkeypatch):
+def test_buffer_load_staging_bit_identical(variant, f32, monkeypatch):
     """GHM_GEMM_BUF=1 (buffer-load staging: rows past M, past a split's last
     token or past K read as hardware zeros instead of clamped re-reads + zeroing
     selects) and =3 (the same with the next tile's split store interleaved into
     the current tile's MFMAs) change only how and when tiles are loaded and
-    stored: every shape class -- forward
+    stored (GHM_GEMM_BUF=0 is the pointer-load staging; the default is 1, and 3
+    for the weight gradients): every shape class -- forward
     store / GELU / residual, data gradient store / product / split-k, split-k
     weight gradient with bias rows, token tails and an empty trailing split, both
     tile heights -- is bit-identical to the pointer-load staging.  The guard rows
@@ -488,10 +490,10 @@ def test_buffer_load_staging_bit_identical(variant, monkeypatch):
 
         def run(X=X, W=W, b=b, R=R, W2=W2, K=K, N=N):
             C, C2, C3, C4, C5 = (torch.empty(M, N, device=DEV) for _ in range(5))
-            _gemm(0, 1, EPI_STORE, X, K, (W,), K, 0, C, N, M, N, K)
-            _gemm(0, 1, EPI_GELU, X, K, (W,), K, 0, C2, N, M, N, K, C2=C3, bias=b)
-            _gemm(0, 1, EPI_RESID, X, K, (W,), K, 0, C4, N, M, N, K, bias=b, R=R, ldr=N)
-            _gemm(0, 0, EPI_MUL, X, K, (W2,), N, 0, C5, N, M, N, K, R=R, ldr=N)
+            _gemm(0, 1, EPI_STORE, X, K, (W,), K, 0, C, N, M, N, K, f32=f32)
+            _gemm(0, 1, EPI_GELU, X, K, (W,), K, 0, C2, N, M, N, K, C2=C3, bias=b, f32=f32)
+            _gemm(0, 1, EPI_RESID, X, K, (W,), K, 0, C4, N, M, N, K, bias=b, R=R, ldr=N, f32=f32)
+            _gemm(0, 0, EPI_MUL, X, K, (W2,), N, 0, C5, N, M, N, K, R=R, ldr=N, f32=f32)
             return C, C2, C3, C4, C5
         cases.append(run)
     Wq = [(torch.randn(256, 256, generator=g) / 16).to(DEV) for _ in range(3)]
@@ -500,7 +502,7 @@ def test_buffer_load_staging_bit_identical(variant, monkeypatch):
     def run_dsplit():
         slab = torch.empty(3 * M * 256, device=DEV)
         out = torch.empty(M, 256, device=DEV)
-        _gemm(0, 0, EPI_SLAB, dQ, 768, Wq, 256, 256, slab, 256, M, 256, 768, nsplit=3)
+        _gemm(0, 0, EPI_SLAB, dQ, 768, Wq, 256, 256, slab, 256, M, 256, 768, nsplit=3, f32=f32)
         _native.call("ghm_gemm_reduce", _ptr(slab), 3, M, 256, _ptr(out), None, None, 0, ctypes_stream())
         return (out,)
     cases.append(run_dsplit)
@@ -512,12 +514,12 @@ def test_buffer_load_staging_bit_identical(variant, monkeypatch):
             slab = torch.empty(ns * m * n, device=DEV)
             bslab = torch.empty(ns * m, device=DEV)
             out, bias = torch.empty(m, n, device=DEV), torch.empty(m, device=DEV)
-            _gemm(1, 0, EPI_SLAB, dY, m, (Xw,), n, 0, slab, n, m, n, Mt, C2=bslab, nsplit=ns)
+            _gemm(1, 0, EPI_SLAB, dY, m, (Xw,), n, 0, slab, n, m, n, Mt, C2=bslab, nsplit=ns, f32=f32)
             _native.call("ghm_gemm_reduce_bias", _ptr(slab), ns, m, n, _ptr(out), None, None, 0, _ptr(bslab),
                          _ptr(bias), ctypes_stream())
             return out, bias
         cases.append(runw)
-    monkeypatch.delenv("GHM_GEMM_BUF", raising=False)
+    monkeypatch.setenv("GHM_GEMM_BUF", "0")
     base = [[t.cpu() for t in c()] for c in cases]
     monkeypatch.setenv("GHM_GEMM_BUF", variant)
     got = [[t.cpu() for t in c()] for c in cases]
