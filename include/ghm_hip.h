@@ -505,6 +505,21 @@ int ghm_gemm_x3(int ta, int tb, int epi, const float* A, int64_t lda, const floa
 int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda, const float* B0, const float* B1,
                  const float* B2, int64_t ldb, int64_t b_chunk, float* C, int64_t ldc, float* C2, const float* bias,
                  const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K, int nsplit, void* stream);
+/* ghm_gemm_x3 with ta = 0 and B pre-split (round 5; the VLM's weight products,
+ * nn.Linear in model.py:132-335): C = A(m,k) B(k,n) with B(k,n) = Bp[n][k], Bp
+ * the bf16 hi image [N][K] (pitch ldbp) and the lo image bplane elements on, as
+ * ghm_split_pack writes them; the K loop copies B's tiles without splitting
+ * them.  Epilogues as ghm_gemm_x3 (C2: GELU' only); N % 128 == 0, K % 32 == 0,
+ * ldbp and bplane % 8 == 0. */
+int ghm_gemm_x3p(int epi, const float* A, int64_t lda, const void* Bp, int64_t ldbp, int64_t bplane, float* C,
+                 int64_t ldc, float* C2, const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N,
+                 int64_t K, int nsplit, void* stream);
+/* Split f32 matrices into bf16 (hi, lo) images for ghm_gemm_x3p: jobs is a
+ * DEVICE array of n_jobs x 8 int64 (src pointer, src pitch, rows, cols, dst
+ * pointer (bf16 hi), dst pitch, lo-plane offset in elements, transpose 0 / 1:
+ * dst[c][r] = split(src[r][c])); max_tiles >= the largest job's count of 64 x 64
+ * tiles.  Once per step, after the optimizer. */
+int ghm_split_pack(const int64_t* jobs, int n_jobs, int max_tiles, void* stream);
 /* D[m][n] = sum_z slab[z][m][n] (z in order: deterministic); rows stacked into
  * D0, D1, D2 by chunk (0: D0 only). */
 int ghm_gemm_reduce(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1, float* D2,

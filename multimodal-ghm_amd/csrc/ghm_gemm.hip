@@ -62,6 +62,8 @@ struct GemmArgs {
   const float* R;
   int64_t ldr;
   int64_t M, N, K, k_per_split;
+  const __bf16* Bp;  // V bit 2: B pre-split, hi image [N][K] (pitch ldb), lo image bplane elements on
+  int64_t bplane;
 };
 
 // k-contiguous tile: rows r0..r0+ROWS-1 (rows >= nrows read row nrows-1: their
@@ -167,12 +169,12 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t rs, int voff) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0);
   return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
 }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const float* p, int64_t bytes) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, int64_t bytes) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   const int n = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes > 0 ? bytes : 0));
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>((static_cast<uint64_t>(hi) << 32) | lo),
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo),
                                            static_cast<short>(0), n, 0x00020000);
 }
 // a thread's byte offsets: k-contiguous tile (row kc_row(idx), 4 floats at k4)
@@ -229,10 +231,15 @@ __device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_
 // V bit 0 (BUF): stage through buffer loads (bload4 / brsrc above) instead of
 // pointer loads; bit 1 (IL, with BUF): the next tile's split store is issued in
 // the same scheduling region as the current tile's MFMAs, interleaved with them
-// by sched_group_barrier (a wave's staging VALU fills its own MFMA gaps)
+// by sched_group_barrier (a wave's staging VALU fills its own MFMA gaps); bit 2
+// (BP, with BUF and TB): B arrives pre-split (g.Bp: bf16 hi / lo images [N][K],
+// written once per step by ghm_split_pack), so its tiles are copied into LDS
+// without a split -- the weights' split, which every workgroup of a column
+// block repeated, is gone from the K loop
 template <bool TA, bool TB, int EPI, int TM, bool F32, int V = 0>
 __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
-  constexpr bool BUF = (V & 1) != 0, IL = (V & 3) == 3;
+  constexpr bool BUF = (V & 1) != 0, IL = (V & 3) == 3, BP = (V & 4) != 0;
+  static_assert(!BP || (BUF && TB && !F32), "pre-split B: buffer loads, k-contiguous, split-bf16");
   constexpr int BM = 64 * TM;
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
   constexpr int NB = TB ? GB_N * 8 / 256 : GB_N / 32;
@@ -281,8 +288,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   if constexpr (BUF) {
     if constexpr (TA) voff_oc<BM>(voa, g.lda);
     else voff_kc<BM>(voa, g.lda);
-    if constexpr (TB) voff_kc<GB_N>(vob, g.ldb);
-    else voff_oc<GB_N>(vob, g.ldb);
+    if constexpr (BP) {
+      // 128 rows x 32 bf16 = 4 16-byte chunks per row and plane: chunk idx & 3 of
+      // row idx >> 2, idx = thread + 256 i (i = 0, 1)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = threadIdx.x + 256 * i;
+        vob[i] = static_cast<int>(((idx >> 2) * g.ldb + 8 * (idx & 3)) * 2);
+      }
+    } else if constexpr (TB) {
+      voff_kc<GB_N>(vob, g.ldb);
+    } else {
+      voff_oc<GB_N>(vob, g.ldb);
+    }
   }
   auto load = [&](float4* va, float4* vb, int64_t k0) {
     if constexpr (BUF) {
@@ -302,7 +320,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
 #pragma unroll
         for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
       }
-      if constexpr (TB) {
+      if constexpr (BP) {
+        // vb[0..1]: the hi chunks, vb[2..3]: the lo chunks (raw bf16 bits)
+        const __bf16* b = g.Bp + n0 * g.ldb + k0;
+        const auto rh = brsrc(b, live ? GB_N * g.ldb * 2 : 0);
+        const auto rl = brsrc(b + g.bplane, live ? GB_N * g.ldb * 2 : 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          vb[i] = bload4(rh, vob[i]);
+          vb[2 + i] = bload4(rl, vob[i]);
+        }
+      } else if constexpr (TB) {
         int64_t ln;
         const float* b = bbase(n0, ln);
         const auto rs = brsrc(b + ln * g.ldb + k0, live ? GB_N * g.ldb * 4 : 0);
@@ -353,7 +381,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     }
     if constexpr (TA) store_oc<BM, !BUF>(va, ah[buf], al[buf], k0, ke);
     else store_kc<BM>(va, ah[buf], al[buf]);
-    if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
+    if constexpr (BP) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = threadIdx.x + 256 * i;
+        const int off = (idx >> 2) * GP + 8 * (idx & 3);
+        *reinterpret_cast<float4*>(bh[buf] + off) = vb[i];
+        *reinterpret_cast<float4*>(bl[buf] + off) = vb[2 + i];
+      }
+    } else if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
     else store_oc<GB_N, false>(vb, bh[buf], bl[buf], k0, ke);
   };
 
@@ -910,6 +946,56 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   }
 }
 
+// pre-split B (V = 5: buffer loads + BP), ta = 0: the VLM's weight products
+template <int EPI>
+void launch_bp(const GemmArgs& g, int nsplit, hipStream_t s) {
+  const int64_t tm2_min = [] {
+    const char* e = getenv("GHM_GEMM_TM2_MIN_N");
+    return e ? static_cast<int64_t>(atoll(e)) : static_cast<int64_t>(768);
+  }();
+  const unsigned gx = static_cast<unsigned>(g.N / GB_N);
+  if (g.N >= tm2_min)
+    hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 2, false, 5>),
+                       dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 1, false, 5>),
+                       dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit), dim3(256), 0, s, g);
+}
+
+// Weight pre-split for the pre-split-B GEMMs: job j (8 int64: src, src pitch,
+// rows, cols, dst, dst pitch, lo-plane offset, transpose) writes the split of the
+// f32 matrix src [rows][cols] into the bf16 hi image at dst (transpose: dst[c][r])
+// and the lo image plane elements on; one workgroup per 64 x 64 tile, through
+// LDS so the reads and the (transposed) writes are both row-contiguous.  The
+// split is split1's, the one the GEMM's staging applies: bit-identical operands.
+__global__ __launch_bounds__(256) void k_split_pack(const int64_t* __restrict__ jobs) {
+  __shared__ float tile[64][65];
+  const int64_t* jb = jobs + 8 * blockIdx.y;
+  const float* src = reinterpret_cast<const float*>(jb[0]);
+  const int64_t lds_ = jb[1], rows = jb[2], cols = jb[3];
+  __bf16* dst = reinterpret_cast<__bf16*>(jb[4]);
+  const int64_t ldd = jb[5], plane = jb[6];
+  const bool tr = jb[7] != 0;
+  const int64_t tcols = (cols + 63) / 64;
+  if (static_cast<int64_t>(blockIdx.x) >= tcols * ((rows + 63) / 64)) return;
+  const int64_t r0 = 64 * (blockIdx.x / tcols), c0 = 64 * (blockIdx.x % tcols);
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    tile[r][c] = (r0 + r < rows && c0 + c < cols) ? src[(r0 + r) * lds_ + c0 + c] : 0.f;
+  }
+  __syncthreads();
+  // output element (a, b) of the tile: row a, column b of the (transposed) image
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int a = i >> 6, b = i & 63;
+    const int64_t orow = (tr ? c0 : r0) + a, ocol = (tr ? r0 : c0) + b;
+    if (orow >= (tr ? cols : rows) || ocol >= (tr ? rows : cols)) continue;
+    __bf16 h, l;
+    split1(tr ? tile[b][a] : tile[a][b], h, l);
+    dst[orow * ldd + ocol] = h;
+    dst[orow * ldd + ocol + plane] = l;
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t ghm_gemm_slab_elems(int64_t M, int64_t N, int nsplit) { return M * N * nsplit; }
@@ -985,6 +1071,52 @@ extern "C" int ghm_gemm_f32(int ta, int tb, int epi, const float* A, int64_t lda
                             int nsplit, void* stream) {
   return gemm_launch(true, ta, tb, epi, A, lda, B0, B1, B2, ldb, b_chunk, C, ldc, C2, bias, R, ldr, M, N, K, nsplit,
                      stream);
+}
+
+extern "C" int ghm_gemm_x3p(int epi, const float* A, int64_t lda, const void* Bp, int64_t ldbp, int64_t bplane,
+                            float* C, int64_t ldc, float* C2, const float* bias, const float* R, int64_t ldr, int64_t M,
+                            int64_t N, int64_t K, int nsplit, void* stream) {
+  GHM_CHECK(A && Bp && C, "null pointer");
+  GHM_CHECK(M >= 1 && N >= GB_N && N % GB_N == 0 && K >= 32 && K % 32 == 0 && nsplit >= 1 && nsplit <= 256,
+            "shape (N % 128 == 0, K % 32 == 0)");
+  GHM_CHECK(epi >= EPI_STORE && epi <= EPI_SLAB, "epilogue");
+  GHM_CHECK(nsplit == 1 || epi == EPI_SLAB, "split k needs the slab epilogue");
+  GHM_CHECK(epi != EPI_GELU || (bias && C2), "GELU epilogue needs bias and C2");
+  GHM_CHECK(epi != EPI_RESID || (bias && R), "residual epilogue needs bias and R");
+  GHM_CHECK(epi != EPI_MUL || R, "product epilogue needs R");
+  GHM_CHECK(!C2 || epi == EPI_GELU, "C2: GELU' only");
+  GHM_CHECK(lda % 4 == 0 && ldc % 4 == 0 && ldr % 4 == 0 && ldbp % 8 == 0 && bplane % 8 == 0 && ldbp >= K,
+            "row strides (pre-split images: pitch and plane % 8 bf16)");
+  GHM_CHECK(lda < (1 << 20) && ldbp < (1 << 20), "row strides < 2^20");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(R) |
+              reinterpret_cast<uintptr_t>(C2) | reinterpret_cast<uintptr_t>(bias) |
+              reinterpret_cast<uintptr_t>(Bp)) & 15) == 0,
+            "16-byte aligned operands");
+  GemmArgs g{};
+  g.A = A; g.lda = lda;
+  g.B[0] = g.B[1] = g.B[2] = nullptr;
+  g.ldb = ldbp; g.b_chunk = 0;
+  g.C = C; g.ldc = ldc; g.C2 = C2; g.bias = bias; g.R = R; g.ldr = ldr;
+  g.M = M; g.N = N; g.K = K;
+  g.k_per_split = ((K + nsplit - 1) / nsplit + GB_K - 1) / GB_K * GB_K;
+  GHM_CHECK((nsplit - 1) * g.k_per_split < K, "split k: every split needs a K tile");
+  g.Bp = static_cast<const __bf16*>(Bp); g.bplane = bplane;
+  hipStream_t s = ghm_stream(stream);
+  switch (epi) {
+    case EPI_STORE: launch_bp<EPI_STORE>(g, nsplit, s); break;
+    case EPI_GELU: launch_bp<EPI_GELU>(g, nsplit, s); break;
+    case EPI_RESID: launch_bp<EPI_RESID>(g, nsplit, s); break;
+    case EPI_MUL: launch_bp<EPI_MUL>(g, nsplit, s); break;
+    default: launch_bp<EPI_SLAB>(g, nsplit, s); break;
+  }
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_split_pack(const int64_t* jobs, int n_jobs, int max_tiles, void* stream) {
+  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= 65535 && max_tiles >= 1, "jobs");
+  hipLaunchKernelGGL(k_split_pack, dim3(static_cast<unsigned>(max_tiles), static_cast<unsigned>(n_jobs)), dim3(256), 0,
+                     ghm_stream(stream), jobs);
+  return ghm_launch_status();
 }
 
 extern "C" int ghm_gemm_reduce_bias(const float* slab, int nsplit, int64_t M, int64_t N, float* D0, float* D1,

@@ -98,6 +98,8 @@ HIP_SIGNATURES = {
     "ghm_stream_wait": [_p, _p],
     "ghm_gemm_f32": [_i, _i, _i, _p, _i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64,
                      _i, _p],
+    "ghm_gemm_x3p": [_i, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _i, _p],
+    "ghm_split_pack": [_p, _i, _i, _p],
     "ghm_gemm_reduce": [_p, _i, _i64, _i64, _p, _p, _p, _i64, _p],
     "ghm_gemm_reduce_bias": [_p, _i, _i64, _i64, _p, _p, _p, _i64, _p, _p, _p],
     "ghm_colsum_part_elems": [_i64, _i64],

@@ -164,6 +164,21 @@ class VlmPlan:
         # N = D products have only 2 x M / 64 output tiles: ~1.3 workgroups per CU)
         self.dsplit = max(1, int(os.environ.get("GHM_VLM_DSPLIT", "1")))
         self.dslab = e(self.dsplit * M * D) if self.dsplit > 1 else None
+        # x3, GHM_VLM_PACK=1 (opt-in): the weights' (hi, lo) bf16 images for
+        # ghm_gemm_x3p, split once per forward by ghm_split_pack, instead of the
+        # GEMMs splitting them per tile
+        self.pack_on = not self.f32 and os.environ.get("GHM_VLM_PACK", "0") == "1"
+        if self.pack_on:
+            self._img_sizes = {"qkv": 3 * D * D, "qkvT": 3 * D * D, "w1": F * D, "w1T": F * D, "w2": F * D,
+                               "w2T": F * D}
+            per = 2 * sum(self._img_sizes.values())
+            self.wpack = torch.empty(L * per, dtype=torch.bfloat16, device=self.device)
+            self._img_off, o = {}, 0
+            for l in range(L):
+                for k, n in self._img_sizes.items():
+                    self._img_off[(l, k)] = o
+                    o += 2 * n
+            self._pack_key, self.pack_jobs = None, None
         lib = _native.hip_lib()
         self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
                              lib.ghm_colsum_part_elems(N, n_token * D),
@@ -198,6 +213,46 @@ class VlmPlan:
     def _gemm(self, *a, **k):
         _gemm(*a, f32=self.f32, **k)
 
+    def _img(self, l, k):
+        """(hi pointer, pitch, lo-plane offset) of layer l's pre-split image k: B(k,n)
+        of a weight product is img[n][k] (qkv / w1 / w2: the forward's W; qkvT /
+        w1T / w2T: the data gradients' W^T)."""
+        D, F = self.D, self.F
+        pitch = {"qkv": D, "qkvT": 3 * D, "w1": D, "w1T": F, "w2": F, "w2T": D}[k]
+        return self.wpack.data_ptr() + 2 * self._img_off[(l, k)], pitch, self._img_sizes[k]
+
+    def _gemmp(self, epi, A, lda, img, C, ldc, M, N, K, C2=None, bias=None, R=None, ldr=0, nsplit=1, s=None):
+        """ghm_gemm_x3p: C = A B with B pre-split (self._img)."""
+        pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
+        bp, ldbp, plane = img
+        _native.call("ghm_gemm_x3p", epi, _ptr(A), lda, ctypes.c_void_p(bp), ldbp, plane, _ptr(C), ldc, pp(C2),
+                     pp(bias), pp(R), ldr, M, N, K, nsplit, _stream() if s is None else s)
+
+    def _split_weights(self, p, s):
+        """Write every layer's six weight images (ghm_split_pack, one launch); the
+        job table is rebuilt only when a weight's storage moved."""
+        D, F = self.D, self.F
+        names = [(f"_queries.{l}.weight", f"_keys.{l}.weight", f"_values.{l}.weight", f"_mlps.{l}.0.weight",
+                  f"_mlps.{l}.2.weight") for l in range(self.L)]
+        key = tuple(p[n].data_ptr() for ns in names for n in ns)
+        if key != self._pack_key:
+            jobs = []
+            for l, (nq, nk, nv, n1, n2) in enumerate(names):
+                qkv, _, pq = self._img(l, "qkv")
+                qkvT, _, pqT = self._img(l, "qkvT")
+                for i, n in enumerate((nq, nk, nv)):
+                    jobs.append((p[n].data_ptr(), D, D, D, qkv + 2 * i * D * D, D, pq, 0))  # rows iD.. of [3D][D]
+                    jobs.append((p[n].data_ptr(), D, D, D, qkvT + 2 * i * D, 3 * D, pqT, 1))  # columns iD.. of [D][3D]
+                for n, (rows, cols), k, kt in ((n1, (F, D), "w1", "w1T"), (n2, (D, F), "w2", "w2T")):
+                    b, _, pl = self._img(l, k)
+                    bt, _, plt = self._img(l, kt)
+                    jobs.append((p[n].data_ptr(), cols, rows, cols, b, cols, pl, 0))
+                    jobs.append((p[n].data_ptr(), cols, rows, cols, bt, rows, plt, 1))
+            self.pack_jobs = torch.tensor(jobs, dtype=torch.int64).to(self.device)
+            self._pack_tiles = max(-(-r // 64) * -(-c // 64) for (_, _, r, c, _, _, _, _) in jobs)
+            self._pack_key = key
+        _native.call("ghm_split_pack", _ptr(self.pack_jobs), len(self.pack_jobs), self._pack_tiles, s)
+
     def _forward_hip(self, p, xt, feat):
         s = _stream()
         c = _native.call
@@ -209,6 +264,8 @@ class VlmPlan:
         else:
             c("ghm_vlm_embed_fwd", _ptr(xt), _ptr(feat), _ptr(p["t_embedding.weight"]),
               _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), None, N, T, self.P, self.V, D, s)
+        if self.pack_on:
+            self._split_weights(p, s)
         for l in range(self.L):
             if self.layernorm:
                 c("ghm_ln_rows_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
@@ -220,7 +277,10 @@ class VlmPlan:
                 c("ghm_vlm_attn_fwd", _ptr(self.q[l]), _ptr(self.k[l]), _ptr(self.v[l]), _ptr(self.H[l]),
                   _ptr(self.Hmid[l]), _ptr(self.Pm[l]), N, T, D, self.P, self.scale_div, s)
             else:
-                self._gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
+                if self.pack_on:
+                    self._gemmp(EPI_STORE, self.X1[l], D, self._img(l, "qkv"), self.qkv[l], 3 * D, M, 3 * D, D, s=s)
+                else:
+                    self._gemm(0, 1, EPI_STORE, self.X1[l], D, wqkv, D, D, self.qkv[l], 3 * D, M, 3 * D, D, s=s)
                 if self.act:  # relu(score) (model.py:287), masked entries 0
                     c("ghm_attn_ext_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]),
                       _ptr(self.Pm[l]), None, N, T, D, self.P, self.scale_div, 1.0 / D, self.act, s)
@@ -230,10 +290,16 @@ class VlmPlan:
             if self.layernorm:
                 c("ghm_ln_rows_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.X2[l]), _ptr(self.st2[l]), M, D, self.eps, s)
-            self._gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
-                  C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
-            self._gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D, F,
-                  bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
+            if self.pack_on:
+                self._gemmp(EPI_GELU, self.X2[l], D, self._img(l, "w1"), self.G[l], F, M, F, D, C2=self.Dg[l],
+                            bias=p[f"_mlps.{l}.0.bias"], s=s)
+                self._gemmp(EPI_RESID, self.G[l], F, self._img(l, "w2"), self.H[l + 1], D, M, D, F,
+                            bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
+            else:
+                self._gemm(0, 1, EPI_GELU, self.X2[l], D, (p[f"_mlps.{l}.0.weight"],), D, 0, self.G[l], F, M, F, D,
+                           C2=self.Dg[l], bias=p[f"_mlps.{l}.0.bias"], s=s)
+                self._gemm(0, 1, EPI_RESID, self.G[l], F, (p[f"_mlps.{l}.2.weight"],), F, 0, self.H[l + 1], D, M, D,
+                           F, bias=p[f"_mlps.{l}.2.bias"], R=self.Hmid[l], ldr=D, s=s)  # :344-347
         c("ghm_rows_linear", _ptr(self.H[self.L]), _ptr(p["_read_out.weight"]), _ptr(p["_read_out.bias"]),
           _ptr(self.logits), M, D, self.V, s)  # model.py:332
         self._xt_fwd = xt
@@ -251,14 +317,20 @@ class VlmPlan:
         _native.call("ghm_gemm_reduce_bias", _ptr(self.slab), self.nsplit, m, n, pp(d[0]), pp(d[1]), pp(d[2]), chunk,
                      pp(bs), pp(bias), s)
 
-    def _dgrad(self, A, lda, Bs, b_chunk, K, s):
-        """self.dX [M][D] = A [M][K] @ B (B [K][D] rows stacked by b_chunk), split-k
-        over dsplit slabs + the fixed-order reduce when dsplit > 1."""
+    def _dgrad(self, A, lda, Bs, b_chunk, K, s, img=None):
+        """self.dX [M][D] = A [M][K] @ B (B [K][D] rows stacked by b_chunk, or the
+        pre-split image img of B^T), split-k over dsplit slabs + the fixed-order
+        reduce when dsplit > 1."""
         M, D = self.M, self.D
         ns = self.dsplit
         if ns > 1 and (ns - 1) * ((-(-K // ns) + 31) // 32 * 32) < K:
-            self._gemm(0, 0, EPI_SLAB, A, lda, Bs, D, b_chunk, self.dslab, D, M, D, K, nsplit=ns, s=s)
+            if img is not None:
+                self._gemmp(EPI_SLAB, A, lda, img, self.dslab, D, M, D, K, nsplit=ns, s=s)
+            else:
+                self._gemm(0, 0, EPI_SLAB, A, lda, Bs, D, b_chunk, self.dslab, D, M, D, K, nsplit=ns, s=s)
             _native.call("ghm_gemm_reduce", _ptr(self.dslab), ns, M, D, _ptr(self.dX), None, None, 0, s)
+        elif img is not None:
+            self._gemmp(EPI_STORE, A, lda, img, self.dX, D, M, D, K, s=s)
         else:
             self._gemm(0, 0, EPI_STORE, A, lda, Bs, D, b_chunk, self.dX, D, M, D, K, s=s)
 
@@ -276,9 +348,12 @@ class VlmPlan:
                 layer_grad[l](cur, s)
             w1, w2 = p[f"_mlps.{l}.0.weight"], p[f"_mlps.{l}.2.weight"]
             self._wgrad(cur, D, D, self.G[l], F, F, (g[f"_mlps.{l}.2.weight"],), 0, s, bias=g[f"_mlps.{l}.2.bias"])
-            self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)  # dU
+            if self.pack_on:  # dU
+                self._gemmp(EPI_MUL, cur, D, self._img(l, "w2T"), self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)
+            else:
+                self._gemm(0, 0, EPI_MUL, cur, D, (w2,), F, 0, self.dG, F, M, F, D, R=self.Dg[l], ldr=F, s=s)
             self._wgrad(self.dG, F, F, self.X2[l], D, D, (g[f"_mlps.{l}.0.weight"],), 0, s, bias=g[f"_mlps.{l}.0.bias"])
-            self._dgrad(self.dG, F, (w1,), 0, F, s)
+            self._dgrad(self.dG, F, (w1,), 0, F, s, img=self._img(l, "w1T") if self.pack_on else None)
             if self.layernorm:
                 c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.Hmid[l]), _ptr(self.st2[l]),
                   _ptr(p[f"_lns_2.{l}.weight"]), _ptr(cur), _ptr(nxt), _ptr(self.part_ln), M, D, s)
@@ -307,7 +382,7 @@ class VlmPlan:
                     c("ghm_attn_ext_bwd_x3", _ptr(self.qkv[l]), _ptr(self.Pm[l]), _ptr(nxt), _ptr(self.dS),
                       _ptr(self.dqkv), self.N, self.T, D, self.P, self.scale_div, 1.0 / D, s)
                 self._wgrad(self.dqkv, 3 * D, 3 * D, self.X1[l], D, D, gqkv, D, s)
-                self._dgrad(self.dqkv, 3 * D, wqkv, D, 3 * D, s)
+                self._dgrad(self.dqkv, 3 * D, wqkv, D, 3 * D, s, img=self._img(l, "qkvT") if self.pack_on else None)
             if self.layernorm:
                 c("ghm_ln_rows_bwd", _ptr(self.dX), _ptr(self.H[l]), _ptr(self.st1[l]),
                   _ptr(p[f"_lns_1.{l}.weight"]), _ptr(nxt), _ptr(cur), _ptr(self.part_ln), M, D, s)

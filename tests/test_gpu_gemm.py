@@ -528,3 +528,80 @@ def test_buffer_load_staging_bit_identical(variant, f32, monkeypatch):
         for j, (x, y) in enumerate(zip(a, b)):
             assert torch.isfinite(x).all(), (i, j)
             assert torch.equal(x, y), (i, j)
+
+
+def _split_ref(x):
+    hi = x.float().bfloat16()
+    lo = (x.float() - hi.float()).bfloat16()
+    return hi, lo
+
+
+def test_split_pack_and_presplit_gemm(monkeypatch):
+    """ghm_split_pack writes split1's (hi, lo) of f32 matrices -- plain and
+    transposed, ragged 64 x 64 tiles, into column / row offsets of a wider image
+    -- equal to torch's round-to-nearest-even bf16 split; ghm_gemm_x3p on those
+    images equals ghm_gemm_x3 on the f32 weights bit for bit in every epilogue
+    (GELU with GELU', bias + residual, product, store, split-k slabs) and both tile
+    heights."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(3)
+    # split kernel: W [100][70] into columns 8.. of a [100][88] image (plain) and
+    # rows 8.. of a [88][100] image (transposed)
+    W = torch.randn(100, 70, generator=g).to(DEV)
+    img = torch.zeros(2, 100, 88, dtype=torch.bfloat16, device=DEV)
+    imgT = torch.zeros(2, 88, 100, dtype=torch.bfloat16, device=DEV)
+    jobs = torch.tensor([[W.data_ptr(), 70, 100, 70, img.data_ptr() + 2 * 8, 88, 100 * 88, 0],
+                         [W.data_ptr(), 70, 100, 70, imgT.data_ptr() + 2 * 8 * 100, 100, 88 * 100, 1]],
+                        dtype=torch.int64).to(DEV)
+    _native.call("ghm_split_pack", _ptr(jobs), 2, 4, ctypes_stream())
+    torch.cuda.synchronize()
+    hi, lo = _split_ref(W)
+    assert torch.equal(img[0, :, 8:78].cpu(), hi.cpu()) and torch.equal(img[1, :, 8:78].cpu(), lo.cpu())
+    assert torch.equal(imgT[0, 8:78, :].cpu(), hi.t().cpu()) and torch.equal(imgT[1, 8:78, :].cpu(), lo.t().cpu())
+    assert (img[:, :, :8] == 0).all() and (img[:, :, 78:] == 0).all()
+
+    def pack(Bkn):  # B(k, n) -> pre-split image [n][k] (hi, lo planes)
+        K, N = Bkn.shape
+        out = torch.empty(2, N, K, dtype=torch.bfloat16, device=DEV)
+        src = Bkn.t().contiguous()
+        j = torch.tensor([[src.data_ptr(), K, N, K, out.data_ptr(), K, N * K, 0]], dtype=torch.int64).to(DEV)
+        _native.call("ghm_split_pack", _ptr(j), 1, -(-N // 64) * -(-K // 64), ctypes_stream())
+        torch.cuda.synchronize()
+        return out, src
+
+    M = 10368 + 5
+    for K, N in [(256, 1024), (256, 768), (1024, 256), (256, 256)]:
+        X = torch.randn(M, K, generator=g).to(DEV)
+        Wnk = (torch.randn(N, K, generator=g) / 16).to(DEV)  # forward weight W[n][k]: B(k,n) = W[n][k]
+        b = torch.randn(N, generator=g).to(DEV)
+        R = torch.randn(M, N, generator=g).to(DEV)
+        img, _ = pack(Wnk.t())
+        for epi in (EPI_STORE, EPI_GELU, EPI_RESID, EPI_MUL):
+            kw = {"C2": torch.empty(M, N, device=DEV), "bias": b} if epi == EPI_GELU else (
+                {"bias": b, "R": R, "ldr": N} if epi == EPI_RESID else ({"R": R, "ldr": N} if epi == EPI_MUL else {}))
+            C0, C1 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+            if epi == EPI_MUL:  # (ta, tb) = (0, 0) is the product epilogue's shape: B = W^T stored [K][N]
+                _gemm(0, 0, epi, X, K, (Wnk.t().contiguous(),), N, 0, C0, N, M, N, K, **kw)
+            else:
+                _gemm(0, 1, epi, X, K, (Wnk,), K, 0, C0, N, M, N, K, **kw)
+            c2 = kw.get("C2")
+            ref2 = c2.clone() if c2 is not None else None
+            pp = lambda t: None if t is None else _ptr(t)  # noqa: E731
+            _native.call("ghm_gemm_x3p", epi, _ptr(X), K, _ptr(img), K, N * K, _ptr(C1), N, pp(c2), pp(kw.get("bias")),
+                         pp(kw.get("R")), kw.get("ldr", 0), M, N, K, 1, ctypes_stream())
+            torch.cuda.synchronize()
+            assert torch.equal(C0.cpu(), C1.cpu()), (K, N, epi)
+            if c2 is not None:
+                assert torch.equal(ref2.cpu(), c2.cpu())
+    # split-k data gradient dX = dY W over K = 1024 in 2 slabs
+    K, N = 1024, 256
+    dY = torch.randn(M, K, generator=g).to(DEV)
+    Wkn = (torch.randn(K, N, generator=g) * 0.05).to(DEV)
+    img, _ = pack(Wkn)
+    s0, s1 = torch.empty(2 * M * N, device=DEV), torch.empty(2 * M * N, device=DEV)
+    _gemm(0, 0, EPI_SLAB, dY, K, (Wkn,), N, 0, s0, N, M, N, K, nsplit=2)
+    _native.call("ghm_gemm_x3p", EPI_SLAB, _ptr(dY), K, _ptr(img), K, N * K, _ptr(s1), N, None, None, None, 0, M, N,
+                 K, 2, ctypes_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(s0.cpu(), s1.cpu())

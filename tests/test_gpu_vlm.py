@@ -215,3 +215,45 @@ def test_nwp_pipeline_matches_sampler_draws():
         np.testing.assert_array_equal(yt.numpy(), tl[:, 1:])
         np.testing.assert_array_equal(i.numpy(), il)
         np.testing.assert_array_equal(p.numpy(), post)
+
+
+@pytest.mark.parametrize("d", [256, 128])
+def test_presplit_weight_images_bit_identical(d, monkeypatch):
+    """x3: the weight products on pre-split images (ghm_split_pack once per
+    forward + ghm_gemm_x3p, GHM_VLM_PACK=1) give logits and every gradient bit for
+    bit as the GEMMs that split the weights per tile (the default): the same
+    split, the same products in the same order -- and a second forward after a
+    weight update re-splits (the images follow the weights)."""
+    from ghmclip import AutoRegressiveTransformer
+    B = 4
+    g = torch.Generator().manual_seed(d)
+    xt = torch.randint(0, 10, (B, 80), generator=g).to(DEV)
+    feat = torch.randn(B, 1, 10, generator=g).to(DEV)
+    R = torch.randn(B, 80, 10, generator=g).to(DEV)
+    outs = []
+    for pack in ("0", "1"):
+        monkeypatch.setenv("GHM_VLM_PACK", pack)
+        torch.manual_seed(5)
+        m = AutoRegressiveTransformer(81, 1, 10, d, 2, [4, 1], 4, 4 * d, auto_regressive=True,
+                                      sequential=True).to(DEV)
+        m.precision = "x3"
+        res = []
+        for it in range(2):
+            fd = feat.clone().requires_grad_(True)
+            logits, _ = m(xt, fd)
+            (logits * R).sum().backward()
+            torch.cuda.synchronize()
+            res.append([logits.detach().cpu(), fd.grad.cpu()] + [p.grad.cpu().clone() for p in m.parameters()
+                                                                  if p.grad is not None])
+            with torch.no_grad():  # a weight update between the two forwards
+                for p in m.parameters():
+                    if p.grad is not None:
+                        p.sub_(1e-2 * p.grad)
+                        p.grad = None
+        plan = next(iter(m._plans.values())) if hasattr(m, "_plans") else None
+        if plan is not None and hasattr(plan, "pack_on"):
+            assert plan.pack_on == (pack == "1")
+        outs.append(res)
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
