@@ -670,7 +670,6 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_ln_mlp_fwd_x3w(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
     float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
-  constexpr int NC = GHM_F / 32;
   __shared__ __attribute__((aligned(16))) __bf16 lds[8 * PLANE + 2 * GHM_F];
   float* sb1 = reinterpret_cast<float*>(lds + 8 * PLANE);
   const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
