@@ -1,6 +1,6 @@
 """Per-kernel HBM traffic from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/traffic.py <fetch_dir> <write_dir> [--json out.json]
+    python tools/traffic.py <fetch_dir> <write_dir> [--json out.json] [--over "what ran"]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports
 half the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM section), so
@@ -42,8 +42,9 @@ def main():
         out[k] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr}
         print(f"{k[:40]:40s} read {rd/1e6:9.2f} MB  write {wr/1e6:9.2f} MB  total {(rd+wr)/1e6:9.2f} MB")
     if "--json" in sys.argv:
+        over = sys.argv[sys.argv.index("--over") + 1] if "--over" in sys.argv else "tools/kbench.py"
         doc = {"source": f"rocprofv3 --pmc FETCH_SIZE ({sys.argv[1]}) and --pmc WRITE_SIZE ({sys.argv[2]}) "
-                         "over tools/kbench.py; bytes per dispatch, FETCH_SIZE doubled (gfx950 correction)",
+                         f"over {over}; bytes per dispatch, FETCH_SIZE doubled (gfx950 correction)",
                "kernels": out}
         json.dump(doc, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
