@@ -172,12 +172,20 @@ __device__ __forceinline__ int vx_key_tiles(int q1, int T, int npre) {
 // also stores GELU'(score) in Pd for the backward
 constexpr int VACT_SOFTMAX = 0, VACT_RELU = 1, VACT_GELU = 2;
 
-template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX>
+// NS: the output's DD / 32 column blocks split over NS workgroups (blockIdx.z);
+// each recomputes the scores and the softmax of its query tiles (P / GELU' stored
+// by z = 0 only), so a batch of 128 one-tile-per-wave sequences puts NS x as many
+// waves on the chip and each runs 1 / NS of the V staging round trips
+template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX, int NS = 1>
 __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __restrict__ qkv,
                                                                  const float* __restrict__ H,
                                                                  float* __restrict__ Hmid, float* __restrict__ P,
                                                                  int T, int npre, float scale_div, float dbl,
                                                                  float* __restrict__ Pd = nullptr) {
+  // no fp contraction in the attention kernels: the compiler fused, e.g., the
+  // normalised P's product into its split's subtraction in some instantiations and
+  // not in others (GHM_VX_SPLIT); every product now rounds where the source does
+#pragma clang fp contract(off)
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
@@ -191,6 +199,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
   const bool qv = q < T;
   const int qc = qv ? q : T - 1;
   const int nk = vx_key_tiles(NW * (static_cast<int>(blockIdx.y) + 1), T, npre);
+  const bool first = NS == 1 || blockIdx.z == 0;  // the split that stores P (and GELU')
   f32x16 s[NKT];
   vx_scores<NKT, DD, NW>(seq, LD, DD, seq + qc * LD, T, j, h, nk, sh, sl, s);
   // one reciprocal and a base-2 exponent per score (as k_attn_fwd_x3)
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
         dv[r] = ok ? d : 0.f;
       }
       if constexpr (ACT == VACT_GELU) {
-        if (qv) {
+        if (qv && first) {
 #pragma unroll
           for (int qd = 0; qd < 4; ++qd)
             st4(drow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
@@ -258,9 +267,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
   for (int kt = 0; kt < NKT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[kt][r] *= inv;
+    if (first) {
 #pragma unroll
-    for (int qd = 0; qd < 4; ++qd)
-      st4(prow + 32 * kt + quad_off(qd, h), s[kt][4 * qd], s[kt][4 * qd + 1], s[kt][4 * qd + 2], s[kt][4 * qd + 3]);
+      for (int qd = 0; qd < 4; ++qd)
+        st4(prow + 32 * kt + quad_off(qd, h), s[kt][4 * qd], s[kt][4 * qd + 1], s[kt][4 * qd + 2], s[kt][4 * qd + 3]);
+    }
     float pv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) pv[r] = s[kt][r];
@@ -268,8 +279,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
     split_acc(pv, 1, ph[2 * kt + 1], pl[2 * kt + 1]);
   }
   // O^T[d][q] = sum_key V[key][d] P[q][key], V column blocks of 32 through LDS
+  constexpr int NDT = DD / 32 / NS;
+  const int dt0 = NS == 1 ? 0 : NDT * static_cast<int>(blockIdx.z);
 #pragma unroll 1
-  for (int dt = 0; dt < DD / 32; ++dt) {
+  for (int dt = dt0; dt < dt0 + NDT; ++dt) {
     vx_stage_cols<NKT, NW>(seq, LD, T, 2 * DD + 32 * dt, sh, sl);
     __syncthreads();
     f32x16 acc = zero16();
@@ -290,10 +303,12 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) hv[qd] = *reinterpret_cast<const float4*>(H + row + quad_off(qd, h));
 #pragma unroll
+      // explicit fma: the same rounding in every instantiation (the compiler's own
+      // contraction of o * dbl + (h + o) differed between NS = 1 and NS > 1)
       for (int qd = 0; qd < 4; ++qd) {
         const float o0 = acc[4 * qd], o1 = acc[4 * qd + 1], o2 = acc[4 * qd + 2], o3 = acc[4 * qd + 3];
-        st4(Hmid + row + quad_off(qd, h), (hv[qd].x + o0) + o0 * dbl, (hv[qd].y + o1) + o1 * dbl,
-            (hv[qd].z + o2) + o2 * dbl, (hv[qd].w + o3) + o3 * dbl);
+        st4(Hmid + row + quad_off(qd, h), __builtin_fmaf(o0, dbl, hv[qd].x + o0), __builtin_fmaf(o1, dbl, hv[qd].y + o1),
+            __builtin_fmaf(o2, dbl, hv[qd].z + o2), __builtin_fmaf(o3, dbl, hv[qd].w + o3));
       }
     }
   }
@@ -301,7 +316,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_fwd_x3(const float* __r
 
 // dA^T = (V dO^T)(1 + 1/D), dS = P (dA - rowsum(P dA)) / scale_div (stored dense),
 // dQ^T = K^T dS^T
-template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX>
+// NS: dQ's column blocks over NS workgroups (blockIdx.z), each recomputing dS (stored by z = 0)
+template <int NKT, int DD, int NW, int ACT = VACT_SOFTMAX, int NS = 1>
 __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* __restrict__ qkv,
                                                                    const float* __restrict__ P,
                                                                    const float* __restrict__ dHmid,
@@ -309,6 +325,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
                                                                    float* __restrict__ dqkv, int T, float scale_div,
                                                                    int npre, float dbl,
                                                                    const float* __restrict__ Pd = nullptr) {
+  // no fp contraction in the attention kernels: the compiler fused, e.g., the
+  // normalised P's product into its split's subtraction in some instantiations and
+  // not in others (GHM_VX_SPLIT); every product now rounds where the source does
+#pragma clang fp contract(off)
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32;
   constexpr int64_t LD = 3 * DD;
@@ -339,9 +359,9 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
       p[kt][4 * qd + 3] = qv ? pv.w : 0.f;
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      dp[kt][r] = dp[kt][r] + dp[kt][r] * dbl;
-      if (ACT == VACT_SOFTMAX) delta += p[kt][r] * dp[kt][r];
+    for (int r = 0; r < 16; ++r) {  // explicit fmas: the same rounding in every instantiation
+      dp[kt][r] = __builtin_fmaf(dp[kt][r], dbl, dp[kt][r]);
+      if (ACT == VACT_SOFTMAX) delta = __builtin_fmaf(p[kt][r], dp[kt][r], delta);
     }
   }
   if (ACT == VACT_SOFTMAX) delta += xhalf(delta);
@@ -359,14 +379,18 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
       else
         dv[r] = (p[kt][r] * dp[kt][r]) * inv_scale;
     }
+    if (NS == 1 || blockIdx.z == 0) {
 #pragma unroll
-    for (int qd = 0; qd < 4; ++qd)
-      st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+      for (int qd = 0; qd < 4; ++qd)
+        st4(srow + 32 * kt + quad_off(qd, h), dv[4 * qd], dv[4 * qd + 1], dv[4 * qd + 2], dv[4 * qd + 3]);
+    }
     split_acc(dv, 0, dh[2 * kt], dl[2 * kt]);
     split_acc(dv, 1, dh[2 * kt + 1], dl[2 * kt + 1]);
   }
+  constexpr int NDT = DD / 32 / NS;
+  const int dt0 = NS == 1 ? 0 : NDT * static_cast<int>(blockIdx.z);
 #pragma unroll 1
-  for (int dt = 0; dt < DD / 32; ++dt) {
+  for (int dt = dt0; dt < dt0 + NDT; ++dt) {
     vx_stage_cols<NKT, NW>(seq, LD, T, DD + 32 * dt, sh, sl);  // K
     __syncthreads();
     f32x16 acc = zero16();
@@ -391,12 +415,17 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_q_x3(const float* _
 }
 
 // dV^T = dO^T P (1 + 1/D) and dK^T = Q^T dS, summed over queries; the key on the lane
-template <int NKT, int DD, int NW>
+// NS: the DD / 32 column blocks of dK / dV over NS workgroups (blockIdx.z)
+template <int NKT, int DD, int NW, int NS = 1>
 __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* __restrict__ qkv,
                                                                     const float* __restrict__ P,
                                                                     const float* __restrict__ dS,
                                                                     const float* __restrict__ dHmid,
                                                                     float* __restrict__ dqkv, int T, int npre, float dbl) {
+  // no fp contraction in the attention kernels: the compiler fused, e.g., the
+  // normalised P's product into its split's subtraction in some instantiations and
+  // not in others (GHM_VX_SPLIT); every product now rounds where the source does
+#pragma clang fp contract(off)
   constexpr int VX_PAD = vx_pad<NKT>();
   constexpr int TP = NKT * 32, KS = TP / 16;
   constexpr int64_t LD = 3 * DD;
@@ -429,8 +458,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
       split8(pv, pbh[st], pbl[st]);
       split8(sv, sbh[st], sbl[st]);
     }
+    constexpr int NDT = DD / 32 / NS;
+    const int dt0 = NS == 1 ? 0 : NDT * static_cast<int>(blockIdx.z);
   #pragma unroll 1
-    for (int dt = 0; dt < DD / 32; ++dt) {
+    for (int dt = dt0; dt < dt0 + NDT; ++dt) {
       vx_stage_cols<NKT, NW>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
       vx_stage_cols<NKT, NW>(qkv + base * LD, LD, T, 32 * dt, sqh, sql);
       __syncthreads();
@@ -438,7 +469,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
   #pragma unroll
       for (int st = 0; st < KS; ++st) {
         if (st < st0) continue;
-      if (st < st0) continue;
         const int r0 = 16 * st + 8 * h;
         aV = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), pbh[st], pbl[st], aV);
         aK = mfma_x3(vx_tr_frag(sqh, r0, r0 + 4, lane), vx_tr_frag(sql, r0, r0 + 4, lane), sbh[st], sbl[st], aK);
@@ -449,7 +479,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
   #pragma unroll
         for (int qd = 0; qd < 4; ++qd) {
           const float v0 = aV[4 * qd], v1 = aV[4 * qd + 1], v2 = aV[4 * qd + 2], v3 = aV[4 * qd + 3];
-          st4(o + 2 * DD + quad_off(qd, h), v0 + v0 * dbl, v1 + v1 * dbl, v2 + v2 * dbl, v3 + v3 * dbl);
+          st4(o + 2 * DD + quad_off(qd, h), __builtin_fmaf(v0, dbl, v0), __builtin_fmaf(v1, dbl, v1),
+              __builtin_fmaf(v2, dbl, v2), __builtin_fmaf(v3, dbl, v3));
           st4(o + DD + quad_off(qd, h), aK[4 * qd], aK[4 * qd + 1], aK[4 * qd + 2], aK[4 * qd + 3]);
         }
       }
@@ -464,14 +495,15 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
         if (st < st0) continue;
-      if (st < st0) continue;
         float v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = src[(16 * st + 8 * h + i) * VX_PAD];
         split8(v, bh[st], bl[st]);
       }
+      constexpr int NDT = DD / 32 / NS;
+      const int dt0 = NS == 1 ? 0 : NDT * static_cast<int>(blockIdx.z);
 #pragma unroll 1
-      for (int dt = 0; dt < DD / 32; ++dt) {
+      for (int dt = dt0; dt < dt0 + NDT; ++dt) {
         if (which == 0) vx_stage_cols<NKT, NW>(dHmid + base * DD, DD, T, 32 * dt, soh, sol);
         else vx_stage_cols<NKT, NW>(qkv + base * LD, LD, T, 32 * dt, soh, sol);
         __syncthreads();
@@ -479,8 +511,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
 #pragma unroll
         for (int st = 0; st < KS; ++st) {
           if (st < st0) continue;
-        if (st < st0) continue;
-      if (st < st0) continue;
           const int r0 = 16 * st + 8 * h;
           acc = mfma_x3(vx_tr_frag(soh, r0, r0 + 4, lane), vx_tr_frag(sol, r0, r0 + 4, lane), bh[st], bl[st], acc);
         }
@@ -491,7 +521,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
 #pragma unroll
           for (int qd = 0; qd < 4; ++qd) {
             const float v0 = acc[4 * qd], v1 = acc[4 * qd + 1], v2 = acc[4 * qd + 2], v3 = acc[4 * qd + 3];
-            st4(o + quad_off(qd, h), v0 + v0 * f, v1 + v1 * f, v2 + v2 * f, v3 + v3 * f);
+            st4(o + quad_off(qd, h), __builtin_fmaf(v0, f, v0), __builtin_fmaf(v1, f, v1), __builtin_fmaf(v2, f, v2),
+                __builtin_fmaf(v3, f, v3));
           }
         }
       }
@@ -504,12 +535,31 @@ __global__ __launch_bounds__(NW * 64, 2) void k_vlm_attn_bwd_kv_x3(const float* 
 template <int NKT>
 constexpr int vx_nw() { return NKT == 6 ? 3 : (NKT == 4 ? 2 : (NKT == 5 ? 5 : 1)); }
 
+// NS, the column blocks' split over workgroups (round 5, profiles/r5_vx_ab.txt):
+// the forward and the dQ kernel recompute scores / dS per split, so 2 (two splits
+// 30.6 -> 25.5 and 33.3 -> 27.6 us, four slower again); the dK / dV kernel only
+// reloads P and dS, so 4 (32.2 -> 17.2 us).  GHM_VX_SPLIT / GHM_VX_SPLIT_KV = 1 / 2
+// / 4 override them (A/B knobs, read per call).
+inline int vx_split(const char* var = "GHM_VX_SPLIT", int dflt = 2) {
+  const char* e = getenv(var);
+  const int v = e ? atoi(e) : dflt;
+  return v == 2 || v == 4 ? v : 1;
+}
+
 template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_fwd_n(unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int T, int npre,
                   float sd, float dbl, float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, H, Hm, P, T,
-                     npre, sd, dbl, Pd);
+  const int ns = vx_split();
+  if (ns == 2)
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT, 2>), dim3(g, NKT / NW, 2), dim3(NW * 64), 0, s, qkv, H, Hm,
+                       P, T, npre, sd, dbl, Pd);
+  else if (ns == 4)
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT, 4>), dim3(g, NKT / NW, 4), dim3(NW * 64), 0, s, qkv, H, Hm,
+                       P, T, npre, sd, dbl, Pd);
+  else
+    hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, H, Hm, P, T,
+                       npre, sd, dbl, Pd);
 }
 
 template <int DD, int ACT = VACT_SOFTMAX>
@@ -527,10 +577,25 @@ template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
                   float* dqkv, int T, int npre, float sd, float dbl, const float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dHm,
-                     dS, dqkv, T, sd, npre, dbl, Pd);
-  hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dS, dHm,
-                     dqkv, T, npre, dbl);
+  const int ns = vx_split(), nkv = vx_split("GHM_VX_SPLIT_KV", 4);
+  if (ns == 2)
+    hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT, 2>), dim3(g, NKT / NW, 2), dim3(NW * 64), 0, s, qkv, P,
+                       dHm, dS, dqkv, T, sd, npre, dbl, Pd);
+  else if (ns == 4)
+    hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT, 4>), dim3(g, NKT / NW, 4), dim3(NW * 64), 0, s, qkv, P,
+                       dHm, dS, dqkv, T, sd, npre, dbl, Pd);
+  else
+    hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dHm,
+                       dS, dqkv, T, sd, npre, dbl, Pd);
+  if (nkv == 2)
+    hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW, 2>), dim3(g, NKT / NW, 2), dim3(NW * 64), 0, s, qkv, P, dS,
+                       dHm, dqkv, T, npre, dbl);
+  else if (nkv == 4)
+    hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW, 4>), dim3(g, NKT / NW, 4), dim3(NW * 64), 0, s, qkv, P, dS,
+                       dHm, dqkv, T, npre, dbl);
+  else
+    hipLaunchKernelGGL((k_vlm_attn_bwd_kv_x3<NKT, DD, NW>), dim3(g, NKT / NW), dim3(NW * 64), 0, s, qkv, P, dS, dHm,
+                       dqkv, T, npre, dbl);
 }
 
 template <int DD, int ACT = VACT_SOFTMAX>

@@ -605,3 +605,46 @@ def test_split_pack_and_presplit_gemm(monkeypatch):
                  K, 2, ctypes_stream())
     torch.cuda.synchronize()
     assert torch.equal(s0.cpu(), s1.cpu())
+
+
+@pytest.mark.parametrize("D,T,npre,act", [(256, 81, 1, 0), (256, 161, 81, 0), (128, 162, 162, 0), (256, 40, 1, 0),
+                                          (256, 81, 1, 1), (128, 130, 130, 2)])
+@pytest.mark.parametrize("split", ["2", "4"])
+def test_attention_forward_column_split_bit_identical(D, T, npre, act, split, monkeypatch):
+    """GHM_VX_SPLIT (the split-bf16 attention kernels' output column blocks over 2
+    or 4 workgroups: the forward and the dQ kernel recompute their query tiles'
+    scores / dS, the dK / dV kernel only reloads P and dS) leaves the output, P,
+    GELU', dS and dq / dk / dv bit-identical: the same products per element in the
+    same order."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    N = 7
+    pad = 96 if T <= 96 else 192
+    g = torch.Generator().manual_seed(D + T + act)
+    qkv = (torch.randn(N, T, 3 * D, generator=g) * 0.5).to(DEV)
+    H = torch.randn(N, T, D, generator=g).to(DEV)
+    dHm = torch.randn(N, T, D, generator=g).to(DEV)
+    out = []
+    for sp in ("1", split):
+        monkeypatch.setenv("GHM_VX_SPLIT", sp)
+        monkeypatch.setenv("GHM_VX_SPLIT_KV", sp)
+        Hm = torch.full((N * T, D), float("nan"), device=DEV)
+        P = torch.zeros(N, pad, pad, device=DEV)
+        Pd = torch.zeros(N, pad, pad, device=DEV)
+        dS = torch.zeros(N, pad, pad, device=DEV)
+        dqkv = torch.full((N * T, 3 * D), float("nan"), device=DEV)
+        if act == 0:
+            _native.call("ghm_attn_ext_fwd_x3", _ptr(qkv), _ptr(H), _ptr(Hm), _ptr(P), N, T, D, npre, math.sqrt(D),
+                         1.0 / D, ctypes_stream())
+            _native.call("ghm_attn_ext_bwd_x3", _ptr(qkv), _ptr(P), _ptr(dHm), _ptr(dS), _ptr(dqkv), N, T, D, npre,
+                         math.sqrt(D), 1.0 / D, ctypes_stream())
+        else:
+            _native.call("ghm_attn_ext_fwd_x3_act", _ptr(qkv), _ptr(H), _ptr(Hm), _ptr(P), _ptr(Pd), N, T, D, npre,
+                         math.sqrt(D), 0.0, act, ctypes_stream())
+            _native.call("ghm_attn_ext_bwd_x3_act", _ptr(qkv), _ptr(P), _ptr(Pd), _ptr(dHm), _ptr(dS), _ptr(dqkv),
+                         N, T, D, npre, math.sqrt(D), 0.0, act, ctypes_stream())
+        torch.cuda.synchronize()
+        out.append((Hm.cpu(), P.cpu(), Pd.cpu(), dS.cpu(), dqkv.cpu()))
+    assert torch.isfinite(out[0][0]).all() and torch.isfinite(out[0][4]).all()
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)

@@ -1,7 +1,7 @@
-# SQ counter passes over a short VLM bench (round 4 "r4_m3"): where the split-bf16
+# usage: bash tools/gpu_vlm_pmc.sh [TAG]   SQ counter passes over a short VLM bench (round 4 "r4_m3"): where the split-bf16
 # GEMM's wave cycles go (waits, LDS conflicts, MFMA busy).  One pass per run, each
 # under its own KILL timeout; summarise with tools/pmc_summary.py.
-cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/r4_m3 && mkdir -p $O
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/${1:-r4_m3} && mkdir -p $O
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU" \
