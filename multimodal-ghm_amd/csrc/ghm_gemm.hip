@@ -236,22 +236,26 @@ __device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_
 // written once per step by ghm_split_pack), so its tiles are copied into LDS
 // without a split -- the weights' split, which every workgroup of a column
 // block repeated, is gone from the K loop
-template <bool TA, bool TB, int EPI, int TM, bool F32, int V = 0>
+template <bool TA, bool TB, int EPI, int TM, bool F32, int V = 0, int BN = GB_N>
 __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   constexpr bool BUF = (V & 1) != 0, IL = (V & 3) == 3, BP = (V & 4) != 0;
   static_assert(!BP || (BUF && TB && !F32), "pre-split B: buffer loads, k-contiguous, split-bf16");
+  // BN: workgroup tile columns, 128 or 64 (split-bf16 only: twice the workgroups
+  // for the N = 256 products); a wave owns JN 32-column blocks
+  static_assert(BN == GB_N || (BN == 64 && !F32 && !BP), "64-column tiles: split-bf16, f32 B");
+  constexpr int JN = BN / 64;
   constexpr int BM = 64 * TM;
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
-  constexpr int NB = TB ? GB_N * 8 / 256 : GB_N / 32;
+  constexpr int NB = TB ? BN * 8 / 256 : BN / 32;
   // double-buffered images: [buf][row][k], split (hi, lo) bf16 or (F32) f32
-  constexpr int SM_X3 = 2 * 2 * (BM + GB_N) * GP * 2, SM_F32 = 2 * (BM + GB_N) * GPF * 4;
+  constexpr int SM_X3 = 2 * 2 * (BM + BN) * GP * 2, SM_F32 = 2 * (BM + BN) * GPF * 4;
   __shared__ __attribute__((aligned(16))) char smem[F32 ? SM_F32 : SM_X3];
   __bf16(*ah)[BM * GP] = reinterpret_cast<__bf16(*)[BM * GP]>(smem);
   __bf16(*al)[BM * GP] = ah + 2;
-  __bf16(*bh)[GB_N * GP] = reinterpret_cast<__bf16(*)[GB_N * GP]>(smem + 2 * 2 * BM * GP * 2);
-  __bf16(*bl)[GB_N * GP] = bh + 2;
+  __bf16(*bh)[BN * GP] = reinterpret_cast<__bf16(*)[BN * GP]>(smem + 2 * 2 * BM * GP * 2);
+  __bf16(*bl)[BN * GP] = bh + 2;
   float(*af)[BM * GPF] = reinterpret_cast<float(*)[BM * GPF]>(smem);
-  float(*bf)[GB_N * GPF] = reinterpret_cast<float(*)[GB_N * GPF]>(smem + 2 * BM * GPF * 4);
+  float(*bf)[BN * GPF] = reinterpret_cast<float(*)[BN * GPF]>(smem + 2 * BM * GPF * 4);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   const int tbx = lin % static_cast<int>(gridDim.x);
   const int tby = (lin / static_cast<int>(gridDim.x)) % static_cast<int>(gridDim.y);
   const int tbz = lin / static_cast<int>(gridDim.x * gridDim.y);
-  const int64_t n0 = static_cast<int64_t>(tbx) * GB_N;
+  const int64_t n0 = static_cast<int64_t>(tbx) * BN;
   const int64_t m0 = static_cast<int64_t>(tby) * BM;
   const int64_t kb = static_cast<int64_t>(tbz) * g.k_per_split;
   const int64_t ke = kb + g.k_per_split < g.K ? kb + g.k_per_split : g.K;
@@ -297,9 +301,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
         vob[i] = static_cast<int>(((idx >> 2) * g.ldb + 8 * (idx & 3)) * 2);
       }
     } else if constexpr (TB) {
-      voff_kc<GB_N>(vob, g.ldb);
+      voff_kc<BN>(vob, g.ldb);
     } else {
-      voff_oc<GB_N>(vob, g.ldb);
+      voff_oc<BN>(vob, g.ldb);
     }
   }
   auto load = [&](float4* va, float4* vb, int64_t k0) {
@@ -323,8 +327,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
       if constexpr (BP) {
         // vb[0..1]: the hi chunks, vb[2..3]: the lo chunks (raw bf16 bits)
         const __bf16* b = g.Bp + n0 * g.ldb + k0;
-        const auto rh = brsrc(b, live ? GB_N * g.ldb * 2 : 0);
-        const auto rl = brsrc(b + g.bplane, live ? GB_N * g.ldb * 2 : 0);
+        const auto rh = brsrc(b, live ? BN * g.ldb * 2 : 0);
+        const auto rl = brsrc(b + g.bplane, live ? BN * g.ldb * 2 : 0);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           vb[i] = bload4(rh, vob[i]);
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
       } else if constexpr (TB) {
         int64_t ln;
         const float* b = bbase(n0, ln);
-        const auto rs = brsrc(b + ln * g.ldb + k0, live ? GB_N * g.ldb * 4 : 0);
+        const auto rs = brsrc(b + ln * g.ldb + k0, live ? BN * g.ldb * 4 : 0);
 #pragma unroll
         for (int i = 0; i < NB; ++i) vb[i] = bload4(rs, vob[i]);
       } else {
@@ -350,11 +354,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     if constexpr (TB) {
       int64_t ln;
       const float* b = bbase(n0, ln);
-      load_kc<GB_N>(vb, b + ln * g.ldb, g.ldb, 0, GB_N, k0);
+      load_kc<BN>(vb, b + ln * g.ldb, g.ldb, 0, BN, k0);
     } else {
       int64_t lk;
       const float* b = bbase(k0, lk);
-      load_oc<GB_N>(vb, b + (lk - k0) * g.ldb, g.ldb, k0, ke, n0);
+      load_oc<BN>(vb, b + (lk - k0) * g.ldb, g.ldb, k0, ke, n0);
     }
   };
   // split-k wgrad with C2 set: per-thread row sums of A (the bias gradient, sum
@@ -375,8 +379,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     if constexpr (F32) {
       if constexpr (TA) store_oc_f32<BM, !BUF>(va, af[buf], k0, ke);
       else store_kc_f32<BM>(va, af[buf]);
-      if constexpr (TB) store_kc_f32<GB_N>(vb, bf[buf]);
-      else store_oc_f32<GB_N, false>(vb, bf[buf], k0, ke);
+      if constexpr (TB) store_kc_f32<BN>(vb, bf[buf]);
+      else store_oc_f32<BN, false>(vb, bf[buf], k0, ke);
       return;
     }
     if constexpr (TA) store_oc<BM, !BUF>(va, ah[buf], al[buf], k0, ke);
@@ -389,19 +393,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
         *reinterpret_cast<float4*>(bh[buf] + off) = vb[i];
         *reinterpret_cast<float4*>(bl[buf] + off) = vb[2 + i];
       }
-    } else if constexpr (TB) store_kc<GB_N>(vb, bh[buf], bl[buf]);
-    else store_oc<GB_N, false>(vb, bh[buf], bl[buf], k0, ke);
+    } else if constexpr (TB) store_kc<BN>(vb, bh[buf], bl[buf]);
+    else store_oc<BN, false>(vb, bh[buf], bl[buf], k0, ke);
   };
 
   // acc[i][j] = C^T tile: rows = 32 n (B image rows), lanes = 32 m (A image rows),
   // so each lane owns one output row m and 4 consecutive n per register quad
-  f32x16 acc[TM][2];
+  f32x16 acc[TM][JN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = zero16();
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) acc[i][j] = zero16();
 
   auto compute = [&](int buf) {
     if constexpr (F32) {
-      float xa[TM][16], yb[2][16];
+      float xa[TM][16], yb[JN][16];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -410,10 +416,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
           xa[i][4 * q] = v.x; xa[i][4 * q + 1] = v.y; xa[i][4 * q + 2] = v.z; xa[i][4 * q + 3] = v.w;
         }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JN; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(bf[buf] + (32 * (2 * wn + j) + r) * GPF + 16 * h + 4 * q);
+          const float4 v = *reinterpret_cast<const float4*>(bf[buf] + (32 * (JN * wn + j) + r) * GPF + 16 * h + 4 * q);
           yb[j][4 * q] = v.x; yb[j][4 * q + 1] = v.y; yb[j][4 * q + 2] = v.z; yb[j][4 * q + 3] = v.w;
         }
 #pragma unroll
@@ -421,12 +427,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(yb[j][kk], xa[i][kk], acc[i][j]);
+          for (int j = 0; j < JN; ++j) acc[i][j] = mfma32(yb[j][kk], xa[i][kk], acc[i][j]);
       return;
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 xh[TM], xl[TM], yh[2], yl[2];
+      bf16x8 xh[TM], xl[TM], yh[JN], yl[JN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int off = (32 * (TM * wm + i) + r) * GP + 16 * s + 8 * h;
@@ -434,15 +440,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
         xl[i] = ldsb8(al[buf] + off);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int off = (32 * (2 * wn + j) + r) * GP + 16 * s + 8 * h;
+      for (int j = 0; j < JN; ++j) {
+        const int off = (32 * (JN * wn + j) + r) * GP + 16 * s + 8 * h;
         yh[j] = ldsb8(bh[buf] + off);
         yl[j] = ldsb8(bl[buf] + off);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x3(yh[j], yl[j], xh[i], xl[i], acc[i][j]);
+        for (int j = 0; j < JN; ++j) acc[i][j] = mfma_x3(yh[j], yl[j], xh[i], xl[i], acc[i][j]);
     }
   };
 
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   // write, repeated over the tile's MFMAs
   auto interleave = [&]() {
 #pragma unroll
-    for (int i = 0; i < TM * 2 * 2 * 3; ++i) {
+    for (int i = 0; i < TM * JN * 2 * 3; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
@@ -550,8 +556,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
     const int64_t m = m0 + 32 * (TM * wm + i) + r;
     if (m >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t nb = n0 + 32 * (2 * wn + j);
+    for (int j = 0; j < JN; ++j) {
+      const int64_t nb = n0 + 32 * (JN * wn + j);
       float4 rv[4], bv[4];
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd) {
@@ -939,11 +945,27 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
     if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, 1>), g2, dim3(256), 0, s, g);
     else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, F32 ? 1 : 3>), g2, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), g2, dim3(256), 0, s, g);
-  } else {
-    if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1>), g1, dim3(256), 0, s, g);
-    else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, F32 ? 1 : 3>), g1, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), g1, dim3(256), 0, s, g);
+    return;
   }
+  // 64 x 64 tiles (split-bf16, buffer staging) for the forward / data-gradient
+  // products with N < tm2_min: twice the workgroups for the N = 256 shapes, which
+  // ran 324 per launch; measured 43.4 -> 34.2 us (dY W2, VLM) and 39.4 -> 36.2 us
+  // (X Wo^T + residual), while the weight gradients ran slower with them (38.4 ->
+  // 44.8 us; profiles/r5_bn_ab.txt).  GHM_GEMM_BN = 64 / 128 forces one tile width
+  // for every shape (A/B knob, read per call).
+  const char* bne = getenv("GHM_GEMM_BN");
+  const bool bn64 = bne ? atoi(bne) == 64 : !TA;
+  if constexpr (!F32) {
+    if (bn64 && (v == 1 || v == 3)) {
+      const dim3 g64(static_cast<unsigned>(g.N / 64), static_cast<unsigned>((g.M + 63) / 64), nsplit);
+      if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1, 64>), g64, dim3(256), 0, s, g);
+      else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 3, 64>), g64, dim3(256), 0, s, g);
+      return;
+    }
+  }
+  if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1>), g1, dim3(256), 0, s, g);
+  else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, F32 ? 1 : 3>), g1, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32>), g1, dim3(256), 0, s, g);
 }
 
 // pre-split B (V = 5: buffer loads + BP), ta = 0: the VLM's weight products

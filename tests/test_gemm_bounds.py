@@ -28,11 +28,11 @@ def _offs_oc(cols, ld):
     return [((rpt * kg + i) * ld + 4 * c4) * 4 for kg in range(kgn) for c4 in range(256 // kgn) for i in range(rpt)]
 
 
-def out_of_allocation(ta, tb, M, N, K, lda, ldb, nsplit, a_rows, b_rows, TM, fixed=True):
+def out_of_allocation(ta, tb, M, N, K, lda, ldb, nsplit, a_rows, b_rows, TM, fixed=True, BN=GB_N):
     BM = 64 * TM
     kps = ((K + nsplit - 1) // nsplit + GB_K - 1) // GB_K * GB_K
     oa = _offs_oc(BM, lda) if ta else _offs_kc(BM, lda)
-    ob = _offs_kc(GB_N, ldb) if tb else _offs_oc(GB_N, ldb)
+    ob = _offs_kc(BN, ldb) if tb else _offs_oc(BN, ldb)
     bad = 0
     for z in range(nsplit):
         kb, ke = z * kps, min(z * kps + kps, K)
@@ -45,9 +45,9 @@ def out_of_allocation(ta, tb, M, N, K, lda, ldb, nsplit, a_rows, b_rows, TM, fix
                 else:
                     base, nrec = m0 * lda + k0, min(M - m0, BM) * lda * 4 if live else 0
                 bad += sum(o < nrec and base * 4 + o + 16 > a_rows * lda * 4 for o in oa)
-            for n0 in range(0, N, GB_N):
+            for n0 in range(0, N, BN):
                 if tb:
-                    base, nrec = n0 * ldb + k0, GB_N * ldb * 4 if live else 0
+                    base, nrec = n0 * ldb + k0, BN * ldb * 4 if live else 0
                 else:
                     base, nrec = k0 * ldb + n0, max(0, krows) * ldb * 4
                 bad += sum(o < nrec and base * 4 + o + 16 > b_rows * ldb * 4 for o in ob)
@@ -55,15 +55,15 @@ def out_of_allocation(ta, tb, M, N, K, lda, ldb, nsplit, a_rows, b_rows, TM, fix
 
 
 @pytest.mark.parametrize("Mtok", [405, 2000])
-@pytest.mark.parametrize("TM", [1, 2])
-def test_buffer_staging_stays_inside_the_operands(Mtok, TM):
+@pytest.mark.parametrize("TM,BN", [(1, 128), (2, 128), (1, 64)])
+def test_buffer_staging_stays_inside_the_operands(Mtok, TM, BN):
     d, F = 256, 1024
     for K, N in ((d, d), (d, 3 * d), (d, F), (F, d)):  # forward X W^T
-        assert out_of_allocation(0, 1, Mtok, N, K, K, K, 1, Mtok, N, TM) == 0
+        assert out_of_allocation(0, 1, Mtok, N, K, K, K, 1, Mtok, N, TM, BN=BN) == 0
     for K, N, ns in ((F, d, 1), (F, d, 3), (3 * d, d, 2), (d, F, 1)):  # data gradients dY W
-        assert out_of_allocation(0, 0, Mtok, N, K, K, N, ns, Mtok, K, TM) == 0
+        assert out_of_allocation(0, 0, Mtok, N, K, K, N, ns, Mtok, K, TM, BN=BN) == 0
     for m, n, ns in ((d, F, 7), (F, d, 16), (3 * d, d, 4)):  # weight gradients over the tokens
-        assert out_of_allocation(1, 0, m, n, Mtok, m, n, ns, Mtok, Mtok, TM) == 0
+        assert out_of_allocation(1, 0, m, n, Mtok, m, n, ns, Mtok, Mtok, TM, BN=BN) == 0
 
 
 def test_the_model_sees_the_first_versions_overrun():
