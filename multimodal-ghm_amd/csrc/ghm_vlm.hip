@@ -129,7 +129,12 @@ __global__ __launch_bounds__(256) void k_ln_rows_fwd(const float* __restrict__ X
 // dX = dres + LN backward of dY (dres may alias dX); per-workgroup partials of
 // dgamma = sum dY * xhat and dbeta = sum dY over the workgroup's rows in fixed
 // order: part [n_blocks][2][D], n_blocks = ceil(M / (4 * LN_ROWS_PER_WAVE)).
-constexpr int LN_ROWS_PER_WAVE = 8;
+// 4 rows per wave (648 workgroups at M = 10,368): the backward 11.0 -> 9.0 us
+// against 8 (324 workgroups, 1.3 waves per SIMD), 2 no better (profiles/r5_rpw_ab.txt)
+#ifndef GHM_LN_RPW
+#define GHM_LN_RPW 4
+#endif
+constexpr int LN_ROWS_PER_WAVE = GHM_LN_RPW;
 template <int R>
 __global__ __launch_bounds__(256) void k_ln_rows_bwd(const float* __restrict__ dY, const float* __restrict__ X,
                                                      const float2* __restrict__ stats, const float* __restrict__ w,
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(256) void k_ln_rows_bwd(const float* __restrict__ d
   for (int r = 0; r < R; ++r) gacc[r] = bacc[r] = 0.f;
   // rows in batches of LN_BATCH whose loads are all issued before the first
   // row's reductions (one row at a time was load-latency bound: 18 us at M = 10,368)
-  constexpr int LN_BATCH = R <= 4 ? 4 : 2;
+  constexpr int LN_BATCH = (R <= 4 ? 4 : 2) < LN_ROWS_PER_WAVE ? (R <= 4 ? 4 : 2) : LN_ROWS_PER_WAVE;
   for (int k0 = 0; k0 < LN_ROWS_PER_WAVE; k0 += LN_BATCH) {
     const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * LN_ROWS_PER_WAVE + k0;
     if (row0 >= M) break;
@@ -203,6 +208,137 @@ __global__ __launch_bounds__(256) void k_ln_rows_bwd(const float* __restrict__ d
     part[static_cast<int64_t>(blockIdx.x) * 2 * D + i] =
         (red[0][which][c] + red[1][which][c]) + (red[2][which][c] + red[3][which][c]);
   }
+}
+
+// The same two kernels for D = 256 J with one float4 per lane and 256-column block
+// (lane owns columns 256 j + 4 lane .. + 3): a row moves in J 1 KB loads per
+// tensor instead of 4 J 256-byte ones.  Same statistics (two-pass, biased
+// variance), summed in a different order.  Measured at par with the scalar form
+// (VLM: fwd 6.6 -> 6.8, bwd 11.4 -> 11.0 us, profiles/r5_lnv_ab.txt): the access
+// width was not what bounds them; the backward's grid was (GHM_LN_RPW below).
+template <int J>
+__global__ __launch_bounds__(256) void k_ln_rows_fwd_v4(const float* __restrict__ X, const float* __restrict__ w,
+                                                        const float* __restrict__ b, float* __restrict__ Y,
+                                                        float2* __restrict__ stats, int64_t M, float eps) {
+  constexpr int D = 256 * J;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float4 v[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) v[j] = *reinterpret_cast<const float4*>(X + row * D + 256 * j + 4 * lane);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  s = sum32(s);
+  s += xhalf(s);
+  const float mean = s / static_cast<float>(D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const float a = v[j].x - mean, bb = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+    q += (a * a + bb * bb) + (c * c + d * d);
+  }
+  q = sum32(q);
+  q += xhalf(q);
+  const float rstd = 1.f / sqrtf(q / static_cast<float>(D) + eps);
+  if (lane == 0) stats[row] = make_float2(mean, rstd);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = 256 * j + 4 * lane;
+    const float4 wv = *reinterpret_cast<const float4*>(w + c), bv = *reinterpret_cast<const float4*>(b + c);
+    st4(Y + row * D + c, (v[j].x - mean) * rstd * wv.x + bv.x, (v[j].y - mean) * rstd * wv.y + bv.y,
+        (v[j].z - mean) * rstd * wv.z + bv.z, (v[j].w - mean) * rstd * wv.w + bv.w);
+  }
+}
+
+template <int J>
+__global__ __launch_bounds__(256) void k_ln_rows_bwd_v4(const float* __restrict__ dY, const float* __restrict__ X,
+                                                        const float2* __restrict__ stats, const float* __restrict__ w,
+                                                        const float* dres, float* dX, float* __restrict__ part,
+                                                        int64_t M) {
+  constexpr int D = 256 * J;
+  __shared__ float4 red[4][2][D / 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float4 gacc[J], bacc[J], wj[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    gacc[j] = bacc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    wj[j] = *reinterpret_cast<const float4*>(w + 256 * j + 4 * lane);
+  }
+  constexpr int LN_BATCH = LN_ROWS_PER_WAVE < 4 ? LN_ROWS_PER_WAVE : 4;
+  for (int k0 = 0; k0 < LN_ROWS_PER_WAVE; k0 += LN_BATCH) {
+    const int64_t row0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * LN_ROWS_PER_WAVE + k0;
+    if (row0 >= M) break;
+    float4 dyv[LN_BATCH][J], xv[LN_BATCH][J], rv[LN_BATCH][J];
+    float2 stv[LN_BATCH];
+#pragma unroll
+    for (int b = 0; b < LN_BATCH; ++b) {
+      const int64_t row = row0 + b < M ? row0 + b : M - 1;  // clamped (unused past M)
+      stv[b] = ld_stats_sys(stats, row);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int64_t o = row * D + 256 * j + 4 * lane;
+        dyv[b][j] = *reinterpret_cast<const float4*>(dY + o);
+        xv[b][j] = *reinterpret_cast<const float4*>(X + o);
+        rv[b][j] = *reinterpret_cast<const float4*>(dres + o);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < LN_BATCH; ++b) {
+      const int64_t row = row0 + b;
+      if (row >= M) break;
+      const float2 st = stv[b];
+      float xh[J][4], g[J][4];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const float dy[4] = {dyv[b][j].x, dyv[b][j].y, dyv[b][j].z, dyv[b][j].w};
+        const float xx[4] = {xv[b][j].x, xv[b][j].y, xv[b][j].z, xv[b][j].w};
+        const float ww[4] = {wj[j].x, wj[j].y, wj[j].z, wj[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[j][e] = (xx[e] - st.x) * st.y;
+          g[j][e] = dy[e] * ww[e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+        }
+        gacc[j].x += dy[0] * xh[j][0]; gacc[j].y += dy[1] * xh[j][1];
+        gacc[j].z += dy[2] * xh[j][2]; gacc[j].w += dy[3] * xh[j][3];
+        bacc[j].x += dy[0]; bacc[j].y += dy[1]; bacc[j].z += dy[2]; bacc[j].w += dy[3];
+      }
+      s1 = sum32(s1);
+      s1 += xhalf(s1);
+      s2 = sum32(s2);
+      s2 += xhalf(s2);
+      const float m1 = s1 / static_cast<float>(D), m2 = s2 / static_cast<float>(D);
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const float4 r = rv[b][j];
+        st4(dX + row * D + 256 * j + 4 * lane, r.x + st.y * (g[j][0] - m1 - xh[j][0] * m2),
+            r.y + st.y * (g[j][1] - m1 - xh[j][1] * m2), r.z + st.y * (g[j][2] - m1 - xh[j][2] * m2),
+            r.w + st.y * (g[j][3] - m1 - xh[j][3] * m2));
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    red[wv][0][64 * j + lane] = gacc[j];
+    red[wv][1][64 * j + lane] = bacc[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D / 4; i += 256) {
+    const int which = i / (D / 4), c4 = i % (D / 4);
+    const float4 a = red[0][which][c4], b = red[1][which][c4], c = red[2][which][c4], d = red[3][which][c4];
+    st4(part + static_cast<int64_t>(blockIdx.x) * 2 * D + which * D + 4 * c4, (a.x + b.x) + (c.x + d.x),
+        (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z), (a.w + b.w) + (c.w + d.w));
+  }
+}
+
+// GHM_LN_VEC = 0: the one-float-per-lane kernels for every D (A/B knob, read per call)
+static bool ln_vec() {
+  const char* e = getenv("GHM_LN_VEC");
+  return !(e && atoi(e) == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,6 +691,8 @@ extern "C" int ghm_ln_rows_fwd(const float* X, const float* w, const float* b, f
   float2* st = reinterpret_cast<float2*>(stats);
   hipStream_t s = ghm_stream(stream);
   if (D == 128) hipLaunchKernelGGL(k_ln_rows_fwd<2>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
+  else if (ln_vec() && D == 256) hipLaunchKernelGGL(k_ln_rows_fwd_v4<1>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
+  else if (ln_vec()) hipLaunchKernelGGL(k_ln_rows_fwd_v4<2>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   else if (D == 256) hipLaunchKernelGGL(k_ln_rows_fwd<4>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   else hipLaunchKernelGGL(k_ln_rows_fwd<8>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   return ghm_launch_status();
@@ -571,6 +709,9 @@ extern "C" int ghm_ln_rows_bwd(const float* dY, const float* X, const float* sta
   const float2* st = reinterpret_cast<const float2*>(stats);
   hipStream_t s = ghm_stream(stream);
   if (D == 128) hipLaunchKernelGGL(k_ln_rows_bwd<2>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
+  else if (ln_vec() && D == 256)
+    hipLaunchKernelGGL(k_ln_rows_bwd_v4<1>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
+  else if (ln_vec()) hipLaunchKernelGGL(k_ln_rows_bwd_v4<2>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
   else if (D == 256) hipLaunchKernelGGL(k_ln_rows_bwd<4>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
   else hipLaunchKernelGGL(k_ln_rows_bwd<8>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
   return ghm_launch_status();

@@ -257,3 +257,45 @@ def test_presplit_weight_images_bit_identical(d, monkeypatch):
     for a, b in zip(outs[0], outs[1]):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("vec", ["1", "0"])
+@pytest.mark.parametrize("D", [128, 256, 512])
+def test_ln_rows_kernels_vs_float64(D, vec, monkeypatch):
+    """ghm_ln_rows_fwd / ghm_ln_rows_bwd (the VLM's and CDM's row LayerNorms,
+    model.py:340-343 nn.LayerNorm) against float64 torch: Y and the (mean, rstd)
+    statistics, dX = dres + the LN backward (dres aliasing dX, as the VLM calls
+    it) and the fixed-order dgamma / dbeta partials, on a ragged token count.
+    GHM_LN_VEC=1 (default) is the float4-per-lane form for D = 256 / 512, 0 the
+    one-float-per-lane kernels; tolerance 2e-5 of each tensor's max-abs."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    monkeypatch.setenv("GHM_LN_VEC", vec)
+    g = torch.Generator().manual_seed(5)
+    M, eps = 1037, 1e-5
+    X = (torch.randn(M, D, generator=g) * 3 + 0.5).double()
+    w, b = torch.randn(D, generator=g).double(), torch.randn(D, generator=g).double()
+    dY, dres = torch.randn(M, D, generator=g).double(), torch.randn(M, D, generator=g).double()
+    import ctypes
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    Xd, wd, bd = X.float().to(DEV), w.float().to(DEV), b.float().to(DEV)
+    Y, st = torch.empty(M, D, device=DEV), torch.empty(M, 2, device=DEV)
+    _native.call("ghm_ln_rows_fwd", _ptr(Xd), _ptr(wd), _ptr(bd), _ptr(Y), _ptr(st), M, D, eps, s)
+    nblk = int(_native.hip_lib().ghm_ln_rows_blocks(M))
+    part = torch.empty(nblk, 2, D, device=DEV)
+    dX = dres.float().to(DEV)  # dres aliases dX
+    _native.call("ghm_ln_rows_bwd", _ptr(dY.float().to(DEV)), _ptr(Xd), _ptr(st), _ptr(wd), _ptr(dX), _ptr(dX),
+                 _ptr(part), M, D, s)
+    torch.cuda.synchronize()
+    Xr = X.float().double().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(Xr, (D,), w.float().double(), b.float().double(), eps)
+    ref.backward(dY.float().double())
+    mean = Xr.detach().mean(1)
+    rstd = 1 / (Xr.detach().var(1, unbiased=False) + eps).sqrt()
+    xhat = (Xr.detach() - mean[:, None]) * rstd[:, None]
+    assert _rel(Y, ref) < 2e-5
+    assert _rel(st[:, 0], mean) < 2e-5 and _rel(st[:, 1], rstd) < 2e-5
+    assert _rel(dX, dres.float().double() + Xr.grad) < 2e-5
+    dYf = dY.float().double()
+    assert _rel(part[:, 0].sum(0), (dYf * xhat).sum(0)) < 2e-5
+    assert _rel(part[:, 1].sum(0), dYf.sum(0)) < 2e-5
