@@ -903,8 +903,8 @@ def main_vlm(a, ws, rank):
         # X2 in [M,D], W1 [F,D], b1 [F], G and GELU' out [M,F] each, fp32
         kbytes = 4 * (M * D + F * D + F + 2 * M * F)
         achieved = kbytes / (kern_ms * 1e-3) / 1e9
-        # the instantiation the step launches: 128 x 128 tiles (N = F >= 768), buffer-load staging
-        twin = "k_gemm_x3<false, true, 1, 2, false, 1, 128>"
+        # the instantiation the step launches: 128 x 128 tiles (N = F >= 768), buffer-load staging, one LDS tile
+        twin = "k_gemm_x3<false, true, 1, 2, false, 9, 128>"
         roofline = {"bound": "hbm", "kernel": f"k_gemm_x3 MLP up + GELU epilogue ([{M},{D}]x[{D},{F}])",
                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(twin, "traffic_vlm.json"),

@@ -237,8 +237,13 @@ __device__ __forceinline__ void store_oc_f32(const float4* v, float* img, int64_
 // without a split -- the weights' split, which every workgroup of a column
 // block repeated, is gone from the K loop
 template <bool TA, bool TB, int EPI, int TM, bool F32, int V = 0, int BN = GB_N>
-__global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
+__global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
   constexpr bool BUF = (V & 1) != 0, IL = (V & 3) == 3, BP = (V & 4) != 0;
+  // SB (V & 8): one LDS tile instead of two (a second barrier per K tile), so
+  // three 128 x 128 workgroups fit a CU's LDS (TM = 2, split-bf16, not IL)
+  constexpr bool SB = (V & 8) != 0;
+  static_assert(!SB || (TM == 2 && !F32 && !IL && !BP), "single LDS tile: TM = 2, split-bf16, no interleave");
+  constexpr int NBUF = SB ? 1 : 2;
   static_assert(!BP || (BUF && TB && !F32), "pre-split B: buffer loads, k-contiguous, split-bf16");
   // BN: workgroup tile columns, 128 or 64 (split-bf16 only: twice the workgroups
   // for the N = 256 products); a wave owns JN 32-column blocks
@@ -248,12 +253,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
   constexpr int NB = TB ? BN * 8 / 256 : BN / 32;
   // double-buffered images: [buf][row][k], split (hi, lo) bf16 or (F32) f32
-  constexpr int SM_X3 = 2 * 2 * (BM + BN) * GP * 2, SM_F32 = 2 * (BM + BN) * GPF * 4;
+  constexpr int SM_X3 = NBUF * 2 * (BM + BN) * GP * 2, SM_F32 = 2 * (BM + BN) * GPF * 4;
   __shared__ __attribute__((aligned(16))) char smem[F32 ? SM_F32 : SM_X3];
   __bf16(*ah)[BM * GP] = reinterpret_cast<__bf16(*)[BM * GP]>(smem);
-  __bf16(*al)[BM * GP] = ah + 2;
-  __bf16(*bh)[BN * GP] = reinterpret_cast<__bf16(*)[BN * GP]>(smem + 2 * 2 * BM * GP * 2);
-  __bf16(*bl)[BN * GP] = bh + 2;
+  __bf16(*al)[BM * GP] = ah + NBUF;
+  __bf16(*bh)[BN * GP] = reinterpret_cast<__bf16(*)[BN * GP]>(smem + NBUF * 2 * BM * GP * 2);
+  __bf16(*bl)[BN * GP] = bh + NBUF;
   float(*af)[BM * GPF] = reinterpret_cast<float(*)[BM * GPF]>(smem);
   float(*bf)[BN * GPF] = reinterpret_cast<float(*)[BN * GPF]>(smem + 2 * BM * GPF * 4);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -480,6 +485,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmArgs g) {
       load(pa, pb, more || BUF ? k0 + GB_K : k0);
       issue_fence();
       compute(buf);
+      if constexpr (SB) {
+        __syncthreads();  // every wave is done with the tile before it is overwritten
+        if (more) store(pa, pb, 0, k0 + GB_K);
+        __syncthreads();
+        continue;
+      }
       if constexpr (IL) {
         store(pa, pb, buf ^ 1, k0 + GB_K);  // past the end: zeros into a buffer nobody reads
         interleave();
@@ -942,6 +953,19 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
   const dim3 g2(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), g1(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit);
   if (g.N >= tm2_min) {
+    // split-bf16: one LDS tile and a second barrier per K tile (V = 9), so that
+    // three workgroups share a CU (40 KB of LDS, 156-164 VGPRs) instead of two (80
+    // KB): GELU forward 42.0 -> 36.5, dU product 47.4 -> 43.5, dW2 39.6 -> 37.2 us,
+    // VLM step -1.3 % (profiles/r5_sb_ab.txt); the same for the 64 x 128 weight
+    // gradients (30 KB, 154 VGPRs) was slower, 37.5 -> 39.2 us (r5_sb1_ab.txt).
+    // GHM_GEMM_SB = 0 restores the double buffer (A/B knob, read per call).
+    if constexpr (!F32) {
+      const char* sb = getenv("GHM_GEMM_SB");
+      if ((sb ? atoi(sb) == 1 : true) && v != 0) {
+        hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, 9>), g2, dim3(256), 0, s, g);
+        return;
+      }
+    }
     if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, 1>), g2, dim3(256), 0, s, g);
     else if (v == 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32, F32 ? 1 : 3>), g2, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 2, F32>), g2, dim3(256), 0, s, g);

@@ -460,14 +460,15 @@ def test_attention_f32_activation(T, act):
 
 
 @pytest.mark.parametrize("f32", [False, True])
-@pytest.mark.parametrize("variant", ["1", "3", "bn64", "bn128"])
+@pytest.mark.parametrize("variant", ["1", "3", "bn64", "bn128", "sb", "sb0"])
 def test_buffer_load_staging_bit_identical(variant, f32, monkeypatch):
     """GHM_GEMM_BUF=1 (buffer-load staging: rows past M, past a split's last
     token or past K read as hardware zeros instead of clamped re-reads + zeroing
     selects) and =3 (the same with the next tile's split store interleaved into
     the current tile's MFMAs) change only how and when tiles are loaded and
     stored (GHM_GEMM_BUF=0 is the pointer-load staging; the default is 1, and 3
-    for the weight gradients), and so do both tile widths (GHM_GEMM_BN=64 / 128): every
+    for the weight gradients), and so do both tile widths (GHM_GEMM_BN=64 / 128) and one or two LDS
+    tiles (GHM_GEMM_SB=1 / 0): every
     shape class -- forward
     store / GELU / residual, data gradient store / product / split-k, split-k
     weight gradient with bias rows, token tails and an empty trailing split, both
@@ -522,7 +523,10 @@ def test_buffer_load_staging_bit_identical(variant, f32, monkeypatch):
         cases.append(runw)
     monkeypatch.setenv("GHM_GEMM_BUF", "0")
     base = [[t.cpu() for t in c()] for c in cases]
-    if variant.startswith("bn"):  # the default staging, one tile width for the N < 768 products (x3 only)
+    if variant.startswith("sb"):  # one LDS tile for the N >= 768 products (default; three workgroups per CU, x3 only) or two
+        monkeypatch.delenv("GHM_GEMM_BUF", raising=False)
+        monkeypatch.setenv("GHM_GEMM_SB", "1" if variant == "sb" else "0")
+    elif variant.startswith("bn"):  # the default staging, one tile width for the N < 768 products (x3 only)
         monkeypatch.delenv("GHM_GEMM_BUF", raising=False)
         monkeypatch.setenv("GHM_GEMM_BN", variant[2:])
     else:
