@@ -350,4 +350,4 @@ def test_bench_finds_the_dominant_kernels_stamped_twin():
     assert rc and all(b._rc_twin(k, 1) in prof for k in rc), (path, sorted(prof))
     assert b.pmc_traffic("k_mlp_bwd_rc_x3") is not None
     # the VLM line's roofline kernel (the instantiation its step launches) in the VLM traffic passes
-    assert b.pmc_traffic("k_gemm_x3<false, true, 1, 2, false, 1, 128>", "traffic_vlm.json") > 0
+    assert b.pmc_traffic("k_gemm_x3<false, true, 1, 2, false, 9, 128>", "traffic_vlm.json") > 0
