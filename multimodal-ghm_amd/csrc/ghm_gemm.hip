@@ -606,6 +606,30 @@ __global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
   }
 }
 
+// s[0] + s[stride] + ... + s[(nsplit - 1) stride], added in z order, with the loads
+// of 8 slabs in flight at once (one load per round trip, as the plain loop
+// compiled, made the 16-slab reduce 16 serial HBM round trips: 6.2 -> 5.2 us,
+// profiles/r5_red_ab.txt)
+__device__ __forceinline__ float4 slab_sum(const float4* s, int nsplit, int64_t stride) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < nsplit; z += 8) {
+    // unconditional loads (past the last slab they re-read it, unused): a load
+    // under a branch drains the wait count at the join
+    float4 b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) b[u] = s[static_cast<int64_t>(z + u < nsplit ? z + u : nsplit - 1) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (z + u == 0) {
+        a = b[0];  // the first slab as is (not 0 + s[0]: the sign of a zero stays)
+      } else if (z + u < nsplit) {
+        a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w;
+      }
+    }
+  }
+  return a;
+}
+
 // dst rows (stacked as B is): out = sum_z slab[z] in z order.  Workgroups past the
 // slab's (nmain) sum the row-sum partials bslab[z][M] into bdst (bias gradient).
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ slab, int nsplit, int64_t M, int64_t N,
@@ -614,24 +638,13 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(const float* __restrict__ s
   if (static_cast<int64_t>(blockIdx.x) >= nmain) {
     const int64_t b4 = (static_cast<int64_t>(blockIdx.x) - nmain) * 256 + threadIdx.x;
     if (4 * b4 >= M) return;
-    const float4* s = reinterpret_cast<const float4*>(bslab) + b4;
-    float4 a = s[0];
-    for (int z = 1; z < nsplit; ++z) {
-      const float4 b = s[static_cast<int64_t>(z) * (M / 4)];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-    reinterpret_cast<float4*>(bdst)[b4] = a;
+    reinterpret_cast<float4*>(bdst)[b4] = slab_sum(reinterpret_cast<const float4*>(bslab) + b4, nsplit, M / 4);
     return;
   }
   const int64_t i4 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   const int64_t total = M * N;
   if (4 * i4 >= total) return;
-  const float4* s = reinterpret_cast<const float4*>(slab) + i4;
-  float4 a = s[0];
-  for (int z = 1; z < nsplit; ++z) {
-    const float4 b = s[static_cast<int64_t>(z) * (total / 4)];
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-  }
+  const float4 a = slab_sum(reinterpret_cast<const float4*>(slab) + i4, nsplit, total / 4);
   const int64_t m = (4 * i4) / N, n = (4 * i4) % N;
   float* d = d0;
   int64_t lm = m;

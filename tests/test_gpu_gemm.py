@@ -657,3 +657,30 @@ def test_attention_forward_column_split_bit_identical(D, T, npre, act, split, mo
     assert torch.isfinite(out[0][0]).all() and torch.isfinite(out[0][4]).all()
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("ns", [1, 3, 8, 9, 16, 17])
+def test_slab_reduce_is_the_z_ordered_sum(ns):
+    """ghm_gemm_reduce_bias (the split-k slabs and the bias row-sum partials,
+    loads of 8 slabs in flight): bit-identical to s[0] + s[1] + ... in z order in
+    f32, signed zeros included, for split counts around the batch of 8."""
+    from ghmclip import _native
+    from ghmclip.models.vlm import _ptr
+    g = torch.Generator().manual_seed(ns)
+    m, n = 96, 256
+    slab = torch.randn(ns, m, n, generator=g)
+    slab[0, 0, :8] = -0.0
+    slab[:, 1, :4] = 0.0
+    slab[0, 1, :4] = -0.0
+    bslab = torch.randn(ns, m, generator=g)
+    want, bwant = slab[0].clone(), bslab[0].clone()
+    for z in range(1, ns):
+        want += slab[z]
+        bwant += bslab[z]
+    out, bias = torch.empty(m, n, device=DEV), torch.empty(m, device=DEV)
+    sd, bd = slab.to(DEV), bslab.to(DEV)
+    _native.call("ghm_gemm_reduce_bias", _ptr(sd), ns, m, n, _ptr(out), None, None, 0, _ptr(bd), _ptr(bias),
+                 ctypes_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), want) and torch.equal(torch.signbit(out.cpu()), torch.signbit(want))
+    assert torch.equal(bias.cpu(), bwant)
