@@ -143,8 +143,13 @@ class CdmPlan(EncoderPlan):
     def __init__(self, n_layer, n_token, n_i_token, n_seq, num_class=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", precision=None, joint=False, activation="softmax",
                  layernorm=True):
-        if precision is None:  # the joint model (T = 162) defaults to exact f32
-            precision = default_precision("f32" if joint else "x3")
+        if precision is None:
+            # exact f32 by default where split-bf16 leaves the parity bound: the joint
+            # model (T = 162), and relu / gelu attention without
+            # LayerNorm (un-normalised scores on un-normalised activations: an MLP
+            # weight gradient 6.2e-4 off at x3 against the 5e-4 bound)
+            f32_default = joint or (activation != "softmax" and not layernorm)
+            precision = default_precision("f32" if f32_default else "x3")
         # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
         # on the split-bf16 attention kernels (EncoderPlan: one-sequence up to 96 tokens,
         # the multi-workgroup ghm_attn_ext_*_act past 96, the joint model's 162)

@@ -45,9 +45,10 @@ class AdamW(torch.optim.Optimizer):
     def step(self, closure: Optional[Callable] = None):
         loss = None if closure is None else closure()
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        work = []  # (param, state, t, consts, hyper row)
         for group in self.param_groups:
             lr, wd = group["lr"], group["weight_decay"]
-            b1, omb1, b2, omb2, eps = adam_consts(group["betas"], group["eps"])
+            consts = adam_consts(group["betas"], group["eps"])
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -60,12 +61,17 @@ class AdamW(torch.optim.Optimizer):
                     state["m"] = torch.zeros_like(p.data)
                     state["v"] = torch.zeros_like(p.data)
                 t = state["t"] + 1
-                hyper = torch.tensor([0.0, 1.0, adam_lr_t(lr, t, group["betas"]), lr * wd],
-                                     dtype=torch.float32).to(p.device, non_blocking=True)
-                _native.call("ghm_adamw", p.data.data_ptr(), p.grad.data_ptr(), state["m"].data_ptr(),
-                             state["v"].data_ptr(), p.numel(), hyper.data_ptr(), b1, omb1, b2, omb2, eps,
-                             stream)
-                state["t"] = t
+                work.append((p, state, t, consts, [0.0, 1.0, adam_lr_t(lr, t, group["betas"]), lr * wd]))
+        if not work:
+            return loss
+        # every parameter's step scalars in one pinned buffer and one H2D copy (the
+        # caching host allocator keeps a pinned block alive until its copy is done)
+        host = torch.tensor([w[4] for w in work], dtype=torch.float32).pin_memory()
+        hyper = host.to(work[0][0].device, non_blocking=True)
+        for k, (p, state, t, (b1, omb1, b2, omb2, eps), _) in enumerate(work):
+            _native.call("ghm_adamw", p.data.data_ptr(), p.grad.data_ptr(), state["m"].data_ptr(),
+                         state["v"].data_ptr(), p.numel(), hyper[k].data_ptr(), b1, omb1, b2, omb2, eps, stream)
+            state["t"] = t
         return loss
 
 

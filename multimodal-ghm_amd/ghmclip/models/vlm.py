@@ -164,10 +164,10 @@ class VlmPlan:
         # N = D products have only 2 x M / 64 output tiles: ~1.3 workgroups per CU)
         self.dsplit = max(1, int(os.environ.get("GHM_VLM_DSPLIT", "1")))
         self.dslab = e(self.dsplit * M * D) if self.dsplit > 1 else None
-        # x3, GHM_VLM_PACK=1 (opt-in): the weights' (hi, lo) bf16 images for
-        # ghm_gemm_x3p, split once per forward by ghm_split_pack, instead of the
-        # GEMMs splitting them per tile
-        self.pack_on = not self.f32 and os.environ.get("GHM_VLM_PACK", "0") == "1"
+        # x3 (default; GHM_VLM_PACK=0 turns it off): the weights' (hi, lo) bf16
+        # images for ghm_gemm_x3p, split once per forward by ghm_split_pack, instead
+        # of the GEMMs splitting them per tile
+        self.pack_on = not self.f32 and os.environ.get("GHM_VLM_PACK", "1") == "1"
         if self.pack_on:
             self._img_sizes = {"qkv": 3 * D * D, "qkvT": 3 * D * D, "w1": F * D, "w1T": F * D, "w2": F * D,
                                "w2T": F * D}
@@ -178,7 +178,13 @@ class VlmPlan:
                 for k, n in self._img_sizes.items():
                     self._img_off[(l, k)] = o
                     o += 2 * n
-            self._pack_key, self.pack_jobs = None, None
+            # the job table lives in one device buffer for the plan's lifetime: a
+            # captured ghm_split_pack node keeps its address, so a table rewritten
+            # for moved weights is refreshed in place (never reallocated), and only
+            # outside a capture (_split_weights)
+            self._pack_key = None
+            self.pack_jobs = torch.zeros(L * 10, 8, dtype=torch.int64, device=self.device)
+            self._pack_tiles = 1
         lib = _native.hip_lib()
         self.colpart = e(max(lib.ghm_colsum_part_elems(M, F), lib.ghm_colsum_part_elems(M, D),
                              lib.ghm_colsum_part_elems(N, n_token * D),
@@ -236,6 +242,9 @@ class VlmPlan:
                   f"_mlps.{l}.2.weight") for l in range(self.L)]
         key = tuple(p[n].data_ptr() for ns in names for n in ns)
         if key != self._pack_key:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("VlmPlan: the weights moved during a graph capture; run one eager forward with "
+                                   "the same parameter tensors before capturing")
             jobs = []
             for l, (nq, nk, nv, n1, n2) in enumerate(names):
                 qkv, _, pq = self._img(l, "qkv")
@@ -248,7 +257,8 @@ class VlmPlan:
                     bt, _, plt = self._img(l, kt)
                     jobs.append((p[n].data_ptr(), cols, rows, cols, b, cols, pl, 0))
                     jobs.append((p[n].data_ptr(), cols, rows, cols, bt, rows, plt, 1))
-            self.pack_jobs = torch.tensor(jobs, dtype=torch.int64).to(self.device)
+            assert len(jobs) == self.pack_jobs.shape[0]
+            self.pack_jobs.copy_(torch.tensor(jobs, dtype=torch.int64))
             self._pack_tiles = max(-(-r // 64) * -(-c // 64) for (_, _, r, c, _, _, _, _) in jobs)
             self._pack_key = key
         _native.call("ghm_split_pack", _ptr(self.pack_jobs), len(self.pack_jobs), self._pack_tiles, s)

@@ -187,6 +187,7 @@ class ClipTrainer:
         self.comm_timing = None
         self._bwd_it = [None, None]  # the towers' running backward launch generators
         self._pending = []  # started data-parallel collectives (distributed.allreduce_ranges_start)
+        self._bucket_checked = [False, False]
         self._setup_guide(penalty, guide_trans)
 
     def _setup_guide(self, penalty, guide_trans):
@@ -315,8 +316,27 @@ class ClipTrainer:
             next(it)
             if k < top:
                 yield  # (the last piece ends with the generator: no empty piece)
+        if not self._bucket_checked[tower]:
+            self._check_bucket_a(tower)
         if flush:
             plan.flush_pending()
+
+    def _check_bucket_a(self, tower):
+        """Bucket A of this tower (all-reduced while the lower layers' backward
+        runs) must hold only gradients whose partials are queued by now, i.e.
+        final once flush_pending() has run: every gradient view inside the bucket's
+        flat range is a destination of a pending reduction job.  Checked on the
+        first step (host only)."""
+        a0, a1 = self.bucket_a[tower]
+        base, esz = self.gflat.data_ptr(), self.gflat.element_size()
+        in_a = {t.data_ptr() for t in self.views[tower][1].values()
+                if a0 <= (t.data_ptr() - base) // esz < a1}
+        queued = {j.dst[i] for j in self.plans[tower].pending for i in range(j.n_seg)}
+        missing = in_a - queued
+        if missing:
+            raise RuntimeError(f"data-parallel bucket A of tower {tower} holds {len(missing)} gradients that are "
+                               "not final after its top layers' backward")
+        self._bucket_checked[tower] = True
 
     def _bwd_b_gen(self, tower):
         """The rest of one tower's backward as pieces (lower layers; the last
@@ -426,6 +446,9 @@ class ClipTrainer:
     def _run(self, graphs=None):
         """One step (eager, or by replaying `graphs` from _capture_graphs)."""
         dp = self._dp()
+        # collectives a failed earlier step started and never finished must not be
+        # waited for (and scaled) again by this one
+        self._pending = []
         self._phase(self._fwd_gen, graphs, "fwd", join=False)
         self._cross_wait()
         # the loss value on the comm stream, off both towers' backward paths (the

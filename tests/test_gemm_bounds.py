@@ -68,3 +68,80 @@ def test_buffer_staging_stays_inside_the_operands(Mtok, TM, BN):
 
 def test_the_model_sees_the_first_versions_overrun():
     assert out_of_allocation(0, 1, 405, 256, 256, 256, 256, 1, 405, 256, 1, fixed=False) > 0
+
+
+def bp_out_of_image(M, N, K, ldbp, nsplit, TM):
+    """Pre-split B (k_gemm_x3 V bit 2, ghm_gemm_x3p): per K tile two 16-byte loads
+    per thread and plane at byte offsets ((idx >> 2) ldbp + 8 (idx & 3)) 2 from the
+    tile's base (n0 ldbp + k0) bf16, records BN ldbp 2 bytes when the tile is live;
+    the hi plane is [N][ldbp] bf16 and the lo plane the next one.  Counts loads
+    inside the records that leave their own plane (either end)."""
+    BN = GB_N
+    kps = ((K + nsplit - 1) // nsplit + GB_K - 1) // GB_K * GB_K
+    ob = [((idx >> 2) * ldbp + 8 * (idx & 3)) * 2 for idx in range(512)]
+    plane = N * ldbp * 2
+    bad = 0
+    for z in range(nsplit):
+        kb, ke = z * kps, min(z * kps + kps, K)
+        for t in range(max(0, -(-(ke - kb) // GB_K)) + 3):
+            k0 = kb + t * GB_K
+            nrec = BN * ldbp * 2 if k0 < ke else 0
+            for n0 in range(0, N, BN):
+                base = (n0 * ldbp + k0) * 2
+                bad += sum(o < nrec and (base + o < 0 or base + o + 16 > plane) for o in ob)
+    return bad
+
+
+@pytest.mark.parametrize("TM", [1, 2])
+def test_presplit_b_loads_stay_inside_their_plane(TM):
+    """Every ghm_gemm_x3p product of models/vlm.py (D = 128 / 256): forward W
+    images (N = 3D / F / D), data-gradient W^T images, split-k data gradients."""
+    for d in (128, 256):
+        F = 4 * d
+        for N, K, ns in ((3 * d, d, 1), (F, d, 1), (d, F, 1), (F, d, 1), (d, F, 2), (d, 3 * d, 1), (d, 3 * d, 3)):
+            assert bp_out_of_image(405, N, K, K, ns, TM) == 0, (d, N, K, ns)
+
+
+def split_pack_writes(L, D):
+    """models/vlm.py VlmPlan._split_weights' job table against k_split_pack's
+    writes: every (hi, lo) element a job writes lies inside its own image of the
+    layer's wpack region, and no element is written twice (the three Q / K / V
+    jobs tile the fused [3D][D] / [D][3D] images exactly)."""
+    F = 4 * D
+    sizes = {"qkv": 3 * D * D, "qkvT": 3 * D * D, "w1": F * D, "w1T": F * D, "w2": F * D, "w2T": F * D}
+    pitch = {"qkv": D, "qkvT": 3 * D, "w1": D, "w1T": F, "w2": F, "w2T": D}
+    off, o = {}, 0
+    for l in range(L):
+        for k, n in sizes.items():
+            off[(l, k)] = o
+            o += 2 * n
+    total = o
+    written = bytearray(total)
+    for l in range(L):
+        jobs = []
+        for i in range(3):
+            jobs.append((D, D, off[(l, "qkv")] + i * D * D, D, sizes["qkv"], 0, (l, "qkv")))
+            jobs.append((D, D, off[(l, "qkvT")] + i * D, 3 * D, sizes["qkvT"], 1, (l, "qkvT")))
+        for (rows, cols), k, kt in (((F, D), "w1", "w1T"), ((D, F), "w2", "w2T")):
+            jobs.append((rows, cols, off[(l, k)], cols, sizes[k], 0, (l, k)))
+            jobs.append((rows, cols, off[(l, kt)], rows, sizes[kt], 1, (l, kt)))
+        for rows, cols, dst, ldd, plane, tr, img in jobs:
+            assert ldd == pitch[img[1]]
+            lo_img, hi_img = off[img], off[img] + 2 * sizes[img[1]]
+            orows, ocols = (cols, rows) if tr else (rows, cols)
+            for r in range(orows):
+                for c in (0, ocols - 1) if r not in (0, orows - 1) else range(ocols):
+                    for e in (dst + r * ldd + c, dst + r * ldd + c + plane):
+                        assert lo_img <= e < hi_img, (img, r, c)
+            for r in range(orows):
+                for c in range(ocols):
+                    for e in (dst + r * ldd + c, dst + r * ldd + c + plane):
+                        assert not written[e], (img, r, c)
+                        written[e] = 1
+    return sum(written), total
+
+
+def test_split_pack_jobs_tile_the_images_exactly():
+    for D in (128, 256):
+        n, total = split_pack_writes(2, D)
+        assert n == total

@@ -7,6 +7,7 @@ absolute (f64 BP, f32 output); losses 2e-5 relative (the CDM loss is a sum of 81
 squared errors, O(10..1000), where the CLIP curve's 1e-4 is absolute on O(1)); the
 long-horizon curve as explained in test_cdm_default_config_curve_vs_reference.
 """
+import copy
 import os
 
 import numpy as np
@@ -138,7 +139,7 @@ def _pair(L=2, seed=11, precision="f32", activation="softmax", layernorm=True):
 
 @pytest.mark.parametrize("precision,activation,layernorm", [
     ("f32", "softmax", True), ("x3", "softmax", True), ("x3", "relu", True), ("x3", "gelu", True),
-    ("f32", "softmax", False), ("x3", "softmax", False), ("f32", "relu", False)])
+    ("f32", "softmax", False), ("x3", "softmax", False), (None, "relu", False), (None, "gelu", False)])
 @pytest.mark.parametrize("B", [7, 20])
 def test_cdm_module_forward_backward(B, precision, activation, layernorm):
     """ConditionalDenoiseEncoderTransformer forward, parameter and conditioning
@@ -153,8 +154,12 @@ def test_cdm_module_forward_backward(B, precision, activation, layernorm):
     LayerNorm runs in f32 here: on the split-bf16 path it measures 6.2e-4 on an MLP
     weight gradient (B=20), outside the 5e-4 split-bf16 bound, with the kernels'
     masks too -- not a mask flip but precision: unnormalised scores on
-    un-normalised activations reach gradients of 2e7 (r5_cdmnoln, r5_relu_mask)."""
+    un-normalised activations reach gradients of 2e7 (r5_cdmnoln, r5_relu_mask).
+    So relu / gelu without LayerNorm default to f32 (CdmPlan): precision None runs
+    the module at its default, which must resolve to f32."""
     prod, ref = _pair(precision=precision, activation=activation, layernorm=layernorm)
+    if precision is None:
+        precision = "f32"
     g = torch.Generator().manual_seed(B)
     z = torch.randint(0, 10, (B, 81), generator=g).float() + torch.randn(B, 81, generator=g)
     cond = torch.randn(B, 1, 10, generator=g)
@@ -163,6 +168,8 @@ def test_cdm_module_forward_backward(B, precision, activation, layernorm):
     pred, gl = prod(cd, z.to(DEV))
     assert gl == [[], []]
     (pred * R.to(DEV)).sum().backward()
+    (plan,) = prod._plans.values()
+    assert plan.precision == precision
     cr = cond.clone().requires_grad_(True)
     want = ref(cr, z)
     (want * R).sum().backward()
@@ -171,11 +178,26 @@ def test_cdm_module_forward_backward(B, precision, activation, layernorm):
     if activation == "relu":  # the kernels' relu masks (see test_gpu_cdm_joint.py)
         cr = cond.double().requires_grad_(True)
         ref = masked_relu_oracle(ref, kernel_relu_masks(prod), lambda m: (m(cr, z.double()) * R.double()).sum())
+    tol = {k: GRAD_TOL[precision] for k, _ in prod.named_parameters()}
+    if activation == "gelu" and not layernorm:
+        # gelu attention on un-normalised activations is ill-conditioned: the
+        # oracle's own float32 run (ref, the comparison target here) leaves its
+        # float64 run by 1.3e-4 (B = 7) / 5.2e-4 (B = 20) on the worst gradient, so
+        # no two f32 implementations need agree within 1e-4.  Bound: 10 x that
+        # spread of the reference's own arithmetic (its worst parameter gradient).
+        ref64 = copy.deepcopy(ref).double()
+        ref64.zero_grad()
+        c64 = cond.double().requires_grad_(True)
+        (ref64(c64, z.double()) * R.double()).sum().backward()
+        spread = max(_rel(pr.grad, p64.grad) for (_, p64), (_, pr) in
+                     zip(ref64.named_parameters(), ref.named_parameters()) if pr.grad is not None)
+        print(f"gelu, no LayerNorm, B={B}: the oracle's own f32 vs f64 spread {spread:.2e}")
+        tol = {k: max(t, 10 * spread) for k, t in tol.items()}
     for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
         if pr.grad is None:
             assert pp.grad is None, k
             continue
-        assert _rel(pp.grad, pr.grad) < GRAD_TOL[precision], k
+        assert _rel(pp.grad, pr.grad) < tol[k], (k, tol[k])
     assert _rel(cd.grad, cr.grad) < GRAD_TOL[precision]
 
 

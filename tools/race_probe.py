@@ -136,7 +136,7 @@ def main():
             return [outQ]
         c("ghm_mlp_bwd_rc_x3", P(dHmid), P(p0.Hmid[l]), P(p0.st2[l]), P(w0[f"_lns_2.{l}.weight"]),
           P(w0[f"_lns_2.{l}.bias"]), P(p0.pack[l]), P(w0[f"_mlps.{l}.0.bias"]), P(outG), P(outU), P(outH), P(outP),
-          M, 128, 512, A)
+          M, 128, 512, 0, A)
         return [outG, outU, outH, outP]
 
     def run_recompute():
