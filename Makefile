@@ -6,7 +6,7 @@ CXX ?= g++
 LIBDIR := multimodal-ghm_amd/ghmclip/_lib
 SRC := multimodal-ghm_amd/csrc
 HIPOBJFLAGS := --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
-HIP_SRCS := $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_x3.hip $(SRC)/ghm_guide.hip $(SRC)/ghm_cdm.hip $(SRC)/ghm_vlm.hip $(SRC)/ghm_gemm.hip $(SRC)/ghm_vlm_x3.hip $(SRC)/ghm_wgrad.hip $(SRC)/ghm_optim.hip $(SRC)/ghm_eval.hip
+HIP_SRCS := $(SRC)/ghm_genc.hip $(SRC)/ghm_fwd.hip $(SRC)/ghm_bwd.hip $(SRC)/ghm_x3.hip $(SRC)/ghm_guide.hip $(SRC)/ghm_cdm.hip $(SRC)/ghm_vlm.hip $(SRC)/ghm_gemm.hip $(SRC)/ghm_vlm_x3.hip $(SRC)/ghm_wgrad.hip $(SRC)/ghm_optim.hip $(SRC)/ghm_eval.hip
 HIP_HDRS := $(SRC)/ghm_common.h $(SRC)/ghm_launch.h $(SRC)/ghm_split.h $(SRC)/ghm_ln.h include/ghm_hip.h
 
 all: $(LIBDIR)/libghm_hip.so $(LIBDIR)/libghm_host.so

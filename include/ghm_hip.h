@@ -550,6 +550,27 @@ int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const float* X, int64
 int ghm_rows_linear(const float* X, const float* W, const float* b, float* Y, int64_t M, int D, int C, void* stream);
 int ghm_rows_linear_t(const float* dZ, const float* W, float* dX, int64_t M, int D, int C, void* stream);
 
+/* ---- generic-width CLIP encoder ends (csrc/ghm_genc.hip, models/gemm_encoder.py:
+ * n_embd != 128, e.g. the reference CLI default clip_{t,i}model_deb = 64,
+ * utils/config.py:58-59; its layers run on ghm_gemm_x3, ghm_ln_rows_* and
+ * ghm_attn_ext_*_x3 at D = n_embd) ------------------------------------------ */
+
+/* H0[n, t, :] = tok_w[tokens[n, t]] + pos_w[t], D floats per row
+ * —  models/model.py:762-765 (token_embeddings(x) + position_embeddings). */
+int ghm_tok_embed_fwd(const uint8_t* tokens, const float* tok_w, const float* pos_w, float* H0, int64_t n_seq, int T,
+                      int V, int D, void* stream);
+
+/* emb[n][c] = b_out + sum_t w_out[t] Z[n][t][c], Z = H_L W_ro^T + b_ro (ghm_rows_linear)
+ * —  models/model.py:802-805 (_read_out, transpose, _out). */
+int ghm_tok_readout_fwd(const float* Z, const float* w_out, const float* b_out, float* emb, int64_t n_seq, int T,
+                        int C, void* stream);
+
+/* Backward of the token-axis Linear(n_token -> 1): dZ[n][t][c] = w_out[t] d_emb[n][c],
+ * d_wout[t] = sum_{n,c} d_emb[n][c] Z[n][t][c], d_bout[0] = sum d_emb (fixed-order
+ * sums; one launch)  —  backward of models/model.py:804-805. */
+int ghm_tok_readout_bwd(const float* Z, const float* d_emb, const float* w_out, float* dZ, float* d_wout,
+                        float* d_bout, int64_t n_seq, int T, int C, void* stream);
+
 /* ---- zero-shot classification (figures/eval-zsc-risk.py:107-118) --------
  * logits[q][r][c] = log( mean_{k < n_list[q]} exp(<i_emb[r], t_emb[proto_idx[c][k]]>) )
  * for every image row r < n_rows and class c < n_class: the reference's

@@ -965,7 +965,8 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   const int v = be ? atoi(be) : (TA ? 3 : 1);
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
   const dim3 g2(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), g1(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit);
-  if (g.N >= tm2_min) {
+  const bool narrow_n = g.N % GB_N != 0 || (TB && g.b_chunk > 0 && g.b_chunk % GB_N != 0);
+  if (g.N >= tm2_min && !narrow_n) {
     // split-bf16: one LDS tile and a second barrier per K tile (V = 9), so that
     // three workgroups share a CU (40 KB of LDS, 156-164 VGPRs) instead of two (80
     // KB): GELU forward 42.0 -> 36.5, dU product 47.4 -> 43.5, dW2 39.6 -> 37.2 us,
@@ -991,11 +992,15 @@ void launch_tm(const GemmArgs& g, int nsplit, hipStream_t s) {
   // 44.8 us; profiles/r5_bn_ab.txt).  GHM_GEMM_BN = 64 / 128 forces one tile width
   // for every shape (A/B knob, read per call).
   const char* bne = getenv("GHM_GEMM_BN");
-  const bool bn64 = bne ? atoi(bne) == 64 : !TA;
+  // N or a stacked tb = 1 operand's chunk not a multiple of 128 (the generic-width
+  // CLIP encoder, n_embd = 64: N = 64 / 192 products, csrc path of
+  // models/gemm_encoder.py): only the 64-column tiles fit
+  const bool narrow = g.N % GB_N != 0 || (TB && g.b_chunk > 0 && g.b_chunk % GB_N != 0);
+  const bool bn64 = narrow || (bne ? atoi(bne) == 64 : !TA);
   if constexpr (!F32) {
-    if (bn64 && (v == 1 || v == 3)) {
+    if (bn64 && (v == 1 || v == 3 || narrow)) {
       const dim3 g64(static_cast<unsigned>(g.N / 64), static_cast<unsigned>((g.M + 63) / 64), nsplit);
-      if (v == 1) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1, 64>), g64, dim3(256), 0, s, g);
+      if (v != 3) hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 1, 64>), g64, dim3(256), 0, s, g);
       else hipLaunchKernelGGL((k_gemm_x3<TA, TB, EPI, 1, F32, 3, 64>), g64, dim3(256), 0, s, g);
       return;
     }
@@ -1064,7 +1069,9 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
                        float* C2, const float* bias, const float* R, int64_t ldr, int64_t M, int64_t N, int64_t K,
                        int nsplit, void* stream) {
   GHM_CHECK(A && B0 && C, "null pointer");
-  GHM_CHECK(M >= 1 && N >= GB_N && N % GB_N == 0 && K >= 1 && nsplit >= 1 && nsplit <= 256, "shape (N % 128 == 0)");
+  // N % 128 == 0, or (split-bf16: 64-column tiles) N % 64 == 0
+  GHM_CHECK(M >= 1 && N >= 64 && N % (f32 ? GB_N : 64) == 0 && K >= 1 && nsplit >= 1 && nsplit <= 256,
+            "shape (N % 128 == 0; split-bf16: N % 64 == 0)");
   GHM_CHECK(!(ta && tb), "TA and TB together are not a VLM shape");
   GHM_CHECK(epi >= EPI_STORE && epi <= EPI_SLAB, "epilogue");
   GHM_CHECK(nsplit == 1 || epi == EPI_SLAB, "split k needs the slab epilogue");
@@ -1084,8 +1091,10 @@ static int gemm_launch(bool f32, int ta, int tb, int epi, const float* A, int64_
   GHM_CHECK(ta || K % 32 == 0, "K % 32 == 0 unless ta = 1");
   if (b_chunk > 0) {
     const int64_t rows = tb ? N : K;
-    GHM_CHECK(b_chunk % GB_N == 0 && rows <= 3 * b_chunk && B1 && (rows <= 2 * b_chunk || B2),
-              "stacked B: chunk % 128 == 0, at most 3 tensors");
+    // a B tile never straddles two tensors: tb = 1 tiles are BN rows of n (128, or
+    // 64 when the chunk is not a multiple of 128), tb = 0 tiles 32 rows of k
+    GHM_CHECK(b_chunk % (f32 ? GB_N : 64) == 0 && rows <= 3 * b_chunk && B1 && (rows <= 2 * b_chunk || B2),
+              "stacked B: chunk % 128 == 0 (split-bf16: % 64), at most 3 tensors");
   }
   GemmArgs g;
   g.A = A; g.lda = lda;
@@ -1270,12 +1279,15 @@ extern "C" int ghm_wcolsum(const float* W, const uint8_t* tok, int C, const floa
 
 extern "C" int ghm_rows_linear(const float* X, const float* W, const float* b, float* Y, int64_t M, int D, int C,
                                void* stream) {
-  GHM_CHECK(X && W && b && Y && M >= 1 && C >= 1 && C <= 64 && (D == 128 || D == 256) && C * D <= 16384, "shape");
+  GHM_CHECK(X && W && b && Y && M >= 1 && C >= 1 && C <= 64 && (D == 64 || D == 128 || D == 256) && C * D <= 16384,
+            "shape");
   GHM_CHECK(((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) == 0, "16-byte aligned X, W");
   const dim3 grid(static_cast<unsigned>((M + 15) / 16));
   const size_t lds = static_cast<size_t>(C) * D * sizeof(float);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128)
+  if (D == 64)
+    hipLaunchKernelGGL(k_rows_linear<64>, grid, dim3(256), lds, s, X, W, b, Y, M, C);
+  else if (D == 128)
     hipLaunchKernelGGL(k_rows_linear<128>, grid, dim3(256), lds, s, X, W, b, Y, M, C);
   else
     hipLaunchKernelGGL(k_rows_linear<256>, grid, dim3(256), lds, s, X, W, b, Y, M, C);
@@ -1283,13 +1295,16 @@ extern "C" int ghm_rows_linear(const float* X, const float* W, const float* b, f
 }
 
 extern "C" int ghm_rows_linear_t(const float* dZ, const float* W, float* dX, int64_t M, int D, int C, void* stream) {
-  GHM_CHECK(dZ && W && dX && M >= 1 && C >= 1 && C <= 64 && (D == 128 || D == 256) && C * D <= 16384, "shape");
+  GHM_CHECK(dZ && W && dX && M >= 1 && C >= 1 && C <= 64 && (D == 64 || D == 128 || D == 256) && C * D <= 16384,
+            "shape");
   GHM_CHECK(((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(dX)) & 15) == 0, "16-byte aligned W, dX");
   const int64_t rpb = 256 / (D / 4);
   const dim3 grid(static_cast<unsigned>((M + rpb - 1) / rpb));
   const size_t lds = static_cast<size_t>(C) * D * sizeof(float);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128)
+  if (D == 64)
+    hipLaunchKernelGGL(k_rows_linear_t<64>, grid, dim3(256), lds, s, dZ, W, dX, M, C);
+  else if (D == 128)
     hipLaunchKernelGGL(k_rows_linear_t<128>, grid, dim3(256), lds, s, dZ, W, dX, M, C);
   else
     hipLaunchKernelGGL(k_rows_linear_t<256>, grid, dim3(256), lds, s, dZ, W, dX, M, C);

@@ -686,11 +686,12 @@ extern "C" int ghm_vlm_embed_joint_fwd(const uint8_t* xt, const uint8_t* it, con
 extern "C" int ghm_ln_rows_fwd(const float* X, const float* w, const float* b, float* Y, float* stats, int64_t M,
                                int D, float eps, void* stream) {
   GHM_CHECK(X && w && b && Y && stats, "null pointer");
-  GHM_CHECK(M >= 1 && (D == 128 || D == 256 || D == 512), "shape (D in {128, 256, 512})");
+  GHM_CHECK(M >= 1 && (D == 64 || D == 128 || D == 256 || D == 512), "shape (D in {64, 128, 256, 512})");
   const dim3 g(static_cast<unsigned>((M + 3) / 4));
   float2* st = reinterpret_cast<float2*>(stats);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128) hipLaunchKernelGGL(k_ln_rows_fwd<2>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
+  if (D == 64) hipLaunchKernelGGL(k_ln_rows_fwd<1>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
+  else if (D == 128) hipLaunchKernelGGL(k_ln_rows_fwd<2>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   else if (ln_vec() && D == 256) hipLaunchKernelGGL(k_ln_rows_fwd_v4<1>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   else if (ln_vec()) hipLaunchKernelGGL(k_ln_rows_fwd_v4<2>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
   else if (D == 256) hipLaunchKernelGGL(k_ln_rows_fwd<4>, g, dim3(256), 0, s, X, w, b, Y, st, M, eps);
@@ -704,11 +705,12 @@ extern "C" int ghm_ln_rows_bwd(const float* dY, const float* X, const float* sta
                                float* dX, float* part, int64_t M, int D, void* stream) {
   GHM_CHECK(dY && X && stats && w && dres && dX && part, "null pointer");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
-  GHM_CHECK(M >= 1 && (D == 128 || D == 256 || D == 512), "shape (D in {128, 256, 512})");
+  GHM_CHECK(M >= 1 && (D == 64 || D == 128 || D == 256 || D == 512), "shape (D in {64, 128, 256, 512})");
   const dim3 g(static_cast<unsigned>(ghm_ln_rows_blocks(M)));
   const float2* st = reinterpret_cast<const float2*>(stats);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128) hipLaunchKernelGGL(k_ln_rows_bwd<2>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
+  if (D == 64) hipLaunchKernelGGL(k_ln_rows_bwd<1>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
+  else if (D == 128) hipLaunchKernelGGL(k_ln_rows_bwd<2>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
   else if (ln_vec() && D == 256)
     hipLaunchKernelGGL(k_ln_rows_bwd_v4<1>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);
   else if (ln_vec()) hipLaunchKernelGGL(k_ln_rows_bwd_v4<2>, g, dim3(256), 0, s, dY, X, st, w, dres, dX, part, M);

@@ -62,10 +62,11 @@ __device__ __forceinline__ constexpr int vx_chunk(int n) {
   return n % 8 == 0 ? 8 : (n % 6 == 0 ? 6 : (n % 4 == 0 ? 4 : (n % 3 == 0 ? 3 : (n % 2 == 0 ? 2 : 1))));
 }
 
-// columns col + 64 hh + 0..31 (hh = 0, 1) of rows 0..TP-1 (row stride ld) as a
+// columns col + HS hh + 0..31 (hh = 0, 1) of rows 0..TP-1 (row stride ld) as a
 // split [row][hh][32] image; rows >= T clamp to T - 1.  NW waves stage it in
-// chunks of at most 8 float4 per thread.
-template <int NKT, int NW>
+// chunks of at most 8 float4 per thread.  HS = 64: a 32-column slab of each
+// 64-feature half of a 128-feature block; HS = 32: the two halves of D = 64.
+template <int NKT, int NW, int HS = 64>
 __device__ __forceinline__ void vx_stage_half(const float* __restrict__ seq, int64_t ld, int T, int col, __bf16* ih,
                                               __bf16* il) {
   constexpr int NT = NW * 64, NIT = NKT * 32 * 16 / NT, CH = vx_chunk(NIT);
@@ -78,7 +79,7 @@ __device__ __forceinline__ void vx_stage_half(const float* __restrict__ seq, int
       const int idx = threadIdx.x + NT * (c0 + k);
       const int row = idx >> 4, hh = (idx >> 3) & 1, q4 = idx & 7;
       const int rc = row < T ? row : T - 1;
-      v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * ld + col + 64 * hh + 4 * q4);
+      v[k] = *reinterpret_cast<const float4*>(seq + static_cast<int64_t>(rc) * ld + col + HS * hh + 4 * q4);
     }
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
@@ -143,6 +144,24 @@ __device__ __forceinline__ void vx_scores(const float* __restrict__ xseq, int64_
                                           __bf16* sl, f32x16* s) {
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) s[kt] = zero16();
+  if constexpr (DD == 64) {
+    // D = 64 (the generic-width CLIP encoder, n_embd = 64): lane half h holds
+    // features 32 h .. 32 h + 31 of Y; one [row][hh][32] image of both halves
+    bf16x8 yh[4], yl[4];
+    float y[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(yrow + 32 * h + 4 * k);
+      y[4 * k] = v.x; y[4 * k + 1] = v.y; y[4 * k + 2] = v.z; y[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) split8(y + 8 * t, yh[t], yl[t]);
+    vx_stage_half<NKT, NW, 32>(xseq, ldx, T, xcol, sh, sl);
+    __syncthreads();
+    vx_rows_dot<NKT>(sh, sl, yh, yl, 0, j, h, nk, s);
+    __syncthreads();
+    return;
+  }
 #pragma unroll 1
   for (int e = 0; e < DD / 128; ++e) {
     bf16x8 yh[8], yl[8];
@@ -550,7 +569,7 @@ template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_fwd_n(unsigned g, hipStream_t s, const float* qkv, const float* H, float* Hm, float* P, int T, int npre,
                   float sd, float dbl, float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  const int ns = vx_split();
+  const int ns = vx_split() <= DD / 32 ? vx_split() : DD / 32;  // at least one 32-column block per split
   if (ns == 2)
     hipLaunchKernelGGL((k_vlm_attn_fwd_x3<NKT, DD, NW, ACT, 2>), dim3(g, NKT / NW, 2), dim3(NW * 64), 0, s, qkv, H, Hm,
                        P, T, npre, sd, dbl, Pd);
@@ -577,7 +596,9 @@ template <int NKT, int DD, int ACT = VACT_SOFTMAX>
 void launch_bwd_n(unsigned g, hipStream_t s, const float* qkv, const float* P, const float* dHm, float* dS,
                   float* dqkv, int T, int npre, float sd, float dbl, const float* Pd = nullptr) {
   constexpr int NW = vx_nw<NKT>();
-  const int ns = vx_split(), nkv = vx_split("GHM_VX_SPLIT_KV", 4);
+  int ns = vx_split(), nkv = vx_split("GHM_VX_SPLIT_KV", 4);
+  if (ns > DD / 32) ns = DD / 32;  // at least one 32-column block per split
+  if (nkv > DD / 32) nkv = DD / 32;
   if (ns == 2)
     hipLaunchKernelGGL((k_vlm_attn_bwd_q_x3<NKT, DD, NW, ACT, 2>), dim3(g, NKT / NW, 2), dim3(NW * 64), 0, s, qkv, P,
                        dHm, dS, dqkv, T, sd, npre, dbl, Pd);
@@ -631,10 +652,11 @@ extern "C" int ghm_vlm_attn_bwd_x3(const float* qkv, const float* P, const float
 extern "C" int ghm_attn_ext_fwd_x3(const float* qkv, const float* H, float* H_mid, float* P, int64_t n_seq, int T,
                                    int D, int n_prefix, float scale_div, float dbl, void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
+  GHM_CHECK((D == 64 || D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {64, 128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  if (D == 64) launch_fwd<64>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
+  else if (D == 128) launch_fwd<128>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
   else launch_fwd<256>(T, g, ghm_stream(stream), qkv, H, H_mid, P, n_prefix, scale_div, dbl);
   return ghm_launch_status();
 }
@@ -643,10 +665,11 @@ extern "C" int ghm_attn_ext_bwd_x3(const float* qkv, const float* P, const float
                                    int64_t n_seq, int T, int D, int n_prefix, float scale_div, float dbl,
                                    void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
+  GHM_CHECK((D == 64 || D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {64, 128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
-  if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  if (D == 64) launch_bwd<64>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
+  else if (D == 128) launch_bwd<128>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
   else launch_bwd<256>(T, g, ghm_stream(stream), qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl);
   return ghm_launch_status();
 }
@@ -656,11 +679,14 @@ extern "C" int ghm_attn_ext_fwd_x3_act(const float* qkv, const float* H, float* 
                                        void* stream) {
   GHM_CHECK(qkv && H && H_mid && P, "null pointer");
   GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
+  GHM_CHECK((D == 64 || D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {64, 128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128) {
+  if (D == 64) {
+    if (act == VACT_RELU) launch_fwd<64, VACT_RELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+    else launch_fwd<64, VACT_GELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
+  } else if (D == 128) {
     if (act == VACT_RELU) launch_fwd<128, VACT_RELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
     else launch_fwd<128, VACT_GELU>(T, g, s, qkv, H, H_mid, P, n_prefix, scale_div, dbl, Pd);
   } else {  // D = 256: the VLM (AutoRegressiveTransformer(activation=...), model.py:163, 287)
@@ -675,11 +701,14 @@ extern "C" int ghm_attn_ext_bwd_x3_act(const float* qkv, const float* P, const f
                                        float scale_div, float dbl, int act, void* stream) {
   GHM_CHECK(qkv && P && dH_mid && dS && dqkv, "null pointer");
   GHM_CHECK(act == VACT_RELU || (act == VACT_GELU && Pd), "act: 1 relu, 2 gelu (with Pd)");
-  GHM_CHECK((D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {128, 256}, T <= 192)");
+  GHM_CHECK((D == 64 || D == 128 || D == 256) && T >= 1 && T <= 192, "shape (D in {64, 128, 256}, T <= 192)");
   GHM_CHECK(n_seq >= 1 && n_prefix >= 0 && n_prefix <= T, "n_seq >= 1, 0 <= n_prefix <= T");
   const unsigned g = static_cast<unsigned>(n_seq);
   hipStream_t s = ghm_stream(stream);
-  if (D == 128) {
+  if (D == 64) {
+    if (act == VACT_RELU) launch_bwd<64, VACT_RELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+    else launch_bwd<64, VACT_GELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
+  } else if (D == 128) {
     if (act == VACT_RELU) launch_bwd<128, VACT_RELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
     else launch_bwd<128, VACT_GELU>(T, g, s, qkv, P, dH_mid, dS, dqkv, n_prefix, scale_div, dbl, Pd);
   } else {

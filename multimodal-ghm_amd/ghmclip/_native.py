@@ -108,6 +108,9 @@ HIP_SIGNATURES = {
     "ghm_wcolsum": [_p, _p, _i, _p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p],
     "ghm_rows_linear": [_p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_rows_linear_t": [_p, _p, _p, _i64, _i, _i, _p],
+    "ghm_tok_embed_fwd": [_p, _p, _p, _p, _i64, _i, _i, _i, _p],
+    "ghm_tok_readout_fwd": [_p, _p, _p, _p, _i64, _i, _i, _p],
+    "ghm_tok_readout_bwd": [_p, _p, _p, _p, _p, _p, _i64, _i, _i, _p],
     "ghm_mul": [_p, _p, _p, _i64, _p],
     "ghm_add": [_p, _p, _p, _i64, _p],
     "ghm_ce_kl": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],

@@ -503,6 +503,11 @@ class EncoderPlan:
         from here on."""
         self._flush(self.pending, _stream())
 
+    def queued_grad_ptrs(self):
+        """Addresses of the parameter gradients whose partials the running
+        backward_iter has queued so far (final once flush_pending() has run)."""
+        return {j.dst[i] for j in self.pending for i in range(j.n_seg)}
+
     def layers_bwd(self, p, g, jobs, s, layer_grad=None):
         """Backward of the n_layer encoder layers from dH[0] (= dL/dH_L, written by
         the caller's readout backward) down to dL/dH_0, which is returned (one of

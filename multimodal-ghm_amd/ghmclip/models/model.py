@@ -14,7 +14,8 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import EncoderPlan, param_names, require_hip
+from .gemm_encoder import make_encoder_plan
+from .hip_encoder import param_names, require_hip
 
 __all__ = ["seed_everything", "get_activation", "EncoderTransformer", "GuidedClipLoss", "ClipLoss"]
 
@@ -70,9 +71,12 @@ class _EncoderFn(torch.autograd.Function):
             if dg is None:
                 continue
             dg = dg.contiguous().float()
-
-            def fn(dH, s, dg=dg):
-                _native.call("ghm_add_cols", dH.data_ptr(), dg.data_ptr(), plan.M, V, s)
+            if ctx.module.n_embd == 128:
+                def fn(dH, s, dg=dg):
+                    _native.call("ghm_add_cols", dH.data_ptr(), dg.data_ptr(), plan.M, V, s)
+            else:  # the GEMM path's residual stream has row pitch n_embd
+                def fn(dH, s, dg=dg):
+                    dH.view(-1, ctx.module.n_embd)[:, :V] += dg.view(-1, V)
             hooks[l] = fn
         plan.backward(dict(zip(names, params)), grads, d_emb=d_emb.contiguous().float(), tokens=tokens,
                       layer_grad=hooks)
@@ -141,10 +145,10 @@ class EncoderTransformer(nn.Module):
         key = (n_seq, T, str(device), self.precision, self.activation)
         if key not in self._plans:
             self._plans.clear()  # keep one workspace set alive per module
-            self._plans[key] = EncoderPlan(self.n_layer, T, n_seq, num_class=self.vocab_size,
-                                           vocab=self.vocab_size, n_embd=self.n_embd,
-                                           normalize_attn=self.normalize_attn, device=device,
-                                           precision=self.precision, activation=self.activation)
+            self._plans[key] = make_encoder_plan(self.n_layer, T, n_seq, num_class=self.vocab_size,
+                                                 vocab=self.vocab_size, n_embd=self.n_embd,
+                                                 normalize_attn=self.normalize_attn, device=device,
+                                                 precision=self.precision, activation=self.activation)
         return self._plans[key]
 
     def _guided_layers(self):

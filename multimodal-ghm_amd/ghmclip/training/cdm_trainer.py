@@ -29,7 +29,8 @@ from ..data.data_random_GHM import DeviceTree
 from .. import _native
 from . import distributed
 from ..models.cdm import CdmPlan, cdm_guide_blocks, cdm_untrained
-from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.gemm_encoder import make_encoder_plan
+from ..models.hip_encoder import require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
 
@@ -95,7 +96,7 @@ class CdmTrainer:
             self.t_tok = self.plan.tok  # text leaves [B, T - T_img], read by the embedding and BP
             n_text = T - Ti
         else:
-            self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+            self.clip_plan = make_encoder_plan(clip_model.n_layer, clip_model.n_token, batch_size,
                                          num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
                                          n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
                                          device=self.device, precision=self.precision)

@@ -26,7 +26,8 @@ import torch
 from .. import _native
 from . import distributed
 from ..data.data_random_GHM import DeviceTree
-from ..models.hip_encoder import EncoderPlan, default_precision, require_hip
+from ..models.gemm_encoder import make_encoder_plan
+from ..models.hip_encoder import default_precision, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
 
@@ -54,6 +55,11 @@ def flat_layout(models, dp_top):
     tower], total numel)."""
     layout, bucket_a, off = [], [], 0
     for m in models:
+        # each tower starts 16-byte aligned (the GEMM-path kernels read the embedding
+        # tables and biases as float4; a tower's parameters are multiples of 4 floats
+        # up to its readout, whose n_token + num_class + 1 floats may not be: n_token = 64
+        # of the reference's default 3-layer, 4-child trees).  The gap stays zero.
+        off = -(-off // 4) * 4
         top = min(dp_top, m.n_layer)  # a tower may have fewer layers than the text tower
         named = dict(m.named_parameters())
         order = [n for l in reversed(range(m.n_layer)) for n in named if _layer_of(n) == l]
@@ -113,18 +119,17 @@ class ClipTrainer:
         params = [p for m in self.models for p in m.parameters()]
         for p in params:
             require_hip(p)
-        n = sum(p.numel() for p in params)
-        self.n_params = n
-        self.pflat = torch.empty(n, dtype=torch.float32, device=self.device)
-        self.gflat = torch.zeros(n, dtype=torch.float32, device=self.device)
-        self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
-        self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
-        self.views = []  # per model: (param dict, grad dict, m dict, v dict)
         L0 = max(m.n_layer for m in self.models)
         # layers in bucket A (clamped per tower in flat_layout / _bwd_a_gen)
         self.dp_top = int(os.environ.get("GHM_DP_BUCKET_LAYERS", str(L0 - L0 // 2)))
         self.dp_top = max(0, min(L0, self.dp_top))
-        layout, self.bucket_a, _ = flat_layout(self.models, self.dp_top)
+        layout, self.bucket_a, n = flat_layout(self.models, self.dp_top)
+        self.n_params = n  # (with the zero gap that aligns the image tower, if any)
+        self.pflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.gflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.mflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.vflat = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.views = []  # per model: (param dict, grad dict, m dict, v dict)
         with torch.no_grad():
             for m, slots in zip(self.models, layout):
                 named = dict(m.named_parameters())
@@ -143,10 +148,14 @@ class ClipTrainer:
         n_seq = batch_size * (K + 1)
         if precision is None:
             precision = default_precision("f32" if all(getattr(m, "guide", False) for m in self.models) else "x3")
-        self.plans = [EncoderPlan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
-                                  n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
-                                  precision=precision, activation=getattr(m, "activation", "softmax"),
-                                  defer_reduce=os.environ.get("GHM_DEFER_REDUCE", "1") != "0")
+        if any(m.n_embd != 128 for m in self.models) and all(getattr(m, "guide", False) for m in self.models):
+            raise NotImplementedError("guided CLIP runs at n_embd = 128 (the guide kernels' row pitch)")
+        # n_embd = 128: the fused token-parallel kernels; other widths (the reference
+        # CLI's default 64): the GEMM path (models/gemm_encoder.py, split-bf16)
+        self.plans = [make_encoder_plan(m.n_layer, m.n_token, n_seq, num_class=m.vocab_size, vocab=m.vocab_size,
+                                        n_embd=m.n_embd, normalize_attn=m.normalize_attn, device=self.device,
+                                        precision=precision, activation=getattr(m, "activation", "softmax"),
+                                        defer_reduce=os.environ.get("GHM_DEFER_REDUCE", "1") != "0")
                       for m in self.models]
         self.precision = self.plans[0].precision
         self.T, self.n_seq = T, n_seq
@@ -331,7 +340,7 @@ class ClipTrainer:
         base, esz = self.gflat.data_ptr(), self.gflat.element_size()
         in_a = {t.data_ptr() for t in self.views[tower][1].values()
                 if a0 <= (t.data_ptr() - base) // esz < a1}
-        queued = {j.dst[i] for j in self.plans[tower].pending for i in range(j.n_seg)}
+        queued = self.plans[tower].queued_grad_ptrs()
         missing = in_a - queued
         if missing:
             raise RuntimeError(f"data-parallel bucket A of tower {tower} holds {len(missing)} gradients that are "

@@ -18,7 +18,8 @@ import torch
 
 from .. import _native
 from . import distributed
-from ..models.hip_encoder import EncoderPlan, require_hip
+from ..models.gemm_encoder import make_encoder_plan
+from ..models.hip_encoder import require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 from ..models.vlm import VlmPlan, vlm_guide_blocks, vlm_guide_plane_elems, vlm_untrained
 
@@ -81,7 +82,7 @@ class VlmTrainer:
             self.clip_plan = None
             self.precision = self.plan.precision
         else:
-            self.clip_plan = EncoderPlan(clip_model.n_layer, clip_model.n_token, batch_size,
+            self.clip_plan = make_encoder_plan(clip_model.n_layer, clip_model.n_token, batch_size,
                                          num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
                                          n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
                                          device=self.device, precision=precision)

@@ -237,17 +237,23 @@ class OracleEncoder(nn.Module):
         pos = torch.arange(T, device=x.device).expand(B, T)
         H = self.token_embeddings(x) + self.position_embeddings(pos)  # :765
         guided = []
-        for q, k, v, mlp, ln1, ln2, flag in zip(self._queries, self._keys, self._values,
-                                                self._mlps, self._lns_1, self._lns_2,
-                                                self.guided_layer_flag):
+        # test hooks: `scores` (a list) records each layer's scaled scores; `relu_masks`
+        # (per layer, [B, T, T]) replaces relu's own mask with given ones, so that a
+        # float64 gradient can be taken with the masks a kernel used (tests/test_gpu_width.py)
+        for l, (q, k, v, mlp, ln1, ln2, flag) in enumerate(zip(self._queries, self._keys, self._values,
+                                                               self._mlps, self._lns_1, self._lns_2,
+                                                               self.guided_layer_flag)):
             H1 = ln1(H)  # :772
             S = torch.matmul(q(H1), k(H1).transpose(-2, -1))  # :778
             if self.normalize_attn:
                 S = S / np.sqrt(self.n_embd)  # :779-780
+            if getattr(self, "scores", None) is not None:
+                self.scores.append(S.detach())
             if self.activation == "softmax":  # :781 through get_activation (:121-130)
                 A = F.softmax(S, dim=-1)
             elif self.activation == "relu":
-                A = F.relu(S)
+                masks = getattr(self, "relu_masks", None)
+                A = F.relu(S) if masks is None else S * masks[l].to(S.dtype)
             else:
                 A = F.gelu(S)
             H = H + torch.einsum("bij,bjd->bid", A, v(H1))  # :782

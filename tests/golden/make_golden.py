@@ -17,6 +17,8 @@ sampler_p40_b16.npz same for p=0.4, B=16 (another shape/probability).
 clip_tiny.npz       tiny CLIP config (L=2, d=16, B=4): init weights, embeddings, loss,
                     raw grads, clip norm, weights after 2 AdamW steps.
 clip_d128.npz       d=128, L=2, B=8 single step: embeddings, loss, grad checksums.
+clip_d64.npz / clip_d256.npz  the same at d = 64 (the reference CLI's default
+                    clip_{t,i}model_deb) and d = 256 (--only d64,d256).
 clip_default_curve.npz  the default CLIP config (p=0.2, L=5, d=128, B=128) loss_history
                     for the first --curve-steps steps of the 3001-step schedule.
 bayes.json          the 20 published Bayes CLIP risks (figures/data/ghm-data/clip-risk.json:90-110).
@@ -354,6 +356,10 @@ if __name__ == "__main__":
         step_fixture("clip_tiny.npz", L=2, d=16, B=4, nsteps=2)
     if "d128" in jobs:
         step_fixture("clip_d128.npz", L=2, d=128, B=8, nsteps=2, checksum_only=True)
+    if "d64" in jobs:  # the reference CLI's default width (utils/config.py:58-59)
+        step_fixture("clip_d64.npz", L=2, d=64, B=8, nsteps=2, checksum_only=True)
+    if "d256" in jobs:
+        step_fixture("clip_d256.npz", L=2, d=256, B=8, nsteps=2, checksum_only=True)
     if "bayes" in jobs:
         bayes_fixture()
     if "curve" in jobs:

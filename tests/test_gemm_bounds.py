@@ -145,3 +145,17 @@ def test_split_pack_jobs_tile_the_images_exactly():
     for D in (128, 256):
         n, total = split_pack_writes(2, D)
         assert n == total
+
+
+@pytest.mark.parametrize("Mtok", [405, 2000])
+def test_narrow_products_stay_inside_the_operands(Mtok):
+    """The generic-width CLIP encoder (models/gemm_encoder.py, n_embd = 64): N = 64 /
+    192 products run on 64-column tiles (N % 128 != 0), the rest as the VLM's."""
+    d, F = 64, 256
+    for K, N in ((d, 3 * d), (d, F), (F, d)):  # forward X W^T
+        assert out_of_allocation(0, 1, Mtok, N, K, K, K, 1, Mtok, N, 1, BN=64 if N % 128 else 128) == 0
+    for K, N in ((F, d), (3 * d, d), (d, F)):  # data gradients dY W
+        assert out_of_allocation(0, 0, Mtok, N, K, K, N, 1, Mtok, K, 1, BN=64 if N % 128 else 128) == 0
+    for m, n, ns in ((d, F, 128), (F, d, 64), (3 * d, d, 85)):  # weight gradients over the tokens
+        ns = min(ns, max(1, Mtok // 256))
+        assert out_of_allocation(1, 0, m, n, Mtok, m, n, ns, Mtok, Mtok, 1, BN=64 if n % 128 else 128) == 0

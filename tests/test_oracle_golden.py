@@ -95,6 +95,13 @@ def test_d128_training_steps():
     _check_steps(_load("clip_d128.npz"), full=False)
 
 
+@pytest.mark.parametrize("d", [64, 256])
+def test_other_width_training_steps(d):
+    """n_embd = 64 (the reference CLI's default clip_{t,i}model_deb,
+    utils/config.py:58-59) and 256: the widths the GEMM encoder path runs."""
+    _check_steps(_load(f"clip_d{d}.npz"), full=False)
+
+
 @pytest.mark.parametrize("act", ["relu", "gelu"])
 def test_d128_training_steps_attention_activation(act):
     """train_CLIP --clip_activation=relu|gelu (model.py:121-130, :781), pinned to

@@ -15,7 +15,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
 cat $OUT/bench.json
 for w in vlm cdm cdm_joint cdm_guided vlm_joint; do
-  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 5
+  timeout -k 10 400 python bench.py --workload $w > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 5
   echo "$w $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$w.json)"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_clip -o run -- \
