@@ -152,5 +152,5 @@ def test_train_clip_cli_default_width(tmp_path, monkeypatch):
     hist = train_CLIP.main(["--batch_size=16", "--total_iters=4", "--raw=False", "--log_interval=2",
                             "--eval_interval=2"])
     assert len(hist) == 5 and np.isfinite(hist).all()
-    ck = glob.glob("logs/CLIP/*/TF_L10H4D64_L10H4D64/*/checkpoint.pth")
-    assert len(ck) == 1, glob.glob("logs/CLIP/*/*")
+    ck = glob.glob("logs/clip/*/TF_L10H4D64_L10H4D64/*/checkpoint.pth")  # job_name default "clip"
+    assert len(ck) == 1, glob.glob("logs/*/*/*")
