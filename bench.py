@@ -443,9 +443,17 @@ def cpu_baseline(B, L, steps=8, guide=False, workload="clip"):
     out["affinity_cpus"] = usable
     out["cores_note"] = ("cores = threads used for value: the GPU job's CPU share on the box ($OMP_NUM_THREADS, 16 "
                          "per GPU); all_cores = the same restatement on os.cpu_count() threads")
-    if host_cpus > share:
+    if host_cpus > share and os.environ.get("GHM_CPU_ALL_CORES") == "1":
         allc = _cpu_baseline_at(host_cpus, B, L, max(2, steps // 4), guide, workload, warmup_limit_s=30.0)
         out["all_cores"] = {k: allc[k] for k in ("value", "cores", "sample") if k in allc}
+    elif host_cpus > share:
+        # os.cpu_count() threads on a box that holds the job to a 16-CPU share
+        # oversubscribe it: round 5 measured one CLIP step in 132 s on 256 threads (a
+        # 0.97 samples/s lower bound, profiles/r5_v8_bench.json), and the VLM's first
+        # step ran past the pool's 180 s silence limit; opt in with GHM_CPU_ALL_CORES=1
+        out["all_cores"] = {"value": None, "cores": host_cpus,
+                            "sample": "not run (GHM_CPU_ALL_CORES=1 runs it): os.cpu_count() threads oversubscribe "
+                                      f"the job's {share}-CPU share"}
     torch.set_num_threads(share)
     return out
 

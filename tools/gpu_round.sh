@@ -6,12 +6,14 @@ TAG=${1:-r1}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 ok() { r=$1; [ $r -eq 0 ] || [ $r -eq 1 ]; }
+if [ "$SKIP_TESTS" != "1" ]; then  # SKIP_TESTS=1: the benches and profiles only
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -rA --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $OUT/gpu_tests.log
 grep -E "^FAILED|^ERROR|passed|failed" $OUT/gpu_tests.log | tail -12
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 3
+fi
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
 cat $OUT/bench.json
 for w in vlm cdm cdm_joint cdm_guided vlm_joint; do
