@@ -218,6 +218,14 @@ def dominant_kernel(trainer):
         plan, pd = trainer.plan, trainer.pd
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    if plan.precision == "x3" and getattr(plan, "ln_presplit", False):
+        # the launch the step makes: the LN2 rows also written pre-split for dW1
+        def launch():
+            _native.call("ghm_ln_mlp_fwd_x3bs", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]),
+                         ptr(pd["_lns_2.0.bias"]), ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]),
+                         ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.st2[0]), ptr(plan.xs[0, 1]), plan.M, 128,
+                         512, plan.eps, sp)
+        return "k_ln_mlp_fwd_x3bs", launch
     if plan.precision == "x3":
         def launch():
             _native.call("ghm_ln_mlp_fwd_x3b", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
@@ -680,8 +688,8 @@ def main():
     samples = a.global_batch * a.steps
     step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
     scale = a.batch / 128
-    traffic = pmc_traffic(kname)
-    x3 = kname.endswith("x3b")
+    traffic = pmc_traffic(kname[:-1] if kname.endswith("x3bs") else kname)  # (the x3b passes when no x3bs pass)
+    x3 = kname.endswith("x3b") or kname.endswith("x3bs")
     # The kernel's work is 13.59 GFLOP (f32 products) per launch; the bytes that
     # MUST move are Hmid in and H out (the hidden activation never needs to leave
     # the chip): AI = 13.59e9 / 53.1e6 = 256 FLOP/B, so the roof is the matrix
@@ -836,7 +844,7 @@ def main_cdm(a, ws, rank):
     # graded on the matrix cores, as the CLIP line's MLP forward: 4 M D F f32-product
     # flops per launch, issued as 3 bf16 MFMA products each in x3 (vs the bf16 peak),
     # as exact-f32 MFMA products in f32 (vs the f32 MFMA peak)
-    x3 = kname.endswith("x3b")
+    x3 = kname.endswith("x3b") or kname.endswith("x3bs")
     mult, peak = (3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (1.0, F32_MFMA_PEAK_TFLOPS)
     kgflop = 4.0 * M * 128 * 512 / 1e9
     achieved = mult * kgflop / (kern_ms * 1e-3) / 1e3

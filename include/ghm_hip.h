@@ -211,6 +211,11 @@ int ghm_split_weights(const ghm_split_job* jobs, int n_jobs, void* stream);
 /* As ghm_ln_qkv_fwd (model.py:772-775). */
 int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, const void* pack, float* qkv,
                       float* stats, int64_t M, int D, float eps, void* stream);
+/* ghm_ln_qkv_fwd_x3 that also writes the split LN1 rows it multiplies as bf16
+ * (hi, lo) planes xs [2][M][128] (the B operand of ghm_wgrad_x3p for dWq|k|v;
+ * round 6)  —  model.py:772-775. */
+int ghm_ln_qkv_fwd_x3s(const float* H, const float* ln_w, const float* ln_b, const void* pack, float* qkv,
+                       float* stats, void* xs, int64_t M, int D, float eps, void* stream);
 /* LN2 + MLP + residual forward of one layer (as ghm_ln_mlp_fwd, model.py:741-747,
  * 784-788) on split-bf16 products, 16 tokens per wave (v_mfma_f32_16x16x32_bf16);
  * b1 [512], b2 [128] stay f32.  Only H_out and the LN2 stats leave the chip: the
@@ -218,6 +223,11 @@ int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float* ln_b, cons
 int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                        const float* b1, const float* b2, float* H_out, float* stats, int64_t M, int D, int F,
                        float eps, void* stream);
+/* ghm_ln_mlp_fwd_x3b that also writes the split LN2 rows as bf16 (hi, lo) planes
+ * xs [2][M][128] (the B operand of ghm_wgrad_x3p for dW1; round 6). */
+int ghm_ln_mlp_fwd_x3bs(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                        const float* b1, const float* b2, float* H_out, float* stats, void* xs, int64_t M, int D,
+                        int F, float eps, void* stream);
 /* MLP + LN2 backward with the up-projection recomputed from H_mid and the LN2
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),
@@ -277,6 +287,12 @@ int ghm_attn_bwd_x3_act(const float* qkv, const float* P, const float* Pd, const
 int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
                  const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part, int64_t M,
                  int tok_per_split, void* stream);
+/* ghm_wgrad_x3 with B pre-split: Bp = the bf16 hi plane [M][ldb] of LN(x) written
+ * by ghm_ln_qkv_fwd_x3s / ghm_ln_mlp_fwd_x3bs, the lo plane bplane elements on (no
+ * LayerNorm transform, statistics or split in the kernel; round 6)  —  the
+ * nn.Linear weight / bias gradients of model.py:772-775, 784-788. */
+int ghm_wgrad_x3p(const float* A, int lda, int A_cols, const void* Bp, int ldb, int B_cols, int64_t bplane,
+                  float* part, float* bias_part, int64_t M, int tok_per_split, void* stream);
 /* Split-K weight (and bias) gradient partials of the encoder projections on an
  * LDS-DMA ring with producer / consumer waves (csrc/ghm_wgrad.hip):
  *   part[z][a][b] = sum_{m in split z} A[m][a] op(B)[m][b], bias_part[z][a] = sum A[m][a]

@@ -265,10 +265,12 @@ __device__ __forceinline__ f32x16 qkv_tile_x3(const __bf16* __restrict__ cb, __b
   return acc;
 }
 
+// xs (optional): the split LN1 rows also leave as bf16 (hi, lo) planes [M][128]
+// (lo plane M * 128 elements on) for the dWq|k|v weight gradient (k_wgrad_x3 MODE 3)
 __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
     const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
-    float eps) {
+    float eps, __bf16* __restrict__ xs) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PLANE];  // 2 buffers x (hi, lo)
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
   const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
@@ -283,6 +285,14 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
     float mean = 0.f, rstd = 0.f;
     ln_row_split(H + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
     if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+    if (xs && active && valid) {  // features 64 h + 8 t .. + 7: 8 chunks per plane
+      __bf16* xr = xs + m * GHM_D + 64 * h;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        *reinterpret_cast<bf16x8*>(xr + 8 * t) = xh[t];
+        *reinterpret_cast<bf16x8*>(xr + M * GHM_D + 8 * t) = xl[t];
+      }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   f32x16 prev = zero16();
@@ -319,11 +329,13 @@ __device__ __forceinline__ float pick16(const float4* b4, int g, int r) {
 // the CLIP's 51,840 tokens.  Only H_out (and the LN statistics) leave the chip:
 // the backward recomputes U (k_mlp_bwd_rc_x3), 2 x [M,128] of HBM traffic
 // instead of 2 x [M,128] + 2 x [M,512] with G and GELU'(U) saved.
+// xs (optional): the split LN2 rows also leave as bf16 (hi, lo) planes [M][128] (lo
+// plane M * 128 elements on) for the dW1 weight gradient (k_wgrad_x3 MODE 3)
 template <int NW>
 __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const float* __restrict__ b1, const float* __restrict__ b2,
-    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
+    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps, __bf16* __restrict__ xs) {
   // ONE __shared__ object: [W1 hi|lo][W2 hi|lo] x 2 buffers, then b1 (f32).  The
   // chunk's b1 values are read at the top of the iteration, before its LDS-DMA
   // fills: any LDS read issued after them gets an s_waitcnt vmcnt(0) on the new
@@ -382,6 +394,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
         x[8 * s2 + i] = (x[8 * s2 + i] - mean) * rstd * lnw[f] + lnb[f];
       }
       split8(x + 8 * s2, xh[s2], xl[s2]);
+    }
+    if (xs && valid) {  // features 32 s2 + 8 g .. + 7: 4 chunks per plane
+      __bf16* xr = xs + m * GHM_D + 8 * g;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        *reinterpret_cast<bf16x8*>(xr + 32 * s2) = xh[s2];
+        *reinterpret_cast<bf16x8*>(xr + M * GHM_D + 32 * s2) = xl[s2];
+      }
     }
   }
   // the residual and b2 seed the accumulators (H = Hmid + b2 + sum_c W2[:, c] G_c):
@@ -835,7 +855,7 @@ __device__ __forceinline__ void store_g_du(const float* gv, const float* du, flo
 // WG_SPLIT operands, ghm_wgrad.hip): grow / drow point at the lane's 8 k-slots
 // 32c + 8g .. + 7 of the hi plane (perm32 column order, one 16-B store per plane),
 // the lo plane `plane` elements on; else f32 [M][512] rows at 32c + 4g
-template <bool SPLITOUT>
+template <int SPLITOUT>
 __device__ __forceinline__ void rc_ud(const __bf16* cb, const float4* bb, const bf16x8* xh, const bf16x8* xl,
                                       const bf16x8* yh, const bf16x8* yl, void* grow, void* drow, int64_t plane,
                                       int t, int g, bf16x8& dh, bf16x8& dl) {
@@ -867,7 +887,28 @@ __device__ __forceinline__ void rc_ud(const __bf16* cb, const float4* bb, const 
     }
   }
   split8(du, dh, dl);
-  if (SPLITOUT) {
+  if (SPLITOUT == 2) {
+    // G as bf16 (hi, lo) planes [M][512] in natural column order (the dW2 weight
+    // gradient's pre-split B operand, ghm_wgrad_x3p); dU stays f32.  grow points at
+    // units 32c + 4g of the hi plane: gv[4 jt + r] is unit 32c + 16 jt + 4g + r
+    bf16x8 gh, gl;
+    split8(gv, gh, gl);
+    __bf16* gp = static_cast<__bf16*>(grow);
+    bf16x4 a, b;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = gh[4 * jt + r];
+        b[r] = gl[4 * jt + r];
+      }
+      *reinterpret_cast<bf16x4*>(gp + 16 * jt) = a;
+      *reinterpret_cast<bf16x4*>(gp + 16 * jt + plane) = b;
+    }
+    float* drw = static_cast<float*>(drow);
+    st4(drw, du[0], du[1], du[2], du[3]);
+    st4(drw + 16, du[4], du[5], du[6], du[7]);
+  } else if (SPLITOUT) {
     bf16x8 gh, gl;
     split8(gv, gh, gl);
     __bf16* gp = static_cast<__bf16*>(grow);
@@ -901,7 +942,7 @@ __device__ __forceinline__ void rc_dx2(const __bf16* cb, bf16x8 dh, bf16x8 dl, f
 // 4-7 one dX2 behind on a 3-buffer ring, so the two waves of a SIMD sit in
 // opposite MFMA / GELU phases (isolated 119 -> 124 us, step +1 %,
 // profiles/r3_ab5).
-template <int NW, bool SPLITOUT>
+template <int NW, int SPLITOUT>
 __device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
                                                 const __bf16* W1n, const __bf16* W2Tn, const float4* bb,
                                                 const bf16x8* xh, const bf16x8* xl, const bf16x8* yh,
@@ -928,7 +969,9 @@ __device__ __forceinline__ void mlp_bwd_rc_iter(const __bf16* __restrict__ cb, _
 // of each workgroup writes the 100 MHz constant clock (s_memrealtime) at its
 // start and after its last store to stamps[2 blockIdx.x + {0, 1}]; the launch
 // spans min(start) .. max(end).  Nothing else differs.
-template <int NW, int STAMP = 0, bool SPLITOUT = false>
+// SPLITOUT: 0 G / dU f32 (the default), 1 both as perm32 bf16 planes (the ring
+// weight gradients), 2 G as natural-order bf16 planes, dU f32 (ghm_wgrad_x3p dW2)
+template <int NW, int STAMP = 0, int SPLITOUT = 0>
 __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     const float* __restrict__ dHout, const float* __restrict__ Hmid, const float2* __restrict__ stats,
     const float* __restrict__ lnw, const float* __restrict__ lnb, const __bf16* pack, const float* __restrict__ b1,
@@ -997,10 +1040,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlp_bwd_rc_x3(
     for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
     issue_fence();
     const int cn = c + 1 < NC ? c + 1 : NC - 1;  // branch-free: the last iteration refills chunk NC-1
-    void* grow = SPLITOUT ? static_cast<void*>(reinterpret_cast<__bf16*>(Gout) + mc * GHM_F + 32 * c + 8 * g)
-                          : static_cast<void*>(Gout + mc * GHM_F + 32 * c + 4 * g);
-    void* drow = SPLITOUT ? static_cast<void*>(reinterpret_cast<__bf16*>(dU) + mc * GHM_F + 32 * c + 8 * g)
-                          : static_cast<void*>(dU + mc * GHM_F + 32 * c + 4 * g);
+    void* grow = SPLITOUT == 1 ? static_cast<void*>(reinterpret_cast<__bf16*>(Gout) + mc * GHM_F + 32 * c + 8 * g)
+                 : SPLITOUT == 2 ? static_cast<void*>(reinterpret_cast<__bf16*>(Gout) + mc * GHM_F + 32 * c + 4 * g)
+                                 : static_cast<void*>(Gout + mc * GHM_F + 32 * c + 4 * g);
+    void* drow = SPLITOUT == 1 ? static_cast<void*>(reinterpret_cast<__bf16*>(dU) + mc * GHM_F + 32 * c + 8 * g)
+                               : static_cast<void*>(dU + mc * GHM_F + 32 * c + 4 * g);
     mlp_bwd_rc_iter<NW, SPLITOUT>(lds + 4 * PLANE * cur, lds + 4 * PLANE * (cur ^ 1), W1 + cn * 32 * GHM_D,
                                   W2T + cn * 32 * GHM_D, bb, xh, xl, yh, yl, dx, grow, drow, M * GHM_F, t, g, lane);
     // retire this iteration's LDS-DMA fills: vmcnt(0), also covering the G / dU
@@ -1460,6 +1504,12 @@ __device__ __forceinline__ int wg_img(int row, int ch) { return row * 32 + 8 * (
 // three products), 0 = the run-time lda / ldb.  A step whose 32 tokens are all
 // valid (every step but a split's last) then loads with constant row offsets
 // (folded into the loads' immediate offsets) and skips the token clamps and mask.
+// MODE 3 (round 6): B arrives pre-split -- the bf16 (hi, lo) planes [M][ldb] of
+// LN(x) that the forward kernel wrote beside its own split (k_ln_qkv_fwd_x3 /
+// k_ln_mlp_fwd_x3b `xs`), the lo plane bplane elements after the hi plane.  A
+// thread stages two columns x 8 tokens of B from dword loads (one per row: the
+// column pair's hi or lo halves) and repacks them with v_perm into the same
+// [column][token] chunks: no LayerNorm transform, no statistics, no split.
 template <int MODE, int NWV = 4, int LDA = 0, int LDB = 0>
 __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __restrict__ A, int lda,
                                                      const float* __restrict__ Bs, int ldb,
@@ -1468,7 +1518,8 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
                                                      const float* __restrict__ lnb,
                                                      float* __restrict__ part,
                                                      float* __restrict__ bias_part, int64_t M,
-                                                     int tok_per_split, int Acols, int Bcols) {
+                                                     int tok_per_split, int Acols, int Bcols, int64_t bplane) {
+  static_assert(MODE != 3 || NWV == 4, "pre-split B: 4 waves (a wave stages 8 tokens of 128 columns)");
   constexpr int KT = 32, IMG = 128 * 32;
   __shared__ __attribute__((aligned(16))) __bf16 sAh[2][IMG];
   __shared__ __attribute__((aligned(16))) __bf16 sAl[2][IMG];
@@ -1520,6 +1571,7 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
   // well under the loaded HBM latency).
   struct Slot {
     float va[TPT], vb[TPT];
+    uint32_t ph[8], pl[8];  // MODE 3: rows 8 tg .. 8 tg + 7 of the column pair, hi / lo planes
     float2 st;  // MODE 2: LayerNorm statistics of the slot's row (lane & (TPT - 1))
     int nvalid;
   };
@@ -1534,18 +1586,49 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
   const auto rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bs), static_cast<short>(0),
                                                      0x7fffffff, 0x00020000);
   const int voa = 4 * ca, vob = 4 * cb;
+  // MODE 3: thread (c2, tg) stages columns b_blk + 2 c2, + 1 of tokens 8 tg .. 8 tg + 7
+  const int c2 = threadIdx.x & 63, tg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const auto rsBh = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bs), static_cast<short>(0), 0x7fffffff,
+                                                      0x00020000);
+  const auto rsBl = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(reinterpret_cast<const __bf16*>(Bs) + (MODE == 3 ? bplane : 0)), static_cast<short>(0),
+      0x7fffffff, 0x00020000);
+  const int vop = 2 * (b_blk + 2 * c2);  // byte offset of the column pair in a bf16 row
+  auto load_p = [&](Slot& S, int step) {
+    // rows past the split re-read its last row (finite values; their A rows are zeroed)
+    const int64_t r0 = m_begin + static_cast<int64_t>(step) * KT + 8 * tg;  // uniform
+    const int64_t rl = m_end - 1;
+    if (LDB > 0 && r0 + 7 <= rl) {
+      const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * LDB * 2));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        S.ph[i] = __builtin_amdgcn_raw_buffer_load_b32(rsBh, vop + i * LDB * 2, sb, 0);
+        S.pl[i] = __builtin_amdgcn_raw_buffer_load_b32(rsBl, vop + i * LDB * 2, sb, 0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t r = r0 + i <= rl ? r0 + i : rl;
+      const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r * ldb * 2));
+      S.ph[i] = __builtin_amdgcn_raw_buffer_load_b32(rsBh, vop, sb, 0);
+      S.pl[i] = __builtin_amdgcn_raw_buffer_load_b32(rsBl, vop, sb, 0);
+    }
+  };
   auto load = [&](Slot& S, int step) {
     const int64_t mb = m_begin + static_cast<int64_t>(step) * KT + TPT * th;  // uniform
     const int64_t left = m_end - mb;
     S.nvalid = left < 0 ? 0 : (left > TPT ? TPT : static_cast<int>(left));
+    if constexpr (MODE == 3) load_p(S, step);
     if (LDA > 0 && LDB > 0 && __builtin_amdgcn_readfirstlane(S.nvalid) == TPT) {
       if (MODE == 2) S.st = ld_stats_sys(stats, mb + (lane & (TPT - 1)));
       const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(mb * LDA * 4));
-      const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(mb * LDB * 4));
+      const int sb = MODE == 3 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(mb * LDB * 4));
 #pragma unroll
       for (int i = 0; i < TPT; ++i) {
         S.va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, voa + i * LDA * 4, sa, 0));
-        S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob + i * LDB * 4, sb, 0));
+        if constexpr (MODE != 3)
+          S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob + i * LDB * 4, sb, 0));
       }
       issue_fence();
       return;
@@ -1558,12 +1641,13 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
       S.st = ld_stats_sys(stats, r0 + (li < nv ? li : nv - 1));
     }
     const int sa = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * lda * 4));
-    const int sb = __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * ldb * 4));
+    const int sb = MODE == 3 ? 0 : __builtin_amdgcn_readfirstlane(static_cast<int>(r0 * ldb * 4));
 #pragma unroll
     for (int i = 0; i < TPT; ++i) {
       const int ri = i < nv ? i : nv - 1;  // uniform
       S.va[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, voa, sa + ri * lda * 4, 0));
-      S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob, sb + ri * ldb * 4, 0));
+      if constexpr (MODE != 3)
+        S.vb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsB, vob, sb + ri * ldb * 4, 0));
     }
     issue_fence();
   };
@@ -1586,12 +1670,32 @@ __global__ __launch_bounds__(64 * NWV, 8 / NWV) void k_wgrad_x3(const float* __r
     for (int half = 0; half < TPT / 8; ++half) {
       bf16x8 ah, al, bh, bl;
       split8(S.va + 8 * half, ah, al);
-      split8(S.vb + 8 * half, bh, bl);
       const int off = wg_img(c, (TPT / 8) * th + half);
       *reinterpret_cast<bf16x8*>(sAh[buf] + off) = ah;
       *reinterpret_cast<bf16x8*>(sAl[buf] + off) = al;
-      *reinterpret_cast<bf16x8*>(sBh[buf] + off) = bh;
-      *reinterpret_cast<bf16x8*>(sBl[buf] + off) = bl;
+      if constexpr (MODE != 3) {
+        split8(S.vb + 8 * half, bh, bl);
+        *reinterpret_cast<bf16x8*>(sBh[buf] + off) = bh;
+        *reinterpret_cast<bf16x8*>(sBl[buf] + off) = bl;
+      }
+    }
+    if constexpr (MODE == 3) {
+      // dword i = (column 2 c2, column 2 c2 + 1) of token 8 tg + i: the even column's
+      // 8 tokens are the low halves, the odd column's the high halves
+      uint4 eh, oh, el, ol;
+      uint32_t* e_h = &eh.x; uint32_t* o_h = &oh.x; uint32_t* e_l = &el.x; uint32_t* o_l = &ol.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        e_h[k] = __builtin_amdgcn_perm(S.ph[2 * k + 1], S.ph[2 * k], 0x05040100u);
+        o_h[k] = __builtin_amdgcn_perm(S.ph[2 * k + 1], S.ph[2 * k], 0x07060302u);
+        e_l[k] = __builtin_amdgcn_perm(S.pl[2 * k + 1], S.pl[2 * k], 0x05040100u);
+        o_l[k] = __builtin_amdgcn_perm(S.pl[2 * k + 1], S.pl[2 * k], 0x07060302u);
+      }
+      const int oe = wg_img(2 * c2, tg), oo = wg_img(2 * c2 + 1, tg);
+      *reinterpret_cast<uint4*>(sBh[buf] + oe) = eh;
+      *reinterpret_cast<uint4*>(sBh[buf] + oo) = oh;
+      *reinterpret_cast<uint4*>(sBl[buf] + oe) = el;
+      *reinterpret_cast<uint4*>(sBl[buf] + oo) = ol;
     }
 #pragma unroll
     for (int i = 0; i < TPT; ++i) bsum += S.va[i];
@@ -2310,7 +2414,18 @@ extern "C" int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float*
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
   hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
                      ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), qkv,
-                     reinterpret_cast<float2*>(stats), M, eps);
+                     reinterpret_cast<float2*>(stats), M, eps, nullptr);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_qkv_fwd_x3s(const float* H, const float* ln_w, const float* ln_b, const void* pack, float* qkv,
+                                  float* stats, void* xs, int64_t M, int D, float eps, void* stream) {
+  GHM_CHECK(H && ln_w && ln_b && pack && qkv && stats && xs, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  GHM_CHECK((reinterpret_cast<uintptr_t>(xs) & 15) == 0, "16-byte aligned xs");
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), qkv,
+                     reinterpret_cast<float2*>(stats), M, eps, static_cast<__bf16*>(xs));
   return ghm_launch_status();
 }
 
@@ -2320,7 +2435,7 @@ extern "C" int64_t ghm_mlp_bwd_rc_x3_blocks(int64_t M) {
   return (M + tok - 1) / tok;
 }
 
-template <int NW, int STAMP, bool SPLITOUT>
+template <int NW, int STAMP, int SPLITOUT>
 static void mlp_bwd_rc_launch(unsigned nblk, hipStream_t s, const float* dH_out, const float* H_mid,
                               const float* stats, const float* ln_w, const float* ln_b, const void* pack,
                               const float* b1, void* G, void* dU, float* dH_mid, float* part_ln, int64_t M,
@@ -2336,15 +2451,19 @@ static void mlp_bwd_rc_dispatch(int64_t M, int split_out, hipStream_t s, const f
                                 uint64_t* stamps) {
   const unsigned nblk = static_cast<unsigned>(ghm_mlp_bwd_rc_x3_blocks(M));
   if (rc_waves(M) == 8) {
-    if (split_out)
-      mlp_bwd_rc_launch<8, STAMP, true>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    if (split_out == 1)
+      mlp_bwd_rc_launch<8, STAMP, 1>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    else if (split_out == 2)
+      mlp_bwd_rc_launch<8, STAMP, 2>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
     else
-      mlp_bwd_rc_launch<8, STAMP, false>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+      mlp_bwd_rc_launch<8, STAMP, 0>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
   } else {
-    if (split_out)
-      mlp_bwd_rc_launch<4, STAMP, true>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    if (split_out == 1)
+      mlp_bwd_rc_launch<4, STAMP, 1>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+    else if (split_out == 2)
+      mlp_bwd_rc_launch<4, STAMP, 2>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
     else
-      mlp_bwd_rc_launch<4, STAMP, false>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
+      mlp_bwd_rc_launch<4, STAMP, 0>(nblk, s, dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid, part_ln, M, stamps);
   }
 }
 
@@ -2355,7 +2474,7 @@ extern "C" int ghm_mlp_bwd_rc_x3(const float* dH_out, const float* H_mid, const 
   GHM_CHECK(dH_out && H_mid && stats && ln_w && ln_b && pack && b1 && G && dU && dH_mid && part_ln, "null pointer");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  GHM_CHECK(split_out == 0 || split_out == 1, "split_out");
+  GHM_CHECK(split_out >= 0 && split_out <= 2, "split_out (0 f32, 1 perm32 planes, 2 natural G planes + f32 dU)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
   mlp_bwd_rc_dispatch<0>(M, split_out, ghm_stream(stream), dH_out, H_mid, stats, ln_w, ln_b, pack, b1, G, dU, dH_mid,
                          part_ln, nullptr);
@@ -2372,7 +2491,7 @@ extern "C" int ghm_mlp_bwd_rc_x3_stamped(const float* dH_out, const float* H_mid
             "null pointer");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
   GHM_CHECK(M < (int64_t(1) << 28), "stats byte offsets must fit 31 bits (M < 2^28 tokens)");
-  GHM_CHECK(split_out == 0 || split_out == 1, "split_out");
+  GHM_CHECK(split_out >= 0 && split_out <= 2, "split_out (0 f32, 1 perm32 planes, 2 natural G planes + f32 dU)");
   GHM_CHECK(dH_mid != dH_out, "dH_mid must not alias dH_out (it is the residual input)");
   GHM_CHECK(twin == 1 || twin == 2, "twin must be 1 or 2");
   hipStream_t s = ghm_stream(stream);
@@ -2432,14 +2551,34 @@ extern "C" int ghm_qkv_bwd_x3_probe(const float* dqkv, const float* H, const flo
   return ghm_launch_status();
 }
 
+static int wgrad_x3_launch(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
+                           const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part,
+                           int64_t M, int tok_per_split, int64_t bplane, void* stream);
+
 extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
                             const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part,
                             int64_t M, int tok_per_split, void* stream) {
+  GHM_CHECK(b_mode == 0 || b_mode == 2, "b_mode (split path: 0 plain, 2 layernorm; 3: ghm_wgrad_x3p)");
+  return wgrad_x3_launch(A, lda, A_cols, B, ldb, B_cols, b_mode, stats, ln_w, ln_b, part, bias_part, M, tok_per_split,
+                         0, stream);
+}
+
+extern "C" int ghm_wgrad_x3p(const float* A, int lda, int A_cols, const void* Bp, int ldb, int B_cols, int64_t bplane,
+                             float* part, float* bias_part, int64_t M, int tok_per_split, void* stream) {
+  GHM_CHECK(Bp && bplane >= M * ldb, "pre-split B: hi plane [M][ldb] bf16, lo plane bplane elements on");
+  GHM_CHECK((reinterpret_cast<uintptr_t>(Bp) & 3) == 0 && ldb % 2 == 0, "4-byte aligned bf16 column pairs");
+  GHM_CHECK(M * ldb * 2 + 2 * bplane < (int64_t(1) << 31), "planes must fit a 31-bit byte range");
+  return wgrad_x3_launch(A, lda, A_cols, static_cast<const float*>(Bp), ldb, B_cols, 3, nullptr, nullptr, nullptr,
+                         part, bias_part, M, tok_per_split, bplane, stream);
+}
+
+static int wgrad_x3_launch(const float* A, int lda, int A_cols, const float* B, int ldb, int B_cols, int b_mode,
+                           const float* stats, const float* ln_w, const float* ln_b, float* part, float* bias_part,
+                           int64_t M, int tok_per_split, int64_t bplane, void* stream) {
   GHM_CHECK(A && B && part, "null pointer");
   GHM_CHECK(A_cols > 0 && B_cols > 0 && A_cols % 128 == 0 && B_cols % 128 == 0, "A_cols/B_cols % 128");
   GHM_CHECK(lda >= A_cols && ldb >= B_cols && M >= 1, "shape");
   GHM_CHECK(tok_per_split > 0 && tok_per_split % 32 == 0, "tok_per_split must be a positive multiple of 32");
-  GHM_CHECK(b_mode == 0 || b_mode == 2, "b_mode (split path: 0 plain, 2 layernorm)");
   GHM_CHECK(M * lda * 4 < (int64_t(1) << 31) && M * ldb * 4 < (int64_t(1) << 31),
             "operands must fit a 31-bit byte range (buffer-load row offsets)");
   GHM_CHECK(b_mode != 2 || (stats && ln_w && ln_b), "layernorm mode needs stats/ln_w/ln_b");
@@ -2448,28 +2587,41 @@ extern "C" int ghm_wgrad_x3(const float* A, int lda, int A_cols, const float* B,
   dim3 grid(A_cols / 128, B_cols / 128, static_cast<unsigned>(nsplit));
   hipStream_t s = ghm_stream(stream);
   const float2* st = reinterpret_cast<const float2*>(stats);
-  if (GHM_WGRAD_WAVES == 8) {
+  if (b_mode == 3) {  // pre-split B (LN1 / LN2 outputs of the forward, or G), 4 waves
+    if (GHM_WGRAD_FAST && lda == GHM_D && ldb == GHM_F)  // dW2 (G from the MLP backward, split_out 2)
+      hipLaunchKernelGGL((k_wgrad_x3<3, 4, GHM_D, GHM_F>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
+                         bias_part, M, tok_per_split, A_cols, B_cols, bplane);
+    else if (GHM_WGRAD_FAST && lda == GHM_F && ldb == GHM_D)  // dW1
+      hipLaunchKernelGGL((k_wgrad_x3<3, 4, GHM_F, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
+                         bias_part, M, tok_per_split, A_cols, B_cols, bplane);
+    else if (GHM_WGRAD_FAST && lda == 3 * GHM_D && ldb == GHM_D)  // dWq|k|v
+      hipLaunchKernelGGL((k_wgrad_x3<3, 4, 3 * GHM_D, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b,
+                         part, bias_part, M, tok_per_split, A_cols, B_cols, bplane);
+    else
+      hipLaunchKernelGGL(k_wgrad_x3<3>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
+                         tok_per_split, A_cols, B_cols, bplane);
+  } else if (GHM_WGRAD_WAVES == 8) {
     if (b_mode == 0)
       hipLaunchKernelGGL((k_wgrad_x3<0, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part,
-                         M, tok_per_split, A_cols, B_cols);
+                         M, tok_per_split, A_cols, B_cols, 0);
     else
       hipLaunchKernelGGL((k_wgrad_x3<2, 8>), grid, dim3(512), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part,
-                         M, tok_per_split, A_cols, B_cols);
+                         M, tok_per_split, A_cols, B_cols, 0);
   } else if (GHM_WGRAD_FAST && b_mode == 0 && lda == GHM_D && ldb == GHM_F) {  // dW2
     hipLaunchKernelGGL((k_wgrad_x3<0, 4, GHM_D, GHM_F>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
-                       bias_part, M, tok_per_split, A_cols, B_cols);
+                       bias_part, M, tok_per_split, A_cols, B_cols, 0);
   } else if (GHM_WGRAD_FAST && b_mode == 2 && lda == GHM_F && ldb == GHM_D) {  // dW1
     hipLaunchKernelGGL((k_wgrad_x3<2, 4, GHM_F, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part,
-                       bias_part, M, tok_per_split, A_cols, B_cols);
+                       bias_part, M, tok_per_split, A_cols, B_cols, 0);
   } else if (GHM_WGRAD_FAST && b_mode == 2 && lda == 3 * GHM_D && ldb == GHM_D) {  // dWq|k|v
     hipLaunchKernelGGL((k_wgrad_x3<2, 4, 3 * GHM_D, GHM_D>), grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b,
-                       part, bias_part, M, tok_per_split, A_cols, B_cols);
+                       part, bias_part, M, tok_per_split, A_cols, B_cols, 0);
   } else if (b_mode == 0) {
     hipLaunchKernelGGL(k_wgrad_x3<0>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
-                       tok_per_split, A_cols, B_cols);
+                       tok_per_split, A_cols, B_cols, 0);
   } else {
     hipLaunchKernelGGL(k_wgrad_x3<2>, grid, dim3(256), 0, s, A, lda, B, ldb, st, ln_w, ln_b, part, bias_part, M,
-                       tok_per_split, A_cols, B_cols);
+                       tok_per_split, A_cols, B_cols, 0);
   }
   return ghm_launch_status();
 }
@@ -2601,7 +2753,7 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
   const int ws = ws_env ? std::atoi(ws_env) : 0;
   if (big && ws == 4)  // the plain schedule at 16 waves / 256 tokens: half the weight streaming per token
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<16>, dim3(static_cast<unsigned>((M + 255) / 256)), dim3(1024), 0, s, H_mid,
-                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps, nullptr);
   else if (big && ws == 3)  // 8 waves at <= 256 VGPRs: one workgroup per CU, deeper operand prefetch
     hipLaunchKernelGGL((k_ln_mlp_fwd_x3w<8, 2>), g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
   else if (big && ws == 2)
@@ -2610,8 +2762,29 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
   else if (big && ws)
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3w<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
   else if (big)
-    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, g8, dim3(512), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps,
+                       nullptr);
   else
-    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps);
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps,
+                       nullptr);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_mlp_fwd_x3bs(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                                   const float* b1, const float* b2, float* H_out, float* stats, void* xs, int64_t M,
+                                   int D, int F, float eps, void* stream) {
+  GHM_CHECK(H_mid && ln_w && ln_b && pack && b1 && b2 && H_out && stats && xs, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  GHM_CHECK((reinterpret_cast<uintptr_t>(xs) & 15) == 0, "16-byte aligned xs");
+  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
+  float2* st = reinterpret_cast<float2*>(stats);
+  hipStream_t s = ghm_stream(stream);
+  __bf16* x = static_cast<__bf16*>(xs);
+  if ((M + 127) / 128 >= 256)
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<8>, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0, s, H_mid,
+                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps, x);
+  else
+    hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, dim3(static_cast<unsigned>((M + 63) / 64)), dim3(256), 0, s, H_mid,
+                       ln_w, ln_b, pk, b1, b2, H_out, st, M, eps, x);
   return ghm_launch_status();
 }

@@ -55,6 +55,7 @@ def make_encoder_plan(n_layer, n_token, n_seq, n_embd=128, **kw):
     if n_embd == 128:
         return EncoderPlan(n_layer, n_token, n_seq, n_embd=n_embd, **kw)
     kw.pop("defer_reduce", None)
+    kw.pop("ln_presplit", None)
     kw.pop("wgrad_target_blocks", None)
     kw.pop("wgrad_min_tokens", None)
     return GemmEncoderPlan(n_layer, n_token, n_seq, n_embd=n_embd, **kw)

@@ -95,8 +95,13 @@ def require_hip(t):
 class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", wgrad_target_blocks=256, precision=None,
-                 wgrad_min_tokens=None, defer_reduce=False, activation="softmax"):
-        """defer_reduce: every layer keeps its own parameter-gradient partial
+                 wgrad_min_tokens=None, defer_reduce=False, activation="softmax", ln_presplit=None):
+        """ln_presplit (x3; default on, $GHM_LN_PRESPLIT=0 off; False for encoders that
+        only run forward): the LN1 / LN2 forwards also write the split rows they
+        multiply as bf16 (hi, lo) planes, which the dWq|k|v / dW1 weight gradients
+        then read directly (ghm_wgrad_x3p) instead of re-normalising and splitting
+        H / Hmid per tile.
+        defer_reduce: every layer keeps its own parameter-gradient partial
         buffers and backward() reduces all of them at its end in batched launches
         of up to 32 jobs (2 launches per encoder instead of one per layer), as a
         fully parallel, bandwidth-bound pass instead of L short latency-bound ones."""
@@ -222,6 +227,17 @@ class EncoderPlan:
         if self.precision == "x3":
             npk = int(_native.GHM_SPLIT_PACK_ELEMS)
             self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
+        # pre-split LN outputs: xs[l][0] = LN1(H_l), xs[l][1] = LN2(Hmid_l), each the hi
+        # plane [M][128] then the lo plane (bf16: the bytes of one f32 plane)
+        if ln_presplit is None:
+            ln_presplit = os.environ.get("GHM_LN_PRESPLIT", "1") == "1"
+        self.ln_presplit = bool(ln_presplit) and self.precision == "x3"
+        # G for dW2 as natural-order bf16 planes from the MLP backward (split_out 2,
+        # ghm_wgrad_x3p): $GHM_G_PRESPLIT=1 (x3, not with the ring weight gradients)
+        self.g_presplit = (self.ln_presplit and not self.wgrad_ring
+                           and os.environ.get("GHM_G_PRESPLIT", "0") == "1")
+        self.xs = (torch.empty(L, 2, 2, M, D_MODEL, dtype=torch.bfloat16, device=dev) if self.ln_presplit
+                   else None)
         self._gen = 0
 
     def mlp_scratch_f32(self, name="G"):
@@ -229,6 +245,9 @@ class EncoderPlan:
         order (inspection / tests): the ring path stores them as bf16 hi / lo
         planes with the columns of each 32-group in perm32 order."""
         t = getattr(self, name)
+        if name == "G" and getattr(self, "g_presplit", False):  # natural-order (hi, lo) planes
+            planes = t.view(torch.bfloat16).view(2, self.M, D_HIDDEN).float()
+            return planes[0] + planes[1]
         if not self.wgrad_ring:
             return t
         planes = t.view(torch.bfloat16).view(2, self.M, D_HIDDEN).float()
@@ -282,12 +301,21 @@ class EncoderPlan:
         if True:
             if x3:
                 pk = _ptr(self.pack[l])
-                c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
-                  pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
+                if self.ln_presplit:
+                    c("ghm_ln_qkv_fwd_x3s", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+                      _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), _ptr(self.xs[l, 0]), M,
+                      D_MODEL, self.eps, s)
+                else:
+                    c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+                      _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
                 self._attn_fwd(l, s)
-                c("ghm_ln_mlp_fwd_x3b", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]),
-                  _ptr(p[f"_lns_2.{l}.bias"]), pk, _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]),
-                  _ptr(self.H[l + 1]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+                mlp_args = (_ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), pk,
+                            _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]),
+                            _ptr(self.st2[l]))
+                if self.ln_presplit:
+                    c("ghm_ln_mlp_fwd_x3bs", *mlp_args, _ptr(self.xs[l, 1]), M, D_MODEL, D_HIDDEN, self.eps, s)
+                else:
+                    c("ghm_ln_mlp_fwd_x3b", *mlp_args, M, D_MODEL, D_HIDDEN, self.eps, s)
                 return
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
@@ -537,7 +565,7 @@ class EncoderPlan:
                 args = (_ptr(cur), _ptr(self.Hmid[l]), _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                         _ptr(p[f"_lns_2.{l}.bias"]), _ptr(self.pack[l]), _ptr(p[f"_mlps.{l}.0.bias"]),
                         _ptr(self.G), _ptr(self.dU), _ptr(nxt), _ptr(P_ln2), M, D_MODEL, D_HIDDEN,
-                        int(self.wgrad_ring))
+                        2 if self.g_presplit else int(self.wgrad_ring))
                 if getattr(self, "stamps", None) is not None:  # bench.py's in-graph timing
                     c("ghm_mlp_bwd_rc_x3_stamped", *args, _ptr(self.stamps[l]), self.stamp_twin, s)
                 else:
@@ -549,7 +577,10 @@ class EncoderPlan:
             nb2 = self.nblk_rc if (x3 and self.mlp_rc) else self.nblk
             jobs.append(J(P_ln2, nb2, [g[f"_lns_2.{l}.weight"], g[f"_lns_2.{l}.bias"]]))
             tps, ns = self.wg["w2"]  # dW2[o][hid] = sum dY[m][o] G[m][hid]; db2 = sum dY
-            if self.wgrad_ring:  # dY f32 (format 0) x G pre-split (format 2)
+            if self.g_presplit:  # dY f32 x G as the MLP backward split it (natural order)
+                c("ghm_wgrad_x3p", _ptr(cur), D_MODEL, D_MODEL, _ptr(self.G), D_HIDDEN, D_HIDDEN, M * D_HIDDEN,
+                  _ptr(P_w2), _ptr(P_b2), M, tps, s)
+            elif self.wgrad_ring:  # dY f32 (format 0) x G pre-split (format 2)
                 c("ghm_wgrad_ring_x3", _ptr(cur), D_MODEL, D_MODEL, 0, 0, _ptr(self.G), D_HIDDEN, D_HIDDEN, 2,
                   M * D_HIDDEN, None, None, None, _ptr(P_w2), _ptr(P_b2), M, tps, s)
             else:
@@ -561,6 +592,9 @@ class EncoderPlan:
                 c("ghm_wgrad_ring_x3", _ptr(self.dU), D_HIDDEN, D_HIDDEN, 2, M * D_HIDDEN, _ptr(self.Hmid[l]),
                   D_MODEL, D_MODEL, 1, 0, _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]),
                   _ptr(p[f"_lns_2.{l}.bias"]), _ptr(P_w1), _ptr(P_b1), M, tps, s)
+            elif x3 and self.ln_presplit:  # dU (f32) x LN2(Hmid) as the forward split it
+                c("ghm_wgrad_x3p", _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.xs[l, 1]), D_MODEL, D_MODEL,
+                  M * D_MODEL, _ptr(P_w1), _ptr(P_b1), M, tps, s)
             else:
                 c(wgrad, _ptr(self.dU), D_HIDDEN, D_HIDDEN, _ptr(self.Hmid[l]), D_MODEL, D_MODEL, 2,
                   _ptr(self.st2[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
@@ -573,6 +607,9 @@ class EncoderPlan:
                 c("ghm_wgrad_ring_x3", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, 0, 0, _ptr(self.H[l]), D_MODEL,
                   D_MODEL, 1, 0, _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
                   _ptr(P_wq), None, M, tps, s)
+            elif x3 and self.ln_presplit:  # dqkv (f32) x LN1(H) as the forward split it
+                c("ghm_wgrad_x3p", _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.xs[l, 0]), D_MODEL, D_MODEL,
+                  M * D_MODEL, _ptr(P_wq), None, M, tps, s)
             else:
                 c(wgrad, _ptr(self.dqkv), 3 * D_MODEL, 3 * D_MODEL, _ptr(self.H[l]), D_MODEL, D_MODEL, 2,
                   _ptr(self.st1[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),

@@ -99,7 +99,7 @@ class CdmTrainer:
             self.clip_plan = make_encoder_plan(clip_model.n_layer, clip_model.n_token, batch_size,
                                          num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
                                          n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
-                                         device=self.device, precision=self.precision)
+                                         device=self.device, precision=self.precision, ln_presplit=False)
             if self.precision == "x3":
                 self.clip_plan.split_weights(self.clip_p)  # frozen: split once
             self.t_tok = self.clip_plan.tokens

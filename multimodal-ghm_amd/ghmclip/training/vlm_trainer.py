@@ -85,7 +85,7 @@ class VlmTrainer:
             self.clip_plan = make_encoder_plan(clip_model.n_layer, clip_model.n_token, batch_size,
                                          num_class=clip_model.vocab_size, vocab=clip_model.vocab_size,
                                          n_embd=clip_model.n_embd, normalize_attn=clip_model.normalize_attn,
-                                         device=self.device, precision=precision)
+                                         device=self.device, precision=precision, ln_presplit=False)
             self.precision = self.clip_plan.precision
             if self.precision == "x3":
                 self.clip_plan.split_weights(self.clip_p)  # frozen: split once

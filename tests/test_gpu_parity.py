@@ -321,6 +321,62 @@ def test_wgrad_stride_specialised_equals_generic(mode, acols, bcols, M, tps):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("acols", [512, 384])
+@pytest.mark.parametrize("M,tps", [(51840, 832), (1000, 96), (333, 64)])
+@pytest.mark.parametrize("ldb", [128, 160])
+def test_wgrad_presplit_b_equals_f32_b(acols, M, tps, ldb):
+    """ghm_wgrad_x3p (B from pre-split bf16 planes, k_wgrad_x3 MODE 3: dword loads
+    of column pairs repacked by v_perm) == ghm_wgrad_x3 b_mode 0 on the f32 values
+    those planes split (hi = bf16(b), lo = bf16(b - hi): the device split1), bit for
+    bit: weight and bias partials, compile-time (ldb = 128) and run-time strides,
+    ragged last splits."""
+    import ctypes
+    from ghmclip import _native
+    g = torch.Generator(device=DEV).manual_seed(M + acols + ldb)
+    A = torch.randn(M, acols, device=DEV, generator=g)
+    B = torch.randn(M, 128, device=DEV, generator=g) * 3
+    hi = B.bfloat16()
+    lo = (B - hi.float()).bfloat16()
+    planes = torch.zeros(2, M, ldb, dtype=torch.bfloat16, device=DEV)
+    planes[0, :, :128], planes[1, :, :128] = hi, lo
+    ns = -(-M // tps)
+    P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for pre in (False, True):
+        part = torch.full((ns * acols * 128,), float("nan"), device=DEV)
+        bias = torch.full((ns * acols,), float("nan"), device=DEV)
+        if pre:
+            _native.call("ghm_wgrad_x3p", P(A), acols, acols, P(planes), ldb, 128, M * ldb, P(part), P(bias), M,
+                         tps, s)
+        else:
+            _native.call("ghm_wgrad_x3", P(A), acols, acols, P(B), 128, 128, 0, None, None, None, P(part), P(bias),
+                         M, tps, s)
+        torch.cuda.synchronize()
+        outs.append((part, bias))
+    assert torch.isfinite(outs[0][0]).all() and torch.isfinite(outs[0][1]).all()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_forward_writes_the_split_ln_rows():
+    """ghm_ln_qkv_fwd_x3s / ghm_ln_mlp_fwd_x3bs: the (hi, lo) planes they write are
+    the split of LN(x) with the forward's own statistics (hi + lo within 2^-16 of
+    LN(x), relative to the plane's max)."""
+    sampler, tr = _trainer(2, 8, 0.2, precision="x3")
+    _run(sampler, tr, 8, 1)
+    plan, p = tr.plans[0], tr.views[0][0]
+    assert plan.ln_presplit and plan.xs is not None
+    plan.forward(p)  # with the weights as they are now (the step's AdamW moved the LN weights)
+    torch.cuda.synchronize()
+    for l in range(plan.L):
+        for which, X, st, w, b in ((0, plan.H[l], plan.st1[l], p[f"_lns_1.{l}.weight"], p[f"_lns_1.{l}.bias"]),
+                                   (1, plan.Hmid[l], plan.st2[l], p[f"_lns_2.{l}.weight"], p[f"_lns_2.{l}.bias"])):
+            ln = ((X.double() - st[:, :1].double()) * st[:, 1:].double() * w.double() + b.double())
+            hi, lo = plan.xs[l, which, 0].double(), plan.xs[l, which, 1].double()
+            err = ((hi + lo) - ln).abs().max().item() / ln.abs().max().item()
+            assert err < 2 ** -16, (l, which, err)
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_train_steps_vs_reference_fixture(precision):
     """Two full steps of the d=128, L=2, B=8 config against the reference's own
@@ -332,6 +388,30 @@ def test_train_steps_vs_reference_fixture(precision):
         assert abs(hist[it] - float(gfx[f"s{it}.loss"])) < 1e-5
     torch.cuda.synchronize()
     # post-step parameters vs reference checksums (sum of squares)
+    for pref, m in (("t", tr.tm), ("i", tr.im)):
+        for k, v in m.state_dict().items():
+            ck = gfx[f"s1.post.{pref}.{k}.cks"] if f"s1.post.{pref}.{k}.cks" in gfx else None
+            if ck is not None:
+                got = (v.double().cpu() ** 2).sum().item()
+                assert abs(got - ck[1]) <= 1e-5 * ck[1] + 1e-9, k
+
+
+@pytest.mark.parametrize("env", [{"GHM_LN_PRESPLIT": "0"}, {"GHM_G_PRESPLIT": "1"}])
+def test_train_steps_presplit_variants_vs_reference_fixture(env, monkeypatch):
+    """The x3 step with the weight-gradient operand variants of round 6 -- LN rows
+    re-normalised and split in the weight gradients (GHM_LN_PRESPLIT=0, the rounds
+    1-5 path) and G pre-split by the MLP backward (GHM_G_PRESPLIT=1) -- against the
+    reference's own two steps at the bounds of test_train_steps_vs_reference_fixture."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    gfx = np.load(os.path.join(GOLDEN, "clip_d128.npz"))
+    sampler, tr = _trainer(2, 8, 0.2, precision="x3")
+    assert tr.plans[0].ln_presplit == (env.get("GHM_LN_PRESPLIT", "1") == "1")
+    assert tr.plans[0].g_presplit == (env.get("GHM_G_PRESPLIT", "0") == "1")
+    hist = _run(sampler, tr, 8, 2)
+    for it in range(2):
+        assert abs(hist[it] - float(gfx[f"s{it}.loss"])) < 1e-5
+    torch.cuda.synchronize()
     for pref, m in (("t", tr.tm), ("i", tr.im)):
         for k, v in m.state_dict().items():
             ck = gfx[f"s1.post.{pref}.{k}.cks"] if f"s1.post.{pref}.{k}.cks" in gfx else None

@@ -132,6 +132,25 @@ def main():
             "wgrad_qkv_x3": (lambda: c("ghm_wgrad_x3", P(plan.dqkv), 384, 384, P(plan.H[l]), 128, 128, 2,
                                        P(plan.st1[l]), P(p["_lns_1.0.weight"]), P(p["_lns_1.0.bias"]),
                                        P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
+            # round 6: the weight gradients on the forward's pre-split LN outputs (ghm_wgrad_x3p),
+            # and the forward kernels that write them
+            "wgrad_w1_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dU), 512, 512, P(plan.xs[l, 1]), 128, 128, M * 128,
+                                       P(plan.part_w1), P(plan.part_b1), M, tps_w1, sp), gf(2 * M * 128 * 512)),
+            "wgrad_qkv_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dqkv), 384, 384, P(plan.xs[l, 0]), 128, 128, M * 128,
+                                        P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
+            "mlp_bwd_rc_x3g": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
+                                         P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
+                                         P(plan.G), P(plan.dU), P(xo["dHm"]), P(plan.part_ln2), M, 128, 512, 2, sp),
+                               gf(6 * M * 128 * 512)),
+            "wgrad_w2_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.H[l + 1]), 128, 128, P(plan.G), 512, 512, M * 512,
+                                       P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp), gf(2 * M * 128 * 512)),
+            "ln_qkv_fwd_x3s": (lambda: c("ghm_ln_qkv_fwd_x3s", P(plan.H[l]), P(p["_lns_1.0.weight"]),
+                                         P(p["_lns_1.0.bias"]), pk, P(plan.qkv[l]), P(plan.st1[l]), P(plan.xs[l, 0]),
+                                         M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
+            "ln_mlp_fwd_x3bs": (lambda: c("ghm_ln_mlp_fwd_x3bs", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                          P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
+                                          P(xo["H"]), P(xo["st"]), P(plan.xs[l, 1]), M, 128, 512, plan.eps, sp),
+                                gf(4 * M * 128 * 512)),
             # the ring weight gradients (ghm_wgrad_ring_x3) on the MLP backward's split G / dU planes
             "wgrad_ring_w2": (lambda: c("ghm_wgrad_ring_x3", P(plan.H[l + 1]), 128, 128, 0, 0, P(plan.G), 512, 512,
                                         2, M * 512, None, None, None, P(plan.part_w2), P(plan.part_b2), M, tps_w2,
