@@ -96,11 +96,12 @@ class EncoderPlan:
     def __init__(self, n_layer, n_token, n_seq, num_class=10, vocab=10, n_embd=128, eps=1e-5,
                  normalize_attn=True, device="cuda", wgrad_target_blocks=256, precision=None,
                  wgrad_min_tokens=None, defer_reduce=False, activation="softmax", ln_presplit=None):
-        """ln_presplit (x3; default on, $GHM_LN_PRESPLIT=0 off; False for encoders that
-        only run forward): the LN1 / LN2 forwards also write the split rows they
-        multiply as bf16 (hi, lo) planes, which the dWq|k|v / dW1 weight gradients
-        then read directly (ghm_wgrad_x3p) instead of re-normalising and splitting
-        H / Hmid per tile.
+        """ln_presplit (x3; $GHM_LN_PRESPLIT=1, default off): the LN1 / LN2 forwards
+        also write the split rows they multiply as bf16 (hi, lo) planes, which the
+        dWq|k|v / dW1 weight gradients then read directly (ghm_wgrad_x3p) instead of
+        re-normalising and splitting H / Hmid per tile.  Faster alone (dW1 44.1 ->
+        39.4, dWq|k|v 35.8 -> 31.5 us) and slower in the step (4.10 -> 4.20 ms: the
+        planes add 530 MB of writes per step, profiles/r6_lnps2_ab.txt).
         defer_reduce: every layer keeps its own parameter-gradient partial
         buffers and backward() reduces all of them at its end in batched launches
         of up to 32 jobs (2 launches per encoder instead of one per layer), as a
@@ -230,7 +231,7 @@ class EncoderPlan:
         # pre-split LN outputs: xs[l][0] = LN1(H_l), xs[l][1] = LN2(Hmid_l), each the hi
         # plane [M][128] then the lo plane (bf16: the bytes of one f32 plane)
         if ln_presplit is None:
-            ln_presplit = os.environ.get("GHM_LN_PRESPLIT", "1") == "1"
+            ln_presplit = os.environ.get("GHM_LN_PRESPLIT", "0") == "1"
         self.ln_presplit = bool(ln_presplit) and self.precision == "x3"
         # G for dW2 as natural-order bf16 planes from the MLP backward (split_out 2,
         # ghm_wgrad_x3p): $GHM_G_PRESPLIT=1 (x3, not with the ring weight gradients)

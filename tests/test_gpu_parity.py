@@ -358,10 +358,11 @@ def test_wgrad_presplit_b_equals_f32_b(acols, M, tps, ldb):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-def test_forward_writes_the_split_ln_rows():
+def test_forward_writes_the_split_ln_rows(monkeypatch):
     """ghm_ln_qkv_fwd_x3s / ghm_ln_mlp_fwd_x3bs: the (hi, lo) planes they write are
     the split of LN(x) with the forward's own statistics (hi + lo within 2^-16 of
     LN(x), relative to the plane's max)."""
+    monkeypatch.setenv("GHM_LN_PRESPLIT", "1")
     sampler, tr = _trainer(2, 8, 0.2, precision="x3")
     _run(sampler, tr, 8, 1)
     plan, p = tr.plans[0], tr.views[0][0]
@@ -396,17 +397,18 @@ def test_train_steps_vs_reference_fixture(precision):
                 assert abs(got - ck[1]) <= 1e-5 * ck[1] + 1e-9, k
 
 
-@pytest.mark.parametrize("env", [{"GHM_LN_PRESPLIT": "0"}, {"GHM_G_PRESPLIT": "1"}])
+@pytest.mark.parametrize("env", [{"GHM_LN_PRESPLIT": "1"}, {"GHM_LN_PRESPLIT": "1", "GHM_G_PRESPLIT": "1"}])
 def test_train_steps_presplit_variants_vs_reference_fixture(env, monkeypatch):
-    """The x3 step with the weight-gradient operand variants of round 6 -- LN rows
-    re-normalised and split in the weight gradients (GHM_LN_PRESPLIT=0, the rounds
-    1-5 path) and G pre-split by the MLP backward (GHM_G_PRESPLIT=1) -- against the
-    reference's own two steps at the bounds of test_train_steps_vs_reference_fixture."""
+    """The x3 step with the weight-gradient operand variants of round 6 (opt-in:
+    slower in the step) -- the LN rows pre-split
+    by the forward kernels (GHM_LN_PRESPLIT=1) and G pre-split by the MLP backward
+    (GHM_G_PRESPLIT=1) -- against the reference's own two steps at the bounds of
+    test_train_steps_vs_reference_fixture."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     gfx = np.load(os.path.join(GOLDEN, "clip_d128.npz"))
     sampler, tr = _trainer(2, 8, 0.2, precision="x3")
-    assert tr.plans[0].ln_presplit == (env.get("GHM_LN_PRESPLIT", "1") == "1")
+    assert tr.plans[0].ln_presplit == (env.get("GHM_LN_PRESPLIT", "0") == "1")
     assert tr.plans[0].g_presplit == (env.get("GHM_G_PRESPLIT", "0") == "1")
     hist = _run(sampler, tr, 8, 2)
     for it in range(2):
