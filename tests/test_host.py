@@ -342,6 +342,7 @@ def test_bench_finds_the_dominant_kernels_stamped_twin():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     assert b._rc_twin("k_mlp_bwd_rc_x3<8, 0, false>", 1) == "k_mlp_bwd_rc_x3<8, 1, false>"
+    assert b._rc_twin("k_mlp_bwd_rc_x3<8, 0, 0>", 1) == "k_mlp_bwd_rc_x3<8, 1, 0>"  # (SPLITOUT an int since round 6)
     assert b._rc_twin("k_mlp_bwd_rc_x3<8, 0>", 2) == "k_mlp_bwd_rc_x3<8, 2>"
     assert b._rc_twin("k_wgrad_x3<0, 4, 128, 512>", 1) is None
     path, prof = b.profiled_kernels()
@@ -349,5 +350,6 @@ def test_bench_finds_the_dominant_kernels_stamped_twin():
     rc = [k for k in prof if k.startswith("k_mlp_bwd_rc_x3<") and b._rc_twin(k, 0) == k]
     assert rc and all(b._rc_twin(k, 1) in prof for k in rc), (path, sorted(prof))
     assert b.pmc_traffic("k_mlp_bwd_rc_x3") is not None
-    # the VLM line's roofline kernel (the instantiation its step launches) in the VLM traffic passes
-    assert b.pmc_traffic("k_gemm_x3<false, true, 1, 2, false, 9, 128>", "traffic_vlm.json") > 0
+    # the VLM line's roofline kernel (the instantiation its step launches: the pre-split
+    # weight images, V = 5, the default since round 6) in the VLM traffic passes
+    assert b.pmc_traffic("k_gemm_x3<false, true, 1, 2, false, 5, 128>", "traffic_vlm.json") > 0
