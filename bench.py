@@ -236,7 +236,8 @@ def dominant_kernel(trainer):
     def launch():
         _native.call("ghm_ln_mlp_fwd", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                      ptr(pd["_mlps.0.0.weight"]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.weight"]),
-                     ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.G[0]), ptr(plan.Dg[0]), ptr(plan.st2[0]),
+                     ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), None if plan.mlp_rc else ptr(plan.G[0]),
+                     None if plan.mlp_rc else ptr(plan.Dg[0]), ptr(plan.st2[0]),
                      plan.M, 128, 512, plan.eps, sp)
     return "k_ln_mlp_fwd", launch
 
@@ -301,7 +302,7 @@ def pmc_traffic(kernel, fname="traffic.json"):
     with open(path) as f:
         t = json.load(f)
     ks = t.get("kernels", {})
-    for suffix in ("", "<8>", "<8, 0>", "<8, false>", "<8, 0, false>"):  # the instantiation the step launches (NW = 8)
+    for suffix in ("", "<8>", "<8, 0>", "<8, false>", "<8, 0, false>", "<true>"):  # the instantiation the step launches (NW = 8)
         if kernel + suffix in ks:
             return ks[kernel + suffix]["hbm_bytes"]
     return None
@@ -602,8 +603,9 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the global batch of 128 rows split over the ranks (128 / N rows per rank; "
                          "default: weak scaling, --batch rows per rank)")
-    ap.add_argument("--precision", default=None, choices=["f32", "x3"],
-                    help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3)")
+    ap.add_argument("--precision", default=None, choices=["f32", "x3", "f32fwd"],
+                    help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3); "
+                         "f32fwd (CLIP only): the forward exact f32, the backward split-bf16")
     a = ap.parse_args()
 
     ws, rank, local = setup_dist(a.gpus)
@@ -677,6 +679,7 @@ def main():
     kern_ms_step = time_kernel_in_step(tr, "ghm_" + kname[2:])
     risk = None if a.no_final_risk else final_risk(a, ws)
     rc = tr.precision == "x3"
+    precision = tr.precision
     graphed = tr.graphs is not None
     del ring, tr
     if rank != 0:
@@ -759,7 +762,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
-        "dtype": "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
+        "dtype": ("f32 (exact-f32 MFMA forward, split-bf16 x3 MFMA backward)" if precision == "f32fwd"
+                  else "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
         "config": {"workload": ("clip_guided: " if a.guide else "clip_default: ")
                    + "2 x EncoderTransformer(L=5, d=128, T=81), K=4, fwd+bwd+clip+AdamW"

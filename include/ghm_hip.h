@@ -61,7 +61,8 @@ int ghm_attn_fwd(const float* qkv, const float* H, float* H_mid, float* P, int64
                  int D, float scale_div, void* stream);
 
 /* H_out = H_mid + W2 GELU(W1 LN2(H_mid) + b1) + b2, U = W1 LN2(H_mid) + b1; saves
- * G = GELU(U) and Dg = GELU'(U) [M][F] for backward; stats = LN2 (mean, rstd)
+ * G = GELU(U) and Dg = GELU'(U) [M][F] for backward (both null: saves nothing, for
+ * a backward that recomputes U); stats = LN2 (mean, rstd)
  * —  models/model.py:741-747,784-788. */
 int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float* ln_b, const float* W1,
                    const float* b1, const float* W2, const float* b2, float* H_out, float* G,

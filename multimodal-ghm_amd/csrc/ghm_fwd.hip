@@ -284,8 +284,11 @@ __global__ __launch_bounds__(NKT * 64, 2) void k_attn_fwd(const float* __restric
 // W2[:, 32c:32c+32] ([128][36]: float4 reads conflict-free) in a double-buffered
 // LDS ring.  G = GELU(U) and D = GELU'(U) are stored for the backward pass
 // (one erf evaluation serves both; the backward needs no transcendentals).
+// SAVE = false (G = Dg = null): nothing stored for the backward -- the "f32fwd"
+// mode, whose split-bf16 backward recomputes U (k_mlp_bwd_rc_x3).
 // ---------------------------------------------------------------------------
 constexpr int PW2 = 36;
+template <bool SAVE>
 __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const float* __restrict__ W1, const float* __restrict__ b1, const float* __restrict__ W2,
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void k_ln_mlp_fwd(
       float dg[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) gelu_and_grad(g[r], g[r], dg[r]);
-      if (valid) {  // G = GELU(U) for dW2, D = GELU'(U) for the backward
+      if (SAVE && valid) {  // G = GELU(U) for dW2, D = GELU'(U) for the backward
         float* grow = G + m * GHM_F + 32 * c;
         float* drow = Dg + m * GHM_F + 32 * c;
 #pragma unroll
@@ -616,11 +619,16 @@ extern "C" int ghm_ln_mlp_fwd(const float* H_mid, const float* ln_w, const float
                               const float* W1, const float* b1, const float* W2, const float* b2,
                               float* H_out, float* G, float* Dg, float* stats, int64_t M, int D, int F,
                               float eps, void* stream) {
-  GHM_CHECK(H_mid && ln_w && ln_b && W1 && b1 && W2 && b2 && H_out && G && Dg && stats, "null pointer");
+  GHM_CHECK(H_mid && ln_w && ln_b && W1 && b1 && W2 && b2 && H_out && stats, "null pointer");
+  GHM_CHECK((G != nullptr) == (Dg != nullptr), "G and Dg: both saved or neither");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  hipLaunchKernelGGL(k_ln_mlp_fwd, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
-                     ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2, b2, H_out, G, Dg,
-                     reinterpret_cast<float2*>(stats), M, eps);
+  const dim3 grid(static_cast<unsigned>(ghm_token_blocks(M)));
+  if (G)
+    hipLaunchKernelGGL(k_ln_mlp_fwd<true>, grid, dim3(256), 0, ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2, b2,
+                       H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
+  else
+    hipLaunchKernelGGL(k_ln_mlp_fwd<false>, grid, dim3(256), 0, ghm_stream(stream), H_mid, ln_w, ln_b, W1, b1, W2,
+                       b2, H_out, G, Dg, reinterpret_cast<float2*>(stats), M, eps);
   return ghm_launch_status();
 }
 

@@ -242,13 +242,15 @@ __global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
   // SB (V & 8): one LDS tile instead of two (a second barrier per K tile), so
   // three 128 x 128 workgroups fit a CU's LDS (TM = 2, split-bf16, not IL)
   constexpr bool SB = (V & 8) != 0;
-  static_assert(!SB || (TM == 2 && !F32 && !IL && !BP), "single LDS tile: TM = 2, split-bf16, no interleave");
+  static_assert(!SB || (TM == 2 && !F32 && !IL), "single LDS tile: TM = 2, split-bf16, no interleave");
   constexpr int NBUF = SB ? 1 : 2;
   static_assert(!BP || (BUF && TB && !F32), "pre-split B: buffer loads, k-contiguous, split-bf16");
   // BN: workgroup tile columns, 128 or 64 (split-bf16 only: twice the workgroups
   // for the N = 256 products); a wave owns JN 32-column blocks
-  static_assert(BN == GB_N || (BN == 64 && !F32 && !BP), "64-column tiles: split-bf16, f32 B");
+  static_assert(BN == GB_N || (BN == 64 && !F32), "64-column tiles: split-bf16");
   constexpr int JN = BN / 64;
+  // pre-split B: BN rows x 32 bf16 = 4 16-byte chunks per row and plane, NBP per thread
+  constexpr int NBP = BN / 64;
   constexpr int BM = 64 * TM;
   constexpr int NA = TA ? BM / 32 : BM * 8 / 256;   // float4 per thread, A tile
   constexpr int NB = TB ? BN * 8 / 256 : BN / 32;
@@ -298,10 +300,10 @@ __global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
     if constexpr (TA) voff_oc<BM>(voa, g.lda);
     else voff_kc<BM>(voa, g.lda);
     if constexpr (BP) {
-      // 128 rows x 32 bf16 = 4 16-byte chunks per row and plane: chunk idx & 3 of
-      // row idx >> 2, idx = thread + 256 i (i = 0, 1)
+      // BN rows x 32 bf16 = 4 16-byte chunks per row and plane: chunk idx & 3 of
+      // row idx >> 2, idx = thread + 256 i (i < NBP)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NBP; ++i) {
         const int idx = threadIdx.x + 256 * i;
         vob[i] = static_cast<int>(((idx >> 2) * g.ldb + 8 * (idx & 3)) * 2);
       }
@@ -330,14 +332,14 @@ __global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
         for (int i = 0; i < NA; ++i) va[i] = bload4(rs, voa[i]);
       }
       if constexpr (BP) {
-        // vb[0..1]: the hi chunks, vb[2..3]: the lo chunks (raw bf16 bits)
+        // vb[0 .. NBP-1]: the hi chunks, vb[NBP ..]: the lo chunks (raw bf16 bits)
         const __bf16* b = g.Bp + n0 * g.ldb + k0;
         const auto rh = brsrc(b, live ? BN * g.ldb * 2 : 0);
         const auto rl = brsrc(b + g.bplane, live ? BN * g.ldb * 2 : 0);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NBP; ++i) {
           vb[i] = bload4(rh, vob[i]);
-          vb[2 + i] = bload4(rl, vob[i]);
+          vb[NBP + i] = bload4(rl, vob[i]);
         }
       } else if constexpr (TB) {
         int64_t ln;
@@ -392,11 +394,11 @@ __global__ __launch_bounds__(256, (V & 8) ? 3 : 2) void k_gemm_x3(GemmArgs g) {
     else store_kc<BM>(va, ah[buf], al[buf]);
     if constexpr (BP) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NBP; ++i) {
         const int idx = threadIdx.x + 256 * i;
         const int off = (idx >> 2) * GP + 8 * (idx & 3);
         *reinterpret_cast<float4*>(bh[buf] + off) = vb[i];
-        *reinterpret_cast<float4*>(bl[buf] + off) = vb[2 + i];
+        *reinterpret_cast<float4*>(bl[buf] + off) = vb[NBP + i];
       }
     } else if constexpr (TB) store_kc<BN>(vb, bh[buf], bl[buf]);
     else store_oc<BN, false>(vb, bh[buf], bl[buf], k0, ke);
@@ -1018,12 +1020,31 @@ void launch_bp(const GemmArgs& g, int nsplit, hipStream_t s) {
     return e ? static_cast<int64_t>(atoll(e)) : static_cast<int64_t>(768);
   }();
   const unsigned gx = static_cast<unsigned>(g.N / GB_N);
-  if (g.N >= tm2_min)
-    hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 2, false, 5>),
-                       dim3(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit), dim3(256), 0, s, g);
-  else
+  if (g.N >= tm2_min) {
+    // one LDS tile (V bit 3) as launch_tm's split-bf16 128 x 128 tiles: three
+    // workgroups per CU (the double-buffered pre-split kernel ran the GELU forward
+    // at 40.4 against 37.6 us without the pre-split, profiles/r6_vpack64); GHM_GEMM_SB
+    // = 0 restores the double buffer
+    const char* sb = getenv("GHM_GEMM_SB");
+    const dim3 g2(gx, static_cast<unsigned>((g.M + 127) / 128), nsplit);
+    if (sb ? atoi(sb) == 1 : true)
+      hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 2, false, 13>), g2, dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 2, false, 5>), g2, dim3(256), 0, s, g);
+    return;
+  }
+  // N < tm2_min: 64 x 64 tiles, as launch_tm's ta = 0 products (the pre-split path
+  // at 64 x 128 ran the N = 256 products on half the workgroups: pack on 4.51 vs
+  // off 4.44-4.45 ms per VLM step, profiles/r6_vpack_ab.txt); GHM_GEMM_BN = 128 keeps
+  // the 128-column tiles
+  const char* bne = getenv("GHM_GEMM_BN");
+  if (bne && atoi(bne) == 128)
     hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 1, false, 5>),
                        dim3(gx, static_cast<unsigned>((g.M + 63) / 64), nsplit), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_x3<false, true, EPI, 1, false, 5, 64>),
+                       dim3(static_cast<unsigned>(g.N / 64), static_cast<unsigned>((g.M + 63) / 64), nsplit),
+                       dim3(256), 0, s, g);
 }
 
 // Weight pre-split for the pre-split-B GEMMs: job j (8 int64: src, src pitch,

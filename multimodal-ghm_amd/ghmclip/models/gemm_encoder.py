@@ -35,7 +35,7 @@ import math
 import torch
 
 from .. import _native
-from .hip_encoder import PRECISIONS, EncoderPlan, default_precision
+from .hip_encoder import ENCODER_PRECISIONS, EncoderPlan, default_precision
 from .vlm import EPI_GELU, EPI_MUL, EPI_RESID, EPI_SLAB, EPI_STORE, _gemm
 
 GEMM_WIDTHS = (64, 256)
@@ -67,9 +67,9 @@ class GemmEncoderPlan:
         if n_embd not in GEMM_WIDTHS:
             raise ValueError(f"the HIP encoder takes n_embd = 128 (fused kernels) or one of {GEMM_WIDTHS} "
                              f"(GEMM path), got {n_embd}")
-        self.precision = default_precision() if precision is None else precision
-        if self.precision not in PRECISIONS:
-            raise ValueError(f"precision must be one of {PRECISIONS}")
+        self.precision = default_precision(allowed=ENCODER_PRECISIONS) if precision is None else precision
+        if self.precision not in ENCODER_PRECISIONS:
+            raise ValueError(f"precision must be one of {ENCODER_PRECISIONS}")
         if self.precision != "x3":
             raise NotImplementedError(f"n_embd = {n_embd}: the encoder's GEMM path is split-bf16 (precision x3) only")
         if n_token > 192:

@@ -71,9 +71,11 @@ def _stream():
 
 
 PRECISIONS = ("f32", "x3")
+# the CLIP encoder plan also takes "f32fwd": exact-f32 forward, split-bf16 backward
+ENCODER_PRECISIONS = PRECISIONS + ("f32fwd",)
 
 
-def default_precision(fallback="x3"):
+def default_precision(fallback="x3", allowed=PRECISIONS):
     """GHM_PRECISION env var: "x3" (split-bf16 MFMA, fp32-accurate to ~1e-5
     relative per product; the CLIP and VLM default: the reference code's whole
     3001-step CLIP run within 1.4e-6) or "f32" (exact-f32 MFMA for the
@@ -81,8 +83,8 @@ def default_precision(fallback="x3"):
     amplifies x3 rounding past the reference's own thread-count spread,
     DESIGN.md §2)."""
     p = os.environ.get("GHM_PRECISION", fallback)
-    if p not in PRECISIONS:
-        raise ValueError(f"GHM_PRECISION must be one of {PRECISIONS} (got {p!r})")
+    if p not in allowed:
+        raise ValueError(f"GHM_PRECISION must be one of {allowed} (got {p!r})")
     return p
 
 
@@ -110,9 +112,23 @@ class EncoderPlan:
             raise ValueError(f"the HIP encoder is built for n_embd=128 (got {n_embd})")
         if num_class != 10 or vocab > 16:
             raise ValueError("the HIP readout is built for num_class == 10 and a vocabulary <= 16")
-        self.precision = default_precision() if precision is None else precision
-        if self.precision not in PRECISIONS:
-            raise ValueError(f"precision must be one of {PRECISIONS}")
+        self.precision = default_precision(allowed=ENCODER_PRECISIONS) if precision is None else precision
+        if self.precision not in ENCODER_PRECISIONS:
+            raise ValueError(f"precision must be one of {ENCODER_PRECISIONS}")
+        # "f32fwd": the forward on the exact-f32 kernels, the backward on the split-bf16
+        # ones (U recomputed from the f32 forward's LN2 statistics, weight packs split
+        # per step as for "x3")
+        self.fwd_x3 = self.precision == "x3"
+        self.bwd_x3 = self.precision in ("x3", "f32fwd")
+        # the forward stages on the exact-f32 kernels: all three for "f32"; for "f32fwd"
+        # $GHM_F32FWD (comma list of qkv / attn / mlp, default all three) -- the others
+        # on the split-bf16 ones
+        parts = {"qkv", "attn", "mlp"}
+        if self.precision == "f32fwd":
+            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv,attn,mlp").split(",") if q}
+            if not parts <= {"qkv", "attn", "mlp"}:
+                raise ValueError(f"GHM_F32FWD: comma list of qkv / attn / mlp (got {sorted(parts)})")
+        self.fwd_f32 = frozenset() if self.fwd_x3 else frozenset(parts)
         if n_token > 192:
             raise ValueError(f"the HIP attention kernels take sequences of <= 192 tokens (got {n_token})")
         # sequences past 96 tokens (the joint CDM's 162) run on ghm_attn_ext_*_x3 with
@@ -146,7 +162,7 @@ class EncoderPlan:
         # gelu attention: GELU'(scores) saved beside P for the backward
         self.Pd = torch.zeros(L, N, pad, pad, dtype=f32, device=dev) if self.act == 2 else None
         # x3: the MLP forward saves nothing and its backward recomputes U
-        self.mlp_rc = self.precision == "x3"
+        self.mlp_rc = self.bwd_x3
         # past 96 tokens the f32 plan runs the attention core on the split-bf16
         # ghm_attn_ext kernels (the joint CDM's curves stay inside the reference's
         # own thread-count spread with them: DESIGN.md §2); GHM_LONG_ATTN=f32
@@ -161,11 +177,12 @@ class EncoderPlan:
         # Default 0: isolated the ring is faster (33.3 / 39.9 / 32.7 vs 42.3 / 45.3 /
         # 35.8 us) but the two-tower step slower (4.19-4.21 vs 4.05-4.09 ms, r5_ring4:
         # its 130-150 KB of LDS hold a whole CU)
-        ring = int(os.environ.get("GHM_WGRAD_RING", "0")) if self.precision == "x3" else 0
+        ring = int(os.environ.get("GHM_WGRAD_RING", "0")) if self.bwd_x3 else 0
         self.wgrad_ring = bool(ring & 3)      # dW2 / dW1 on the ring, G / dU pre-split
         self.wgrad_ring_qkv = bool(ring & 4)  # dWq|k|v on the ring
         if self.mlp_rc:  # backward scratch (k_mlp_bwd_rc_x3 -> dW2): f32 [M][512], or the
             # bf16 hi / lo planes [2][M][512] of the ring path in the same bytes
+            # (f32fwd: the f32 forward saves no G / GELU' either)
             self.G, self.Dg = e(M, D_HIDDEN), None
         else:
             self.G, self.Dg = e(L, M, D_HIDDEN), e(L, M, D_HIDDEN)
@@ -225,7 +242,7 @@ class EncoderPlan:
                               lib.ghm_embed_bwd_part_elems(T, vocab)))
         self.d_emb = e(N, num_class)
         self.pack = None
-        if self.precision == "x3":
+        if self.bwd_x3:
             npk = int(_native.GHM_SPLIT_PACK_ELEMS)
             self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
         # pre-split LN outputs: xs[l][0] = LN1(H_l), xs[l][1] = LN2(Hmid_l), each the hi
@@ -277,7 +294,7 @@ class EncoderPlan:
         c = _native.call
         T, N, L = self.T, self.N, self.L
         s = _stream()
-        if self.precision == "x3" and split:
+        if self.bwd_x3 and split:
             self.split_weights(p, s)
         c("ghm_embed_fwd", _ptr(tok), _ptr(p["token_embeddings.weight"]),
           _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), N, T, self.V, D_MODEL, s)
@@ -298,34 +315,32 @@ class EncoderPlan:
     def _layer_fwd(self, p, l, s):
         c = _native.call
         M = self.M
-        x3 = self.precision == "x3"
-        if True:
-            if x3:
-                pk = _ptr(self.pack[l])
-                if self.ln_presplit:
-                    c("ghm_ln_qkv_fwd_x3s", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-                      _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), _ptr(self.xs[l, 0]), M,
-                      D_MODEL, self.eps, s)
-                else:
-                    c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
-                      _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-                self._attn_fwd(l, s)
-                mlp_args = (_ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), pk,
-                            _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]),
-                            _ptr(self.st2[l]))
-                if self.ln_presplit:
-                    c("ghm_ln_mlp_fwd_x3bs", *mlp_args, _ptr(self.xs[l, 1]), M, D_MODEL, D_HIDDEN, self.eps, s)
-                else:
-                    c("ghm_ln_mlp_fwd_x3b", *mlp_args, M, D_MODEL, D_HIDDEN, self.eps, s)
-                return
+        pk = _ptr(self.pack[l]) if self.bwd_x3 else None
+        if "qkv" in self.fwd_f32:
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
-            self._attn_fwd(l, s)
+        elif self.ln_presplit:
+            c("ghm_ln_qkv_fwd_x3s", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+              _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), _ptr(self.xs[l, 0]), M,
+              D_MODEL, self.eps, s)
+        else:
+            c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
+              _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
+        self._attn_fwd(l, s)
+        if "mlp" in self.fwd_f32:
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
-              _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), _ptr(self.G[l]), _ptr(self.Dg[l]),
-              _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+              _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]), None if self.mlp_rc else _ptr(self.G[l]),
+              None if self.mlp_rc else _ptr(self.Dg[l]), _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+            return
+        mlp_args = (_ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), pk,
+                    _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]),
+                    _ptr(self.st2[l]))
+        if self.ln_presplit:
+            c("ghm_ln_mlp_fwd_x3bs", *mlp_args, _ptr(self.xs[l, 1]), M, D_MODEL, D_HIDDEN, self.eps, s)
+        else:
+            c("ghm_ln_mlp_fwd_x3b", *mlp_args, M, D_MODEL, D_HIDDEN, self.eps, s)
 
     def _attn_fwd(self, l, s):
         """Layer l's attention + residual (model.py:776-783): Hmid[l] = H[l] + A V
@@ -336,7 +351,7 @@ class EncoderPlan:
             self._attn_fwd_f32(l)
         elif self.long_attn:  # unmasked (n_prefix = T), plain residual (dbl = 0)
             self._attn_ext_fwd(l, s)
-        elif self.precision == "x3":
+        elif "attn" not in self.fwd_f32:
             if self.act:
                 c("ghm_attn_fwd_x3_act", _ptr(self.qkv[l]), _ptr(self.H[l]), _ptr(self.Hmid[l]), _ptr(self.P[l]),
                   None if self.Pd is None else _ptr(self.Pd[l]), N, T, D_MODEL, self.scale_div, self.act, s)
@@ -355,7 +370,7 @@ class EncoderPlan:
         stays the caller's)."""
         c = _native.call
         N, T = self.N, self.T
-        x3 = self.precision == "x3"
+        x3 = self.bwd_x3
         if self.attn_f32:
             self._attn_bwd_f32(l, cur)
         elif self.long_attn:
@@ -553,7 +568,7 @@ class EncoderPlan:
         c = _native.call
         J = self._job
         M = self.M
-        x3 = self.precision == "x3"
+        x3 = self.bwd_x3
         wgrad = "ghm_wgrad_x3" if x3 else "ghm_wgrad"
         P_ln, P_ln2 = self._lp("ln", l), self._lp("ln2", l)
         P_w2, P_w1, P_wq = self._lp("w2", l), self._lp("w1", l), self._lp("wq", l)

@@ -27,7 +27,7 @@ from .. import _native
 from . import distributed
 from ..data.data_random_GHM import DeviceTree
 from ..models.gemm_encoder import make_encoder_plan
-from ..models.hip_encoder import default_precision, require_hip
+from ..models.hip_encoder import ENCODER_PRECISIONS, default_precision, require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
 
 
@@ -101,7 +101,8 @@ class ClipTrainer:
                  precision=None, penalty=1e-3, guide_trans=None):
         """lr_schedule: sequence of python-float learning rates, one per step
         (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
-        precision: "f32" (exact-f32 MFMA) or "x3" (split-bf16 MFMA); None ->
+        precision: "f32" (exact-f32 MFMA), "x3" (split-bf16 MFMA) or "f32fwd" (the
+        forward exact f32, the backward split-bf16; n_embd = 128); None ->
         $GHM_PRECISION, else "x3" (unguided) / "f32" (guided: the guided run
         amplifies the split products' 2^-17 rounding 20x past an f32 path's, which
         sits at the level of any one-ulp perturbation of the reference's own
@@ -147,7 +148,8 @@ class ClipTrainer:
         T = tmodel.n_token
         n_seq = batch_size * (K + 1)
         if precision is None:
-            precision = default_precision("f32" if all(getattr(m, "guide", False) for m in self.models) else "x3")
+            precision = default_precision("f32" if all(getattr(m, "guide", False) for m in self.models) else "x3",
+                                          allowed=ENCODER_PRECISIONS)
         if any(m.n_embd != 128 for m in self.models) and all(getattr(m, "guide", False) for m in self.models):
             raise NotImplementedError("guided CLIP runs at n_embd = 128 (the guide kernels' row pitch)")
         # n_embd = 128: the fused token-parallel kernels; other widths (the reference

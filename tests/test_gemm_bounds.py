@@ -70,15 +70,14 @@ def test_the_model_sees_the_first_versions_overrun():
     assert out_of_allocation(0, 1, 405, 256, 256, 256, 256, 1, 405, 256, 1, fixed=False) > 0
 
 
-def bp_out_of_image(M, N, K, ldbp, nsplit, TM):
-    """Pre-split B (k_gemm_x3 V bit 2, ghm_gemm_x3p): per K tile two 16-byte loads
-    per thread and plane at byte offsets ((idx >> 2) ldbp + 8 (idx & 3)) 2 from the
-    tile's base (n0 ldbp + k0) bf16, records BN ldbp 2 bytes when the tile is live;
-    the hi plane is [N][ldbp] bf16 and the lo plane the next one.  Counts loads
-    inside the records that leave their own plane (either end)."""
-    BN = GB_N
+def bp_out_of_image(M, N, K, ldbp, nsplit, TM, BN=GB_N):
+    """Pre-split B (k_gemm_x3 V bit 2, ghm_gemm_x3p): per K tile BN / 64 16-byte
+    loads per thread and plane at byte offsets ((idx >> 2) ldbp + 8 (idx & 3)) 2
+    from the tile's base (n0 ldbp + k0) bf16, records BN ldbp 2 bytes when the tile
+    is live; the hi plane is [N][ldbp] bf16 and the lo plane the next one.  Counts
+    loads inside the records that leave their own plane (either end)."""
     kps = ((K + nsplit - 1) // nsplit + GB_K - 1) // GB_K * GB_K
-    ob = [((idx >> 2) * ldbp + 8 * (idx & 3)) * 2 for idx in range(512)]
+    ob = [((idx >> 2) * ldbp + 8 * (idx & 3)) * 2 for idx in range(4 * BN)]
     plane = N * ldbp * 2
     bad = 0
     for z in range(nsplit):
@@ -92,14 +91,15 @@ def bp_out_of_image(M, N, K, ldbp, nsplit, TM):
     return bad
 
 
-@pytest.mark.parametrize("TM", [1, 2])
-def test_presplit_b_loads_stay_inside_their_plane(TM):
+@pytest.mark.parametrize("TM,BN", [(1, 128), (2, 128), (1, 64)])
+def test_presplit_b_loads_stay_inside_their_plane(TM, BN):
     """Every ghm_gemm_x3p product of models/vlm.py (D = 128 / 256): forward W
-    images (N = 3D / F / D), data-gradient W^T images, split-k data gradients."""
+    images (N = 3D / F / D), data-gradient W^T images, split-k data gradients;
+    64 x 64 tiles (launch_bp below 768 columns) as well as the 128-column ones."""
     for d in (128, 256):
         F = 4 * d
         for N, K, ns in ((3 * d, d, 1), (F, d, 1), (d, F, 1), (F, d, 1), (d, F, 2), (d, 3 * d, 1), (d, 3 * d, 3)):
-            assert bp_out_of_image(405, N, K, K, ns, TM) == 0, (d, N, K, ns)
+            assert bp_out_of_image(405, N, K, K, ns, TM, BN) == 0, (d, N, K, ns)
 
 
 def split_pack_writes(L, D):
