@@ -218,7 +218,10 @@ def dominant_kernel(trainer):
         plan, pd = trainer.plan, trainer.pd
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    if plan.precision == "x3" and getattr(plan, "ln_presplit", False):
+    # the MLP forward the step launches: split-bf16 unless the plan keeps it on the f32
+    # kernels (precision "f32", or "f32fwd" with mlp among its f32 stages)
+    mlp_x3 = "mlp" not in plan.fwd_f32 if hasattr(plan, "fwd_f32") else plan.precision == "x3"
+    if mlp_x3 and getattr(plan, "ln_presplit", False):
         # the launch the step makes: the LN2 rows also written pre-split for dW1
         def launch():
             _native.call("ghm_ln_mlp_fwd_x3bs", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]),
@@ -226,7 +229,7 @@ def dominant_kernel(trainer):
                          ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]), ptr(plan.st2[0]), ptr(plan.xs[0, 1]), plan.M, 128,
                          512, plan.eps, sp)
         return "k_ln_mlp_fwd_x3bs", launch
-    if plan.precision == "x3":
+    if mlp_x3:
         def launch():
             _native.call("ghm_ln_mlp_fwd_x3b", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                          ptr(plan.pack[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]), ptr(plan.H[1]),

@@ -121,11 +121,13 @@ class EncoderPlan:
         self.fwd_x3 = self.precision == "x3"
         self.bwd_x3 = self.precision in ("x3", "f32fwd")
         # the forward stages on the exact-f32 kernels: all three for "f32"; for "f32fwd"
-        # $GHM_F32FWD (comma list of qkv / attn / mlp, default all three) -- the others
-        # on the split-bf16 ones
+        # $GHM_F32FWD (comma list of qkv / attn / mlp), the others on the split-bf16
+        # ones.  Default LN1 + QKV and LN2 + MLP: the guided 3001-step run needs both
+        # (worst ratio to its bound 0.377; mlp alone 4.96, attn + mlp 4.44, qkv + attn
+        # 4.22, all three 0.359; profiles/r6_f32mix_curves.txt)
         parts = {"qkv", "attn", "mlp"}
         if self.precision == "f32fwd":
-            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv,attn,mlp").split(",") if q}
+            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv,mlp").split(",") if q}
             if not parts <= {"qkv", "attn", "mlp"}:
                 raise ValueError(f"GHM_F32FWD: comma list of qkv / attn / mlp (got {sorted(parts)})")
         self.fwd_f32 = frozenset() if self.fwd_x3 else frozenset(parts)

@@ -102,11 +102,12 @@ class ClipTrainer:
         """lr_schedule: sequence of python-float learning rates, one per step
         (get_lr_cosine_schedule(i, ...) for i in range(total_iters+1)).
         precision: "f32" (exact-f32 MFMA), "x3" (split-bf16 MFMA) or "f32fwd" (the
-        forward exact f32, the backward split-bf16; n_embd = 128); None ->
-        $GHM_PRECISION, else "x3" (unguided) / "f32" (guided: the guided run
-        amplifies the split products' 2^-17 rounding 20x past an f32 path's, which
-        sits at the level of any one-ulp perturbation of the reference's own
-        arithmetic).
+        LN + projection and LN + MLP forwards exact f32, the rest split-bf16;
+        n_embd = 128); None -> $GHM_PRECISION, else "x3" (unguided) / "f32fwd"
+        (guided: the guided run amplifies the split products' 2^-17 rounding in
+        the forward 20x past an f32 path's, which sits at the level of any one-ulp
+        perturbation of the reference's own arithmetic, while split-bf16 gradients
+        and attention stay inside the reference's spread).
         Guided CLIP (train_CLIP.py --clip_guide=True) is on when the encoders were
         built with guide=True: guide_trans = (text, image) transition templates
         [L][C][V][V] (ClipSampler.t_templ / i_templ) for the on-device BP guide
@@ -148,7 +149,7 @@ class ClipTrainer:
         T = tmodel.n_token
         n_seq = batch_size * (K + 1)
         if precision is None:
-            precision = default_precision("f32" if all(getattr(m, "guide", False) for m in self.models) else "x3",
+            precision = default_precision("f32fwd" if all(getattr(m, "guide", False) for m in self.models) else "x3",
                                           allowed=ENCODER_PRECISIONS)
         if any(m.n_embd != 128 for m in self.models) and all(getattr(m, "guide", False) for m in self.models):
             raise NotImplementedError("guided CLIP runs at n_embd = 128 (the guide kernels' row pitch)")

@@ -619,7 +619,7 @@ def _cks_rel(t, g, key):
                abs(t.abs().max().item() - ck[2]) / max(ck[2], 1e-30))
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", MODES)
 def test_guided_nonti_steps_vs_reference(precision):
     """Guided CLIP on --translation_invariance=False trees: the fused step with
     per-edge on-device BP targets == the reference's own two steps (L=5, d=128,
@@ -704,7 +704,7 @@ def test_guided_steps_vs_oracle(precision):
             assert _rel(p_gpu, p_ref) < 1e-4
 
 
-@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("precision", MODES)
 def test_guided_curve_vs_reference(precision):
     """Guided default config (exp_clip_guidedTF.sh) vs the reference's own run on
     identical GHM draws: penalty-free loss within 1e-4, penalised loss within 1e-4
@@ -723,11 +723,13 @@ def test_guided_curve_vs_reference(precision):
     assert pdev.max() <= 1e-4
 
 
-@pytest.mark.parametrize("precision", [None, "f32fwd"])
+@pytest.mark.parametrize("precision", [None, "f32"])
 def test_guided_full_run_final_risk_vs_reference_cpu_run(precision):
     """The whole guided run (exp_clip_guidedTF.sh: lr 1e-3 -> 1e-6, penalty 1e-3,
     total_iters=3000, 3001 steps) at the product default precision for guided
-    CLIP (exact f32: ClipTrainer precision=None) against the reference's own code
+    CLIP (ClipTrainer precision=None: "f32fwd", the LN + projection and LN + MLP
+    forwards in exact f32, attention and the backward split-bf16) and in exact f32
+    throughout, against the reference's own code
     run here on the CPU (clip_guided_curve3001.npz: 5 threads, AVX-512 kernels,
     all 3001 steps).  The reference's own arithmetic spread over steps 0-1100
     comes from three reruns of the same code on the same draws:
@@ -748,7 +750,7 @@ def test_guided_full_run_final_risk_vs_reference_cpu_run(precision):
     alts = [np.load(os.path.join(GOLDEN, f"clip_guided_curve3001_{k}.npz"))["loss_history"]
             for k in ("t2", "avx2", "scalar")]
     sampler, tr = _guided_trainer(5, 128, precision)
-    assert tr.precision == (precision or "f32")
+    assert tr.precision == (precision or "f32fwd")
     hist = _run(sampler, tr, 128, 3001, graph_after=3)
     ph = tr.ploss_history()
     risk, ref_risk = hist[-100:].mean(), ref[-100:].mean()

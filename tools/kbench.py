@@ -77,6 +77,11 @@ def main():
                                      P(p["_lns_2.0.bias"]), P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]),
                                      P(p["_mlps.0.2.weight"]), P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), P(plan.G[l]),
                                      P(plan.Dg[l]), P(plan.st2[l]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
+            # the same with nothing saved for the backward (precision "f32fwd")
+            "ln_mlp_fwd_nosave": (lambda: c("ghm_ln_mlp_fwd", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                            P(p["_lns_2.0.bias"]), P(p["_mlps.0.0.weight"]), P(p["_mlps.0.0.bias"]),
+                                            P(p["_mlps.0.2.weight"]), P(p["_mlps.0.2.bias"]), P(plan.H[l + 1]), None,
+                                            None, P(plan.st2[l]), M, 128, 512, plan.eps, sp), gf(4 * M * 128 * 512)),
             "mlp_bwd": (lambda: c("ghm_mlp_bwd", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                   P(p["_lns_2.0.weight"]), P(p["_mlps.0.0.weight"]), P(p["_mlps.0.2.weight"]),
                                   P(plan.Dg[l]), P(plan.dU), P(plan.dH[1]), P(plan.part_ln), M, 128, 512, sp),
