@@ -16,6 +16,8 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 fi
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 4
 cat $OUT/bench.json
+timeout -k 10 400 python bench.py --guide > $OUT/bench_clip_guided.json 2> $OUT/bench_clip_guided.err || exit 4
+echo "clip_guided $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_clip_guided.json)"
 for w in vlm cdm cdm_joint cdm_guided vlm_joint; do
   timeout -k 10 400 python bench.py --workload $w > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 5
   echo "$w $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$w.json)"
