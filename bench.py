@@ -221,6 +221,12 @@ def dominant_kernel(trainer):
     # the MLP forward the step launches: split-bf16 unless the plan keeps it on the f32
     # kernels (precision "f32", or "f32fwd" with mlp among its f32 stages)
     mlp_x3 = "mlp" not in plan.fwd_f32 if hasattr(plan, "fwd_f32") else plan.precision == "x3"
+    if getattr(plan, "mlp6", False):  # three-way split operands (f32fwd's mlp6 stage)
+        def launch():
+            _native.call("ghm_ln_mlp_fwd_x6", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
+                         ptr(plan.pack[0]), ptr(plan.pack3[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]),
+                         ptr(plan.H[1]), ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
+        return "k_ln_mlp_fwd_x6", launch
     if mlp_x3 and getattr(plan, "ln_presplit", False):
         # the launch the step makes: the LN2 rows also written pre-split for dW1
         def launch():
@@ -683,6 +689,7 @@ def main():
     risk = None if a.no_final_risk else final_risk(a, ws)
     rc = tr.precision == "x3"
     precision = tr.precision
+    fwd_f32 = sorted(getattr(tr.plans[0], "fwd_f32", ()))
     graphed = tr.graphs is not None
     del ring, tr
     if rank != 0:
@@ -696,13 +703,15 @@ def main():
     scale = a.batch / 128
     traffic = pmc_traffic(kname[:-1] if kname.endswith("x3bs") else kname)  # (the x3b passes when no x3bs pass)
     x3 = kname.endswith("x3b") or kname.endswith("x3bs")
+    x6 = kname.endswith("x6")
     # The kernel's work is 13.59 GFLOP (f32 products) per launch; the bytes that
     # MUST move are Hmid in and H out (the hidden activation never needs to leave
     # the chip): AI = 13.59e9 / 53.1e6 = 256 FLOP/B, so the roof is the matrix
     # cores.  x3 evaluates each f32 product as 3 bf16 MFMA products: its
     # achieved rate is counted in those (3 x 13.59 GF) against the dense bf16
-    # peak; the f32 mode against the f32 MFMA peak.
-    mult, peak = (3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (1.0, F32_MFMA_PEAK_TFLOPS)
+    # peak (x6, three-way split operands: 6 x); the f32 mode against the f32 MFMA peak.
+    mult, peak = ((3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (6.0, BF16_MFMA_PEAK_TFLOPS) if x6
+                  else (1.0, F32_MFMA_PEAK_TFLOPS))
     kflop = mult * MLP_FWD_GFLOP_PER_LAUNCH * scale
     achieved = kflop / (kern_ms * 1e-3) / 1e3
     achieved_step = kflop / (kern_ms_step * 1e-3) / 1e3
@@ -765,7 +774,9 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
-        "dtype": ("f32 (exact-f32 MFMA forward, split-bf16 x3 MFMA backward)" if precision == "f32fwd"
+        "dtype": (f"f32 (f32fwd: forward stages {fwd_f32} at f32 accuracy -- qkv / attn / mlp exact-f32 MFMA, "
+                  f"qkv6 / mlp6 three-way split-bf16 (six products); the rest of the forward and the backward "
+                  f"split-bf16 x3)" if precision == "f32fwd"
                   else "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
         "config": {"workload": ("clip_guided: " if a.guide else "clip_default: ")
@@ -779,8 +790,9 @@ def main():
         "sequences_per_s": round(samples * 10 / elapsed, 1),
         "dist": comm,
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
-        "step_mfma_frac": round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
-        "step_mfma_basis": f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s",
+        "step_mfma_frac": None if precision == "f32fwd" else round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
+        "step_mfma_basis": ("f32fwd mixes f32, x3 and x6 products: no single count" if precision == "f32fwd" else
+                            f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s"),
         "step_hbm": None if step_bytes is None else {
             "bytes": round(step_bytes * scale), "gbs": round(step_bytes * scale / (ms * 1e-3) / 1e9, 1),
             "peak": HBM_PEAK_GBS, "frac": round(step_bytes * scale / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -229,6 +229,21 @@ int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const float* ln_b,
 int ghm_ln_mlp_fwd_x3bs(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                         const float* b1, const float* b2, float* H_out, float* stats, void* xs, int64_t M, int D,
                         int F, float eps, void* stream);
+/* Third split planes ("lo2": x = hi + lo + lo2) of each job's weights into job.pack,
+ * a pack3 of GHM_SPLIT3_PACK_ELEMS bf16: W1 as the pack's W1_N image, W2 as its
+ * W2_P32 image, [Wq; Wk; Wv] as its QKV_N image (round 6). */
+#define GHM_SPLIT3_PACK_ELEMS 180224
+int ghm_split3_weights(const ghm_split_job* jobs, int n_jobs, void* stream);
+/* ghm_ln_qkv_fwd_x3 on three-way split operands (six bf16 MFMAs per product); pack3
+ * from ghm_split3_weights (precision "f32fwd", $GHM_F32FWD qkv6; round 6). */
+int ghm_ln_qkv_fwd_x6(const float* H, const float* ln_w, const float* ln_b, const void* pack, const void* pack3,
+                      float* qkv, float* stats, int64_t M, int D, float eps, void* stream);
+/* ghm_ln_mlp_fwd_x3b with every product on three-way split operands (six bf16
+ * MFMAs, ~2^-24 relative: the exact-f32 level) and the exact GELU; pack3 from
+ * ghm_split3_weights (precision "f32fwd", $GHM_F32FWD mlp6; round 6). */
+int ghm_ln_mlp_fwd_x6(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                      const void* pack3, const float* b1, const float* b2, float* H_out, float* stats, int64_t M,
+                      int D, int F, float eps, void* stream);
 /* MLP + LN2 backward with the up-projection recomputed from H_mid and the LN2
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),

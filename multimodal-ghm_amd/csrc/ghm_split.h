@@ -31,6 +31,18 @@ __device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x
   return mfma_bf(ah, bh, c);
 }
 
+// six products of three-way split operands on the 32x32x16 MFMA (see mfma16_x6z),
+// chained: for accumulators that start from zero per output tile
+__device__ __forceinline__ f32x16 mfma_x6(bf16x8 a0, bf16x8 a1, bf16x8 a2, bf16x8 b0, bf16x8 b1, bf16x8 b2,
+                                         f32x16 c) {
+  c = mfma_bf(a2, b0, c);
+  c = mfma_bf(a1, b1, c);
+  c = mfma_bf(a0, b2, c);
+  c = mfma_bf(a1, b0, c);
+  c = mfma_bf(a0, b1, c);
+  return mfma_bf(a0, b0, c);
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // 16x16x32 bf16: lane l holds A[row l&15][k = 8(l>>4) + i], B[k = 8(l>>4) + i][col l&15];
@@ -42,6 +54,20 @@ __device__ __forceinline__ f32x4 mfma16_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16
   c = mfma16_bf(al, bh, c);
   c = mfma16_bf(ah, bl, c);
   return mfma16_bf(ah, bh, c);
+}
+// six products of three-way split operands, a.b ~ a2 b0 + a1 b1 + a0 b2 + a1 b0 +
+// a0 b1 + a0 b0 (the dropped terms ~2^-27 |a||b|), as two zero-started partial sums
+// added on the VALU: the five cross terms, smallest first, then hi x hi alone (an MFMA adding into an accumulator drops
+// the low bits of the smaller side at alignment, so the large term is kept apart)
+__device__ __forceinline__ f32x4 mfma16_x6z(bf16x8 a0, bf16x8 a1, bf16x8 a2, bf16x8 b0, bf16x8 b1, bf16x8 b2) {
+  f32x4 z;
+  z[0] = z[1] = z[2] = z[3] = 0.f;
+  f32x4 c = mfma16_bf(a2, b0, z);
+  c = mfma16_bf(a1, b1, c);
+  c = mfma16_bf(a0, b2, c);
+  c = mfma16_bf(a1, b0, c);
+  c = mfma16_bf(a0, b1, c);
+  return c + mfma16_bf(a0, b0, z);
 }
 __device__ __forceinline__ f32x4 zero4() {
   f32x4 z;
@@ -62,6 +88,20 @@ __device__ __forceinline__ void split8(const float* x, bf16x8& hi, bf16x8& lo) {
     split1(x[i], a, b);
     hi[i] = a;
     lo[i] = b;
+  }
+}
+
+// three-way split: x = hi + lo + lo2 to ~2^-26 relative (hi, lo as split1; lo2 the
+// bf16 of what is left, exact in f32 before its rounding)
+__device__ __forceinline__ void split3_8(const float* x, bf16x8& hi, bf16x8& lo, bf16x8& lo2) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const __bf16 a = static_cast<__bf16>(x[i]);
+    const float r = x[i] - static_cast<float>(a);
+    const __bf16 b = static_cast<__bf16>(r);
+    hi[i] = a;
+    lo[i] = b;
+    lo2[i] = static_cast<__bf16>(r - static_cast<float>(b));
   }
 }
 

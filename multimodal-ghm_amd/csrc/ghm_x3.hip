@@ -55,6 +55,12 @@ constexpr int PK_W1_T32 = PK_W2_T + 2 * PK_W;   // [128][512]: row d, col q     
 constexpr int PK_W2_P32 = PK_W1_T32 + 2 * PK_W;  // [128][512]: row o, col q          = W2[o][perm32(q)]
 constexpr int PK_ELEMS = PK_W2_P32 + 2 * PK_W;   // 983040
 static_assert(PK_ELEMS == GHM_SPLIT_PACK_ELEMS, "pack layout mismatch with include/ghm_hip.h");
+// pack3: the third split planes (lo2) of the x6 kernels' weight images, in the pack's layouts
+constexpr int PK3_W1_N = 0;                   // [512][128] as PK_W1_N
+constexpr int PK3_W2_P32 = PK_W;              // [128][512] as PK_W2_P32
+constexpr int PK3_QKV_N = 2 * PK_W;           // [384][128] as PK_QKV_N
+constexpr int PK3_ELEMS = 2 * PK_W + PK_QKV;  // 180224
+static_assert(PK3_ELEMS == GHM_SPLIT3_PACK_ELEMS, "pack3 layout mismatch with include/ghm_hip.h");
 
 // column permutation inside each 16-group for operands met by an accumulator
 // tile (ghm_split.h): position q holds original column perm_col(q)
@@ -155,6 +161,20 @@ __device__ __forceinline__ void ln_row_split(const float* __restrict__ row, cons
   for (int t = 0; t < 8; ++t) split8(x + 8 * t, xh[t], xl[t]);
 }
 
+__device__ __forceinline__ void ln_row_split3(const float* __restrict__ row, const float* __restrict__ lnw,
+                                              const float* __restrict__ lnb, int h, float eps, bool active,
+                                              bf16x8* x0, bf16x8* x1, bf16x8* x2, float& mean, float& rstd) {
+  float x[64];
+  if (active) {
+    ln_row(row, lnw, lnb, h, eps, x, mean, rstd);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) x[k] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) split3_8(x + 8 * t, x0[t], x1[t], x2[t]);
+}
+
 // load a row-layout token vector (64 floats at p) and split it
 __device__ __forceinline__ void load_split64(const float* __restrict__ p, bool active, bf16x8* xh, bf16x8* xl) {
   float x[64];
@@ -225,6 +245,32 @@ __device__ __forceinline__ void fill_r128_w8(const __bf16* g, int ldg, int lo_of
       const __bf16* src = g + row * ldg + 8 * lc;
       glds16(src, ih + 512 * b);
       glds16(src + lo_off, il + 512 * b);
+    }
+  }
+}
+
+// one plane (the x6 kernels' third, lo2, plane) with fill_r32_w8 / fill_r128_w8's swizzles
+template <int NW>
+__device__ __forceinline__ void fill_r32_1(const __bf16* g, int ldg, __bf16* ih) {
+  const int L = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < (8 + NW - 1) / NW; ++k) {
+    const int b = (threadIdx.x >> 6) + NW * k;
+    if (8 % NW == 0 || b < 8) {
+      const int row = 4 * b + (L >> 4), lc = (L & 15) ^ (row & 15);
+      glds16(g + row * ldg + 8 * lc, ih + 512 * b);
+    }
+  }
+}
+template <int NW>
+__device__ __forceinline__ void fill_r128_1(const __bf16* g, int ldg, __bf16* ih) {
+  const int L = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < (8 + NW - 1) / NW; ++k) {
+    const int b = (threadIdx.x >> 6) + NW * k;
+    if (8 % NW == 0 || b < 8) {
+      const int row = 16 * b + (L >> 2), lc = (L & 3) ^ r128_swz(row);
+      glds16(g + row * ldg + 8 * lc, ih + 512 * b);
     }
   }
 }
@@ -308,6 +354,70 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
     const int bn = b + 1 < 12 ? b + 1 : 11;  // branch-free: the last tile refills tile 11
     prev = qkv_tile_x3(lds + 2 * PLANE * cur, lds + 2 * PLANE * (cur ^ 1), W + bn * 32 * GHM_D, GHM_D, j, h,
                        active, xh, xl, zero16());
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (active && valid) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      st4(orow + 32 * 11 + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
+  }
+}
+
+// qkv_tile_x3 on three planes (cb / nb __restrict__ for the same reason)
+__device__ __forceinline__ f32x16 qkv_tile_x6(const __bf16* __restrict__ cb, __bf16* __restrict__ nb,
+                                              const __bf16* g, const __bf16* gc, int row, int h, bool active,
+                                              const bf16x8* x0, const bf16x8* x1, const bf16x8* x2) {
+  fill_r32_w8<4>(g, GHM_D, PK_QKV, nb, nb + PLANE);
+  fill_r32_1<4>(gc, GHM_D, nb + 2 * PLANE);
+  f32x16 acc = zero16();
+  if (active) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int o = r32_off(row, 8 * h + t);
+      acc = mfma_x6(ldsb8(cb + o), ldsb8(cb + PLANE + o), ldsb8(cb + 2 * PLANE + o), x0[t], x1[t], x2[t], acc);
+    }
+  }
+  return acc;
+}
+
+// LN1 + Q/K/V on three-way split operands (the "f32fwd" precision's qkv6 stage):
+// k_ln_qkv_fwd_x3 with six bf16 MFMAs per product (mfma_x6) and the weights' third
+// plane from pack3 (PK3_QKV_N); the ring holds three planes per buffer (48 KB).
+__global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x6(
+    const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* pack, const __bf16* pack3, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
+    float eps) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[6 * PLANE];  // 2 buffers x (hi, lo, lo2)
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const bool active = m0 < M;
+  const int64_t m = m0 + j;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W = pack + PK_QKV_N;
+  const __bf16* Wc = pack3 + PK3_QKV_N;
+  fill_r32_w8<4>(W, GHM_D, PK_QKV, lds, lds + PLANE);  // tile 0, in flight over the LayerNorm
+  fill_r32_1<4>(Wc, GHM_D, lds + 2 * PLANE);
+  bf16x8 x0[8], x1[8], x2[8];
+  {
+    float mean = 0.f, rstd = 0.f;
+    ln_row_split3(H + mc * GHM_D, lnw, lnb, h, eps, active, x0, x1, x2, mean, rstd);
+    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  f32x16 prev = zero16();
+  float* orow = qkv + m * (3 * GHM_D);
+#pragma unroll 1
+  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
+    const int cur = b & 1;
+    if (b > 0 && active && valid) {  // tile b - 1's outputs
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(orow + 32 * (b - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
+    }
+    const int bn = b + 1 < 12 ? b + 1 : 11;  // branch-free: the last tile refills tile 11
+    prev = qkv_tile_x6(lds + 3 * PLANE * cur, lds + 3 * PLANE * (cur ^ 1), W + bn * 32 * GHM_D,
+                       Wc + bn * 32 * GHM_D, j, h, active, x0, x1, x2);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if (active && valid) {
@@ -479,6 +589,173 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
     float* orow = Hout + m * GHM_D;
 #pragma unroll
     for (int j = 0; j < 8; ++j) st4(orow + 16 * j + 4 * g, y[j][0], y[j][1], y[j][2], y[j][3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LN2 + MLP forward on three-way split operands (the "f32fwd" precision's MLP stage
+// as `mlp6`): the k_ln_mlp_fwd_x3b schedule with every product as six bf16 MFMAs
+// (mfma16_x6z, ~2^-24 relative: near the exact-f32 kernel's level, on the bf16 pipe)
+// instead of three, and the exact GELU of the f32 kernel.  The weights' third
+// planes come from pack3 ([W1 n | W2 p32] lo2 planes in the pack's layouts, written
+// by ghm_split3_weights); the LDS ring holds six planes per buffer (96 KB
+// double-buffered): one 8-wave workgroup per CU.
+// ---------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
+    const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
+    const __bf16* pack, const __bf16* pack3, const float* __restrict__ b1, const float* __restrict__ b2,
+    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
+  // ONE __shared__ object (see k_ln_mlp_fwd_x3b): [W1 hi|lo|lo2][W2 hi|lo|lo2] x 2, b1
+  __shared__ __attribute__((aligned(16))) __bf16 lds[12 * PLANE + 2 * GHM_F];
+  float* sb1 = reinterpret_cast<float*>(lds + 12 * PLANE);
+  auto s1 = [&](int buf, int q) { return lds + 6 * PLANE * buf + q * PLANE; };
+  auto s2 = [&](int buf, int q) { return lds + 6 * PLANE * buf + (3 + q) * PLANE; };
+  constexpr int NC = GHM_F / 32;
+  const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int64_t m = (static_cast<int64_t>(blockIdx.x) * NW + (threadIdx.x >> 6)) * 16 + t;
+  const bool valid = m < M;
+  const int64_t mc = valid ? m : M - 1;
+  const __bf16* W1 = pack + PK_W1_N;
+  const __bf16* W2 = pack + PK_W2_P32;
+  const __bf16* W1c = pack3;         // W1 lo2, [512][128]
+  const __bf16* W2c = pack3 + PK_W;  // W2 lo2, [128][512] perm32 columns
+  fill_r32_w8<NW>(W1, GHM_D, PK_W, s1(0, 0), s1(0, 1));
+  fill_r32_1<NW>(W1c, GHM_D, s1(0, 2));
+  fill_r128_w8<NW>(W2, GHM_F, PK_W, s2(0, 0), s2(0, 1));
+  fill_r128_1<NW>(W2c, GHM_F, s2(0, 2));
+  if (threadIdx.x < GHM_F / 4)
+    reinterpret_cast<float4*>(sb1)[threadIdx.x] = reinterpret_cast<const float4*>(b1)[threadIdx.x];
+  // LN2 of the token row, lane holds features 32s + 8g + i, split three ways
+  bf16x8 x0[4], x1[4], x2[4];
+  {
+    const float* row = Hmid + mc * GHM_D;
+    float x[32];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const float4 a = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g);
+      const float4 b = *reinterpret_cast<const float4*>(row + 32 * s2 + 8 * g + 4);
+      x[8 * s2 + 0] = a.x; x[8 * s2 + 1] = a.y; x[8 * s2 + 2] = a.z; x[8 * s2 + 3] = a.w;
+      x[8 * s2 + 4] = b.x; x[8 * s2 + 5] = b.y; x[8 * s2 + 6] = b.z; x[8 * s2 + 7] = b.w;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) sm += x[k];
+    sm += __shfl_xor(sm, 16, 64);
+    sm += __shfl_xor(sm, 32, 64);
+    const float mean = sm * (1.f / 128.f);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float d = x[k] - mean;
+      v += d * d;
+    }
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const float rstd = 1.f / sqrtf(v * (1.f / 128.f) + eps);
+    if (g == 0 && valid) stats[m] = make_float2(mean, rstd);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int f = 32 * s2 + 8 * g + i;
+        x[8 * s2 + i] = (x[8 * s2 + i] - mean) * rstd * lnw[f] + lnb[f];
+      }
+      split3_8(x + 8 * s2, x0[s2], x1[s2], x2[s2]);
+    }
+  }
+  f32x4 y[8];
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const float* hr = Hmid + mc * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * j + 4 * g;
+      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
+      y[j][0] = hv.x + bv.x;
+      y[j][1] = hv.y + bv.y;
+      y[j][2] = hv.z + bv.z;
+      y[j][3] = hv.w + bv.w;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+    const int cur = c & 1;
+    float4 bb[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) bb[jt] = lds4(sb1 + 32 * c + 16 * jt + 4 * g);
+    issue_fence();
+    {  // branch-free: the last iteration refills chunk NC-1 into the idle buffer
+      const int cn = c + 1 < NC ? c + 1 : NC - 1;
+      fill_r32_w8<NW>(W1 + cn * 32 * GHM_D, GHM_D, PK_W, s1(cur ^ 1, 0), s1(cur ^ 1, 1));
+      fill_r32_1<NW>(W1c + cn * 32 * GHM_D, GHM_D, s1(cur ^ 1, 2));
+      fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2(cur ^ 1, 0), s2(cur ^ 1, 1));
+      fill_r128_1<NW>(W2c + cn * 32, GHM_F, s2(cur ^ 1, 2));
+    }
+    // every six-product group starts from zero accumulators and is added to the
+    // running sum on the VALU (round to nearest): an MFMA adding small products into
+    // a large accumulator drops their low bits (measured against float64: seeded with
+    // the residual as k_ln_mlp_fwd_x3b is, 8.3e-6 -- the split-bf16 kernel's 1.1e-5
+    // level; zero-started groups 2.0e-6; the f32 kernel 1.05e-6)
+    f32x4 u[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      u[jt] = zero4();
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int o = r32_off(16 * jt + t, 4 * s2 + g);
+        u[jt] += mfma16_x6z(ldsb8(s1(cur, 0) + o), ldsb8(s1(cur, 1) + o), ldsb8(s1(cur, 2) + o), x0[s2], x1[s2],
+                            x2[s2]);
+      }
+    }
+    float gv[8];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      gv[4 * jt + 0] = gelu_f(u[jt][0] + bb[jt].x);
+      gv[4 * jt + 1] = gelu_f(u[jt][1] + bb[jt].y);
+      gv[4 * jt + 2] = gelu_f(u[jt][2] + bb[jt].z);
+      gv[4 * jt + 3] = gelu_f(u[jt][3] + bb[jt].w);
+    }
+    bf16x8 g0, g1, g2;
+    split3_8(gv, g0, g1, g2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = r128_off(16 * j + t, g);
+      y[j] += mfma16_x6z(ldsb8(s2(cur, 0) + o), ldsb8(s2(cur, 1) + o), ldsb8(s2(cur, 2) + o), g0, g1, g2);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (valid) {
+    float* orow = Hout + m * GHM_D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) st4(orow + 16 * j + 4 * g, y[j][0], y[j][1], y[j][2], y[j][3]);
+  }
+}
+
+// The lo2 planes of pack3 (the third split planes of the x6 kernels' weight images):
+// [0, PK_W): W1 in the pack's W1_N layout (row f, col d); [PK_W, 2 PK_W): W2 in its
+// W2_P32 layout (row o, col q = W2[o][perm32(q)]).  One thread per element of each.
+__device__ __forceinline__ __bf16 lo2_of(float v) {
+  const __bf16 a = static_cast<__bf16>(v);
+  const float r = v - static_cast<float>(a);
+  const __bf16 b = static_cast<__bf16>(r);
+  return static_cast<__bf16>(r - static_cast<float>(b));
+}
+// blocks [0, PK_W / 256): W1 and W2 element i; [PK_W / 256, + PK_QKV / 256): the
+// [Wq; Wk; Wv] image element i (row 128 mat + o, col d = W_mat[o][d])
+__global__ __launch_bounds__(256) void k_split3_weights(SplitJobs J) {
+  const ghm_split_job& jb = J.job[blockIdx.y];
+  __bf16* out = static_cast<__bf16*>(jb.pack);
+  if (blockIdx.x < PK_W / 256) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    out[PK3_W1_N + i] = lo2_of(jb.W1[i]);
+    out[PK3_W2_P32 + i] = lo2_of(jb.W2[(i >> 9) * GHM_F + perm32(i & 511)]);
+  } else {
+    const int i = (blockIdx.x - PK_W / 256) * 256 + threadIdx.x, r = i >> 7, mat = r >> 7;
+    const float* W = mat == 0 ? jb.Wq : (mat == 1 ? jb.Wk : jb.Wv);
+    out[PK3_QKV_N + i] = lo2_of(W[(r & 127) * GHM_D + (i & 127)]);
   }
 }
 
@@ -2767,6 +3044,46 @@ extern "C" int ghm_ln_mlp_fwd_x3b(const float* H_mid, const float* ln_w, const f
   else
     hipLaunchKernelGGL(k_ln_mlp_fwd_x3b<4>, g4, dim3(256), 0, s, H_mid, ln_w, ln_b, pk, b1, b2, H_out, st, M, eps,
                        nullptr);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_split3_weights(const ghm_split_job* jobs, int n_jobs, void* stream) {
+  GHM_CHECK(jobs && n_jobs >= 1 && n_jobs <= GHM_SPLIT_MAX_JOBS, "jobs");
+  SplitJobs J;
+  for (int i = 0; i < n_jobs; ++i) {
+    GHM_CHECK(jobs[i].Wq && jobs[i].Wk && jobs[i].Wv && jobs[i].W1 && jobs[i].W2 && jobs[i].pack,
+              "null pointer in job");
+    GHM_CHECK((reinterpret_cast<uintptr_t>(jobs[i].pack) & 15) == 0, "pack3 must be 16-byte aligned");
+    J.job[i] = jobs[i];
+  }
+  hipLaunchKernelGGL(k_split3_weights, dim3((PK_W + PK_QKV) / 256, static_cast<unsigned>(n_jobs)), dim3(256), 0,
+                     ghm_stream(stream), J);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_qkv_fwd_x6(const float* H, const float* ln_w, const float* ln_b, const void* pack,
+                                 const void* pack3, float* qkv, float* stats, int64_t M, int D, float eps,
+                                 void* stream) {
+  GHM_CHECK(H && ln_w && ln_b && pack && pack3 && qkv && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && M >= 1, "shape");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(pack) | reinterpret_cast<uintptr_t>(pack3)) & 15) == 0,
+            "16-byte aligned packs");
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x6, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+                     ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack),
+                     reinterpret_cast<const __bf16*>(pack3), qkv, reinterpret_cast<float2*>(stats), M, eps);
+  return ghm_launch_status();
+}
+
+extern "C" int ghm_ln_mlp_fwd_x6(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
+                                 const void* pack3, const float* b1, const float* b2, float* H_out, float* stats,
+                                 int64_t M, int D, int F, float eps, void* stream) {
+  GHM_CHECK(H_mid && ln_w && ln_b && pack && pack3 && b1 && b2 && H_out && stats, "null pointer");
+  GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(pack) | reinterpret_cast<uintptr_t>(pack3)) & 15) == 0,
+            "16-byte aligned packs");
+  hipLaunchKernelGGL(k_ln_mlp_fwd_x6<8>, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
+                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack),
+                     reinterpret_cast<const __bf16*>(pack3), b1, b2, H_out, reinterpret_cast<float2*>(stats), M, eps);
   return ghm_launch_status();
 }
 

@@ -29,6 +29,7 @@ class SplitJob(ctypes.Structure):
 
 
 GHM_SPLIT_PACK_ELEMS = 983040  # include/ghm_hip.h
+GHM_SPLIT3_PACK_ELEMS = 180224  # include/ghm_hip.h
 
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -119,6 +120,9 @@ HIP_SIGNATURES = {
     "ghm_ln_mlp_fwd_x3b": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_ln_qkv_fwd_x3s": [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
     "ghm_ln_mlp_fwd_x3bs": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_split3_weights": [_p, _i, _p],
+    "ghm_ln_qkv_fwd_x6": [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
+    "ghm_ln_mlp_fwd_x6": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_wgrad_x3p": [_p, _i, _i, _p, _i, _i, _i64, _p, _p, _i64, _i, _p],
     "ghm_mlp_bwd_rc_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_mlp_bwd_rc_x3_stamped": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p, _i, _p],

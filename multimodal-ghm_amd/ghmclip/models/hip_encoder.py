@@ -120,17 +120,27 @@ class EncoderPlan:
         # per step as for "x3")
         self.fwd_x3 = self.precision == "x3"
         self.bwd_x3 = self.precision in ("x3", "f32fwd")
-        # the forward stages on the exact-f32 kernels: all three for "f32"; for "f32fwd"
-        # $GHM_F32FWD (comma list of qkv / attn / mlp), the others on the split-bf16
-        # ones.  Default LN1 + QKV and LN2 + MLP: the guided 3001-step run needs both
-        # (worst ratio to its bound 0.377; mlp alone 4.96, attn + mlp 4.44, qkv + attn
-        # 4.22, all three 0.359; profiles/r6_f32mix_curves.txt)
+        # the forward stages kept at f32 accuracy: all three on the exact-f32 kernels for
+        # "f32"; for "f32fwd" $GHM_F32FWD, a comma list of qkv / attn / mlp (exact-f32
+        # kernels) or qkv6 / mlp6 (three-way split operands, six bf16 MFMAs per product:
+        # 2e-6 from float64 where the f32 kernel is at 1e-6 and x3 at 1e-5), the others
+        # split-bf16 x3.  The guided 3001-step run needs both projections' stages at f32
+        # accuracy (worst ratio to its bound: qkv,mlp 0.377, all three 0.359; mlp alone
+        # 4.96, attn + mlp 4.44, qkv + attn 4.22, profiles/r6_f32mix_curves.txt); default
+        # qkv6,mlp6: 0.499, guided step 4.72 ms against 5.44-5.68 for qkv,mlp
+        # (profiles/r6_x6_curves.txt, r6_x6_ab.txt)
         parts = {"qkv", "attn", "mlp"}
         if self.precision == "f32fwd":
-            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv,mlp").split(",") if q}
-            if not parts <= {"qkv", "attn", "mlp"}:
-                raise ValueError(f"GHM_F32FWD: comma list of qkv / attn / mlp (got {sorted(parts)})")
+            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv6,mlp6").split(",") if q}
+            if (not parts <= {"qkv", "qkv6", "attn", "mlp", "mlp6"} or {"mlp", "mlp6"} <= parts
+                    or {"qkv", "qkv6"} <= parts):
+                raise ValueError(f"GHM_F32FWD: comma list of qkv or qkv6 / attn / mlp or mlp6 (got {sorted(parts)})")
         self.fwd_f32 = frozenset() if self.fwd_x3 else frozenset(parts)
+        # mlp6 / qkv6: the LN2 + MLP / LN1 + QKV forward on three-way split operands
+        # (ghm_ln_mlp_fwd_x6 / ghm_ln_qkv_fwd_x6: near the exact-f32 level, on the bf16
+        # pipe), the weights' third planes in pack3
+        self.mlp6 = "mlp6" in self.fwd_f32
+        self.qkv6 = "qkv6" in self.fwd_f32
         if n_token > 192:
             raise ValueError(f"the HIP attention kernels take sequences of <= 192 tokens (got {n_token})")
         # sequences past 96 tokens (the joint CDM's 162) run on ghm_attn_ext_*_x3 with
@@ -247,6 +257,8 @@ class EncoderPlan:
         if self.bwd_x3:
             npk = int(_native.GHM_SPLIT_PACK_ELEMS)
             self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
+        self.pack3 = (torch.empty(L, int(_native.GHM_SPLIT3_PACK_ELEMS), dtype=torch.bfloat16, device=dev)
+                      if self.mlp6 or self.qkv6 else None)
         # pre-split LN outputs: xs[l][0] = LN1(H_l), xs[l][1] = LN2(Hmid_l), each the hi
         # plane [M][128] then the lo plane (bf16: the bytes of one f32 plane)
         if ln_presplit is None:
@@ -318,7 +330,10 @@ class EncoderPlan:
         c = _native.call
         M = self.M
         pk = _ptr(self.pack[l]) if self.bwd_x3 else None
-        if "qkv" in self.fwd_f32:
+        if self.qkv6:
+            c("ghm_ln_qkv_fwd_x6", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]), pk,
+              _ptr(self.pack3[l]), _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
+        elif "qkv" in self.fwd_f32:
             c("ghm_ln_qkv_fwd", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]),
               _ptr(p[f"_queries.{l}.weight"]), _ptr(p[f"_keys.{l}.weight"]), _ptr(p[f"_values.{l}.weight"]),
               _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
@@ -330,6 +345,11 @@ class EncoderPlan:
             c("ghm_ln_qkv_fwd_x3", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]),
               _ptr(p[f"_lns_1.{l}.bias"]), pk, _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
         self._attn_fwd(l, s)
+        if self.mlp6:
+            c("ghm_ln_mlp_fwd_x6", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), pk,
+              _ptr(self.pack3[l]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]),
+              _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+            return
         if "mlp" in self.fwd_f32:
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),
               _ptr(p[f"_mlps.{l}.0.weight"]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.weight"]),
@@ -454,6 +474,12 @@ class EncoderPlan:
         for a in range(0, len(jobs), 16):
             chunk = jobs[a:a + 16]
             _native.call("ghm_split_weights", (_native.SplitJob * len(chunk))(*chunk), len(chunk), s)
+        if self.pack3 is not None:  # the weights' third planes for the x6 kernels
+            for j, l in zip(jobs, range(self.L)):
+                j.pack = self.pack3[l].data_ptr()
+            for a in range(0, len(jobs), 16):
+                chunk = jobs[a:a + 16]
+                _native.call("ghm_split3_weights", (_native.SplitJob * len(chunk))(*chunk), len(chunk), s)
 
     # ------------------------------------------------------------------
     @staticmethod

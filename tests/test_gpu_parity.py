@@ -136,6 +136,64 @@ def test_encoder_backward(T, nseq, precision):
         assert _rel(pp.grad, pr.grad) < GRAD_TOL[precision], k
 
 
+@pytest.mark.parametrize("stages", ["qkv,mlp6", "qkv6,mlp6"])
+@pytest.mark.parametrize("T,nseq", [(81, 20), (27, 33)])
+def test_mlp6_forward_and_backward(T, nseq, stages, monkeypatch):
+    """precision "f32fwd" with $GHM_F32FWD = qkv,mlp6 / qkv6,mlp6: the LN2 + MLP (and
+    LN1 + QKV) forward on three-way split operands (ghm_ln_mlp_fwd_x6 /
+    ghm_ln_qkv_fwd_x6, six bf16 MFMAs per product) --
+    every forward stage within the exact-f32 bound of the float64 oracle (2e-5),
+    and the LN2 + MLP output within 3x the f32 kernel's distance from a float64
+    evaluation and at a third of the split-bf16 kernel's or less;
+    every gradient within the split-bf16 backward's bound (5e-4)."""
+    monkeypatch.setenv("GHM_F32FWD", stages)
+    prod, ref = _pair(L=2, T=T, precision="f32fwd")
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(0, 10, (nseq, T), generator=g)
+    R = torch.randn(nseq, 10, generator=g)
+    emb, _ = prod(x.to(DEV))
+    torch.cuda.synchronize()
+    plan = next(iter(prod._plans.values()))
+    assert plan.mlp6 and plan.pack3 is not None and plan.qkv6 == ("qkv6" in stages)
+    want = _oracle_intermediates(ref, x)
+    M = nseq * T
+    for l in range(2):
+        assert _rel(plan.qkv[l].view(nseq, T, 384), want["qkv"][l]) < FWD_TOL["f32"], f"qkv[{l}]"
+        assert _rel(plan.Hmid[l].view(nseq, T, 128), want["Hmid"][l]) < FWD_TOL["f32"], f"Hmid[{l}]"
+        assert _rel(plan.H[l + 1][:M].view(nseq, T, 128), want["H"][l + 1]) < FWD_TOL["f32"], f"H[{l + 1}]"
+    # the x6 MLP output against the f32 kernel on the same input (layer 0)
+    from ghmclip import _native
+    import ctypes
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    pd = dict(prod.named_parameters())
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out32, out3 = torch.empty_like(plan.H[1]), torch.empty_like(plan.H[1])
+    st = torch.empty_like(plan.st2[0])
+    _native.call("ghm_ln_mlp_fwd", P(plan.Hmid[0]), P(pd["_lns_2.0.weight"]), P(pd["_lns_2.0.bias"]),
+                 P(pd["_mlps.0.0.weight"]), P(pd["_mlps.0.0.bias"]), P(pd["_mlps.0.2.weight"]), P(pd["_mlps.0.2.bias"]),
+                 P(out32), None, None, P(st), M, 128, 512, plan.eps, sp)
+    _native.call("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[0]), P(pd["_lns_2.0.weight"]), P(pd["_lns_2.0.bias"]),
+                 P(plan.pack[0]), P(pd["_mlps.0.0.bias"]), P(pd["_mlps.0.2.bias"]), P(out3), P(st), M, 128, 512,
+                 plan.eps, sp)
+    torch.cuda.synchronize()
+    # float64 LN2 + MLP of the same Hmid: the x6 kernel at the f32 kernel's distance from it
+    hm = plan.Hmid[0][:M].double()
+    mu, var = hm.mean(-1, keepdim=True), hm.var(-1, unbiased=False, keepdim=True)
+    xn = (hm - mu) / torch.sqrt(var + 1e-5) * pd["_lns_2.0.weight"].double() + pd["_lns_2.0.bias"].double()
+    u = xn @ pd["_mlps.0.0.weight"].double().T + pd["_mlps.0.0.bias"].double()
+    want64 = hm + torch.nn.functional.gelu(u) @ pd["_mlps.0.2.weight"].double().T + pd["_mlps.0.2.bias"].double()
+    dev = {k: (v[:M].double() - want64).abs().max().item() for k, v in
+           (("x6", plan.H[1]), ("f32", out32), ("x3", out3))}
+    print(f"LN2 + MLP forward vs float64: {dev}")
+    # measured: x6 2.0e-6 / 2.1e-6, f32 1.05e-6 / 0.87e-6, x3 1.07e-5 / 8.7e-6
+    assert dev["x6"] < 3 * dev["f32"] and dev["x6"] < dev["x3"] / 3
+    (emb * R.to(DEV)).sum().backward()
+    (ref(x)[0] * R).sum().backward()
+    torch.cuda.synchronize()
+    for (k, pp), (_, pr) in zip(prod.named_parameters(), ref.named_parameters()):
+        assert _rel(pp.grad, pr.grad) < GRAD_TOL["f32fwd"], k
+
+
 def test_clip_loss_and_grad():
     from ghmclip import GuidedClipLoss
     B, K = 16, 4

@@ -12,7 +12,7 @@ shift
 mkdir -p $OUT
 for v in "$@"; do
   GHM_F32FWD=$v timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-    "tests/test_gpu_parity.py::test_guided_full_run_final_risk_vs_reference_cpu_run[f32fwd]" -s > $OUT/tests_$v.log 2>&1
+    "tests/test_gpu_parity.py::test_guided_full_run_final_risk_vs_reference_cpu_run[None]" -s > $OUT/tests_$v.log 2>&1
   rc=$?
   echo "$v rc=$rc $(grep -o 'worst ratio[^;]*' $OUT/tests_$v.log) $(grep -o 'final risk [0-9.]* vs reference CPU run [0-9.]* (rel [0-9.e-]*)' $OUT/tests_$v.log)"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 2

@@ -91,13 +91,29 @@ def main():
         pk = P(plan.pack[l])
         xo = {"H": torch.empty_like(plan.H[l + 1]), "st": torch.empty_like(plan.st2[l]),
               "G": torch.empty(M, 512, device=plan.H.device), "Dg": torch.empty(M, 512, device=plan.H.device),
-              "dHm": torch.empty_like(plan.H[l + 1])}
+              "dHm": torch.empty_like(plan.H[l + 1]),
+              "pack3": torch.empty(_native.GHM_SPLIT3_PACK_ELEMS, dtype=torch.bfloat16, device=plan.H.device)}
+        # the pre-split LN planes (the plan's own when GHM_LN_PRESPLIT=1)
+        xs = plan.xs[l] if plan.xs is not None else torch.zeros(2, 2, M, 128, dtype=torch.bfloat16,
+                                                                 device=plan.H.device)
+        j3 = _native.SplitJob()
+        j3.Wq, j3.Wk, j3.Wv = (p[f"_{k}.0.weight"].data_ptr() for k in ("queries", "keys", "values"))
+        j3.W1, j3.W2, j3.pack = p["_mlps.0.0.weight"].data_ptr(), p["_mlps.0.2.weight"].data_ptr(), xo["pack3"].data_ptr()
+        c("ghm_split3_weights", (_native.SplitJob * 1)(j3), 1, sp)
         kernels.update({
             "ln_qkv_fwd_x3": (lambda: c("ghm_ln_qkv_fwd_x3", P(plan.H[l]), P(p["_lns_1.0.weight"]),
                                         P(p["_lns_1.0.bias"]), pk, P(plan.qkv[l]), P(plan.st1[l]), M, 128, plan.eps,
                                         sp), gf(2 * M * 128 * 384)),
             "attn_fwd_x3": (lambda: c("ghm_attn_fwd_x3", P(plan.qkv[l]), P(plan.H[l]), P(plan.Hmid[l]), P(plan.P[l]),
                                       N, T, 128, plan.scale_div, sp), gf(4 * N * T * T * 128)),
+            # three-way split operands (precision f32fwd's mlp6 stage): pack3 of layer 0
+            "ln_mlp_fwd_x6": (lambda: c("ghm_ln_mlp_fwd_x6", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
+                                        P(p["_lns_2.0.bias"]), pk, P(xo["pack3"]), P(p["_mlps.0.0.bias"]),
+                                        P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp),
+                              gf(4 * M * 128 * 512)),
+            "ln_qkv_fwd_x6": (lambda: c("ghm_ln_qkv_fwd_x6", P(plan.H[l]), P(p["_lns_1.0.weight"]),
+                                        P(p["_lns_1.0.bias"]), pk, P(xo["pack3"]), P(plan.qkv[l]), P(plan.st1[l]), M,
+                                        128, plan.eps, sp), gf(2 * M * 128 * 384)),
             "ln_mlp_fwd_x3b": (lambda: c("ghm_ln_mlp_fwd_x3b", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                          P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
                                          P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp),
@@ -139,9 +155,9 @@ def main():
                                        P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
             # round 6: the weight gradients on the forward's pre-split LN outputs (ghm_wgrad_x3p),
             # and the forward kernels that write them
-            "wgrad_w1_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dU), 512, 512, P(plan.xs[l, 1]), 128, 128, M * 128,
+            "wgrad_w1_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dU), 512, 512, P(xs[1]), 128, 128, M * 128,
                                        P(plan.part_w1), P(plan.part_b1), M, tps_w1, sp), gf(2 * M * 128 * 512)),
-            "wgrad_qkv_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dqkv), 384, 384, P(plan.xs[l, 0]), 128, 128, M * 128,
+            "wgrad_qkv_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.dqkv), 384, 384, P(xs[0]), 128, 128, M * 128,
                                         P(plan.part_wq), None, M, tps_q, sp), gf(2 * M * 128 * 384)),
             "mlp_bwd_rc_x3g": (lambda: c("ghm_mlp_bwd_rc_x3", P(plan.H[l + 1]), P(plan.Hmid[l]), P(plan.st2[l]),
                                          P(p["_lns_2.0.weight"]), P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]),
@@ -150,11 +166,11 @@ def main():
             "wgrad_w2_x3p": (lambda: c("ghm_wgrad_x3p", P(plan.H[l + 1]), 128, 128, P(plan.G), 512, 512, M * 512,
                                        P(plan.part_w2), P(plan.part_b2), M, tps_w2, sp), gf(2 * M * 128 * 512)),
             "ln_qkv_fwd_x3s": (lambda: c("ghm_ln_qkv_fwd_x3s", P(plan.H[l]), P(p["_lns_1.0.weight"]),
-                                         P(p["_lns_1.0.bias"]), pk, P(plan.qkv[l]), P(plan.st1[l]), P(plan.xs[l, 0]),
+                                         P(p["_lns_1.0.bias"]), pk, P(plan.qkv[l]), P(plan.st1[l]), P(xs[0]),
                                          M, 128, plan.eps, sp), gf(2 * M * 128 * 384)),
             "ln_mlp_fwd_x3bs": (lambda: c("ghm_ln_mlp_fwd_x3bs", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                           P(p["_lns_2.0.bias"]), pk, P(p["_mlps.0.0.bias"]), P(p["_mlps.0.2.bias"]),
-                                          P(xo["H"]), P(xo["st"]), P(plan.xs[l, 1]), M, 128, 512, plan.eps, sp),
+                                          P(xo["H"]), P(xo["st"]), P(xs[1]), M, 128, 512, plan.eps, sp),
                                 gf(4 * M * 128 * 512)),
             # the ring weight gradients (ghm_wgrad_ring_x3) on the MLP backward's split G / dU planes
             "wgrad_ring_w2": (lambda: c("ghm_wgrad_ring_x3", P(plan.H[l + 1]), 128, 128, 0, 0, P(plan.G), 512, 512,
