@@ -877,7 +877,9 @@ def main_cdm(a, ws, rank):
         "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True,
         "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
-        "dtype": "f32" if tr.precision == "f32" else "f32 (split-bf16 x3 MFMA, f32 accumulate)",
+        "dtype": ("f32" if tr.precision == "f32" else
+                  "f32 (f32fwd: the LN + QKV / LN + MLP forwards on three-way split-bf16 MFMA, the rest split-bf16 x3)"
+                  if tr.precision == "f32fwd" else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
         "data": f"synthetic GHM draws (native ConditionalDenoiseSampler, p=0.2, sigma=1), ring of {a.ring} "
                 f"batches resident in HBM",
         "config": {"workload": (f"cdm_joint: ConditionalDenoiseEncoderTransformer(L={L}, d=128, T=162 = 81 text "

@@ -153,6 +153,8 @@ class CdmPlan(EncoderPlan):
         # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
         # on the split-bf16 attention kernels (EncoderPlan: one-sequence up to 96 tokens,
         # the multi-workgroup ghm_attn_ext_*_act past 96, the joint model's 162)
+        if precision == "f32fwd" and not layernorm:
+            raise NotImplementedError("precision f32fwd: the LayerNorm-fused forward kernels (layernorm=True)")
         super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
                          normalize_attn=normalize_attn, device=device, precision=precision, activation=activation)
         if not 1 <= n_i_token <= n_token:
@@ -177,7 +179,7 @@ class CdmPlan(EncoderPlan):
         """z: f32 [N, T_img] noisy observations; cond: f32 [N, T - T_img, cond_ld]
         conditioning features (first V used).  Returns self.pred [N, T_img]."""
         s = _stream()
-        if self.precision == "x3" and split and self.layernorm:
+        if self.bwd_x3 and split and self.layernorm:
             self.split_weights(p, s)
         if self.joint:  # cond unused: self.tok holds the text leaves
             _native.call("ghm_cdm_embed_joint_fwd", _ptr(z), _ptr(self.tok), _ptr(p["t_embedding.weight"]),
