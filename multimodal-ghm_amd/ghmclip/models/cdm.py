@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from .hip_encoder import D_HIDDEN, D_MODEL, EncoderPlan, default_precision, require_hip
+from .hip_encoder import D_HIDDEN, D_MODEL, ENCODER_PRECISIONS, EncoderPlan, default_precision, require_hip
 from .vlm import EPI_GELU, EPI_MUL, EPI_RESID, EPI_SLAB, EPI_STORE, _gemm
 
 __all__ = ["ConditionalDenoiseEncoderTransformer", "ConditionalGuidedLsLoss", "LsLoss", "CdmPlan",
@@ -149,7 +149,7 @@ class CdmPlan(EncoderPlan):
             # LayerNorm (un-normalised scores on un-normalised activations: an MLP
             # weight gradient 6.2e-4 off at x3 against the 5e-4 bound)
             f32_default = joint or (activation != "softmax" and not layernorm)
-            precision = default_precision("f32" if f32_default else "x3")
+            precision = default_precision("f32" if f32_default else "x3", allowed=ENCODER_PRECISIONS)
         # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
         # on the split-bf16 attention kernels (EncoderPlan: one-sequence up to 96 tokens,
         # the multi-workgroup ghm_attn_ext_*_act past 96, the joint model's 162)
