@@ -311,7 +311,7 @@ def pmc_traffic(kernel, fname="traffic.json"):
     with open(path) as f:
         t = json.load(f)
     ks = t.get("kernels", {})
-    for suffix in ("", "<8>", "<8, 0>", "<8, false>", "<8, 0, false>", "<true>"):  # the instantiation the step launches (NW = 8)
+    for suffix in ("", "<8>", "<8, 0>", "<8, false>", "<8, 0, false>", "<8, 0, 0>", "<true>"):  # the instantiation the step launches (NW = 8)
         if kernel + suffix in ks:
             return ks[kernel + suffix]["hbm_bytes"]
     return None
