@@ -11,6 +11,7 @@ embedding (continuous leaf features), the Linear(d -> 1) readout and the
 position-embedding gradient (csrc/ghm_cdm.hip).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -39,6 +40,18 @@ def cdm_untrained(model):
         names = names + tuple(f"_lns_{k}.{l}.{w}" for k in (1, 2) for l in range(model.n_layer)
                               for w in ("weight", "bias"))
     return names
+
+
+def cdm_precision(precision, joint, guide, layernorm):
+    """The CDM's matrix-product mode: an explicit `precision` (or $GHM_PRECISION)
+    wins; else the unguided joint model with LayerNorm runs "f32fwd" (the LN + QKV /
+    LN + MLP forwards on the f32-accurate three-way split kernels, the rest
+    split-bf16: its reference curve at f32's distance, 4.66 -> 3.22 ms per step,
+    DESIGN.md section 4b) and everything else CdmPlan's default (exact f32 for the
+    guided joint model, whose lr-1e-2 curve needs an f32 backward)."""
+    if precision is None and joint and not guide and layernorm and "GHM_PRECISION" not in os.environ:
+        return "f32fwd"
+    return precision
 
 
 class NoLnLayers:
@@ -350,8 +363,10 @@ class ConditionalDenoiseEncoderTransformer(nn.Module):
             self._plans.clear()
             self._plans[key] = CdmPlan(self.n_layer, T, T_img, n_seq, num_class=self.vocab_size,
                                        n_embd=self.n_embd, normalize_attn=self.normalize_attn, device=device,
-                                       precision=self.precision, joint=not self.sequential,
-                                       activation=self.activation, layernorm=self.layernorm)
+                                       precision=cdm_precision(self.precision, not self.sequential,
+                                                               getattr(self, "guide", False), self.layernorm),
+                                       joint=not self.sequential, activation=self.activation,
+                                       layernorm=self.layernorm)
         return self._plans[key]
 
     def forward(self, xt, zi):

@@ -21,7 +21,6 @@ Data parallel (optional): the loss is a mean over samples, so ranks take equal
 row shards and average gradients with one RCCL all-reduce.
 """
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -29,7 +28,7 @@ import torch
 from ..data.data_random_GHM import DeviceTree
 from .. import _native
 from . import distributed
-from ..models.cdm import CdmPlan, cdm_guide_blocks, cdm_untrained
+from ..models.cdm import CdmPlan, cdm_guide_blocks, cdm_precision, cdm_untrained
 from ..models.gemm_encoder import make_encoder_plan
 from ..models.hip_encoder import require_hip
 from ..models.optimizer import adam_consts, adam_lr_t
@@ -87,14 +86,11 @@ class CdmTrainer:
         self.clip_p = None if self.joint else {k: v.data for k, v in clip_model.named_parameters()}
         T, Ti = model.n_token, model.n_i_token
         self.T, self.Ti = T, Ti
-        if (precision is None and self.joint and not getattr(model, "guide", False)
-                and getattr(model, "layernorm", True) and "GHM_PRECISION" not in os.environ):
-            # the unguided joint model: its f32 default's accuracy from the forward alone
-            # (the f32-accurate x6 LN + QKV / LN + MLP kernels, the rest split-bf16): the
-            # 30-step reference curve at f32's distance (7.8e-6 / 1.5e-5 against 7.2e-6 /
-            # 1.4e-5), step 4.66 -> 3.22 ms.  The guided joint model (lr 1e-2) keeps f32:
-            # there the split-bf16 backward leaves its bound
-            precision = "f32fwd"
+        # the unguided joint model: "f32fwd" (its 30-step reference curve at f32's
+        # distance, 7.8e-6 / 1.5e-5 against 7.2e-6 / 1.4e-5; step 4.66 -> 3.22 ms); the
+        # guided one (lr 1e-2) keeps exact f32 (models/cdm.py cdm_precision)
+        precision = cdm_precision(precision, self.joint, getattr(model, "guide", False),
+                                  getattr(model, "layernorm", True))
         self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,
                             normalize_attn=model.normalize_attn, device=self.device, precision=precision,
                             joint=self.joint, activation=getattr(model, "activation", "softmax"),

@@ -166,8 +166,9 @@ def test_joint_cdm_graph_replay_matches_eager():
 
 
 def test_joint_trainer_default_precision(monkeypatch):
-    """CdmTrainer(precision=None): the unguided joint model runs "f32fwd" (its curve
-    at f32's distance from the reference, below), the guided one exact f32."""
+    """precision None (CdmTrainer and the module API): the unguided joint model runs
+    "f32fwd" (its curve at f32's distance from the reference, below), the guided one
+    exact f32."""
     from ghmclip import ConditionalDenoiseEncoderTransformer, get_lr_cosine_schedule
     from ghmclip.training.cdm_trainer import CdmTrainer
     from ghmclip import ConditionalDenoiseSampler
@@ -177,6 +178,7 @@ def test_joint_trainer_default_precision(monkeypatch):
     for guide, want in ((False, "f32fwd"), (True, "f32")):
         model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 9, [4, 4], 4, 512, sequential=False,
                                                      guide=guide).to(DEV)
+        assert model._plan(20, 162, 81, torch.device(DEV)).precision == want  # the module API agrees
         tr = CdmTrainer(model, None, 4, sched, s.t_templ, s.i_templ, sigma=1.0, device=DEV)
         assert tr.precision == want, (guide, tr.precision)
 
