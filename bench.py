@@ -225,7 +225,8 @@ def dominant_kernel(trainer):
         def launch():
             _native.call("ghm_ln_mlp_fwd_x6", ptr(plan.Hmid[0]), ptr(pd["_lns_2.0.weight"]), ptr(pd["_lns_2.0.bias"]),
                          ptr(plan.pack[0]), ptr(plan.pack3[0]), ptr(pd["_mlps.0.0.bias"]), ptr(pd["_mlps.0.2.bias"]),
-                         ptr(plan.H[1]), ptr(plan.st2[0]), plan.M, 128, 512, plan.eps, sp)
+                         ptr(plan.H[1]), ptr(plan.st2[0]), None if plan.mlp_rc else ptr(plan.G[0]),
+                         None if plan.mlp_rc else ptr(plan.Dg[0]), plan.M, 128, 512, plan.eps, sp)
         return "k_ln_mlp_fwd_x6", launch
     if mlp_x3 and getattr(plan, "ln_presplit", False):
         # the launch the step makes: the LN2 rows also written pre-split for dW1
@@ -612,7 +613,7 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: the global batch of 128 rows split over the ranks (128 / N rows per rank; "
                          "default: weak scaling, --batch rows per rank)")
-    ap.add_argument("--precision", default=None, choices=["f32", "x3", "f32fwd"],
+    ap.add_argument("--precision", default=None, choices=["f32", "x3", "f32fwd", "f32x6"],
                     help="matrix products: exact-f32 MFMA or split-bf16 (x3) MFMA (default $GHM_PRECISION or x3); "
                          "f32fwd (CLIP only): the forward exact f32, the backward split-bf16")
     a = ap.parse_args()
@@ -774,9 +775,10 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if a.strong else "weak",
         "vs_baseline": None,
-        "dtype": (f"f32 (f32fwd: forward stages {fwd_f32} at f32 accuracy -- qkv / attn / mlp exact-f32 MFMA, "
-                  f"qkv6 / mlp6 three-way split-bf16 (six products); the rest of the forward and the backward "
-                  f"split-bf16 x3)" if precision == "f32fwd"
+        "dtype": (f"f32 ({precision}: forward stages {fwd_f32} at f32 accuracy -- qkv / attn / mlp exact-f32 MFMA, "
+                  f"qkv6 / mlp6 three-way split-bf16 (six products); the rest of the forward split-bf16 x3, the "
+                  f"backward {'split-bf16 x3' if precision == 'f32fwd' else 'exact-f32 MFMA'})"
+                  if precision in ("f32fwd", "f32x6")
                   else "f32" if not x3 else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
         "data": f"synthetic GHM draws (native sampler, p=0.2), ring of {a.ring} batches resident in HBM",
         "config": {"workload": ("clip_guided: " if a.guide else "clip_default: ")
@@ -790,8 +792,8 @@ def main():
         "sequences_per_s": round(samples * 10 / elapsed, 1),
         "dist": comm,
         "step_tflops": round(step_gflop * ws * steps_per_s / 1e3, 2),
-        "step_mfma_frac": None if precision == "f32fwd" else round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
-        "step_mfma_basis": ("f32fwd mixes f32, x3 and x6 products: no single count" if precision == "f32fwd" else
+        "step_mfma_frac": None if precision in ("f32fwd", "f32x6") else round(mult * step_gflop * steps_per_s / 1e3 / peak, 4),
+        "step_mfma_basis": ("f32fwd mixes f32, x3 and x6 products: no single count" if precision in ("f32fwd", "f32x6") else
                             f"{'3 x ' if x3 else ''}{step_gflop:.2f} GFLOP per step per GPU vs {peak} TFLOP/s"),
         "step_hbm": None if step_bytes is None else {
             "bytes": round(step_bytes * scale), "gbs": round(step_bytes * scale / (ms * 1e-3) / 1e9, 1),
@@ -879,7 +881,9 @@ def main_cdm(a, ws, rank):
         "vs_baseline": None,
         "dtype": ("f32" if tr.precision == "f32" else
                   "f32 (f32fwd: the LN + QKV / LN + MLP forwards on three-way split-bf16 MFMA, the rest split-bf16 x3)"
-                  if tr.precision == "f32fwd" else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
+                  if tr.precision == "f32fwd" else
+                  "f32 (f32x6: the LN + QKV / LN + MLP forwards on three-way split-bf16 MFMA, the backward exact-f32 "
+                  "MFMA)" if tr.precision == "f32x6" else "f32 (split-bf16 x3 MFMA, f32 accumulate)"),
         "data": f"synthetic GHM draws (native ConditionalDenoiseSampler, p=0.2, sigma=1), ring of {a.ring} "
                 f"batches resident in HBM",
         "config": {"workload": (f"cdm_joint: ConditionalDenoiseEncoderTransformer(L={L}, d=128, T=162 = 81 text "

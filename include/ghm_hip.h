@@ -240,10 +240,12 @@ int ghm_ln_qkv_fwd_x6(const float* H, const float* ln_w, const float* ln_b, cons
                       float* qkv, float* stats, int64_t M, int D, float eps, void* stream);
 /* ghm_ln_mlp_fwd_x3b with every product on three-way split operands (six bf16
  * MFMAs, ~2^-24 relative: the exact-f32 level) and the exact GELU; pack3 from
- * ghm_split3_weights (precision "f32fwd", $GHM_F32FWD mlp6; round 6). */
+ * ghm_split3_weights (precision "f32fwd", $GHM_F32FWD mlp6; round 6).  G / Dg
+ * (both or neither): also saves GELU(U) and GELU'(U) [M][F] as ghm_ln_mlp_fwd does,
+ * for the exact-f32 backward (precision "f32x6"). */
 int ghm_ln_mlp_fwd_x6(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
-                      const void* pack3, const float* b1, const float* b2, float* H_out, float* stats, int64_t M,
-                      int D, int F, float eps, void* stream);
+                      const void* pack3, const float* b1, const float* b2, float* H_out, float* stats, float* G,
+                      float* Dg, int64_t M, int D, int F, float eps, void* stream);
 /* MLP + LN2 backward with the up-projection recomputed from H_mid and the LN2
  * stats of the forward (which then saves no [M][F] tensor): writes G = GELU(U)
  * and dU = (dH_out W2) * GELU'(U) [M][F] (inputs of the dW2 / dW1 reductions),

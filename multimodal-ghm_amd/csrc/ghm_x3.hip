@@ -601,11 +601,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
 // by ghm_split3_weights); the LDS ring holds six planes per buffer (96 KB
 // double-buffered): one 8-wave workgroup per CU.
 // ---------------------------------------------------------------------------
-template <int NW>
+// SAVE: also store G = GELU(U) and Dg = GELU'(U) [M][512] (f32, natural columns) for
+// an exact-f32 backward (ghm_mlp_bwd; precision "f32x6")
+template <int NW, bool SAVE>
 __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
     const float* __restrict__ Hmid, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const __bf16* pack3, const float* __restrict__ b1, const float* __restrict__ b2,
-    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps) {
+    float* __restrict__ Hout, float2* __restrict__ stats, int64_t M, float eps, float* __restrict__ G,
+    float* __restrict__ Dg) {
   // ONE __shared__ object (see k_ln_mlp_fwd_x3b): [W1 hi|lo|lo2][W2 hi|lo|lo2] x 2, b1
   __shared__ __attribute__((aligned(16))) __bf16 lds[12 * PLANE + 2 * GHM_F];
   float* sb1 = reinterpret_cast<float*>(lds + 12 * PLANE);
@@ -711,12 +714,30 @@ __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
       }
     }
     float gv[8];
+    if constexpr (SAVE) {  // gv[4 jt + r] is unit 32c + 16 jt + 4g + r of token m
+      float dv[8];
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      gv[4 * jt + 0] = gelu_f(u[jt][0] + bb[jt].x);
-      gv[4 * jt + 1] = gelu_f(u[jt][1] + bb[jt].y);
-      gv[4 * jt + 2] = gelu_f(u[jt][2] + bb[jt].z);
-      gv[4 * jt + 3] = gelu_f(u[jt][3] + bb[jt].w);
+      for (int jt = 0; jt < 2; ++jt) {
+        const float bs[4] = {bb[jt].x, bb[jt].y, bb[jt].z, bb[jt].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gelu_and_grad(u[jt][r] + bs[r], gv[4 * jt + r], dv[4 * jt + r]);
+      }
+      if (valid) {
+        float* grow = G + m * GHM_F + 32 * c + 4 * g;
+        float* drow = Dg + m * GHM_F + 32 * c + 4 * g;
+        st4(grow, gv[0], gv[1], gv[2], gv[3]);
+        st4(grow + 16, gv[4], gv[5], gv[6], gv[7]);
+        st4(drow, dv[0], dv[1], dv[2], dv[3]);
+        st4(drow + 16, dv[4], dv[5], dv[6], dv[7]);
+      }
+    } else {
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        gv[4 * jt + 0] = gelu_f(u[jt][0] + bb[jt].x);
+        gv[4 * jt + 1] = gelu_f(u[jt][1] + bb[jt].y);
+        gv[4 * jt + 2] = gelu_f(u[jt][2] + bb[jt].z);
+        gv[4 * jt + 3] = gelu_f(u[jt][3] + bb[jt].w);
+      }
     }
     bf16x8 g0, g1, g2;
     split3_8(gv, g0, g1, g2);
@@ -3076,14 +3097,23 @@ extern "C" int ghm_ln_qkv_fwd_x6(const float* H, const float* ln_w, const float*
 
 extern "C" int ghm_ln_mlp_fwd_x6(const float* H_mid, const float* ln_w, const float* ln_b, const void* pack,
                                  const void* pack3, const float* b1, const float* b2, float* H_out, float* stats,
-                                 int64_t M, int D, int F, float eps, void* stream) {
+                                 float* G, float* Dg, int64_t M, int D, int F, float eps, void* stream) {
   GHM_CHECK(H_mid && ln_w && ln_b && pack && pack3 && b1 && b2 && H_out && stats, "null pointer");
+  GHM_CHECK((G != nullptr) == (Dg != nullptr), "G and Dg: both saved or neither");
   GHM_CHECK(D == GHM_D && F == GHM_F && M >= 1, "shape (D == 128, F == 512)");
-  GHM_CHECK(((reinterpret_cast<uintptr_t>(pack) | reinterpret_cast<uintptr_t>(pack3)) & 15) == 0,
-            "16-byte aligned packs");
-  hipLaunchKernelGGL(k_ln_mlp_fwd_x6<8>, dim3(static_cast<unsigned>((M + 127) / 128)), dim3(512), 0,
-                     ghm_stream(stream), H_mid, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack),
-                     reinterpret_cast<const __bf16*>(pack3), b1, b2, H_out, reinterpret_cast<float2*>(stats), M, eps);
+  GHM_CHECK(((reinterpret_cast<uintptr_t>(pack) | reinterpret_cast<uintptr_t>(pack3) |
+              reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(Dg)) & 15) == 0,
+            "16-byte aligned packs and G / Dg");
+  const dim3 grid(static_cast<unsigned>((M + 127) / 128));
+  const __bf16* pk = reinterpret_cast<const __bf16*>(pack);
+  const __bf16* pk3 = reinterpret_cast<const __bf16*>(pack3);
+  float2* st = reinterpret_cast<float2*>(stats);
+  if (G)
+    hipLaunchKernelGGL((k_ln_mlp_fwd_x6<8, true>), grid, dim3(512), 0, ghm_stream(stream), H_mid, ln_w, ln_b, pk, pk3,
+                       b1, b2, H_out, st, M, eps, G, Dg);
+  else
+    hipLaunchKernelGGL((k_ln_mlp_fwd_x6<8, false>), grid, dim3(512), 0, ghm_stream(stream), H_mid, ln_w, ln_b, pk,
+                       pk3, b1, b2, H_out, st, M, eps, nullptr, nullptr);
   return ghm_launch_status();
 }
 

@@ -122,7 +122,7 @@ HIP_SIGNATURES = {
     "ghm_ln_mlp_fwd_x3bs": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_split3_weights": [_p, _i, _p],
     "ghm_ln_qkv_fwd_x6": [_p, _p, _p, _p, _p, _p, _p, _i64, _i, _f, _p],
-    "ghm_ln_mlp_fwd_x6": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
+    "ghm_ln_mlp_fwd_x6": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _f, _p],
     "ghm_wgrad_x3p": [_p, _i, _i, _p, _i, _i, _i64, _p, _p, _i64, _i, _p],
     "ghm_mlp_bwd_rc_x3": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p],
     "ghm_mlp_bwd_rc_x3_stamped": [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i, _i, _i, _p, _i, _p],

@@ -44,13 +44,14 @@ def cdm_untrained(model):
 
 def cdm_precision(precision, joint, guide, layernorm):
     """The CDM's matrix-product mode: an explicit `precision` (or $GHM_PRECISION)
-    wins; else the unguided joint model with LayerNorm runs "f32fwd" (the LN + QKV /
-    LN + MLP forwards on the f32-accurate three-way split kernels, the rest
-    split-bf16: its reference curve at f32's distance, 4.66 -> 3.22 ms per step,
-    DESIGN.md section 4b) and everything else CdmPlan's default (exact f32 for the
-    guided joint model, whose lr-1e-2 curve needs an f32 backward)."""
-    if precision is None and joint and not guide and layernorm and "GHM_PRECISION" not in os.environ:
-        return "f32fwd"
+    wins; else the joint model with LayerNorm runs the LN + QKV / LN + MLP forwards
+    on the f32-accurate three-way split kernels and, unguided, the rest split-bf16
+    ("f32fwd": its reference curve at f32's distance, 4.66 -> 3.22 ms per step) or,
+    guided (lr 1e-2, whose curve needs an f32 backward), the backward exact f32
+    ("f32x6": 4.91 -> 4.37 ms, its curve inside the f32 bound); everything else
+    CdmPlan's default."""
+    if precision is None and joint and layernorm and "GHM_PRECISION" not in os.environ:
+        return "f32x6" if guide else "f32fwd"
     return precision
 
 
@@ -166,8 +167,8 @@ class CdmPlan(EncoderPlan):
         # attention activation (model.py:485 through get_activation, :121-130): relu / gelu
         # on the split-bf16 attention kernels (EncoderPlan: one-sequence up to 96 tokens,
         # the multi-workgroup ghm_attn_ext_*_act past 96, the joint model's 162)
-        if precision == "f32fwd" and not layernorm:
-            raise NotImplementedError("precision f32fwd: the LayerNorm-fused forward kernels (layernorm=True)")
+        if precision in ("f32fwd", "f32x6") and not layernorm:
+            raise NotImplementedError(f"precision {precision}: the LayerNorm-fused forward kernels (layernorm=True)")
         super().__init__(n_layer, n_token, n_seq, num_class=num_class, vocab=num_class, n_embd=n_embd, eps=eps,
                          normalize_attn=normalize_attn, device=device, precision=precision, activation=activation)
         if not 1 <= n_i_token <= n_token:
@@ -192,7 +193,7 @@ class CdmPlan(EncoderPlan):
         """z: f32 [N, T_img] noisy observations; cond: f32 [N, T - T_img, cond_ld]
         conditioning features (first V used).  Returns self.pred [N, T_img]."""
         s = _stream()
-        if self.bwd_x3 and split and self.layernorm:
+        if self.pack is not None and split and self.layernorm:
             self.split_weights(p, s)
         if self.joint:  # cond unused: self.tok holds the text leaves
             _native.call("ghm_cdm_embed_joint_fwd", _ptr(z), _ptr(self.tok), _ptr(p["t_embedding.weight"]),

@@ -71,8 +71,10 @@ def _stream():
 
 
 PRECISIONS = ("f32", "x3")
-# the CLIP encoder plan also takes "f32fwd": exact-f32 forward, split-bf16 backward
-ENCODER_PRECISIONS = PRECISIONS + ("f32fwd",)
+# the encoder plans (n_embd = 128) also take "f32fwd" (the forward at f32 accuracy,
+# the backward split-bf16) and "f32x6" (the forward's LN + QKV / LN + MLP on the
+# three-way split kernels, the backward exact f32)
+ENCODER_PRECISIONS = PRECISIONS + ("f32fwd", "f32x6")
 
 
 def default_precision(fallback="x3", allowed=PRECISIONS):
@@ -130,6 +132,8 @@ class EncoderPlan:
         # qkv6,mlp6: 0.499, guided step 4.72 ms against 5.44-5.68 for qkv,mlp
         # (profiles/r6_x6_curves.txt, r6_x6_ab.txt)
         parts = {"qkv", "attn", "mlp"}
+        if self.precision == "f32x6":
+            parts = {"qkv6", "attn", "mlp6"}
         if self.precision == "f32fwd":
             parts = {q for q in os.environ.get("GHM_F32FWD", "qkv6,mlp6").split(",") if q}
             if (not parts <= {"qkv", "qkv6", "attn", "mlp", "mlp6"} or {"mlp", "mlp6"} <= parts
@@ -259,6 +263,8 @@ class EncoderPlan:
             self.pack = torch.empty(L, npk, dtype=torch.bfloat16, device=dev)
         self.pack3 = (torch.empty(L, int(_native.GHM_SPLIT3_PACK_ELEMS), dtype=torch.bfloat16, device=dev)
                       if self.mlp6 or self.qkv6 else None)
+        if self.pack is None and self.pack3 is not None:  # the x6 kernels read the hi / lo planes too
+            self.pack = torch.empty(L, int(_native.GHM_SPLIT_PACK_ELEMS), dtype=torch.bfloat16, device=dev)
         # pre-split LN outputs: xs[l][0] = LN1(H_l), xs[l][1] = LN2(Hmid_l), each the hi
         # plane [M][128] then the lo plane (bf16: the bytes of one f32 plane)
         if ln_presplit is None:
@@ -308,7 +314,7 @@ class EncoderPlan:
         c = _native.call
         T, N, L = self.T, self.N, self.L
         s = _stream()
-        if self.bwd_x3 and split:
+        if self.pack is not None and split:
             self.split_weights(p, s)
         c("ghm_embed_fwd", _ptr(tok), _ptr(p["token_embeddings.weight"]),
           _ptr(p["position_embeddings.weight"]), _ptr(self.H[0]), N, T, self.V, D_MODEL, s)
@@ -329,7 +335,7 @@ class EncoderPlan:
     def _layer_fwd(self, p, l, s):
         c = _native.call
         M = self.M
-        pk = _ptr(self.pack[l]) if self.bwd_x3 else None
+        pk = _ptr(self.pack[l]) if self.pack is not None else None
         if self.qkv6:
             c("ghm_ln_qkv_fwd_x6", _ptr(self.H[l]), _ptr(p[f"_lns_1.{l}.weight"]), _ptr(p[f"_lns_1.{l}.bias"]), pk,
               _ptr(self.pack3[l]), _ptr(self.qkv[l]), _ptr(self.st1[l]), M, D_MODEL, self.eps, s)
@@ -348,7 +354,8 @@ class EncoderPlan:
         if self.mlp6:
             c("ghm_ln_mlp_fwd_x6", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]), pk,
               _ptr(self.pack3[l]), _ptr(p[f"_mlps.{l}.0.bias"]), _ptr(p[f"_mlps.{l}.2.bias"]), _ptr(self.H[l + 1]),
-              _ptr(self.st2[l]), M, D_MODEL, D_HIDDEN, self.eps, s)
+              _ptr(self.st2[l]), None if self.mlp_rc else _ptr(self.G[l]), None if self.mlp_rc else _ptr(self.Dg[l]),
+              M, D_MODEL, D_HIDDEN, self.eps, s)
             return
         if "mlp" in self.fwd_f32:
             c("ghm_ln_mlp_fwd", _ptr(self.Hmid[l]), _ptr(p[f"_lns_2.{l}.weight"]), _ptr(p[f"_lns_2.{l}.bias"]),

@@ -86,9 +86,9 @@ class CdmTrainer:
         self.clip_p = None if self.joint else {k: v.data for k, v in clip_model.named_parameters()}
         T, Ti = model.n_token, model.n_i_token
         self.T, self.Ti = T, Ti
-        # the unguided joint model: "f32fwd" (its 30-step reference curve at f32's
-        # distance, 7.8e-6 / 1.5e-5 against 7.2e-6 / 1.4e-5; step 4.66 -> 3.22 ms); the
-        # guided one (lr 1e-2) keeps exact f32 (models/cdm.py cdm_precision)
+        # the joint model: "f32fwd" unguided (its 30-step reference curve at f32's
+        # distance, 7.8e-6 / 1.5e-5 against 7.2e-6 / 1.4e-5; step 4.66 -> 3.22 ms),
+        # "f32x6" guided (the backward exact f32; 4.91 -> 4.37 ms; models/cdm.py)
         precision = cdm_precision(precision, self.joint, getattr(model, "guide", False),
                                   getattr(model, "layernorm", True))
         self.plan = CdmPlan(model.n_layer, T, Ti, batch_size, num_class=model.vocab_size, n_embd=model.n_embd,

@@ -168,14 +168,14 @@ def test_joint_cdm_graph_replay_matches_eager():
 def test_joint_trainer_default_precision(monkeypatch):
     """precision None (CdmTrainer and the module API): the unguided joint model runs
     "f32fwd" (its curve at f32's distance from the reference, below), the guided one
-    exact f32."""
+    "f32x6" (the exact-f32 backward; test_gpu_cdm_guided.py)."""
     from ghmclip import ConditionalDenoiseEncoderTransformer, get_lr_cosine_schedule
     from ghmclip.training.cdm_trainer import CdmTrainer
     from ghmclip import ConditionalDenoiseSampler
     monkeypatch.delenv("GHM_PRECISION", raising=False)
     s = ConditionalDenoiseSampler([4, 4], [3, 3], [P_Y, P_Y], [0.2, 0.2], sigma=1)
     sched = [get_lr_cosine_schedule(k, 1e-3, 1e-6, 0, 10) for k in range(11)]
-    for guide, want in ((False, "f32fwd"), (True, "f32")):
+    for guide, want in ((False, "f32fwd"), (True, "f32x6")):
         model = ConditionalDenoiseEncoderTransformer(162, 81, 10, 128, 9, [4, 4], 4, 512, sequential=False,
                                                      guide=guide).to(DEV)
         assert model._plan(20, 162, 81, torch.device(DEV)).precision == want  # the module API agrees
@@ -183,7 +183,7 @@ def test_joint_trainer_default_precision(monkeypatch):
         assert tr.precision == want, (guide, tr.precision)
 
 
-@pytest.mark.parametrize("precision", ["x3", "f32", "f32fwd"])
+@pytest.mark.parametrize("precision", ["x3", "f32", "f32fwd", "f32x6"])
 def test_joint_cdm_default_config_curve_vs_reference(precision):
     """The default joint config (exp_cdm_jointtrain.sh: p=0.2, L=9, d=128, B=128,
     lr 1e-3 -> 1e-6): loss and compare histories vs the reference PyTorch-CPU run
@@ -203,7 +203,7 @@ def test_joint_cdm_default_config_curve_vs_reference(precision):
     print(f"joint CDM curve ({precision}): {n} steps, max rel dloss {dev.max():.3e} (reference spread "
           f"{sl[-1]:.3e}, self-consistent window {wl} steps), dcompare {cdev.max():.3e} (spread {sc[-1]:.3e}, "
           f"window {wc}); in-window max {dev[:wl].max() if wl else 0:.3e} / {cdev[:wc].max() if wc else 0:.3e}")
-    if precision in ("f32", "f32fwd"):  # the joint CDM default: the parity claim
+    if precision in ("f32", "f32fwd", "f32x6"):  # the joint CDM defaults: the parity claim
         assert (dev <= bl).all() and (cdev <= bc).all()
     else:  # opt-in speed mode (GHM_PRECISION=x3): measured 8.3e-5 / 1.6e-4, envelope 1e-3
         assert dev.max() <= 1e-3 and cdev.max() <= 1e-3

@@ -25,9 +25,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 PRECISIONS = ["f32", "x3"]
 # + the CLIP plan's mixed mode: exact-f32 forward, split-bf16 backward
-MODES = PRECISIONS + ["f32fwd"]
-FWD_TOL = {"f32": 2e-5, "x3": 1e-4, "f32fwd": 2e-5}
-GRAD_TOL = {"f32": 1e-4, "x3": 5e-4, "f32fwd": 5e-4}
+# and "f32x6": the forward's LN + QKV / LN + MLP on three-way split kernels, the backward exact f32
+MODES = PRECISIONS + ["f32fwd", "f32x6"]
+FWD_TOL = {"f32": 2e-5, "x3": 1e-4, "f32fwd": 2e-5, "f32x6": 2e-5}
+GRAD_TOL = {"f32": 1e-4, "x3": 5e-4, "f32fwd": 5e-4, "f32x6": 1e-4}
 
 
 def _rel(a, b):

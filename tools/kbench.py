@@ -109,7 +109,8 @@ def main():
             # three-way split operands (precision f32fwd's mlp6 stage): pack3 of layer 0
             "ln_mlp_fwd_x6": (lambda: c("ghm_ln_mlp_fwd_x6", P(plan.Hmid[l]), P(p["_lns_2.0.weight"]),
                                         P(p["_lns_2.0.bias"]), pk, P(xo["pack3"]), P(p["_mlps.0.0.bias"]),
-                                        P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), M, 128, 512, plan.eps, sp),
+                                        P(p["_mlps.0.2.bias"]), P(xo["H"]), P(xo["st"]), None, None, M, 128, 512,
+                                        plan.eps, sp),
                               gf(4 * M * 128 * 512)),
             "ln_qkv_fwd_x6": (lambda: c("ghm_ln_qkv_fwd_x6", P(plan.H[l]), P(p["_lns_1.0.weight"]),
                                         P(p["_lns_1.0.bias"]), pk, P(xo["pack3"]), P(plan.qkv[l]), P(plan.st1[l]), M,
