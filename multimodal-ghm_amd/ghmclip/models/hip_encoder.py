@@ -90,6 +90,33 @@ def default_precision(fallback="x3", allowed=PRECISIONS):
     return p
 
 
+def forward_stages(precision, env=None):
+    """The forward stages an encoder plan keeps at f32 accuracy, as a frozenset of
+    qkv / attn / mlp (the exact-f32 kernels) and qkv6 / mlp6 (three-way split
+    operands, six bf16 MFMAs per product: 2e-6 from float64 where the f32 kernel is
+    at 1e-6 and x3 at 1e-5); the stages not named run split-bf16 x3.  "x3": none;
+    "f32": all three exact; "f32x6": qkv6, attn, mlp6 (with the exact-f32
+    backward); "f32fwd" (split-bf16 backward): $GHM_F32FWD (env: a mapping standing
+    in for os.environ), default qkv6,mlp6.  The guided 3001-step CLIP run needs
+    both projections' stages at f32 accuracy (worst ratio to its bound: qkv,mlp
+    0.377, all three 0.359; mlp alone 4.96, attn + mlp 4.44, qkv + attn 4.22,
+    profiles/r6_f32mix_curves.txt); qkv6,mlp6 0.499 at 4.72 ms per guided step
+    against 5.44-5.68 for qkv,mlp (profiles/r6_x6_curves.txt, r6_x6_ab.txt)."""
+    if precision == "x3":
+        return frozenset()
+    if precision == "f32":
+        return frozenset({"qkv", "attn", "mlp"})
+    if precision == "f32x6":
+        return frozenset({"qkv6", "attn", "mlp6"})
+    if precision != "f32fwd":
+        raise ValueError(f"precision must be one of {ENCODER_PRECISIONS}")
+    env = os.environ if env is None else env
+    parts = {q for q in env.get("GHM_F32FWD", "qkv6,mlp6").split(",") if q}
+    if not parts <= {"qkv", "qkv6", "attn", "mlp", "mlp6"} or {"mlp", "mlp6"} <= parts or {"qkv", "qkv6"} <= parts:
+        raise ValueError(f"GHM_F32FWD: comma list of qkv or qkv6 / attn / mlp or mlp6 (got {sorted(parts)})")
+    return frozenset(parts)
+
+
 def require_hip(t):
     if not (isinstance(t, torch.Tensor) and t.is_cuda and torch.version.hip):
         raise RuntimeError("ghmclip (MI355X build) runs on a HIP device only; "
@@ -117,29 +144,9 @@ class EncoderPlan:
         self.precision = default_precision(allowed=ENCODER_PRECISIONS) if precision is None else precision
         if self.precision not in ENCODER_PRECISIONS:
             raise ValueError(f"precision must be one of {ENCODER_PRECISIONS}")
-        # "f32fwd": the forward on the exact-f32 kernels, the backward on the split-bf16
-        # ones (U recomputed from the f32 forward's LN2 statistics, weight packs split
-        # per step as for "x3")
         self.fwd_x3 = self.precision == "x3"
         self.bwd_x3 = self.precision in ("x3", "f32fwd")
-        # the forward stages kept at f32 accuracy: all three on the exact-f32 kernels for
-        # "f32"; for "f32fwd" $GHM_F32FWD, a comma list of qkv / attn / mlp (exact-f32
-        # kernels) or qkv6 / mlp6 (three-way split operands, six bf16 MFMAs per product:
-        # 2e-6 from float64 where the f32 kernel is at 1e-6 and x3 at 1e-5), the others
-        # split-bf16 x3.  The guided 3001-step run needs both projections' stages at f32
-        # accuracy (worst ratio to its bound: qkv,mlp 0.377, all three 0.359; mlp alone
-        # 4.96, attn + mlp 4.44, qkv + attn 4.22, profiles/r6_f32mix_curves.txt); default
-        # qkv6,mlp6: 0.499, guided step 4.72 ms against 5.44-5.68 for qkv,mlp
-        # (profiles/r6_x6_curves.txt, r6_x6_ab.txt)
-        parts = {"qkv", "attn", "mlp"}
-        if self.precision == "f32x6":
-            parts = {"qkv6", "attn", "mlp6"}
-        if self.precision == "f32fwd":
-            parts = {q for q in os.environ.get("GHM_F32FWD", "qkv6,mlp6").split(",") if q}
-            if (not parts <= {"qkv", "qkv6", "attn", "mlp", "mlp6"} or {"mlp", "mlp6"} <= parts
-                    or {"qkv", "qkv6"} <= parts):
-                raise ValueError(f"GHM_F32FWD: comma list of qkv or qkv6 / attn / mlp or mlp6 (got {sorted(parts)})")
-        self.fwd_f32 = frozenset() if self.fwd_x3 else frozenset(parts)
+        self.fwd_f32 = forward_stages(self.precision)
         # mlp6 / qkv6: the LN2 + MLP / LN1 + QKV forward on three-way split operands
         # (ghm_ln_mlp_fwd_x6 / ghm_ln_qkv_fwd_x6: near the exact-f32 level, on the bf16
         # pipe), the weights' third planes in pack3
