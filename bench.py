@@ -703,7 +703,7 @@ def main():
     step_gflop = STEP_GFLOP * a.batch / 128 * a.layers / 5
     scale = a.batch / 128
     traffic = pmc_traffic(kname[:-1] if kname.endswith("x3bs") else kname)  # (the x3b passes when no x3bs pass)
-    x3 = kname.endswith("x3b") or kname.endswith("x3bs")
+    x3 = kname.endswith(("x3b", "x3bs"))
     x6 = kname.endswith("x6")
     # The kernel's work is 13.59 GFLOP (f32 products) per launch; the bytes that
     # MUST move are Hmid in and H out (the hidden activation never needs to leave
@@ -865,11 +865,14 @@ def main_cdm(a, ws, rank):
     # graded on the matrix cores, as the CLIP line's MLP forward: 4 M D F f32-product
     # flops per launch, issued as 3 bf16 MFMA products each in x3 (vs the bf16 peak),
     # as exact-f32 MFMA products in f32 (vs the f32 MFMA peak)
-    x3 = kname.endswith("x3b") or kname.endswith("x3bs")
-    mult, peak = (3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (1.0, F32_MFMA_PEAK_TFLOPS)
+    x3 = kname.endswith(("x3b", "x3bs"))
+    x6 = kname.endswith("x6")  # f32fwd / f32x6: the three-way split MLP forward, 6 bf16 products each
+    mult, peak = ((3.0, BF16_MFMA_PEAK_TFLOPS) if x3 else (6.0, BF16_MFMA_PEAK_TFLOPS) if x6
+                  else (1.0, F32_MFMA_PEAK_TFLOPS))
     kgflop = 4.0 * M * 128 * 512 / 1e9
     achieved = mult * kgflop / (kern_ms * 1e-3) / 1e3
-    mlp_bytes = 4 * M * (128 + 128) if x3 else 4 * M * (128 + 128 + 512 + 512)
+    # (bytes: Hmid in, H out; + G / GELU' [M][512] where the forward saves them: f32, and x6 under f32x6)
+    mlp_bytes = 4 * M * (128 + 128) if x3 or tr.precision == "f32fwd" else 4 * M * (128 + 128 + 512 + 512)
     out = {
         "metric": f"GHM training samples/sec ({'guided joint' if guide else 'joint' if joint else 'sequential'} "
                   f"CDM config)",
@@ -898,8 +901,8 @@ def main_cdm(a, ws, rank):
         "roofline": {"bound": "mfma", "kernel": f"{kname} (LN2+MLP fwd, one CDM layer, M={M})",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
-                     "basis": (f"bf16 MFMA products issued: 3 x {kgflop:.2f} GFLOP f32-product work per launch" if x3
-                               else f"{kgflop:.2f} GFLOP exact-f32 MFMA products per launch"),
+                     "basis": (f"bf16 MFMA products issued: {int(mult)} x {kgflop:.2f} GFLOP f32-product work per "
+                               f"launch" if x3 or x6 else f"{kgflop:.2f} GFLOP exact-f32 MFMA products per launch"),
                      "algorithmic_bytes": mlp_bytes,
                      "hbm_gbs": round(mlp_bytes / (kern_ms * 1e-3) / 1e9, 1),
                      "kernel_ms": round(kern_ms, 4)},

@@ -313,25 +313,31 @@ __device__ __forceinline__ f32x16 qkv_tile_x3(const __bf16* __restrict__ cb, __b
 
 // xs (optional): the split LN1 rows also leave as bf16 (hi, lo) planes [M][128]
 // (lo plane M * 128 elements on) for the dWq|k|v weight gradient (k_wgrad_x3 MODE 3)
+// tpg: weight tiles per workgroup (12 / tpg workgroups per token block, blockIdx.x =
+// token block * (12 / tpg) + group): for token counts too small to fill the chip
+// (the CDM's 10.5 K tokens: 82 token blocks on 256 CUs) each group recomputes the
+// LayerNorm and writes its own 32-column tiles; group 0 writes the statistics
 __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
     const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
-    float eps, __bf16* __restrict__ xs) {
+    float eps, __bf16* __restrict__ xs, int tpg) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PLANE];  // 2 buffers x (hi, lo)
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const int ngrp = 12 / tpg, grp = static_cast<int>(blockIdx.x) % ngrp;
+  const int b0 = grp * tpg, b1 = b0 + tpg;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x / ngrp) * 4 + (threadIdx.x >> 6)) * 32;
   const bool active = m0 < M;
   const int64_t m = m0 + j;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
   const __bf16* W = pack + PK_QKV_N;
-  fill_r32_w8<4>(W, GHM_D, PK_QKV, lds, lds + PLANE);  // tile 0, in flight over the LayerNorm
+  fill_r32_w8<4>(W + b0 * 32 * GHM_D, GHM_D, PK_QKV, lds, lds + PLANE);  // tile b0, in flight over the LayerNorm
   bf16x8 xh[8], xl[8];
   {
     float mean = 0.f, rstd = 0.f;
     ln_row_split(H + mc * GHM_D, lnw, lnb, h, eps, active, xh, xl, mean, rstd);
-    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
-    if (xs && active && valid) {  // features 64 h + 8 t .. + 7: 8 chunks per plane
+    if (active && h == 0 && valid && grp == 0) stats[m] = make_float2(mean, rstd);
+    if (xs && active && valid && grp == 0) {  // features 64 h + 8 t .. + 7: 8 chunks per plane
       __bf16* xr = xs + m * GHM_D + 64 * h;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -344,14 +350,14 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
   f32x16 prev = zero16();
   float* orow = qkv + m * (3 * GHM_D);
 #pragma unroll 1
-  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
-    const int cur = b & 1;
-    if (b > 0 && active && valid) {  // tile b - 1's outputs
+  for (int b = b0; b < b1; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
+    const int cur = (b - b0) & 1;
+    if (b > b0 && active && valid) {  // tile b - 1's outputs
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         st4(orow + 32 * (b - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
     }
-    const int bn = b + 1 < 12 ? b + 1 : 11;  // branch-free: the last tile refills tile 11
+    const int bn = b + 1 < b1 ? b + 1 : b1 - 1;  // branch-free: the last tile refills itself
     prev = qkv_tile_x3(lds + 2 * PLANE * cur, lds + 2 * PLANE * (cur ^ 1), W + bn * 32 * GHM_D, GHM_D, j, h,
                        active, xh, xl, zero16());
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -359,8 +365,20 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x3(
   if (active && valid) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      st4(orow + 32 * 11 + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
+      st4(orow + 32 * (b1 - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
   }
+}
+
+// weight tiles per workgroup of the LN1 + QKV forwards: all 12 when the token blocks
+// alone give every CU a workgroup; else split over 2, 3 or 4 groups of tiles
+static int qkv_tiles_per_group(int64_t M) {
+  const char* e = getenv("GHM_QKV_TPG");  // A/B knob: 12, 6, 4 or 3
+  if (e) {
+    const int t = atoi(e);
+    if (t == 12 || t == 6 || t == 4 || t == 3) return t;
+  }
+  const int64_t nb = ghm_token_blocks(M);
+  return nb >= 256 ? 12 : nb >= 128 ? 6 : nb >= 86 ? 4 : 3;
 }
 
 // qkv_tile_x3 on three planes (cb / nb __restrict__ for the same reason)
@@ -386,36 +404,38 @@ __device__ __forceinline__ f32x16 qkv_tile_x6(const __bf16* __restrict__ cb, __b
 __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x6(
     const float* __restrict__ H, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const __bf16* pack, const __bf16* pack3, float* __restrict__ qkv, float2* __restrict__ stats, int64_t M,
-    float eps) {
+    float eps, int tpg) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[6 * PLANE];  // 2 buffers x (hi, lo, lo2)
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-  const int64_t m0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 32;
+  const int ngrp = 12 / tpg, grp = static_cast<int>(blockIdx.x) % ngrp;  // (k_ln_qkv_fwd_x3)
+  const int b0 = grp * tpg, b1 = b0 + tpg;
+  const int64_t m0 = (static_cast<int64_t>(blockIdx.x / ngrp) * 4 + (threadIdx.x >> 6)) * 32;
   const bool active = m0 < M;
   const int64_t m = m0 + j;
   const bool valid = m < M;
   const int64_t mc = valid ? m : M - 1;
   const __bf16* W = pack + PK_QKV_N;
   const __bf16* Wc = pack3 + PK3_QKV_N;
-  fill_r32_w8<4>(W, GHM_D, PK_QKV, lds, lds + PLANE);  // tile 0, in flight over the LayerNorm
-  fill_r32_1<4>(Wc, GHM_D, lds + 2 * PLANE);
+  fill_r32_w8<4>(W + b0 * 32 * GHM_D, GHM_D, PK_QKV, lds, lds + PLANE);  // tile b0, in flight over the LayerNorm
+  fill_r32_1<4>(Wc + b0 * 32 * GHM_D, GHM_D, lds + 2 * PLANE);
   bf16x8 x0[8], x1[8], x2[8];
   {
     float mean = 0.f, rstd = 0.f;
     ln_row_split3(H + mc * GHM_D, lnw, lnb, h, eps, active, x0, x1, x2, mean, rstd);
-    if (active && h == 0 && valid) stats[m] = make_float2(mean, rstd);
+    if (active && h == 0 && valid && grp == 0) stats[m] = make_float2(mean, rstd);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   f32x16 prev = zero16();
   float* orow = qkv + m * (3 * GHM_D);
 #pragma unroll 1
-  for (int b = 0; b < 12; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
-    const int cur = b & 1;
-    if (b > 0 && active && valid) {  // tile b - 1's outputs
+  for (int b = b0; b < b1; ++b) {  // tile b = rows 32b..32b+31 of [Wq; Wk; Wv]
+    const int cur = (b - b0) & 1;
+    if (b > b0 && active && valid) {  // tile b - 1's outputs
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         st4(orow + 32 * (b - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
     }
-    const int bn = b + 1 < 12 ? b + 1 : 11;  // branch-free: the last tile refills tile 11
+    const int bn = b + 1 < b1 ? b + 1 : b1 - 1;  // branch-free: the last tile refills itself
     prev = qkv_tile_x6(lds + 3 * PLANE * cur, lds + 3 * PLANE * (cur ^ 1), W + bn * 32 * GHM_D,
                        Wc + bn * 32 * GHM_D, j, h, active, x0, x1, x2);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -423,7 +443,7 @@ __global__ __launch_bounds__(256, 2) void k_ln_qkv_fwd_x6(
   if (active && valid) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      st4(orow + 32 * 11 + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
+      st4(orow + 32 * (b1 - 1) + quad_off(q, h), prev[4 * q], prev[4 * q + 1], prev[4 * q + 2], prev[4 * q + 3]);
   }
 }
 
@@ -2710,9 +2730,10 @@ extern "C" int ghm_ln_qkv_fwd_x3(const float* H, const float* ln_w, const float*
                                  float* qkv, float* stats, int64_t M, int D, float eps, void* stream) {
   GHM_CHECK(H && ln_w && ln_b && pack && qkv && stats, "null pointer");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
-  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+  const int tpg = qkv_tiles_per_group(M);
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M) * (12 / tpg))), dim3(256), 0,
                      ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), qkv,
-                     reinterpret_cast<float2*>(stats), M, eps, nullptr);
+                     reinterpret_cast<float2*>(stats), M, eps, nullptr, tpg);
   return ghm_launch_status();
 }
 
@@ -2721,9 +2742,10 @@ extern "C" int ghm_ln_qkv_fwd_x3s(const float* H, const float* ln_w, const float
   GHM_CHECK(H && ln_w && ln_b && pack && qkv && stats && xs, "null pointer");
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
   GHM_CHECK((reinterpret_cast<uintptr_t>(xs) & 15) == 0, "16-byte aligned xs");
-  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+  const int tpg = qkv_tiles_per_group(M);
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x3, dim3(static_cast<unsigned>(ghm_token_blocks(M) * (12 / tpg))), dim3(256), 0,
                      ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack), qkv,
-                     reinterpret_cast<float2*>(stats), M, eps, static_cast<__bf16*>(xs));
+                     reinterpret_cast<float2*>(stats), M, eps, static_cast<__bf16*>(xs), tpg);
   return ghm_launch_status();
 }
 
@@ -3089,9 +3111,10 @@ extern "C" int ghm_ln_qkv_fwd_x6(const float* H, const float* ln_w, const float*
   GHM_CHECK(D == GHM_D && M >= 1, "shape");
   GHM_CHECK(((reinterpret_cast<uintptr_t>(pack) | reinterpret_cast<uintptr_t>(pack3)) & 15) == 0,
             "16-byte aligned packs");
-  hipLaunchKernelGGL(k_ln_qkv_fwd_x6, dim3(static_cast<unsigned>(ghm_token_blocks(M))), dim3(256), 0,
+  const int tpg = qkv_tiles_per_group(M);
+  hipLaunchKernelGGL(k_ln_qkv_fwd_x6, dim3(static_cast<unsigned>(ghm_token_blocks(M) * (12 / tpg))), dim3(256), 0,
                      ghm_stream(stream), H, ln_w, ln_b, reinterpret_cast<const __bf16*>(pack),
-                     reinterpret_cast<const __bf16*>(pack3), qkv, reinterpret_cast<float2*>(stats), M, eps);
+                     reinterpret_cast<const __bf16*>(pack3), qkv, reinterpret_cast<float2*>(stats), M, eps, tpg);
   return ghm_launch_status();
 }
 

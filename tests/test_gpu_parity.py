@@ -195,6 +195,26 @@ def test_mlp6_forward_and_backward(T, nseq, stages, monkeypatch):
         assert _rel(pp.grad, pr.grad) < GRAD_TOL["f32fwd"], k
 
 
+@pytest.mark.parametrize("precision", ["x3", "f32fwd"])
+def test_qkv_forward_tile_groups_bit_identical(precision, monkeypatch):
+    """The LN1 + QKV forward split over groups of weight tiles (small token counts:
+    GHM_QKV_TPG = 6 / 4 / 3 tiles per workgroup) writes exactly the all-12-tile
+    kernel's Q|K|V and LN1 statistics (x3 and the x6 kernel of f32fwd)."""
+    prod, _ = _pair(L=1, T=81, precision=precision)
+    x = torch.randint(0, 10, (33, 81), generator=torch.Generator().manual_seed(2)).to(DEV)
+    plan = None
+    outs = {}
+    for tpg in ("12", "6", "4", "3"):
+        monkeypatch.setenv("GHM_QKV_TPG", tpg)
+        prod(x)
+        torch.cuda.synchronize()
+        plan = next(iter(prod._plans.values()))
+        outs[tpg] = (plan.qkv[0].clone(), plan.st1[0].clone())
+    for tpg in ("6", "4", "3"):
+        assert torch.equal(outs[tpg][0], outs["12"][0]), tpg
+        assert torch.equal(outs[tpg][1], outs["12"][1]), tpg
+
+
 def test_clip_loss_and_grad():
     from ghmclip import GuidedClipLoss
     B, K = 16, 4
