@@ -31,7 +31,7 @@ __device__ __forceinline__ f32x16 mfma_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x
   return mfma_bf(ah, bh, c);
 }
 
-// six products of three-way split operands on the 32x32x16 MFMA (see mfma16_x6z),
+// six products of three-way split operands on the 32x32x16 MFMA (see mfma16_x6),
 // chained: for accumulators that start from zero per output tile
 __device__ __forceinline__ f32x16 mfma_x6(bf16x8 a0, bf16x8 a1, bf16x8 a2, bf16x8 b0, bf16x8 b1, bf16x8 b2,
                                          f32x16 c) {
@@ -56,18 +56,17 @@ __device__ __forceinline__ f32x4 mfma16_x3(bf16x8 ah, bf16x8 al, bf16x8 bh, bf16
   return mfma16_bf(ah, bh, c);
 }
 // six products of three-way split operands, a.b ~ a2 b0 + a1 b1 + a0 b2 + a1 b0 +
-// a0 b1 + a0 b0 (the dropped terms ~2^-27 |a||b|), as two zero-started partial sums
-// added on the VALU: the five cross terms, smallest first, then hi x hi alone (an MFMA adding into an accumulator drops
-// the low bits of the smaller side at alignment, so the large term is kept apart)
-__device__ __forceinline__ f32x4 mfma16_x6z(bf16x8 a0, bf16x8 a1, bf16x8 a2, bf16x8 b0, bf16x8 b1, bf16x8 b2) {
-  f32x4 z;
-  z[0] = z[1] = z[2] = z[3] = 0.f;
-  f32x4 c = mfma16_bf(a2, b0, z);
+// a0 b1 + a0 b0 (the dropped terms ~2^-27 |a||b|), smallest first, chained into one
+// accumulator: for sums that start from zero and stay at the magnitude of their own
+// terms (an MFMA adding products into a much larger accumulator drops their low bits)
+__device__ __forceinline__ f32x4 mfma16_x6(bf16x8 a0, bf16x8 a1, bf16x8 a2, bf16x8 b0, bf16x8 b1, bf16x8 b2,
+                                           f32x4 c) {
+  c = mfma16_bf(a2, b0, c);
   c = mfma16_bf(a1, b1, c);
   c = mfma16_bf(a0, b2, c);
   c = mfma16_bf(a1, b0, c);
   c = mfma16_bf(a0, b1, c);
-  return c + mfma16_bf(a0, b0, z);
+  return mfma16_bf(a0, b0, c);
 }
 __device__ __forceinline__ f32x4 zero4() {
   f32x4 z;

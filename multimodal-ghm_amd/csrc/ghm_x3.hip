@@ -615,7 +615,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_ln_mlp_fwd_x3b(
 // ---------------------------------------------------------------------------
 // LN2 + MLP forward on three-way split operands (the "f32fwd" precision's MLP stage
 // as `mlp6`): the k_ln_mlp_fwd_x3b schedule with every product as six bf16 MFMAs
-// (mfma16_x6z, ~2^-24 relative: near the exact-f32 kernel's level, on the bf16 pipe)
+// (mfma16_x6, ~2^-24 relative: the exact-f32 kernel's level, on the bf16 pipe)
 // instead of three, and the exact GELU of the f32 kernel.  The weights' third
 // planes come from pack3 ([W1 n | W2 p32] lo2 planes in the pack's layouts, written
 // by ghm_split3_weights); the LDS ring holds six planes per buffer (96 KB
@@ -687,21 +687,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
       split3_8(x + 8 * s2, x0[s2], x1[s2], x2[s2]);
     }
   }
+  // the MLP's own sum from zero; the residual and b2 are added once at the end
   f32x4 y[8];
-  __builtin_amdgcn_sched_barrier(0);
-  {
-    const float* hr = Hmid + mc * GHM_D;
+  __builtin_amdgcn_sched_barrier(0);  // (after the LN block, as k_ln_mlp_fwd_x3b)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = 16 * j + 4 * g;
-      const float4 hv = *reinterpret_cast<const float4*>(hr + f);
-      const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
-      y[j][0] = hv.x + bv.x;
-      y[j][1] = hv.y + bv.y;
-      y[j][2] = hv.z + bv.z;
-      y[j][3] = hv.w + bv.w;
-    }
-  }
+  for (int j = 0; j < 8; ++j) y[j] = zero4();
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
@@ -717,11 +707,12 @@ __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
       fill_r128_w8<NW>(W2 + cn * 32, GHM_F, PK_W, s2(cur ^ 1, 0), s2(cur ^ 1, 1));
       fill_r128_1<NW>(W2c + cn * 32, GHM_F, s2(cur ^ 1, 2));
     }
-    // every six-product group starts from zero accumulators and is added to the
-    // running sum on the VALU (round to nearest): an MFMA adding small products into
-    // a large accumulator drops their low bits (measured against float64: seeded with
-    // the residual as k_ln_mlp_fwd_x3b is, 8.3e-6 -- the split-bf16 kernel's 1.1e-5
-    // level; zero-started groups 2.0e-6; the f32 kernel 1.05e-6)
+    // the products chain into accumulators that start from zero (u per chunk, y over
+    // all chunks): an MFMA adding small products into a much larger accumulator drops
+    // their low bits, so y is not seeded with the residual as in k_ln_mlp_fwd_x3b
+    // (measured against float64: residual-seeded 8.3e-6 -- the split-bf16 kernel's
+    // 1.1e-5 level; zero-started six-product groups added on the VALU 2.0e-6; chained
+    // from zero with the residual added at the end 8.0e-7, the f32 kernel 1.05e-6)
     f32x4 u[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -729,8 +720,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
         const int o = r32_off(16 * jt + t, 4 * s2 + g);
-        u[jt] += mfma16_x6z(ldsb8(s1(cur, 0) + o), ldsb8(s1(cur, 1) + o), ldsb8(s1(cur, 2) + o), x0[s2], x1[s2],
-                            x2[s2]);
+        u[jt] = mfma16_x6(ldsb8(s1(cur, 0) + o), ldsb8(s1(cur, 1) + o), ldsb8(s1(cur, 2) + o), x0[s2], x1[s2],
+                          x2[s2], u[jt]);
       }
     }
     float gv[8];
@@ -764,12 +755,25 @@ __global__ __launch_bounds__(64 * NW, 1) void k_ln_mlp_fwd_x6(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int o = r128_off(16 * j + t, g);
-      y[j] += mfma16_x6z(ldsb8(s2(cur, 0) + o), ldsb8(s2(cur, 1) + o), ldsb8(s2(cur, 2) + o), g0, g1, g2);
+      y[j] = mfma16_x6(ldsb8(s2(cur, 0) + o), ldsb8(s2(cur, 1) + o), ldsb8(s2(cur, 2) + o), g0, g1, g2, y[j]);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if (valid) {
     float* orow = Hout + m * GHM_D;
+    {  // the residual and b2 added once, on the VALU, to the MLP's own sum
+      const float* hr = Hmid + m * GHM_D;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 16 * j + 4 * g;
+        const float4 hv = *reinterpret_cast<const float4*>(hr + f);
+        const float4 bv = *reinterpret_cast<const float4*>(b2 + f);
+        y[j][0] = hv.x + (y[j][0] + bv.x);
+        y[j][1] = hv.y + (y[j][1] + bv.y);
+        y[j][2] = hv.z + (y[j][2] + bv.z);
+        y[j][3] = hv.w + (y[j][3] + bv.w);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) st4(orow + 16 * j + 4 * g, y[j][0], y[j][1], y[j][2], y[j][3]);
   }

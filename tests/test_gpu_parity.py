@@ -144,8 +144,8 @@ def test_mlp6_forward_and_backward(T, nseq, stages, monkeypatch):
     LN1 + QKV) forward on three-way split operands (ghm_ln_mlp_fwd_x6 /
     ghm_ln_qkv_fwd_x6, six bf16 MFMAs per product) --
     every forward stage within the exact-f32 bound of the float64 oracle (2e-5),
-    and the LN2 + MLP output within 3x the f32 kernel's distance from a float64
-    evaluation and at a third of the split-bf16 kernel's or less;
+    and the LN2 + MLP output within 1.5x the f32 kernel's distance from a float64
+    evaluation and at a fifth of the split-bf16 kernel's or less;
     every gradient within the split-bf16 backward's bound (5e-4)."""
     monkeypatch.setenv("GHM_F32FWD", stages)
     prod, ref = _pair(L=2, T=T, precision="f32fwd")
@@ -186,8 +186,8 @@ def test_mlp6_forward_and_backward(T, nseq, stages, monkeypatch):
     dev = {k: (v[:M].double() - want64).abs().max().item() for k, v in
            (("x6", plan.H[1]), ("f32", out32), ("x3", out3))}
     print(f"LN2 + MLP forward vs float64: {dev}")
-    # measured: x6 2.0e-6 / 2.1e-6, f32 1.05e-6 / 0.87e-6, x3 1.07e-5 / 8.7e-6
-    assert dev["x6"] < 3 * dev["f32"] and dev["x6"] < dev["x3"] / 3
+    # measured: x6 8.0e-7 / 7.2e-7, f32 1.05e-6 / 1.02e-6, x3 1.07e-5 / 1.07e-5
+    assert dev["x6"] < 1.5 * dev["f32"] and dev["x6"] < dev["x3"] / 5
     (emb * R.to(DEV)).sum().backward()
     (ref(x)[0] * R).sum().backward()
     torch.cuda.synchronize()
